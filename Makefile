@@ -1,0 +1,22 @@
+# Host-side builds.  The HIP product library is built by
+# compression_without_quantization_amd/build.py (called from __graft_entry__.build()).
+CC ?= gcc
+CXX ?= g++
+
+ORACLE_SO := oracle/libcwq_oracle.so
+MATHCHECK_SO := tests/native/libcwq_mathcheck.so
+
+all: $(ORACLE_SO) $(MATHCHECK_SO)
+
+# Oracle: plain C, glibc libm, no FMA contraction, OpenMP over blocks.
+$(ORACLE_SO): oracle/cwq_oracle.c
+	$(CC) -O2 -ffp-contract=off -fno-fast-math -fopenmp -fPIC -shared -o $@ $< -lm
+
+# Product math header compiled for the host (test shim).
+$(MATHCHECK_SO): tests/native/mathcheck.cpp compression_without_quantization_amd/csrc/cwq_math.h
+	$(CXX) -std=c++17 -O2 -ffp-contract=off -fno-fast-math -mfma -fPIC -shared -o $@ $<
+
+clean:
+	rm -f $(ORACLE_SO) $(MATHCHECK_SO)
+
+.PHONY: all clean

@@ -1,0 +1,22 @@
+"""MI355X-native greedy coded sampler (compression without quantization).
+
+Public surface mirrors the reference's code/coded_greedy_sampler.py,
+code/misc.py and code/binary_io.py (bit-string helpers); every sample is
+computed by the gfx950 kernels in libcwq.so (see include/cwq.h).
+"""
+from .binary_io import (bitcode_to_indices, from_bit_string, indices_to_bitcode,
+                        to_bit_string)
+from .coded_greedy_sampler import (Normal, code_greedy_sample, code_grouped_greedy_sample,
+                                   decode, decode_blocks, decode_greedy_sample,
+                                   decode_grouped_greedy_sample, encode, encode_blocks,
+                                   encode_workspace_bytes, group_size_threshold, group_starts)
+from .misc import stateless_normal_sample
+from .parallel import gather_indices, shard_range
+
+__all__ = [
+    "Normal", "code_greedy_sample", "decode_greedy_sample", "code_grouped_greedy_sample",
+    "decode_grouped_greedy_sample", "encode", "decode", "encode_blocks", "decode_blocks",
+    "encode_workspace_bytes", "group_starts", "group_size_threshold",
+    "stateless_normal_sample", "to_bit_string", "from_bit_string", "indices_to_bitcode",
+    "bitcode_to_indices", "shard_range", "gather_indices",
+]

@@ -1,0 +1,74 @@
+"""ctypes binding of libcwq.so (the C ABI in include/cwq.h).
+
+The product path has exactly one implementation: the gfx950 HIP kernels in
+``csrc/``.  If the library is missing or cannot be loaded this module raises;
+there is no CPU fallback.
+"""
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libcwq.so")
+
+c_int = ctypes.c_int
+c_i32 = ctypes.c_int32
+c_i64 = ctypes.c_int64
+c_f32 = ctypes.c_float
+c_f64 = ctypes.c_double
+c_size = ctypes.c_size_t
+c_vp = ctypes.c_void_p
+c_str = ctypes.c_char_p
+
+# name -> (restype, argtypes); mirrors include/cwq.h one-to-one.
+SIGNATURES = {
+    "cwq_version": (c_int, []),
+    "cwq_last_error": (c_str, []),
+    "cwq_stateless_normal_sample": (c_int, [c_vp, c_vp, c_i64, c_i64, c_i32, c_vp, c_vp]),
+    "cwq_greedy_encode_workspace_size": (c_size, [c_i64, c_i64]),
+    "cwq_greedy_encode": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_int,
+                                  c_int, c_i32, c_f32, c_i64, c_vp, c_vp, c_vp, c_size, c_vp]),
+    "cwq_greedy_encode_uniform": (c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_int, c_int,
+                                          c_i32, c_f32, c_i64, c_vp, c_vp, c_vp, c_size, c_vp]),
+    "cwq_greedy_decode": (c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_int, c_int,
+                                  c_i32, c_f32, c_i64, c_vp, c_vp]),
+    "cwq_greedy_decode_uniform": (c_int, [c_vp, c_vp, c_vp, c_i64, c_i64, c_int, c_int, c_i32,
+                                          c_f32, c_i64, c_vp, c_vp]),
+    "cwq_standardise": (c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp]),
+    "cwq_kl_normal_normal": (c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp]),
+    "cwq_destandardise": (c_int, [c_vp, c_vp, c_vp, c_i64, c_vp, c_vp]),
+    "cwq_group_starts": (c_i64, [c_vp, c_i64, c_i64, c_f64, c_vp, c_i64]),
+    "cwq_selftest_bm_tables": (c_int, [ctypes.c_uint32, c_i64, c_vp, c_vp, c_vp, c_vp]),
+    "cwq_selftest_logf": (c_int, [c_vp, c_i64, c_vp, c_vp]),
+    "cwq_profile_set_eval_events": (c_int, [c_vp, c_vp]),
+}
+
+_lib = None
+
+
+class CwqError(RuntimeError):
+    """A libcwq call returned an error code."""
+
+
+def load():
+    """Load libcwq.so (once).  Raises if it is absent: no fallback exists."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            f"{LIB_PATH} not found: build the HIP extension first "
+            "(python -c 'import __graft_entry__ as g; g.build()')")
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def check(rc, what):
+    if rc < 0:
+        msg = load().cwq_last_error().decode("utf-8", "replace")
+        raise CwqError(f"{what} failed ({rc}): {msg}")
+    return rc

@@ -1,0 +1,368 @@
+"""Greedy coded sampler -- the reference's API on the gfx950 kernels.
+
+Mirrors code/coded_greedy_sampler.py of the reference function for function:
+
+  code_greedy_sample            (:29-89)
+  decode_greedy_sample          (:93-167)
+  code_grouped_greedy_sample    (:170-296)
+  decode_grouped_greedy_sample  (:299-364)
+
+plus the batched block API the north star asks for:
+
+  encode(prior_loc, prior_scale, post_loc, post_scale, seed, kl_bits)
+  decode(indices_or_bitcode, prior_loc, prior_scale, seed, kl_bits)
+  encode_blocks / decode_blocks   (CSR or uniform blocks, explicit n_steps)
+
+Differences from the TF1 reference (deliberate, documented in DESIGN.md):
+  * functions return concrete values instead of graph tensors; ``sess`` is
+    accepted and ignored;
+  * decode_grouped_greedy_sample does not append to the caller's
+    ``group_start_indices`` list (the reference mutates it, :323); the decoded
+    groups are the same;
+  * ``adaptive``, ``backfitting_steps`` and ``use_log_prob`` are accepted and
+    ignored, exactly as in the reference.
+
+All arithmetic runs in libcwq.so; nothing here computes samples on the CPU.
+"""
+import numpy as np
+import torch
+
+from . import _lib
+from .binary_io import bitcode_to_indices, indices_to_bitcode
+
+VERBOSE = True
+
+
+# ---------------------------------------------------------------------------
+# tensor plumbing
+# ---------------------------------------------------------------------------
+def _device_of(*xs):
+    for x in xs:
+        if isinstance(x, torch.Tensor) and x.is_cuda:
+            return x.device
+    if not torch.cuda.is_available():
+        raise RuntimeError("compression_without_quantization_amd needs a ROCm GPU "
+                           "(torch.cuda.is_available() is False); there is no CPU path")
+    return torch.device("cuda", torch.cuda.current_device())
+
+
+def _is_float32(x):
+    if isinstance(x, torch.Tensor):
+        return x.dtype == torch.float32
+    return np.asarray(x).dtype == np.float32
+
+
+def _f32(x, device, what):
+    if isinstance(x, torch.Tensor):
+        t = x
+    else:
+        t = torch.from_numpy(np.ascontiguousarray(np.asarray(x)))
+    if t.dtype != torch.float32:
+        raise TypeError(f"{what} must be float32, got {t.dtype}")
+    return t.to(device=device).contiguous().reshape(-1)
+
+
+def _ptr(t):
+    return t.data_ptr() if t is not None and t.numel() > 0 else None
+
+
+def _like_input(t, ref):
+    """Return ``t`` (a cuda tensor) as the caller's array type."""
+    if isinstance(ref, torch.Tensor):
+        return t
+    return t.cpu().numpy()
+
+
+class Normal:
+    """Minimal stand-in for tfd.Normal: anything with .loc/.scale/.dtype works."""
+
+    def __init__(self, loc, scale):
+        self.loc = loc
+        self.scale = scale
+
+    @property
+    def dtype(self):
+        return self.loc.dtype
+
+
+# ---------------------------------------------------------------------------
+# batched block API (C ABI: cwq_greedy_encode[_uniform], cwq_greedy_decode[_uniform])
+# ---------------------------------------------------------------------------
+def encode_workspace_bytes(nb, total_dims):
+    return int(_lib.load().cwq_greedy_encode_workspace_size(int(nb), int(total_dims)))
+
+
+def encode_blocks(t_loc, t_scale, p_loc, p_scale, n_bits_per_step, n_steps, seed, rho=1.,
+                  block_dim=None, block_off=None, max_block_dim=None, block_id_base=0,
+                  out_idx=None, out_sample=None, workspace=None):
+    """code_greedy_sample over many blocks at once.
+
+    Blocks are either uniform (``block_dim``) or CSR (``block_off``, nb+1
+    offsets).  Block g is coded with seed ``seed + block_id_base + g``
+    (coded_greedy_sampler.py:282).  Returns (idx int32 [nb, n_steps],
+    sample f32 [D]) as cuda tensors.
+    """
+    lib = _lib.load()
+    dev = _device_of(t_loc, t_scale, p_loc, p_scale)
+    tl = _f32(t_loc, dev, "t_loc")
+    ts = _f32(t_scale, dev, "t_scale")
+    pl = _f32(p_loc, dev, "p_loc")
+    ps = _f32(p_scale, dev, "p_scale")
+    D = tl.numel()
+    if not (ts.numel() == pl.numel() == ps.numel() == D):
+        raise ValueError("t_loc, t_scale, p_loc, p_scale must have the same size")
+    if (block_dim is None) == (block_off is None):
+        raise ValueError("give exactly one of block_dim / block_off")
+    if block_dim is not None:
+        block_dim = int(block_dim)
+        if block_dim < 0 or (block_dim == 0 and D != 0) or (block_dim and D % block_dim):
+            raise ValueError(f"D={D} is not a multiple of block_dim={block_dim}")
+        nb = D // block_dim if block_dim else 0
+        offs = None
+    else:
+        offs_h = np.asarray(block_off.cpu() if isinstance(block_off, torch.Tensor)
+                            else block_off, dtype=np.int64).reshape(-1)
+        nb = offs_h.size - 1
+        if nb < 0 or offs_h[0] != 0 or offs_h[-1] != D or (np.diff(offs_h) < 0).any():
+            raise ValueError("block_off must be non-decreasing from 0 to D")
+        if max_block_dim is None:
+            max_block_dim = int(np.diff(offs_h).max()) if nb > 0 else 0
+        offs = torch.from_numpy(offs_h).to(dev)
+    n_steps = int(n_steps)
+    if out_idx is None:
+        out_idx = torch.empty((nb, n_steps), dtype=torch.int32, device=dev)
+    if out_sample is None:
+        out_sample = torch.empty(D, dtype=torch.float32, device=dev)
+    need = encode_workspace_bytes(nb, D)
+    if workspace is None or workspace.numel() < need:
+        workspace = torch.empty(max(need, 1), dtype=torch.uint8, device=dev)
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    seed32 = int(np.int32(np.uint32(int(seed) & 0xFFFFFFFF)))
+    if offs is None:
+        rc = lib.cwq_greedy_encode_uniform(
+            _ptr(tl), _ptr(ts), _ptr(pl), _ptr(ps), nb, block_dim, int(n_bits_per_step),
+            n_steps, seed32, float(rho), int(block_id_base), _ptr(out_idx), _ptr(out_sample),
+            workspace.data_ptr(), workspace.numel(), stream)
+    else:
+        rc = lib.cwq_greedy_encode(
+            _ptr(tl), _ptr(ts), _ptr(pl), _ptr(ps), offs.data_ptr(), nb, D, int(max_block_dim),
+            int(n_bits_per_step), n_steps, seed32, float(rho), int(block_id_base),
+            _ptr(out_idx), _ptr(out_sample), workspace.data_ptr(), workspace.numel(), stream)
+    _lib.check(rc, "cwq_greedy_encode")
+    return out_idx, out_sample
+
+
+def decode_blocks(idx, p_loc, p_scale, n_bits_per_step, n_steps, seed, rho=1.,
+                  block_dim=None, block_off=None, block_id_base=0, out_sample=None):
+    """decode_greedy_sample over many blocks (inverse of encode_blocks)."""
+    lib = _lib.load()
+    dev = _device_of(idx, p_loc, p_scale)
+    pl = _f32(p_loc, dev, "p_loc")
+    ps = _f32(p_scale, dev, "p_scale")
+    D = pl.numel()
+    if ps.numel() != D:
+        raise ValueError("p_loc and p_scale must have the same size")
+    it = idx if isinstance(idx, torch.Tensor) else torch.from_numpy(np.asarray(idx))
+    it = it.to(device=dev, dtype=torch.int32).contiguous().reshape(-1)
+    n_steps = int(n_steps)
+    if out_sample is None:
+        out_sample = torch.empty(D, dtype=torch.float32, device=dev)
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    seed32 = int(np.int32(np.uint32(int(seed) & 0xFFFFFFFF)))
+    if (block_dim is None) == (block_off is None):
+        raise ValueError("give exactly one of block_dim / block_off")
+    if block_dim is not None:
+        block_dim = int(block_dim)
+        nb = D // block_dim if block_dim else 0
+        if it.numel() != nb * n_steps:
+            raise ValueError("idx must hold nb * n_steps entries")
+        rc = lib.cwq_greedy_decode_uniform(
+            _ptr(it), _ptr(pl), _ptr(ps), nb, block_dim, int(n_bits_per_step), n_steps, seed32,
+            float(rho), int(block_id_base), _ptr(out_sample), stream)
+    else:
+        offs_h = np.asarray(block_off.cpu() if isinstance(block_off, torch.Tensor)
+                            else block_off, dtype=np.int64).reshape(-1)
+        nb = offs_h.size - 1
+        if nb < 0 or offs_h[0] != 0 or offs_h[-1] != D or (np.diff(offs_h) < 0).any():
+            raise ValueError("block_off must be non-decreasing from 0 to D")
+        if it.numel() != nb * n_steps:
+            raise ValueError("idx must hold nb * n_steps entries")
+        offs = torch.from_numpy(offs_h).to(dev)
+        mbd = int(np.diff(offs_h).max()) if nb > 0 else 0
+        rc = lib.cwq_greedy_decode(
+            _ptr(it), _ptr(pl), _ptr(ps), offs.data_ptr(), nb, D, mbd, int(n_bits_per_step),
+            n_steps, seed32, float(rho), int(block_id_base), _ptr(out_sample), stream)
+    _lib.check(rc, "cwq_greedy_decode")
+    return out_sample
+
+
+# ---------------------------------------------------------------------------
+# north-star convenience surface
+# ---------------------------------------------------------------------------
+def encode(prior_loc, prior_scale, post_loc, post_scale, seed, kl_bits, block_id_base=0):
+    """Code every block (row) of [nb, d] (or one [d] block) at ``kl_bits`` bits.
+
+    = code_greedy_sample(t=post, p=prior, n_bits_per_step=kl_bits, n_steps=1,
+    seed=seed + block_id_base + g) for each row g.  Returns (indices int32 [nb],
+    samples f32 [nb, d]) in the input's array type.
+    """
+    shape = tuple(np.shape(prior_loc)) if not isinstance(prior_loc, torch.Tensor) \
+        else tuple(prior_loc.shape)
+    d = shape[-1] if len(shape) else 1
+    idx, sample = encode_blocks(post_loc, post_scale, prior_loc, prior_scale, kl_bits, 1, seed,
+                                block_dim=d, block_id_base=block_id_base)
+    return _like_input(idx.reshape(shape[:-1]), prior_loc), \
+        _like_input(sample.reshape(shape), prior_loc)
+
+
+def decode(indices_or_bitcode, prior_loc, prior_scale, seed, kl_bits, block_id_base=0):
+    """Inverse of encode: indices (int [nb]) or the LSB-first bitcode str."""
+    shape = tuple(np.shape(prior_loc)) if not isinstance(prior_loc, torch.Tensor) \
+        else tuple(prior_loc.shape)
+    d = shape[-1] if len(shape) else 1
+    nb = int(np.prod(shape[:-1])) if len(shape) > 1 else 1
+    if isinstance(indices_or_bitcode, (str, bytes)):
+        indices_or_bitcode = bitcode_to_indices(indices_or_bitcode, int(kl_bits), nb)
+    sample = decode_blocks(indices_or_bitcode, prior_loc, prior_scale, kl_bits, 1, seed,
+                           block_dim=d, block_id_base=block_id_base)
+    return _like_input(sample.reshape(shape), prior_loc)
+
+
+# ---------------------------------------------------------------------------
+# reference surface
+# ---------------------------------------------------------------------------
+def code_greedy_sample(t_loc, t_scale, p_loc, p_scale, n_bits_per_step, n_steps, seed, rho=1.):
+    """coded_greedy_sampler.py:29-89 for one block.
+
+    Returns (best_sample [d] f32, sample_index str of n_bits_per_step*n_steps
+    LSB-first bits), best_sample in the caller's array type.
+    """
+    d = int(np.prod(np.shape(t_loc))) if not isinstance(t_loc, torch.Tensor) else t_loc.numel()
+    idx, sample = encode_blocks(t_loc, t_scale, p_loc, p_scale, n_bits_per_step, n_steps, seed,
+                                rho=rho, block_off=[0, d])
+    bits = indices_to_bitcode(idx.cpu().numpy(), int(n_bits_per_step))
+    return _like_input(sample, t_loc), bits
+
+
+def decode_greedy_sample(sample_index, p_loc, p_scale, n_bits_per_step, n_steps, seed, rho=1.):
+    """coded_greedy_sampler.py:93-167 for one block."""
+    d = int(np.prod(np.shape(p_loc))) if not isinstance(p_loc, torch.Tensor) else p_loc.numel()
+    if isinstance(sample_index, (str, bytes)):
+        idx = bitcode_to_indices(sample_index, int(n_bits_per_step), int(n_steps))
+    else:
+        idx = np.asarray(sample_index, dtype=np.int64).reshape(-1)
+    sample = decode_blocks(idx.astype(np.int32), p_loc, p_scale, n_bits_per_step, n_steps, seed,
+                           rho=rho, block_off=[0, d])
+    return _like_input(sample, p_loc)
+
+
+def group_size_threshold(max_group_size_bits):
+    """Smallest s with np.log(s + 1) / np.log(2) >= max_group_size_bits (:230-232)."""
+    bits = max_group_size_bits
+    s = max(int(2 ** bits) - 3, 0)
+    while np.log(s + 1) / np.log(2) >= bits and s > 0:
+        s -= 1
+    while not (np.log(s + 1) / np.log(2) >= bits):
+        s += 1
+    return s
+
+
+def group_starts(kl_divs, n_bits_per_group, max_group_size_bits=12):
+    """coded_greedy_sampler.py:207-252 -> group_start_indices (a list, with D appended)."""
+    kl = np.ascontiguousarray(np.asarray(kl_divs, dtype=np.float32).reshape(-1))
+    D = kl.size
+    n_nats = n_bits_per_group * np.log(2) - 1
+    cap = D + 2
+    starts = np.empty(cap, dtype=np.int64)
+    lib = _lib.load()
+    n = lib.cwq_group_starts(kl.ctypes.data if D else None, D,
+                             group_size_threshold(max_group_size_bits), float(n_nats),
+                             starts.ctypes.data, cap)
+    _lib.check(n, "cwq_group_starts")
+    return [int(v) for v in starts[:n]]
+
+
+def _dist_parts(dist, dev, what):
+    if not _is_float32(dist.loc) or not _is_float32(dist.scale):
+        raise Exception(f"{what} datatype must be float32!")
+    return _f32(dist.loc, dev, what + ".loc"), _f32(dist.scale, dev, what + ".scale")
+
+
+def code_grouped_greedy_sample(sess, target, proposal, n_steps, n_bits_per_step, seed,
+                               max_group_size_bits=12, adaptive=True, backfitting_steps=0,
+                               use_log_prob=False, rho=1.):
+    """coded_greedy_sampler.py:170-296.
+
+    Returns (sample np.float32 [D], bitcode str, group_start_indices list).
+    """
+    lib = _lib.load()
+    dev = _device_of(target.loc, target.scale, proposal.loc, proposal.scale)
+    # :183-187
+    if not _is_float32(target.loc) or not _is_float32(target.scale):
+        raise Exception("Target datatype must be float32!")
+    if not _is_float32(proposal.loc) or not _is_float32(proposal.scale):
+        raise Exception("Proposal datatype must be float32!")
+    q_loc, q_scale = _dist_parts(target, dev, "Target")
+    p_loc, p_scale = _dist_parts(proposal, dev, "Proposal")
+    D = p_loc.numel()
+    n_bits_per_group = n_bits_per_step * n_steps
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    # :193-199 standardise the target by the proposal; proposal -> N(0, 1)
+    t_loc = torch.empty(D, dtype=torch.float32, device=dev)
+    t_scale = torch.empty(D, dtype=torch.float32, device=dev)
+    _lib.check(lib.cwq_standardise(_ptr(q_loc), _ptr(q_scale), _ptr(p_loc), _ptr(p_scale), D,
+                                   _ptr(t_loc), _ptr(t_scale), stream), "cwq_standardise")
+    # :201, :210 per-dim KL(target || proposal)
+    kl = torch.empty(D, dtype=torch.float32, device=dev)
+    _lib.check(lib.cwq_kl_normal_normal(_ptr(q_loc), _ptr(q_scale), _ptr(p_loc), _ptr(p_scale),
+                                        D, _ptr(kl), stream), "cwq_kl_normal_normal")
+    kl_divs = kl.cpu().numpy()
+    if VERBOSE:
+        total_kl_bits = np.sum(kl_divs) / np.log(2)
+        print("Total KL to split up: {:.2f} bits, "
+              "maximum bits per group: {}, "
+              "estimated number of groups: {},"
+              "coding {} dimensions".format(total_kl_bits, n_bits_per_group,
+                                            total_kl_bits // n_bits_per_group + 1, D))
+    # :207-252 grouping (sequential; host)
+    starts = group_starts(kl_divs, n_bits_per_group, max_group_size_bits)
+    zeros = torch.zeros(D, dtype=torch.float32, device=dev)
+    ones = torch.ones(D, dtype=torch.float32, device=dev)
+    idx, sample = encode_blocks(t_loc, t_scale, zeros, ones, n_bits_per_step, n_steps, seed,
+                                rho=rho, block_off=starts)
+    bitcode = indices_to_bitcode(idx.cpu().numpy(), int(n_bits_per_step))
+    # :292 rescale the sample
+    out = torch.empty(D, dtype=torch.float32, device=dev)
+    _lib.check(lib.cwq_destandardise(_ptr(sample), _ptr(p_loc), _ptr(p_scale), D, _ptr(out),
+                                     stream), "cwq_destandardise")
+    return out.cpu().numpy(), bitcode, starts
+
+
+def decode_grouped_greedy_sample(sess, bitcode, group_start_indices, proposal, n_bits_per_step,
+                                 n_steps, seed, adaptive=True, rho=1.):
+    """coded_greedy_sampler.py:299-364.  Returns np.float32 [D]."""
+    lib = _lib.load()
+    dev = _device_of(proposal.loc, proposal.scale)
+    if not _is_float32(proposal.loc) or not _is_float32(proposal.scale):
+        raise Exception("Proposal datatype must be float32!")
+    p_loc, p_scale = _dist_parts(proposal, dev, "Proposal")
+    D = p_loc.numel()
+    n_bits_per_group = n_bits_per_step * n_steps
+    starts = [int(s) for s in group_start_indices] + [D]  # :323 (without mutating)
+    n_listed = len(starts) - 1
+    # :345-347 decode group i while its bit slice is non-empty
+    n_avail = -(-len(bitcode) // n_bits_per_group) if n_bits_per_group else n_listed
+    G = min(n_listed, n_avail)
+    idx = bitcode_to_indices(bitcode, int(n_bits_per_step), G * int(n_steps))
+    offs = np.asarray(starts[:G + 1], dtype=np.int64)
+    if G == 0 or offs[-1] != D:
+        raise ValueError(f"decoded groups cover {int(offs[-1]) if G else 0} of {D} dims")
+    zeros = torch.zeros(D, dtype=torch.float32, device=dev)
+    ones = torch.ones(D, dtype=torch.float32, device=dev)
+    sample = decode_blocks(idx.astype(np.int32), zeros, ones, n_bits_per_step, n_steps, seed,
+                           rho=rho, block_off=offs)
+    out = torch.empty(D, dtype=torch.float32, device=dev)
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    _lib.check(lib.cwq_destandardise(_ptr(sample), _ptr(p_loc), _ptr(p_scale), D, _ptr(out),
+                                     stream), "cwq_destandardise")
+    return out.cpu().numpy()

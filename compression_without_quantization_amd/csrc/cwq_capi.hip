@@ -1,0 +1,294 @@
+// cwq_capi.hip -- the C ABI declared in include/cwq.h.
+//
+// Thin: validates arguments, carves the caller's workspace, picks the tiling
+// and enqueues the kernels on the caller's stream.  Never allocates, never
+// synchronises, never throws.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <string.h>
+
+#include "../../include/cwq.h"
+#include "cwq_kernels.h"
+
+namespace {
+
+thread_local char g_err[512] = {0};
+thread_local void* g_ev_start = nullptr;
+thread_local void* g_ev_stop = nullptr;
+
+int fail(int code, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
+int fail(int code, const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof(g_err), fmt, ap);
+  va_end(ap);
+  return code;
+}
+
+int ok() {
+  g_err[0] = 0;
+  return CWQ_OK;
+}
+
+int hip_fail(hipError_t e, const char* where) {
+  return fail(CWQ_ERR_HIP, "%s: %s", where, hipGetErrorString(e));
+}
+
+size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
+
+struct WsLayout {
+  size_t keys, loc_s, scale_s, lognorm, total;
+};
+
+WsLayout ws_layout(int64_t nb, int64_t total_dims) {
+  WsLayout l;
+  size_t o = 0;
+  l.keys = o;
+  o = align_up(o + (size_t)nb * 8, 256);
+  l.loc_s = o;
+  o = align_up(o + (size_t)total_dims * 4, 256);
+  l.scale_s = o;
+  o = align_up(o + (size_t)total_dims * 4, 256);
+  l.lognorm = o;
+  o = align_up(o + (size_t)total_dims * 4, 256);
+  l.total = o;
+  return l;
+}
+
+// Tiling: split a block's 2^b candidates over several workgroups only when
+// there are too few blocks to fill the chip (256 CUs x several workgroups).
+void choose_tiling(int64_t nb, int64_t n_cand, int64_t* tiles_per_block, int64_t* cand_per_tile) {
+  const int64_t kTargetTiles = 16384;
+  int64_t want = nb > 0 ? (kTargetTiles + nb - 1) / nb : 1;
+  int64_t max_split = (n_cand + 255) / 256;  // at least one candidate per lane
+  if (want > max_split) want = max_split;
+  if (want < 1) want = 1;
+  int64_t cpt = (n_cand + want - 1) / want;
+  cpt = (cpt + 255) / 256 * 256;
+  if (cpt < 256) cpt = 256;
+  *cand_per_tile = cpt;
+  *tiles_per_block = (n_cand + cpt - 1) / cpt;
+}
+
+int check_common(int n_bits, int n_steps, int64_t nb) {
+  if (n_bits < 0 || n_bits > CWQ_MAX_BITS_PER_STEP)
+    return fail(CWQ_ERR_INVALID, "n_bits_per_step=%d outside [0, %d]", n_bits,
+                CWQ_MAX_BITS_PER_STEP);
+  if (n_steps < 1) return fail(CWQ_ERR_INVALID, "n_steps=%d must be >= 1", n_steps);
+  if (nb < 0) return fail(CWQ_ERR_INVALID, "nb=%lld must be >= 0", (long long)nb);
+  return CWQ_OK;
+}
+
+int encode_impl(const float* t_loc, const float* t_scale, const float* p_loc,
+                const float* p_scale, const int64_t* block_off, int64_t ud, int64_t nb,
+                int64_t total_dims, int n_bits, int n_steps, int32_t seed, float rho,
+                int64_t block_id_base, int32_t* out_idx, float* out_sample, void* workspace,
+                size_t workspace_bytes, void* stream) {
+  int rc = check_common(n_bits, n_steps, nb);
+  if (rc) return rc;
+  if (total_dims < 0) return fail(CWQ_ERR_INVALID, "total_dims must be >= 0");
+  if (nb > 0 && (!out_idx)) return fail(CWQ_ERR_INVALID, "out_idx is null");
+  if (total_dims > 0 && (!t_loc || !t_scale || !p_loc || !p_scale || !out_sample))
+    return fail(CWQ_ERR_INVALID, "null input/output pointer");
+  const WsLayout l = ws_layout(nb, total_dims);
+  if (workspace_bytes < l.total || (l.total && !workspace))
+    return fail(CWQ_ERR_WORKSPACE, "workspace %zu bytes < required %zu", workspace_bytes,
+                l.total);
+  cwq::EncodeArgs a;
+  a.t_loc = t_loc;
+  a.t_scale = t_scale;
+  a.p_loc = p_loc;
+  a.p_scale = p_scale;
+  a.block_off = block_off;
+  a.ud = ud;
+  a.nb = nb;
+  a.total_dims = total_dims;
+  a.n_cand = (int64_t)1 << n_bits;
+  choose_tiling(nb, a.n_cand, &a.tiles_per_block, &a.cand_per_tile);
+  a.n_steps = n_steps;
+  a.seed = seed;
+  a.rho = rho;
+  a.block_id_base = block_id_base;
+  a.out_idx = out_idx;
+  a.out_sample = out_sample;
+  char* w = (char*)workspace;
+  a.keys = (unsigned long long*)(w + l.keys);
+  a.loc_s = (float*)(w + l.loc_s);
+  a.scale_s = (float*)(w + l.scale_s);
+  a.lognorm = (float*)(w + l.lognorm);
+  a.ev_start = g_ev_start;
+  a.ev_stop = g_ev_stop;
+  hipError_t e = cwq::launch_encode(a, (hipStream_t)stream);
+  if (e != hipSuccess) return hip_fail(e, "cwq_greedy_encode");
+  return ok();
+}
+
+}  // namespace
+
+extern "C" {
+
+int cwq_version(void) { return (0 << 16) | 1; }
+
+const char* cwq_last_error(void) { return g_err; }
+
+int cwq_stateless_normal_sample(const float* loc, const float* scale, int64_t d,
+                                int64_t num_samples, int32_t seed, float* out, void* stream) {
+  if (d < 0 || num_samples < 0) return fail(CWQ_ERR_INVALID, "negative size");
+  if (d * num_samples > 0 && (!loc || !scale || !out))
+    return fail(CWQ_ERR_INVALID, "null pointer");
+  hipError_t e =
+      cwq::launch_stateless_normal_sample(loc, scale, d, num_samples, seed, out, (hipStream_t)stream);
+  if (e != hipSuccess) return hip_fail(e, "cwq_stateless_normal_sample");
+  return ok();
+}
+
+size_t cwq_greedy_encode_workspace_size(int64_t nb, int64_t total_dims) {
+  if (nb < 0 || total_dims < 0) return 0;
+  return ws_layout(nb, total_dims).total;
+}
+
+int cwq_greedy_encode(const float* t_loc, const float* t_scale, const float* p_loc,
+                      const float* p_scale, const int64_t* block_off, int64_t nb,
+                      int64_t total_dims, int64_t max_block_dim, int n_bits_per_step,
+                      int n_steps, int32_t seed, float rho, int64_t block_id_base,
+                      int32_t* out_idx, float* out_sample, void* workspace,
+                      size_t workspace_bytes, void* stream) {
+  if (nb > 0 && !block_off) return fail(CWQ_ERR_INVALID, "block_off is null");
+  if (max_block_dim < 0) return fail(CWQ_ERR_INVALID, "max_block_dim must be >= 0");
+  return encode_impl(t_loc, t_scale, p_loc, p_scale, block_off, 0, nb, total_dims,
+                     n_bits_per_step, n_steps, seed, rho, block_id_base, out_idx, out_sample,
+                     workspace, workspace_bytes, stream);
+}
+
+int cwq_greedy_encode_uniform(const float* t_loc, const float* t_scale, const float* p_loc,
+                              const float* p_scale, int64_t nb, int64_t d,
+                              int n_bits_per_step, int n_steps, int32_t seed, float rho,
+                              int64_t block_id_base, int32_t* out_idx, float* out_sample,
+                              void* workspace, size_t workspace_bytes, void* stream) {
+  if (d < 0) return fail(CWQ_ERR_INVALID, "d must be >= 0");
+  return encode_impl(t_loc, t_scale, p_loc, p_scale, nullptr, d, nb, nb * d, n_bits_per_step,
+                     n_steps, seed, rho, block_id_base, out_idx, out_sample, workspace,
+                     workspace_bytes, stream);
+}
+
+int cwq_greedy_decode(const int32_t* idx, const float* p_loc, const float* p_scale,
+                      const int64_t* block_off, int64_t nb, int64_t total_dims,
+                      int64_t max_block_dim, int n_bits_per_step, int n_steps, int32_t seed,
+                      float rho, int64_t block_id_base, float* out_sample, void* stream) {
+  int rc = check_common(n_bits_per_step, n_steps, nb);
+  if (rc) return rc;
+  if (nb > 0 && (!block_off || !idx)) return fail(CWQ_ERR_INVALID, "null pointer");
+  if (total_dims > 0 && (!p_loc || !p_scale || !out_sample))
+    return fail(CWQ_ERR_INVALID, "null pointer");
+  (void)max_block_dim;
+  hipError_t e = cwq::launch_decode(idx, p_loc, p_scale, block_off, 0, nb, n_bits_per_step,
+                                    n_steps, seed, rho, block_id_base, out_sample,
+                                    (hipStream_t)stream);
+  if (e != hipSuccess) return hip_fail(e, "cwq_greedy_decode");
+  return ok();
+}
+
+int cwq_greedy_decode_uniform(const int32_t* idx, const float* p_loc, const float* p_scale,
+                              int64_t nb, int64_t d, int n_bits_per_step, int n_steps,
+                              int32_t seed, float rho, int64_t block_id_base, float* out_sample,
+                              void* stream) {
+  int rc = check_common(n_bits_per_step, n_steps, nb);
+  if (rc) return rc;
+  if (d < 0) return fail(CWQ_ERR_INVALID, "d must be >= 0");
+  if (nb > 0 && !idx) return fail(CWQ_ERR_INVALID, "null pointer");
+  if (nb * d > 0 && (!p_loc || !p_scale || !out_sample))
+    return fail(CWQ_ERR_INVALID, "null pointer");
+  hipError_t e = cwq::launch_decode(idx, p_loc, p_scale, nullptr, d, nb, n_bits_per_step,
+                                    n_steps, seed, rho, block_id_base, out_sample,
+                                    (hipStream_t)stream);
+  if (e != hipSuccess) return hip_fail(e, "cwq_greedy_decode_uniform");
+  return ok();
+}
+
+int cwq_standardise(const float* q_loc, const float* q_scale, const float* p_loc,
+                    const float* p_scale, int64_t n, float* t_loc, float* t_scale, void* stream) {
+  if (n < 0) return fail(CWQ_ERR_INVALID, "negative size");
+  if (n > 0 && (!q_loc || !q_scale || !p_loc || !p_scale || !t_loc || !t_scale))
+    return fail(CWQ_ERR_INVALID, "null pointer");
+  hipError_t e = cwq::launch_standardise(q_loc, q_scale, p_loc, p_scale, n, t_loc, t_scale,
+                                         (hipStream_t)stream);
+  if (e != hipSuccess) return hip_fail(e, "cwq_standardise");
+  return ok();
+}
+
+int cwq_kl_normal_normal(const float* q_loc, const float* q_scale, const float* p_loc,
+                         const float* p_scale, int64_t n, float* out, void* stream) {
+  if (n < 0) return fail(CWQ_ERR_INVALID, "negative size");
+  if (n > 0 && (!q_loc || !q_scale || !p_loc || !p_scale || !out))
+    return fail(CWQ_ERR_INVALID, "null pointer");
+  hipError_t e = cwq::launch_kl(q_loc, q_scale, p_loc, p_scale, n, out, (hipStream_t)stream);
+  if (e != hipSuccess) return hip_fail(e, "cwq_kl_normal_normal");
+  return ok();
+}
+
+int cwq_destandardise(const float* sample, const float* p_loc, const float* p_scale, int64_t n,
+                      float* out, void* stream) {
+  if (n < 0) return fail(CWQ_ERR_INVALID, "negative size");
+  if (n > 0 && (!sample || !p_loc || !p_scale || !out))
+    return fail(CWQ_ERR_INVALID, "null pointer");
+  hipError_t e =
+      cwq::launch_destandardise(sample, p_loc, p_scale, n, out, (hipStream_t)stream);
+  if (e != hipSuccess) return hip_fail(e, "cwq_destandardise");
+  return ok();
+}
+
+int64_t cwq_group_starts(const float* kl, int64_t D, int64_t size_threshold, double n_nats,
+                         int64_t* starts, int64_t cap) {
+  if (D < 0 || (D > 0 && !kl) || !starts || cap < 2)
+    return fail(CWQ_ERR_INVALID, "cwq_group_starts: bad arguments");
+  int64_t ns = 0;
+  starts[ns++] = 0;
+  int64_t cur_size = 0;
+  float cur_kl = 0.0f;  // numpy float32 scalar accumulator (:224, :243)
+  for (int64_t i = 0; i < D; ++i) {
+    const float s = cur_kl + kl[i];  // float32 + float32
+    // :230-234  group_bits >= max bits | f32 sum (as f64) >= n_nats | last dim
+    if (cur_size >= size_threshold || (double)s >= n_nats || i == D - 1) {
+      if (ns >= cap) return fail(CWQ_ERR_INVALID, "cwq_group_starts: cap too small");
+      starts[ns++] = i;
+      cur_size = 1;
+      cur_kl = kl[i];
+    } else {
+      cur_kl = s;
+      cur_size += 1;
+    }
+  }
+  if (ns >= cap) return fail(CWQ_ERR_INVALID, "cwq_group_starts: cap too small");
+  starts[ns++] = D;  // :252
+  ok();
+  return ns;
+}
+
+int cwq_profile_set_eval_events(void* start_event, void* stop_event) {
+  if ((start_event == nullptr) != (stop_event == nullptr))
+    return fail(CWQ_ERR_INVALID, "give both events or neither");
+  g_ev_start = start_event;
+  g_ev_stop = stop_event;
+  return ok();
+}
+
+int cwq_selftest_bm_tables(uint32_t m0, int64_t count, float* radius, float* sin_out,
+                           float* cos_out, void* stream) {
+  if (count < 0 || (count > 0 && (!radius || !sin_out || !cos_out)))
+    return fail(CWQ_ERR_INVALID, "cwq_selftest_bm_tables: bad arguments");
+  hipError_t e = cwq::launch_selftest_bm(m0, count, radius, sin_out, cos_out, (hipStream_t)stream);
+  if (e != hipSuccess) return hip_fail(e, "cwq_selftest_bm_tables");
+  return ok();
+}
+
+int cwq_selftest_logf(const float* x, int64_t n, float* out, void* stream) {
+  if (n < 0 || (n > 0 && (!x || !out)))
+    return fail(CWQ_ERR_INVALID, "cwq_selftest_logf: bad arguments");
+  hipError_t e = cwq::launch_selftest_logf(x, n, out, (hipStream_t)stream);
+  if (e != hipSuccess) return hip_fail(e, "cwq_selftest_logf");
+  return ok();
+}
+
+}  // extern "C"

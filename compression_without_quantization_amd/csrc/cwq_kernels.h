@@ -1,0 +1,56 @@
+// cwq_kernels.h -- launchers shared between the kernels and the C ABI layer.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace cwq {
+
+struct EncodeArgs {
+  const float* t_loc;
+  const float* t_scale;
+  const float* p_loc;
+  const float* p_scale;
+  const int64_t* block_off;  // nullptr -> uniform blocks of dimension ud
+  int64_t ud;
+  int64_t nb;
+  int64_t total_dims;
+  int64_t n_cand;            // 2^n_bits_per_step
+  int64_t tiles_per_block;
+  int64_t cand_per_tile;     // multiple of 256
+  int n_steps;
+  int32_t seed;
+  float rho;
+  int64_t block_id_base;
+  int32_t* out_idx;
+  float* out_sample;
+  // workspace
+  unsigned long long* keys;  // [nb]
+  float* loc_s;              // [total_dims]
+  float* scale_s;            // [total_dims]
+  float* lognorm;            // [total_dims]
+  // optional profiling events around the eval launches (hipEvent_t)
+  void* ev_start;
+  void* ev_stop;
+};
+
+hipError_t launch_encode(const EncodeArgs& a, hipStream_t stream);
+hipError_t launch_decode(const int32_t* idx, const float* p_loc, const float* p_scale,
+                         const int64_t* block_off, int64_t ud, int64_t nb, int n_bits,
+                         int n_steps, int32_t seed, float rho, int64_t block_id_base,
+                         float* out_sample, hipStream_t stream);
+hipError_t launch_stateless_normal_sample(const float* loc, const float* scale, int64_t d,
+                                          int64_t num_samples, int32_t seed, float* out,
+                                          hipStream_t stream);
+hipError_t launch_standardise(const float* q_loc, const float* q_scale, const float* p_loc,
+                              const float* p_scale, int64_t n, float* t_loc, float* t_scale,
+                              hipStream_t stream);
+hipError_t launch_kl(const float* q_loc, const float* q_scale, const float* p_loc,
+                     const float* p_scale, int64_t n, float* out, hipStream_t stream);
+hipError_t launch_destandardise(const float* sample, const float* p_loc, const float* p_scale,
+                                int64_t n, float* out, hipStream_t stream);
+
+hipError_t launch_selftest_bm(uint32_t m0, int64_t count, float* rad, float* sn, float* cs,
+                              hipStream_t stream);
+hipError_t launch_selftest_logf(const float* x, int64_t n, float* out, hipStream_t stream);
+
+}  // namespace cwq

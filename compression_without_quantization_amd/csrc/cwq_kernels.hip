@@ -1,0 +1,481 @@
+// cwq_kernels.hip -- gfx950 kernels of the greedy coded sampler.
+//
+// Hot path: for every block (the reference's "group")
+// and every step, 2^b candidates are drawn from the proposal shard with the
+// stateless Philox stream, scored by the target log-density and reduced to
+// the argmax; the decoder regenerates only the selected row.
+//
+// Mapping:
+//   * one "tile" = (block g, candidate range [n0, n1)), one 256-thread
+//     workgroup per tile; a block whose 2^b candidates would leave the chip
+//     idle is split over several tiles and merged with one 64-bit atomicMax
+//     per workgroup on an orderable (value, ~index) key.
+//   * inside a workgroup, wave v owns the candidates n == n0 + v (mod 4), so
+//     the Philox word alignment (n*d) mod 4 is uniform within a wave and the
+//     "start a new Philox block" branch is a scalar branch even for odd d.
+//   * candidates are never materialised: each lane regenerates its row's
+//     normals in registers (Philox -> Box-Muller -> shard -> log-prob) and
+//     accumulates them in the Eigen AVX summation order.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "cwq_kernels.h"
+#include "cwq_math.h"
+
+namespace cwq {
+
+__constant__ double kLogTabConst[32] = CWQ_LOGF_TAB_INIT;
+
+__device__ __forceinline__ void fill_logtab(double* lds) {
+  if (threadIdx.x < 32) lds[threadIdx.x] = kLogTabConst[threadIdx.x];
+  __syncthreads();
+}
+
+__device__ __forceinline__ uint32_t wave_id() {
+  return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+}
+
+__device__ __forceinline__ uint64_t wave_max_u64(uint64_t v) {
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) {
+    uint64_t o = __shfl_xor(v, off, 64);
+    v = o > v ? o : v;
+  }
+  return v;
+}
+
+struct BlockSpan {
+  int64_t off;
+  int64_t d;
+};
+
+__device__ __forceinline__ BlockSpan block_span(const int64_t* __restrict__ block_off,
+                                                int64_t ud, int64_t g) {
+  if (block_off == nullptr) return BlockSpan{g * ud, ud};
+  int64_t a = block_off[g];
+  int64_t b = block_off[g + 1];
+  return BlockSpan{a, b - a};
+}
+
+__device__ __forceinline__ int32_t block_seed(int32_t seed, int64_t block_id) {
+  return (int32_t)((uint32_t)seed + (uint32_t)block_id);
+}
+
+// ---------------------------------------------------------------------------
+// Per-dimension constants of a step (coded_greedy_sampler.py:42-48).
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) k_prep_dims(
+    const float* __restrict__ t_scale, const float* __restrict__ p_loc,
+    const float* __restrict__ p_scale, int64_t n, float nst, float sdiv, float rho,
+    float* __restrict__ loc_s, float* __restrict__ scale_s, float* __restrict__ lognorm,
+    float* __restrict__ out_sample) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    loc_s[i] = p_loc[i] / nst;                // p_loc / n_steps
+    float rs = rho * p_scale[i];              // rho * p_scale
+    scale_s[i] = rs / sdiv;                   //   / sqrt(n_steps)
+    lognorm[i] = kHalfLog2Pi + logf_full(t_scale[i], kLogTabConst);
+    out_sample[i] = 0.0f;                     // best_sample = tf.zeros (:68)
+  }
+}
+
+// ---------------------------------------------------------------------------
+// One candidate row: sum_j log N(best_j + loc_s_j + scale_s_j z_j; mu_j, s_j)
+// in the Eigen 3.3 AVX inner-dim reduction order.
+//   kbase = n*d (flat index of the row's first normal), align = kbase & 3
+//   (wave-uniform).  DC > 0: compile-time dimension (DC % 4 == 0 -> align 0).
+// ---------------------------------------------------------------------------
+template <int DC, bool STEP0>
+__device__ __forceinline__ float eval_row(const PhiloxStream& st, uint64_t kbase, int64_t d_rt,
+                                          int align_rt, const float* __restrict__ loc_s,
+                                          const float* __restrict__ scale_s,
+                                          const float* __restrict__ mu,
+                                          const float* __restrict__ sg,
+                                          const float* __restrict__ lognorm,
+                                          const float* __restrict__ best,
+                                          const double* logtab) {
+  const int64_t d = DC > 0 ? (int64_t)DC : d_rt;
+  const int align = (DC > 0 && (DC % 4) == 0) ? 0 : align_rt;
+  const int64_t vec = d & ~(int64_t)7;
+  float p[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  F4 z = {0.f, 0.f, 0.f, 0.f};
+
+  auto elem = [&](int64_t e) -> float {
+    const int w = (align + (int)(e & 3)) & 3;  // wave-uniform
+    if (w == 0 || e == 0) z = normal4(st, (kbase + (uint64_t)e) >> 2, logtab);
+    const float zz = w == 0 ? z.a : (w == 1 ? z.b : (w == 2 ? z.c : z.d));
+    float s = scale_s[e] * zz;  // misc.py:14
+    s = loc_s[e] + s;           // misc.py:15
+    const float tv = STEP0 ? s : best[e] + s;  // :57 (best == +0 at step 0)
+    return log_prob(tv, mu[e], sg[e], lognorm[e]);
+  };
+
+  for (int64_t j = 0; j < vec; j += 8) {
+#pragma unroll
+    for (int l = 0; l < 8; ++l) p[l] = p[l] + elem(j + l);
+  }
+  float t = 0.0f;
+  for (int64_t j = vec; j < d; ++j) t = t + elem(j);
+  const float q0 = p[0] + p[4], q1 = p[1] + p[5], q2 = p[2] + p[6], q3 = p[3] + p[7];
+  return t + ((q0 + q2) + (q1 + q3));
+}
+
+// ---------------------------------------------------------------------------
+// Encoder, one step: every tile scores its candidate range and folds its best
+// (value, index) into keys[g] with one atomicMax.
+// ---------------------------------------------------------------------------
+template <int DC, bool STEP0>
+__global__ void __launch_bounds__(256) k_encode_eval(
+    const float* __restrict__ t_loc, const float* __restrict__ t_scale,
+    const float* __restrict__ loc_s, const float* __restrict__ scale_s,
+    const float* __restrict__ lognorm, const float* __restrict__ best,
+    const int64_t* __restrict__ block_off, int64_t ud, int64_t ntiles, int64_t tiles_per_block,
+    int64_t cand_per_tile, int64_t n_cand, int32_t seed, int64_t block_id_base, int32_t step,
+    unsigned long long* __restrict__ keys) {
+  __shared__ double logtab[32];
+  __shared__ unsigned long long wkey[4];
+  fill_logtab(logtab);
+  const uint32_t wv = wave_id();
+  const uint32_t lane = threadIdx.x & 63u;
+
+  for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const int64_t g = tile / tiles_per_block;
+    const int64_t tt = tile - g * tiles_per_block;
+    const BlockSpan sp = block_span(block_off, ud, g);
+    const int64_t n0 = tt * cand_per_tile;
+    const int64_t n1 = (n0 + cand_per_tile < n_cand) ? n0 + cand_per_tile : n_cand;
+    const PhiloxStream st =
+        generate_key(step_seed(block_seed(seed, block_id_base + g), step), 42);
+    const int align = (int)(((uint64_t)(n0 + wv) * (uint64_t)sp.d) & 3u);
+
+    uint64_t bestk = 0;
+    for (int64_t n = n0 + 4 * (int64_t)lane + wv; n < n1; n += 256) {
+      const float v = eval_row<DC, STEP0>(st, (uint64_t)n * (uint64_t)sp.d, sp.d, align,
+                                          loc_s + sp.off, scale_s + sp.off, t_loc + sp.off,
+                                          t_scale + sp.off, lognorm + sp.off,
+                                          STEP0 ? nullptr : best + sp.off, logtab);
+      const uint64_t k = argmax_key(v, (uint32_t)n);
+      bestk = k > bestk ? k : bestk;
+    }
+    bestk = wave_max_u64(bestk);
+    if (lane == 0) wkey[wv] = bestk;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      uint64_t m = wkey[0];
+      for (int i = 1; i < 4; ++i) m = wkey[i] > m ? wkey[i] : m;
+      if (m) atomicMax(&keys[g], (unsigned long long)m);
+    }
+    __syncthreads();
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Encoder, end of a step: index -> out_idx; best += winning candidate (:63).
+// One wave per block.
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) k_encode_finalize(
+    const float* __restrict__ loc_s, const float* __restrict__ scale_s,
+    const int64_t* __restrict__ block_off, int64_t ud, int64_t nb, int32_t seed,
+    int64_t block_id_base, int32_t step, int n_steps,
+    const unsigned long long* __restrict__ keys, int32_t* __restrict__ out_idx,
+    float* __restrict__ out_sample) {
+  __shared__ double logtab[32];
+  fill_logtab(logtab);
+  const uint32_t wv = wave_id();
+  const uint32_t lane = threadIdx.x & 63u;
+  for (int64_t g = (int64_t)blockIdx.x * 4 + wv; g < nb; g += (int64_t)gridDim.x * 4) {
+    const BlockSpan sp = block_span(block_off, ud, g);
+    const uint64_t key = keys[g];
+    const uint32_t idx = key ? argmax_key_index(key) : 0u;
+    if (lane == 0) out_idx[g * n_steps + step] = (int32_t)idx;
+    const PhiloxStream st =
+        generate_key(step_seed(block_seed(seed, block_id_base + g), step), 42);
+    for (int64_t j = lane; j < sp.d; j += 64) {
+      const uint64_t k = (uint64_t)idx * (uint64_t)sp.d + (uint64_t)j;
+      const F4 z = normal4(st, k >> 2, logtab);
+      const uint32_t w = (uint32_t)(k & 3u);
+      const float zz = w == 0 ? z.a : (w == 1 ? z.b : (w == 2 ? z.c : z.d));
+      float s = scale_s[sp.off + j] * zz;
+      s = loc_s[sp.off + j] + s;
+      out_sample[sp.off + j] = out_sample[sp.off + j] + s;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Decoder (coded_greedy_sampler.py:93-167), O(n_steps * d) per block.
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) k_decode(
+    const int32_t* __restrict__ idx, const float* __restrict__ p_loc,
+    const float* __restrict__ p_scale, const int64_t* __restrict__ block_off, int64_t ud,
+    int64_t nb, int n_steps, int64_t n_cand, float nst, float sdiv, float rho, int32_t seed,
+    int64_t block_id_base, float* __restrict__ out_sample) {
+  __shared__ double logtab[32];
+  fill_logtab(logtab);
+  const uint32_t wv = wave_id();
+  const uint32_t lane = threadIdx.x & 63u;
+  for (int64_t g = (int64_t)blockIdx.x * 4 + wv; g < nb; g += (int64_t)gridDim.x * 4) {
+    const BlockSpan sp = block_span(block_off, ud, g);
+    const int32_t sg = block_seed(seed, block_id_base + g);
+    for (int64_t j = lane; j < sp.d; j += 64) {
+      const float ls = p_loc[sp.off + j] / nst;
+      const float rs = rho * p_scale[sp.off + j];
+      const float ss = rs / sdiv;
+      float v = 0.0f;  // sample = tf.zeros (:143)
+      for (int i = 0; i < n_steps; ++i) {
+        const int64_t n = idx[g * n_steps + i];
+        if (n < 0 || n >= n_cand) {
+          v = __builtin_nanf("");
+          continue;
+        }
+        const PhiloxStream st = generate_key(step_seed(sg, i), 42);
+        const uint64_t k = (uint64_t)n * (uint64_t)sp.d + (uint64_t)j;
+        const F4 z = normal4(st, k >> 2, logtab);
+        const uint32_t w = (uint32_t)(k & 3u);
+        const float zz = w == 0 ? z.a : (w == 1 ? z.b : (w == 2 ? z.c : z.d));
+        float s = ss * zz;
+        s = ls + s;
+        v = v + s;  // :153 tile(sample) + samples, row indices[i]
+      }
+      out_sample[sp.off + j] = v;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// misc.py:3-17 materialised: out[n*d+j] = loc[j] + scale[j] * (z*1 + 0).
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) k_stateless_normal_sample(
+    const float* __restrict__ loc, const float* __restrict__ scale, int64_t d, int64_t total,
+    int32_t seed, float* __restrict__ out) {
+  __shared__ double logtab[32];
+  fill_logtab(logtab);
+  const PhiloxStream st = generate_key(seed, 42);
+  const int64_t ngrp = (total + 3) >> 2;
+  for (int64_t G = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; G < ngrp;
+       G += (int64_t)gridDim.x * blockDim.x) {
+    const F4 z = normal4(st, (uint64_t)G, logtab);
+    const float zz[4] = {z.a, z.b, z.c, z.d};
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      const int64_t f = 4 * G + w;
+      if (f < total) {
+        const int64_t j = f % d;
+        const float r = zz[w] * 1.0f + 0.0f;  // rnd * stddev + mean
+        const float s = scale[j] * r;
+        out[f] = loc[j] + s;
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Grouped-wrapper elementwise pieces.
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) k_standardise(
+    const float* __restrict__ q_loc, const float* __restrict__ q_scale,
+    const float* __restrict__ p_loc, const float* __restrict__ p_scale, int64_t n,
+    float* __restrict__ t_loc, float* __restrict__ t_scale) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const float dl = q_loc[i] - p_loc[i];
+    t_loc[i] = dl / p_scale[i];
+    t_scale[i] = q_scale[i] / p_scale[i];
+  }
+}
+
+__global__ void __launch_bounds__(256) k_kl_normal_normal(
+    const float* __restrict__ a_loc, const float* __restrict__ a_scale,
+    const float* __restrict__ b_loc, const float* __restrict__ b_scale, int64_t n,
+    float* __restrict__ out) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const float sa2 = a_scale[i] * a_scale[i];
+    const float sb2 = b_scale[i] * b_scale[i];
+    const float ratio = sa2 / sb2;
+    const float dl = a_loc[i] - b_loc[i];
+    const float t1 = (dl * dl) / (2.0f * sb2);
+    const float t2 = 0.5f * ((ratio - 1.0f) - logf_full(ratio, kLogTabConst));
+    out[i] = t1 + t2;
+  }
+}
+
+__global__ void __launch_bounds__(256) k_destandardise(const float* sample,
+                                                       const float* __restrict__ p_loc,
+                                                       const float* __restrict__ p_scale,
+                                                       int64_t n, float* out) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const float m = p_scale[i] * sample[i];
+    out[i] = m + p_loc[i];
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Diagnostics: device transcendentals over explicit inputs.
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) k_selftest_bm(uint32_t m0, int64_t count,
+                                                     float* __restrict__ rad,
+                                                     float* __restrict__ sn,
+                                                     float* __restrict__ cs) {
+  __shared__ double logtab[32];
+  fill_logtab(logtab);
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < count;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const uint32_t m = m0 + (uint32_t)i;
+    rad[i] = bm_radius(m, logtab);
+    float s, c;
+    sincosf_pos(bm_angle(m), s, c);
+    sn[i] = s;
+    cs[i] = c;
+  }
+}
+
+__global__ void __launch_bounds__(256) k_selftest_logf(const float* __restrict__ x, int64_t n,
+                                                       float* __restrict__ out) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x)
+    out[i] = logf_full(x[i], kLogTabConst);
+}
+
+// ---------------------------------------------------------------------------
+// Host-side launchers.
+// ---------------------------------------------------------------------------
+static inline unsigned grid_for(int64_t work, int64_t per_block, unsigned cap) {
+  int64_t g = (work + per_block - 1) / per_block;
+  if (g < 1) g = 1;
+  if (g > cap) g = cap;
+  return (unsigned)g;
+}
+
+hipError_t launch_prep_dims(const float* t_scale, const float* p_loc, const float* p_scale,
+                            int64_t n, int n_steps, float rho, float* loc_s, float* scale_s,
+                            float* lognorm, float* out_sample, hipStream_t stream) {
+  if (n <= 0) return hipSuccess;
+  const float nst = (float)n_steps;
+  const float sdiv = (float)__builtin_sqrt((double)n_steps);
+  hipLaunchKernelGGL(k_prep_dims, dim3(grid_for(n, 256, 65536)), dim3(256), 0, stream, t_scale,
+                     p_loc, p_scale, n, nst, sdiv, rho, loc_s, scale_s, lognorm, out_sample);
+  return hipGetLastError();
+}
+
+template <int DC, bool STEP0>
+static void launch_eval_t(const EncodeArgs& a, int step, hipStream_t stream) {
+  const int64_t ntiles = a.nb * a.tiles_per_block;
+  const unsigned grid = (unsigned)(ntiles < (1LL << 30) ? ntiles : (1LL << 30));
+  hipLaunchKernelGGL((k_encode_eval<DC, STEP0>), dim3(grid), dim3(256), 0, stream, a.t_loc,
+                     a.t_scale, a.loc_s, a.scale_s, a.lognorm, a.out_sample, a.block_off, a.ud,
+                     ntiles, a.tiles_per_block, a.cand_per_tile, a.n_cand, a.seed,
+                     a.block_id_base, step, a.keys);
+}
+
+template <bool STEP0>
+static void launch_eval_dc(const EncodeArgs& a, int step, hipStream_t stream) {
+  if (a.block_off == nullptr) {
+    switch (a.ud) {
+      case 8: return launch_eval_t<8, STEP0>(a, step, stream);
+      case 16: return launch_eval_t<16, STEP0>(a, step, stream);
+      case 32: return launch_eval_t<32, STEP0>(a, step, stream);
+      default: break;
+    }
+  }
+  launch_eval_t<0, STEP0>(a, step, stream);
+}
+
+hipError_t launch_encode(const EncodeArgs& a, hipStream_t stream) {
+  hipError_t e;
+  e = launch_prep_dims(a.t_scale, a.p_loc, a.p_scale, a.total_dims, a.n_steps, a.rho, a.loc_s,
+                       a.scale_s, a.lognorm, a.out_sample, stream);
+  if (e != hipSuccess) return e;
+  if (a.nb == 0) return hipSuccess;
+  const unsigned fgrid = grid_for(a.nb, 4, 65536);
+  for (int s = 0; s < a.n_steps; ++s) {
+    e = hipMemsetAsync(a.keys, 0, (size_t)a.nb * sizeof(unsigned long long), stream);
+    if (e != hipSuccess) return e;
+    if (s == 0 && a.ev_start) {
+      e = hipEventRecord((hipEvent_t)a.ev_start, stream);
+      if (e != hipSuccess) return e;
+    }
+    if (s == 0)
+      launch_eval_dc<true>(a, s, stream);
+    else
+      launch_eval_dc<false>(a, s, stream);
+    if (s == a.n_steps - 1 && a.ev_stop) {
+      e = hipEventRecord((hipEvent_t)a.ev_stop, stream);
+      if (e != hipSuccess) return e;
+    }
+    e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_encode_finalize, dim3(fgrid), dim3(256), 0, stream, a.loc_s,
+                       a.scale_s, a.block_off, a.ud, a.nb, a.seed, a.block_id_base, s,
+                       a.n_steps, a.keys, a.out_idx, a.out_sample);
+    e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
+}
+
+hipError_t launch_decode(const int32_t* idx, const float* p_loc, const float* p_scale,
+                         const int64_t* block_off, int64_t ud, int64_t nb, int n_bits,
+                         int n_steps, int32_t seed, float rho, int64_t block_id_base,
+                         float* out_sample, hipStream_t stream) {
+  if (nb <= 0) return hipSuccess;
+  const float nst = (float)n_steps;
+  const float sdiv = (float)__builtin_sqrt((double)n_steps);
+  hipLaunchKernelGGL(k_decode, dim3(grid_for(nb, 4, 65536)), dim3(256), 0, stream, idx, p_loc,
+                     p_scale, block_off, ud, nb, n_steps, (int64_t)1 << n_bits, nst, sdiv, rho,
+                     seed, block_id_base, out_sample);
+  return hipGetLastError();
+}
+
+hipError_t launch_stateless_normal_sample(const float* loc, const float* scale, int64_t d,
+                                          int64_t num_samples, int32_t seed, float* out,
+                                          hipStream_t stream) {
+  const int64_t total = d * num_samples;
+  if (total <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_stateless_normal_sample, dim3(grid_for((total + 3) / 4, 256, 65536)),
+                     dim3(256), 0, stream, loc, scale, d, total, seed, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_standardise(const float* q_loc, const float* q_scale, const float* p_loc,
+                              const float* p_scale, int64_t n, float* t_loc, float* t_scale,
+                              hipStream_t stream) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_standardise, dim3(grid_for(n, 256, 65536)), dim3(256), 0, stream, q_loc,
+                     q_scale, p_loc, p_scale, n, t_loc, t_scale);
+  return hipGetLastError();
+}
+
+hipError_t launch_kl(const float* q_loc, const float* q_scale, const float* p_loc,
+                     const float* p_scale, int64_t n, float* out, hipStream_t stream) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_kl_normal_normal, dim3(grid_for(n, 256, 65536)), dim3(256), 0, stream,
+                     q_loc, q_scale, p_loc, p_scale, n, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_destandardise(const float* sample, const float* p_loc, const float* p_scale,
+                                int64_t n, float* out, hipStream_t stream) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_destandardise, dim3(grid_for(n, 256, 65536)), dim3(256), 0, stream,
+                     sample, p_loc, p_scale, n, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_selftest_bm(uint32_t m0, int64_t count, float* rad, float* sn, float* cs,
+                              hipStream_t stream) {
+  if (count <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_selftest_bm, dim3(grid_for(count, 256, 65536)), dim3(256), 0, stream, m0,
+                     count, rad, sn, cs);
+  return hipGetLastError();
+}
+
+hipError_t launch_selftest_logf(const float* x, int64_t n, float* out, hipStream_t stream) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_selftest_logf, dim3(grid_for(n, 256, 65536)), dim3(256), 0, stream, x, n,
+                     out);
+  return hipGetLastError();
+}
+
+}  // namespace cwq

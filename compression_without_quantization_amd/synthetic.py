@@ -1,0 +1,77 @@
+"""Synthetic diagonal-Gaussian latent blocks.
+
+No Kodak images or trained PLN checkpoints exist offline, so benchmarks and
+parity tests use blocks of the configured shape:
+
+  prior      p_loc ~ N(0,1), p_scale ~ U[0.5, 2]
+  target     t_scale ~ U[0.3, 0.9], t_loc = alpha * m, m ~ N(0,1), with alpha
+             solved per block so that the block KL
+             sum_j 0.5 (t_loc^2 + t_scale^2 - 1 - 2 ln t_scale) equals K nats
+             (K = kl_bits*ln2 - 1, the reference's n_nats_per_group,
+             coded_greedy_sampler.py:226; C1 uses K = 4 ln2 exactly);
+             blocks whose RHS is <= 0 are redrawn.
+  posterior  post_loc = p_loc + p_scale * t_loc, post_scale = p_scale * t_scale
+
+Generator: numpy PCG64(20261015) unless a seed is given.
+"""
+import numpy as np
+
+DEFAULT_SEED = 20261015
+
+
+def target_nats(kl_bits, exact=False):
+    return kl_bits * np.log(2) if exact else kl_bits * np.log(2) - 1
+
+
+def make_blocks(nb, d, kl_bits, seed=DEFAULT_SEED, exact_kl=False, chunk=1 << 16):
+    """Returns dict of float32 arrays [nb, d]: prior_loc, prior_scale, post_loc, post_scale."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    K = target_nats(kl_bits, exact_kl)
+    out = {k: np.empty((nb, d), dtype=np.float32)
+           for k in ("prior_loc", "prior_scale", "post_loc", "post_scale")}
+    for b0 in range(0, nb, chunk):
+        n = min(chunk, nb - b0)
+        p_loc = rng.standard_normal((n, d))
+        p_scale = rng.uniform(0.5, 2.0, (n, d))
+        t_scale = rng.uniform(0.3, 0.9, (n, d))
+        m = rng.standard_normal((n, d))
+        while True:
+            rhs = 2 * K - np.sum(t_scale ** 2 - 1 - 2 * np.log(t_scale), axis=1)
+            bad = (rhs <= 0) | (np.sum(m ** 2, axis=1) == 0)
+            if not bad.any():
+                break
+            k = int(bad.sum())
+            t_scale[bad] = rng.uniform(0.3, 0.9, (k, d))
+            m[bad] = rng.standard_normal((k, d))
+        alpha = np.sqrt(rhs / np.sum(m ** 2, axis=1))
+        t_loc = alpha[:, None] * m
+        out["prior_loc"][b0:b0 + n] = p_loc
+        out["prior_scale"][b0:b0 + n] = p_scale
+        out["post_loc"][b0:b0 + n] = p_loc + p_scale * t_loc
+        out["post_scale"][b0:b0 + n] = p_scale * t_scale
+    return out
+
+
+def make_latents(D, bits_per_dim=1.1, off_fraction=0.5, seed=DEFAULT_SEED):
+    """Flat PLN-like latents for the grouped path (configs C2/C3).
+
+    A fraction of dims carries ~no information (posterior == prior up to
+    noise, as inactive latent channels do); the rest have per-dim KL drawn
+    from a Gamma distribution so the mean KL is ``bits_per_dim`` bits.
+    Returns float32 arrays (q_loc, q_scale, p_loc, p_scale) of length D.
+    """
+    rng = np.random.Generator(np.random.PCG64(seed))
+    p_loc = rng.standard_normal(D)
+    p_scale = rng.uniform(0.5, 2.0, D)
+    active = rng.uniform(size=D) >= off_fraction
+    mean_nats = bits_per_dim * np.log(2) / max(1e-9, 1 - off_fraction)
+    kl = np.where(active, rng.gamma(1.5, mean_nats / 1.5, D), rng.uniform(0, 1e-3, D))
+    # split each dim's KL between a scale and a mean part
+    t_scale = np.exp(-rng.uniform(0, 1, D) * np.sqrt(kl))  # <= 1
+    kl_scale = 0.5 * (t_scale ** 2 - 1 - 2 * np.log(t_scale))
+    t_loc2 = np.maximum(2 * (kl - kl_scale), 0.0)
+    t_loc = np.sqrt(t_loc2) * np.where(rng.uniform(size=D) < 0.5, -1, 1)
+    q_loc = p_loc + p_scale * t_loc
+    q_scale = p_scale * t_scale
+    f = lambda a: a.astype(np.float32)
+    return f(q_loc), f(q_scale), f(p_loc), f(p_scale)

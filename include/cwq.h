@@ -1,0 +1,153 @@
+/*
+ * cwq.h -- C ABI of the MI355X (gfx950) greedy coded sampler (libcwq.so).
+ *
+ * Drop-in boundary for the reference's relative-entropy coding hot path.  The
+ * reference has no native ABI (its sampler is a TF1 graph); each entry point
+ * below replaces the graph op named next to it:
+ *
+ *   cwq_stateless_normal_sample  <- code/misc.py:3-17 stateless_normal_sample
+ *                                   (tf.random.stateless_normal, seed=[seed,42],
+ *                                   then scale*z and loc+ at misc.py:14-15)
+ *   cwq_greedy_encode[_uniform]  <- code/coded_greedy_sampler.py:29-89
+ *                                   code_greedy_sample, batched over the groups
+ *                                   that code_grouped_greedy_sample (:170-296)
+ *                                   feeds one sess.run at a time (:273-284);
+ *                                   group g uses seed + block_id_base + g (:282)
+ *   cwq_greedy_decode[_uniform]  <- code/coded_greedy_sampler.py:93-167
+ *                                   decode_greedy_sample, batched the same way
+ *                                   as decode_grouped_greedy_sample (:345-356)
+ *   cwq_standardise              <- code/coded_greedy_sampler.py:193-199
+ *   cwq_kl_normal_normal         <- code/coded_greedy_sampler.py:201
+ *                                   (tfd.kl_divergence(target, proposal))
+ *   cwq_destandardise            <- code/coded_greedy_sampler.py:292 / :362
+ *   cwq_group_starts             <- code/coded_greedy_sampler.py:207-252
+ *                                   (host-side sequential partition)
+ *
+ * Conventions
+ *   - All float/index pointers are DEVICE pointers (hipMalloc / torch cuda
+ *     tensors) unless documented as host.  `stream` is a hipStream_t (NULL =
+ *     default stream).  Calls are stream-ordered and asynchronous; nothing is
+ *     allocated and nothing synchronises (graph-capturable), except
+ *     cwq_group_starts which is pure host code.
+ *   - Blocks ("groups" in the reference) are described in CSR form:
+ *     block g covers dims [block_off[g], block_off[g+1]) of the flat arrays;
+ *     block_off is a device int64 array of nb+1 entries.  The *_uniform
+ *     variants take a fixed block dimension instead.
+ *   - target = posterior q (t_loc, t_scale); proposal = prior p (p_loc,
+ *     p_scale), as in the reference's argument order.
+ *   - Return value: 0 on success, a negative CWQ_ERR_* code otherwise; the
+ *     message is available from cwq_last_error() (thread-local).  Nothing
+ *     throws across this ABI.
+ */
+#ifndef CWQ_H_
+#define CWQ_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CWQ_OK 0
+#define CWQ_ERR_INVALID (-1)   /* bad argument (sizes, bits, null pointer) */
+#define CWQ_ERR_HIP (-2)       /* HIP runtime error (launch, memset) */
+#define CWQ_ERR_WORKSPACE (-3) /* workspace too small */
+
+#define CWQ_MAX_BITS_PER_STEP 30
+
+/* Library version, (major << 16) | minor. */
+int cwq_version(void);
+
+/* Thread-local description of the last error ("" if none). */
+const char* cwq_last_error(void);
+
+/* misc.py:3-17.  out[n*d + j] = loc[j] + scale[j] * Z[n*d + j] for
+ * n < num_samples, j < d, where Z = tf.random.stateless_normal(
+ * [num_samples, d], seed=[seed, 42]) (flat Philox4x32-10 + Box-Muller). */
+int cwq_stateless_normal_sample(const float* loc, const float* scale, int64_t d,
+                                int64_t num_samples, int32_t seed, float* out, void* stream);
+
+/* Workspace bytes needed by cwq_greedy_encode / cwq_greedy_encode_uniform for
+ * nb blocks holding total_dims dims in all. */
+size_t cwq_greedy_encode_workspace_size(int64_t nb, int64_t total_dims);
+
+/* Greedy coded sampling, encoder (coded_greedy_sampler.py:29-89) for nb
+ * independent blocks.
+ *   out_idx    [nb * n_steps] int32: the argmax index of every step (the
+ *              reference emits these as LSB-first bit strings, :81-87)
+ *   out_sample [total_dims] f32: best_sample of every block (:89)
+ *   max_block_dim: an upper bound on the largest block's dimension.
+ * Block g is coded with seed (seed + block_id_base + g) (int32 wrap), step i of
+ * it with the stateless seed [1000*(that) + i, 42] (:55). */
+int cwq_greedy_encode(const float* t_loc, const float* t_scale, const float* p_loc,
+                      const float* p_scale, const int64_t* block_off, int64_t nb,
+                      int64_t total_dims, int64_t max_block_dim, int n_bits_per_step,
+                      int n_steps, int32_t seed, float rho, int64_t block_id_base,
+                      int32_t* out_idx, float* out_sample, void* workspace,
+                      size_t workspace_bytes, void* stream);
+
+/* Same with every block of dimension d (block g = dims [g*d, (g+1)*d)). */
+int cwq_greedy_encode_uniform(const float* t_loc, const float* t_scale, const float* p_loc,
+                              const float* p_scale, int64_t nb, int64_t d,
+                              int n_bits_per_step, int n_steps, int32_t seed, float rho,
+                              int64_t block_id_base, int32_t* out_idx, float* out_sample,
+                              void* workspace, size_t workspace_bytes, void* stream);
+
+/* Decoder (coded_greedy_sampler.py:93-167): sample = sum over steps of the
+ * proposal-shard candidate idx[g*n_steps + i] of step i.  O(n_steps * d) per
+ * block (only the selected row of the candidate stream is regenerated). */
+int cwq_greedy_decode(const int32_t* idx, const float* p_loc, const float* p_scale,
+                      const int64_t* block_off, int64_t nb, int64_t total_dims,
+                      int64_t max_block_dim, int n_bits_per_step, int n_steps, int32_t seed,
+                      float rho, int64_t block_id_base, float* out_sample, void* stream);
+
+int cwq_greedy_decode_uniform(const int32_t* idx, const float* p_loc, const float* p_scale,
+                              int64_t nb, int64_t d, int n_bits_per_step, int n_steps,
+                              int32_t seed, float rho, int64_t block_id_base, float* out_sample,
+                              void* stream);
+
+/* coded_greedy_sampler.py:198-199: t_loc = (q_loc - p_loc) / p_scale,
+ * t_scale = q_scale / p_scale (float32). */
+int cwq_standardise(const float* q_loc, const float* q_scale, const float* p_loc,
+                    const float* p_scale, int64_t n, float* t_loc, float* t_scale, void* stream);
+
+/* coded_greedy_sampler.py:201: per-dim KL(q || p) of two diagonal Gaussians
+ * (TFP <= 0.7 formula, float32). */
+int cwq_kl_normal_normal(const float* q_loc, const float* q_scale, const float* p_loc,
+                         const float* p_scale, int64_t n, float* out, void* stream);
+
+/* coded_greedy_sampler.py:292: out = p_scale * sample + p_loc (float32, two
+ * roundings).  out may alias sample. */
+int cwq_destandardise(const float* sample, const float* p_loc, const float* p_scale, int64_t n,
+                      float* out, void* stream);
+
+/* HOST function (coded_greedy_sampler.py:207-252).  kl: HOST float32 [D].
+ * size_threshold: the smallest group size s for which the reference's
+ * `np.log(s + 1) / np.log(2) >= max_group_size_bits` holds.  n_nats:
+ * n_bits_per_group * np.log(2) - 1 (float64).  Writes the reference's
+ * group_start_indices (including the leading 0, the forced boundary at D-1 and
+ * the trailing D) to starts[0..n) and returns n, or a negative error code if
+ * cap is too small. */
+int64_t cwq_group_starts(const float* kl, int64_t D, int64_t size_threshold, double n_nats,
+                         int64_t* starts, int64_t cap);
+
+/* Diagnostics (used by the parity tests): evaluate the device restatement of
+ * the Box-Muller transcendentals for the 23-bit mantissas m0 .. m0+count-1:
+ *   radius[i] = sqrtf(-2 logf(max(m*2^-23, 1e-7f)))    (BoxMullerFloat u2)
+ *   sin[i], cos[i] = sincosf((float)(2*pi * m*2^-23))   (BoxMullerFloat v1)
+ * and logf(x[i]) for arbitrary floats (the per-dimension normaliser's log). */
+int cwq_selftest_bm_tables(uint32_t m0, int64_t count, float* radius, float* sin_out,
+                           float* cos_out, void* stream);
+int cwq_selftest_logf(const float* x, int64_t n, float* out, void* stream);
+
+/* Profiling hook (bench.py): when set, every later encode call made by this
+ * host thread records hipEvent_t `start_event` on its stream right before its
+ * first candidate-scoring (eval) launch and `stop_event` right after its last
+ * one, so the caller can time the dominant kernel alone.  NULL, NULL clears. */
+int cwq_profile_set_eval_events(void* start_event, void* stop_event);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CWQ_H_ */

@@ -1,0 +1,466 @@
+/*
+ * cwq_oracle.c -- CPU ORACLE for the greedy coded sampling loop.
+ *
+ *   *** TEST INFRASTRUCTURE ONLY. ***
+ *   Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may
+ *   load this library, and only as the checker / the reported CPU baseline.
+ *   The product path (compression_without_quantization_amd) never links it.
+ *
+ * What it restates (plain C, glibc libm, -O2 -ffp-contract=off):
+ *   - code/coded_greedy_sampler.py:29-89   code_greedy_sample (encoder loop)
+ *   - code/coded_greedy_sampler.py:93-167  decode_greedy_sample
+ *   - code/coded_greedy_sampler.py:170-296 the grouped wrapper's numeric parts
+ *     (standardisation :193-199, KL :201, grouping :207-244, seed+g :282,
+ *     de-standardisation :292)
+ *   - code/misc.py:3-17                    stateless_normal_sample
+ *   - third-party semantics the reference calls into (SURVEY.md Appendix A,
+ *     recalled from TF/TFP/Eigen public sources, NOT verifiable offline):
+ *       A.1 Philox4x32-10, A.2 TF GenerateKey, A.3 FillPhiloxRandom layout,
+ *       A.4 BoxMullerFloat (glibc logf/sqrtf/sincosf), A.5 TFP<=0.7
+ *       Normal.log_prob, A.6 Eigen 3.3 AVX inner-dim sum order,
+ *       A.7 argmax lowest-index-on-ties, A.9 TFP<=0.7 KL(Normal||Normal).
+ *
+ * Parity status: the reference (TF1 graph code) cannot be imported or run in
+ * this environment (TF/TFP absent; building/importing anything
+ * from /root/reference was refused).  This oracle is pinned by
+ *   (1) published Random123 Philox4x32-10 known-answer vectors (tests/golden),
+ *   (2) the bit-string examples readable in code/binary_io.py:41-67,
+ *   (3) the host glibc 2.35 libm itself (logf, sincosf, sqrtf are called
+ *       directly here, so the Box-Muller transcendentals ARE the declared
+ *       semantics, not a restatement of them).
+ * Everything that depends on TF/TFP/Eigen internals is declared semantics:
+ * PARITY AGAINST THE REFERENCE IS UNPINNED beyond those pins.
+ */
+#define _GNU_SOURCE
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+#include <float.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+#define CWQO_API __attribute__((visibility("default")))
+
+/* ------------------------------------------------------------------------ */
+/* A.1 Philox4x32-10 (TF random::PhiloxRandom; same round as Random123).     */
+/* ------------------------------------------------------------------------ */
+#define PHILOX_M0 0xD2511F53u
+#define PHILOX_M1 0xCD9E8D57u
+#define PHILOX_W0 0x9E3779B9u
+#define PHILOX_W1 0xBB67AE85u
+
+CWQO_API void cwqo_philox4x32_10(const uint32_t ctr_in[4], const uint32_t key_in[2],
+                                 uint32_t out[4]) {
+  uint32_t c0 = ctr_in[0], c1 = ctr_in[1], c2 = ctr_in[2], c3 = ctr_in[3];
+  uint32_t k0 = key_in[0], k1 = key_in[1];
+  for (int r = 0; r < 10; ++r) {
+    uint64_t p0 = (uint64_t)PHILOX_M0 * c0;
+    uint64_t p1 = (uint64_t)PHILOX_M1 * c2;
+    uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
+    uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
+    uint32_t n0 = hi1 ^ c1 ^ k0;
+    uint32_t n1 = lo1;
+    uint32_t n2 = hi0 ^ c3 ^ k1;
+    uint32_t n3 = lo0;
+    c0 = n0; c1 = n1; c2 = n2; c3 = n3;
+    if (r < 9) { k0 += PHILOX_W0; k1 += PHILOX_W1; }
+  }
+  out[0] = c0; out[1] = c1; out[2] = c2; out[3] = c3;
+}
+
+/* A.2 TF stateless seed scrambling (stateless_random_ops.cc GenerateKey).
+ * seed = [s0, s1] int32 (misc.py:11 passes [1000*seed+i, 42]); each is
+ * sign-extended to 64 bits. */
+CWQO_API void cwqo_generate_key(int32_t s0, int32_t s1, uint32_t key[2], uint32_t ctr[4]) {
+  uint64_t seed0 = (uint64_t)(int64_t)s0;
+  uint64_t seed1 = (uint64_t)(int64_t)s1;
+  uint32_t k[2] = {0x3ec8f720u, 0x02461e29u};
+  uint32_t c[4] = {(uint32_t)seed0, (uint32_t)(seed0 >> 32), (uint32_t)seed1,
+                   (uint32_t)(seed1 >> 32)};
+  uint32_t mix[4];
+  cwqo_philox4x32_10(c, k, mix);
+  key[0] = mix[0];
+  key[1] = mix[1];
+  ctr[0] = 0;
+  ctr[1] = 0;
+  ctr[2] = mix[2];
+  ctr[3] = mix[3];
+}
+
+/* 128-bit counter skip (PhiloxRandom::Skip). */
+static void philox_skip(const uint32_t base[4], uint64_t count, uint32_t out[4]) {
+  uint32_t lo = (uint32_t)count, hi = (uint32_t)(count >> 32);
+  out[0] = base[0] + lo;
+  if (out[0] < lo) ++hi;
+  out[1] = base[1] + hi;
+  out[2] = base[2];
+  out[3] = base[3];
+  if (out[1] < hi) {
+    if (++out[2] == 0) ++out[3];
+  }
+}
+
+/* ------------------------------------------------------------------------ */
+/* A.4 BoxMullerFloat with TF Uint32ToFloat, glibc transcendentals.          */
+/* ------------------------------------------------------------------------ */
+static inline float uint32_to_float(uint32_t x) {
+  uint32_t val = (127u << 23) | (x & 0x7fffffu);
+  float f;
+  memcpy(&f, &val, 4);
+  return f - 1.0f;
+}
+
+CWQO_API float cwqo_bm_radius(uint32_t x0) {
+  float u1 = uint32_to_float(x0);
+  if (u1 < 1.0e-7f) u1 = 1.0e-7f;
+  return sqrtf(-2.0f * logf(u1));
+}
+
+CWQO_API float cwqo_bm_angle(uint32_t x1) {
+  /* `2.0f * M_PI * Uint32ToFloat(x1)` is evaluated in double (M_PI is a
+   * double literal) and then narrowed to float. */
+  return (float)(2.0f * M_PI * (double)uint32_to_float(x1));
+}
+
+CWQO_API void cwqo_bm_sincos(uint32_t x1, float* s, float* c) {
+  float v1 = cwqo_bm_angle(x1);
+  sincosf(v1, s, c);
+}
+
+CWQO_API void cwqo_box_muller(uint32_t x0, uint32_t x1, float* f0, float* f1) {
+  float u2 = cwqo_bm_radius(x0);
+  float s, c;
+  cwqo_bm_sincos(x1, &s, &c);
+  *f0 = s * u2;
+  *f1 = c * u2;
+}
+
+/* Philox group `grp` of stream (key, ctr) -> 4 normals (NormalDistribution). */
+static void normal_group(const uint32_t key[2], const uint32_t ctr[4], uint64_t grp,
+                         float z[4]) {
+  uint32_t c[4], x[4];
+  philox_skip(ctr, grp, c);
+  cwqo_philox4x32_10(c, key, x);
+  cwqo_box_muller(x[0], x[1], &z[0], &z[1]);
+  cwqo_box_muller(x[2], x[3], &z[2], &z[3]);
+}
+
+/* tf.random.stateless_normal(shape=[n], seed=[s0,s1]) flattened, including the
+ * python wrapper's `rnd * stddev + mean` with stddev=1, mean=0 (A.3, A.4). */
+CWQO_API void cwqo_stateless_normal(int32_t s0, int32_t s1, int64_t n, float* out) {
+  uint32_t key[2], ctr[4];
+  cwqo_generate_key(s0, s1, key, ctr);
+  float z[4];
+  for (int64_t k = 0; k < n; ++k) {
+    if ((k & 3) == 0) normal_group(key, ctr, (uint64_t)k >> 2, z);
+    out[k] = z[k & 3] * 1.0f + 0.0f;
+  }
+}
+
+/* misc.py:3-17 stateless_normal_sample(loc, scale, num_samples, seed) for a
+ * rank-1 loc/scale of length d: out[n*d+j] = loc[j] + scale[j]*Z[n*d+j]. */
+CWQO_API void cwqo_stateless_normal_sample(const float* loc, const float* scale, int64_t d,
+                                           int64_t num_samples, int32_t seed, float* out) {
+  cwqo_stateless_normal(seed, 42, num_samples * d, out);
+  for (int64_t n = 0; n < num_samples; ++n)
+    for (int64_t j = 0; j < d; ++j) {
+      float s = scale[j] * out[n * d + j]; /* misc.py:14 */
+      out[n * d + j] = loc[j] + s;         /* misc.py:15 */
+    }
+}
+
+/* ------------------------------------------------------------------------ */
+/* A.5 TFP (<=0.7) Normal.log_prob; A.6 Eigen inner-dim sum; A.7 argmax.     */
+/* ------------------------------------------------------------------------ */
+/* 0.5*math.log(2.*math.pi) converted to float32 by TF. */
+static float half_log_2pi_f32(void) { return (float)(0.5 * log(2.0 * M_PI)); }
+
+CWQO_API float cwqo_log_normalization(float scale) {
+  return half_log_2pi_f32() + logf(scale);
+}
+
+static inline float log_prob_c(float x, float loc, float scale, float lognorm) {
+  float z = (x - loc) / scale;      /* _z(x) */
+  float u = -0.5f * (z * z);        /* _log_unnormalized_prob: -0.5*square(z) */
+  return u - lognorm;               /* minus _log_normalization() */
+}
+
+CWQO_API float cwqo_normal_log_prob(float x, float loc, float scale) {
+  return log_prob_c(x, loc, scale, cwqo_log_normalization(scale));
+}
+
+/* Eigen 3.3 InnerMostDimReducer<SumReducer>, Packet8f (AVX): 8 lane partials,
+ * predux((p0+p4,p1+p5,p2+p6,p3+p7)) = (q0+q2)+(q1+q3), scalar tail, t + r. */
+CWQO_API float cwqo_eigen_rowsum(const float* x, int64_t d) {
+  int64_t vec = (d / 8) * 8;
+  float p[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  for (int64_t j = 0; j < vec; j += 8)
+    for (int l = 0; l < 8; ++l) p[l] = p[l] + x[j + l];
+  float t = 0.0f;
+  for (int64_t j = vec; j < d; ++j) t = t + x[j];
+  float q0 = p[0] + p[4], q1 = p[1] + p[5], q2 = p[2] + p[6], q3 = p[3] + p[7];
+  float r = (q0 + q2) + (q1 + q3);
+  return t + r;
+}
+
+static inline int32_t step_seed(int32_t seed, int32_t i) {
+  /* `1000 * seed + i` in int32 (wraps, as TF int32 arithmetic does). */
+  return (int32_t)((uint32_t)1000u * (uint32_t)seed + (uint32_t)i);
+}
+
+/* Per-block proposal shard constants (coded_greedy_sampler.py:42-45). */
+static void shard_params(const float* p_loc, const float* p_scale, int64_t d, int n_steps,
+                         float rho, float* loc_s, float* scale_s) {
+  float nst = (float)n_steps;
+  float sdiv = (float)sqrt((double)n_steps); /* np.sqrt(n_steps) -> float32 */
+  for (int64_t j = 0; j < d; ++j) {
+    loc_s[j] = p_loc[j] / nst;
+    float rs = rho * p_scale[j];
+    scale_s[j] = rs / sdiv;
+  }
+}
+
+/* Streaming evaluation of candidate rows: the reference materialises the
+ * [2^b, d] tensors; the values computed per element are identical. */
+typedef struct {
+  uint32_t key[2], ctr[4];
+  uint64_t cur_grp;
+  int have;
+  float z[4];
+} normal_stream;
+
+static inline float stream_normal(normal_stream* st, uint64_t k) {
+  uint64_t g = k >> 2;
+  if (!st->have || st->cur_grp != g) {
+    normal_group(st->key, st->ctr, g, st->z);
+    st->cur_grp = g;
+    st->have = 1;
+  }
+  return st->z[k & 3] * 1.0f + 0.0f;
+}
+
+/* code_greedy_sample for ONE block of d dims (coded_greedy_sampler.py:29-89).
+ * out_idx[n_steps], out_sample[d].  Returns 0 on success. */
+CWQO_API int cwqo_code_greedy_sample(const float* t_loc, const float* t_scale,
+                                     const float* p_loc, const float* p_scale, int64_t d,
+                                     int n_bits_per_step, int n_steps, int32_t seed, float rho,
+                                     int32_t* out_idx, float* out_sample) {
+  if (n_bits_per_step < 0 || n_bits_per_step > 30 || n_steps < 1 || d < 0) return -1;
+  int64_t n_samples = (int64_t)1 << n_bits_per_step;
+  size_t db = (size_t)(d > 0 ? d : 1) * sizeof(float);
+  float* loc_s = (float*)malloc(db);
+  float* scale_s = (float*)malloc(db);
+  float* lognorm = (float*)malloc(db);
+  float* row = (float*)malloc(db);
+  if (!loc_s || !scale_s || !lognorm || !row) {
+    free(loc_s); free(scale_s); free(lognorm); free(row);
+    return -2;
+  }
+  shard_params(p_loc, p_scale, d, n_steps, rho, loc_s, scale_s);
+  for (int64_t j = 0; j < d; ++j) lognorm[j] = cwqo_log_normalization(t_scale[j]);
+  for (int64_t j = 0; j < d; ++j) out_sample[j] = 0.0f; /* tf.zeros */
+
+  for (int i = 0; i < n_steps; ++i) {
+    normal_stream st;
+    memset(&st, 0, sizeof(st));
+    cwqo_generate_key(step_seed(seed, i), 42, st.key, st.ctr);
+    int64_t best_idx = 0;
+    float best_val = -FLT_MAX; /* ArgMaxTupleReducer initial accumulator */
+    for (int64_t n = 0; n < n_samples; ++n) {
+      for (int64_t j = 0; j < d; ++j) {
+        float z = stream_normal(&st, (uint64_t)(n * d + j));
+        float s = scale_s[j] * z;       /* misc.py:14 */
+        s = loc_s[j] + s;               /* misc.py:15 */
+        float tv = out_sample[j] + s;   /* coded_greedy_sampler.py:57 */
+        row[j] = log_prob_c(tv, t_loc[j], t_scale[j], lognorm[j]); /* :59 */
+      }
+      float v = cwqo_eigen_rowsum(row, d); /* :59 reduce_sum axis=1 */
+      if (v > best_val) { best_val = v; best_idx = n; } /* :61 argmax */
+    }
+    /* :63 best_sample = test_samples[index, :] */
+    for (int64_t j = 0; j < d; ++j) {
+      float z = stream_normal(&st, (uint64_t)(best_idx * d + j));
+      float s = scale_s[j] * z;
+      s = loc_s[j] + s;
+      row[j] = out_sample[j] + s;
+    }
+    memcpy(out_sample, row, (size_t)d * sizeof(float));
+    out_idx[i] = (int32_t)best_idx;
+  }
+  free(loc_s); free(scale_s); free(lognorm); free(row);
+  return 0;
+}
+
+/* decode_greedy_sample for ONE block (coded_greedy_sampler.py:93-167). */
+CWQO_API int cwqo_decode_greedy_sample(const int32_t* idx, const float* p_loc,
+                                       const float* p_scale, int64_t d, int n_bits_per_step,
+                                       int n_steps, int32_t seed, float rho, float* out_sample) {
+  if (n_bits_per_step < 0 || n_bits_per_step > 30 || n_steps < 1 || d < 0) return -1;
+  size_t db = (size_t)(d > 0 ? d : 1) * sizeof(float);
+  float* loc_s = (float*)malloc(db);
+  float* scale_s = (float*)malloc(db);
+  if (!loc_s || !scale_s) { free(loc_s); free(scale_s); return -2; }
+  shard_params(p_loc, p_scale, d, n_steps, rho, loc_s, scale_s);
+  for (int64_t j = 0; j < d; ++j) out_sample[j] = 0.0f;
+  for (int i = 0; i < n_steps; ++i) {
+    normal_stream st;
+    memset(&st, 0, sizeof(st));
+    cwqo_generate_key(step_seed(seed, i), 42, st.key, st.ctr);
+    int64_t n = idx[i];
+    if (n < 0 || n >= ((int64_t)1 << n_bits_per_step)) { free(loc_s); free(scale_s); return -3; }
+    for (int64_t j = 0; j < d; ++j) {
+      float z = stream_normal(&st, (uint64_t)(n * d + j));
+      float s = scale_s[j] * z;
+      s = loc_s[j] + s;
+      out_sample[j] = out_sample[j] + s; /* :151-158 samples = tile(sample) + ... */
+    }
+  }
+  free(loc_s); free(scale_s);
+  return 0;
+}
+
+/* Batched (CSR) encoder: block g = dims [off[g], off[g+1]), seed + block_id_base + g
+ * (coded_greedy_sampler.py:282 `seed_feed: seed + i`).  OpenMP over blocks.
+ * nthreads <= 0 -> OpenMP default. */
+CWQO_API int cwqo_greedy_encode(const float* t_loc, const float* t_scale, const float* p_loc,
+                                const float* p_scale, const int64_t* block_off, int64_t nb,
+                                int n_bits_per_step, int n_steps, int32_t seed, float rho,
+                                int64_t block_id_base, int32_t* out_idx, float* out_sample,
+                                int nthreads) {
+  int err = 0;
+#ifdef _OPENMP
+  if (nthreads > 0) omp_set_num_threads(nthreads);
+#pragma omp parallel for schedule(dynamic, 1) reduction(| : err)
+#endif
+  for (int64_t g = 0; g < nb; ++g) {
+    int64_t o = block_off[g], d = block_off[g + 1] - block_off[g];
+    int32_t sg = (int32_t)((uint32_t)seed + (uint32_t)(block_id_base + g));
+    int rc = cwqo_code_greedy_sample(t_loc + o, t_scale + o, p_loc + o, p_scale + o, d,
+                                     n_bits_per_step, n_steps, sg, rho,
+                                     out_idx + g * n_steps, out_sample + o);
+    if (rc) err |= 1;
+  }
+  return err ? -1 : 0;
+}
+
+CWQO_API int cwqo_greedy_decode(const int32_t* idx, const float* p_loc, const float* p_scale,
+                                const int64_t* block_off, int64_t nb, int n_bits_per_step,
+                                int n_steps, int32_t seed, float rho, int64_t block_id_base,
+                                float* out_sample, int nthreads) {
+  int err = 0;
+#ifdef _OPENMP
+  if (nthreads > 0) omp_set_num_threads(nthreads);
+#pragma omp parallel for schedule(dynamic, 16) reduction(| : err)
+#endif
+  for (int64_t g = 0; g < nb; ++g) {
+    int64_t o = block_off[g], d = block_off[g + 1] - block_off[g];
+    int32_t sg = (int32_t)((uint32_t)seed + (uint32_t)(block_id_base + g));
+    int rc = cwqo_decode_greedy_sample(idx + g * n_steps, p_loc + o, p_scale + o, d,
+                                       n_bits_per_step, n_steps, sg, rho, out_sample + o);
+    if (rc) err |= 1;
+  }
+  return err ? -1 : 0;
+}
+
+/* ------------------------------------------------------------------------ */
+/* Grouped wrapper numerics (coded_greedy_sampler.py:193-244, 292).          */
+/* ------------------------------------------------------------------------ */
+/* :198-199 standardise the target by the proposal (float32 ops). */
+CWQO_API void cwqo_standardise(const float* q_loc, const float* q_scale, const float* p_loc,
+                               const float* p_scale, int64_t n, float* t_loc, float* t_scale) {
+  for (int64_t i = 0; i < n; ++i) {
+    float dl = q_loc[i] - p_loc[i];
+    t_loc[i] = dl / p_scale[i];
+    t_scale[i] = q_scale[i] / p_scale[i];
+  }
+}
+
+/* A.9 TFP (<=0.7) _kl_normal_normal(a=target, b=proposal), float32. */
+CWQO_API void cwqo_kl_normal_normal(const float* a_loc, const float* a_scale,
+                                    const float* b_loc, const float* b_scale, int64_t n,
+                                    float* out) {
+  for (int64_t i = 0; i < n; ++i) {
+    float sa2 = a_scale[i] * a_scale[i];
+    float sb2 = b_scale[i] * b_scale[i];
+    float ratio = sa2 / sb2;
+    float dl = a_loc[i] - b_loc[i];
+    float t1 = (dl * dl) / (2.0f * sb2);
+    float t2 = 0.5f * ((ratio - 1.0f) - logf(ratio));
+    out[i] = t1 + t2;
+  }
+}
+
+/* :207-244 greedy grouping.  size_threshold = smallest s with
+ * np.log(s+1)/np.log(2) >= max_group_size_bits (computed by the caller with
+ * NumPy, exactly as the reference evaluates it).  The running group KL is a
+ * float32 (numpy float32 scalar arithmetic); the comparison is done in float64
+ * against n_nats = n_bits_per_group*np.log(2) - 1.
+ * Writes starts[0..n_starts) = [0, ...boundaries..., D]; returns n_starts or
+ * -1 if cap is too small. */
+CWQO_API int64_t cwqo_group_starts(const float* kl, int64_t D, int64_t size_threshold,
+                                   double n_nats, int64_t* starts, int64_t cap) {
+  int64_t ns = 0;
+  if (cap < 1) return -1;
+  starts[ns++] = 0;
+  int64_t cur_size = 0;
+  float cur_kl = 0.0f;
+  for (int64_t idx = 0; idx < D; ++idx) {
+    float s = cur_kl + kl[idx];
+    if (cur_size >= size_threshold || (double)s >= n_nats || idx == D - 1) {
+      if (ns >= cap) return -1;
+      starts[ns++] = idx;
+      cur_size = 1;
+      cur_kl = kl[idx];
+    } else {
+      cur_kl = s;
+      cur_size += 1;
+    }
+  }
+  if (ns >= cap) return -1;
+  starts[ns++] = D; /* :252 group_start_indices += [num_dimensions] */
+  return ns;
+}
+
+/* :292 sample = proposal.scale * sample + proposal.loc (float32, two roundings) */
+CWQO_API void cwqo_destandardise(const float* sample, const float* p_loc, const float* p_scale,
+                                 int64_t n, float* out) {
+  for (int64_t i = 0; i < n; ++i) {
+    float m = p_scale[i] * sample[i];
+    out[i] = m + p_loc[i];
+  }
+}
+
+CWQO_API int cwqo_num_threads(void) {
+#ifdef _OPENMP
+  return omp_get_max_threads();
+#else
+  return 1;
+#endif
+}
+
+/* ------------------------------------------------------------------------ */
+/* Batch tables for exhaustive transcendental checks (glibc = declared       */
+/* semantics).  m is the 23-bit mantissa field of the Philox word.           */
+/* ------------------------------------------------------------------------ */
+CWQO_API void cwqo_bm_radius_table(uint32_t m0, int64_t count, float* out) {
+#ifdef _OPENMP
+#pragma omp parallel for schedule(static)
+#endif
+  for (int64_t i = 0; i < count; ++i) out[i] = cwqo_bm_radius((uint32_t)(m0 + i));
+}
+
+CWQO_API void cwqo_bm_sincos_table(uint32_t m0, int64_t count, float* s, float* c) {
+#ifdef _OPENMP
+#pragma omp parallel for schedule(static)
+#endif
+  for (int64_t i = 0; i < count; ++i) cwqo_bm_sincos((uint32_t)(m0 + i), &s[i], &c[i]);
+}
+
+CWQO_API void cwqo_logf_table(const float* x, int64_t n, float* out) {
+#ifdef _OPENMP
+#pragma omp parallel for schedule(static)
+#endif
+  for (int64_t i = 0; i < n; ++i) out[i] = logf(x[i]);
+}

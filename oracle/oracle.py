@@ -1,0 +1,221 @@
+"""ctypes wrapper of the CPU oracle (oracle/cwq_oracle.c).
+
+TEST INFRASTRUCTURE ONLY -- imported by tests/, __graft_entry__.smoke() and
+bench.py's cpu_baseline leg, as the checker / the reported CPU baseline.  The
+product package never imports this module.  Parity vs the TF reference is
+unpinned beyond the pins listed in cwq_oracle.c's header.
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(HERE)
+LIB = os.path.join(HERE, "libcwq_oracle.so")
+
+_lib = None
+
+
+def build(force=False):
+    src = os.path.join(HERE, "cwq_oracle.c")
+    if force or not os.path.exists(LIB) or os.path.getmtime(LIB) < os.path.getmtime(src):
+        subprocess.check_call(["make", "-C", REPO, "oracle/libcwq_oracle.so"],
+                              stdout=subprocess.DEVNULL)
+    return LIB
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        build()
+        L = ctypes.CDLL(LIB)
+        vp, i64, i32, f32, f64, ci = (ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32,
+                                      ctypes.c_float, ctypes.c_double, ctypes.c_int)
+        sig = {
+            "cwqo_philox4x32_10": (None, [vp, vp, vp]),
+            "cwqo_generate_key": (None, [i32, i32, vp, vp]),
+            "cwqo_stateless_normal": (None, [i32, i32, i64, vp]),
+            "cwqo_stateless_normal_sample": (None, [vp, vp, i64, i64, i32, vp]),
+            "cwqo_bm_radius": (f32, [ctypes.c_uint32]),
+            "cwqo_bm_radius_table": (None, [ctypes.c_uint32, i64, vp]),
+            "cwqo_bm_sincos_table": (None, [ctypes.c_uint32, i64, vp, vp]),
+            "cwqo_logf_table": (None, [vp, i64, vp]),
+            "cwqo_log_normalization": (f32, [f32]),
+            "cwqo_normal_log_prob": (f32, [f32, f32, f32]),
+            "cwqo_eigen_rowsum": (f32, [vp, i64]),
+            "cwqo_code_greedy_sample": (ci, [vp, vp, vp, vp, i64, ci, ci, i32, f32, vp, vp]),
+            "cwqo_decode_greedy_sample": (ci, [vp, vp, vp, i64, ci, ci, i32, f32, vp]),
+            "cwqo_greedy_encode": (ci, [vp, vp, vp, vp, vp, i64, ci, ci, i32, f32, i64, vp, vp,
+                                        ci]),
+            "cwqo_greedy_decode": (ci, [vp, vp, vp, vp, i64, ci, ci, i32, f32, i64, vp, ci]),
+            "cwqo_standardise": (None, [vp, vp, vp, vp, i64, vp, vp]),
+            "cwqo_kl_normal_normal": (None, [vp, vp, vp, vp, i64, vp]),
+            "cwqo_group_starts": (i64, [vp, i64, i64, f64, vp, i64]),
+            "cwqo_destandardise": (None, [vp, vp, vp, i64, vp]),
+            "cwqo_num_threads": (ci, []),
+        }
+        for name, (res, args) in sig.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def _p(a):
+    return a.ctypes.data_as(ctypes.c_void_p) if a is not None and a.size else None
+
+
+def _f32(a):
+    return np.ascontiguousarray(np.asarray(a, dtype=np.float32).reshape(-1))
+
+
+def philox(ctr, key):
+    c = np.asarray(ctr, dtype=np.uint32)
+    k = np.asarray(key, dtype=np.uint32)
+    out = np.zeros(4, dtype=np.uint32)
+    lib().cwqo_philox4x32_10(_p(c), _p(k), _p(out))
+    return out
+
+
+def generate_key(s0, s1):
+    key = np.zeros(2, dtype=np.uint32)
+    ctr = np.zeros(4, dtype=np.uint32)
+    lib().cwqo_generate_key(int(s0), int(s1), _p(key), _p(ctr))
+    return key, ctr
+
+
+def stateless_normal(s0, s1, n):
+    out = np.empty(int(n), dtype=np.float32)
+    lib().cwqo_stateless_normal(int(s0), int(s1), int(n), _p(out))
+    return out
+
+
+def stateless_normal_sample(loc, scale, num_samples, seed):
+    l, s = _f32(loc), _f32(scale)
+    out = np.empty(int(num_samples) * l.size, dtype=np.float32)
+    lib().cwqo_stateless_normal_sample(_p(l), _p(s), l.size, int(num_samples), int(seed),
+                                       _p(out))
+    return out.reshape(int(num_samples), l.size)
+
+
+def bm_radius_table(m0, count):
+    out = np.empty(int(count), dtype=np.float32)
+    lib().cwqo_bm_radius_table(int(m0), int(count), _p(out))
+    return out
+
+
+def bm_sincos_table(m0, count):
+    s = np.empty(int(count), dtype=np.float32)
+    c = np.empty(int(count), dtype=np.float32)
+    lib().cwqo_bm_sincos_table(int(m0), int(count), _p(s), _p(c))
+    return s, c
+
+
+def logf_table(x):
+    x = _f32(x)
+    out = np.empty_like(x)
+    lib().cwqo_logf_table(_p(x), x.size, _p(out))
+    return out
+
+
+def eigen_rowsum(x):
+    x = _f32(x)
+    return float(lib().cwqo_eigen_rowsum(_p(x), x.size))
+
+
+def code_greedy_sample(t_loc, t_scale, p_loc, p_scale, n_bits_per_step, n_steps, seed, rho=1.):
+    tl, ts, pl, ps = map(_f32, (t_loc, t_scale, p_loc, p_scale))
+    idx = np.zeros(int(n_steps), dtype=np.int32)
+    sample = np.zeros(tl.size, dtype=np.float32)
+    rc = lib().cwqo_code_greedy_sample(_p(tl), _p(ts), _p(pl), _p(ps), tl.size,
+                                       int(n_bits_per_step), int(n_steps), int(seed),
+                                       float(rho), _p(idx), _p(sample))
+    assert rc == 0, rc
+    return idx, sample
+
+
+def decode_greedy_sample(idx, p_loc, p_scale, n_bits_per_step, n_steps, seed, rho=1.):
+    pl, ps = _f32(p_loc), _f32(p_scale)
+    ix = np.ascontiguousarray(np.asarray(idx, dtype=np.int32).reshape(-1))
+    out = np.zeros(pl.size, dtype=np.float32)
+    rc = lib().cwqo_decode_greedy_sample(_p(ix), _p(pl), _p(ps), pl.size, int(n_bits_per_step),
+                                         int(n_steps), int(seed), float(rho), _p(out))
+    assert rc == 0, rc
+    return out
+
+
+def greedy_encode(t_loc, t_scale, p_loc, p_scale, block_off, n_bits_per_step, n_steps, seed,
+                  rho=1., block_id_base=0, nthreads=0):
+    tl, ts, pl, ps = map(_f32, (t_loc, t_scale, p_loc, p_scale))
+    off = np.ascontiguousarray(np.asarray(block_off, dtype=np.int64))
+    nb = off.size - 1
+    idx = np.zeros(nb * int(n_steps), dtype=np.int32)
+    sample = np.zeros(tl.size, dtype=np.float32)
+    rc = lib().cwqo_greedy_encode(_p(tl), _p(ts), _p(pl), _p(ps), _p(off), nb,
+                                  int(n_bits_per_step), int(n_steps), int(seed), float(rho),
+                                  int(block_id_base), _p(idx), _p(sample), int(nthreads))
+    assert rc == 0, rc
+    return idx.reshape(nb, int(n_steps)), sample
+
+
+def greedy_decode(idx, p_loc, p_scale, block_off, n_bits_per_step, n_steps, seed, rho=1.,
+                  block_id_base=0, nthreads=0):
+    pl, ps = _f32(p_loc), _f32(p_scale)
+    off = np.ascontiguousarray(np.asarray(block_off, dtype=np.int64))
+    ix = np.ascontiguousarray(np.asarray(idx, dtype=np.int32).reshape(-1))
+    nb = off.size - 1
+    out = np.zeros(pl.size, dtype=np.float32)
+    rc = lib().cwqo_greedy_decode(_p(ix), _p(pl), _p(ps), _p(off), nb, int(n_bits_per_step),
+                                  int(n_steps), int(seed), float(rho), int(block_id_base),
+                                  _p(out), int(nthreads))
+    assert rc == 0, rc
+    return out
+
+
+def standardise(q_loc, q_scale, p_loc, p_scale):
+    ql, qs, pl, ps = map(_f32, (q_loc, q_scale, p_loc, p_scale))
+    tl, ts = np.empty_like(ql), np.empty_like(ql)
+    lib().cwqo_standardise(_p(ql), _p(qs), _p(pl), _p(ps), ql.size, _p(tl), _p(ts))
+    return tl, ts
+
+
+def kl_normal_normal(q_loc, q_scale, p_loc, p_scale):
+    ql, qs, pl, ps = map(_f32, (q_loc, q_scale, p_loc, p_scale))
+    out = np.empty_like(ql)
+    lib().cwqo_kl_normal_normal(_p(ql), _p(qs), _p(pl), _p(ps), ql.size, _p(out))
+    return out
+
+
+def group_starts(kl, n_bits_per_group, size_threshold):
+    k = _f32(kl)
+    cap = k.size + 2
+    st = np.empty(cap, dtype=np.int64)
+    n = lib().cwqo_group_starts(_p(k), k.size, int(size_threshold),
+                                float(n_bits_per_group * np.log(2) - 1), _p(st), cap)
+    assert n > 0
+    return [int(v) for v in st[:n]]
+
+
+def destandardise(sample, p_loc, p_scale):
+    s, pl, ps = map(_f32, (sample, p_loc, p_scale))
+    out = np.empty_like(s)
+    lib().cwqo_destandardise(_p(s), _p(pl), _p(ps), s.size, _p(out))
+    return out
+
+
+def code_grouped_greedy_sample(q_loc, q_scale, p_loc, p_scale, n_steps, n_bits_per_step, seed,
+                               size_threshold, rho=1., nthreads=0):
+    """Whole grouped pipeline (coded_greedy_sampler.py:170-296) on the CPU.
+
+    Returns (sample [D], indices [G, n_steps], starts list).
+    """
+    tl, ts = standardise(q_loc, q_scale, p_loc, p_scale)
+    kl = kl_normal_normal(q_loc, q_scale, p_loc, p_scale)
+    starts = group_starts(kl, n_bits_per_step * n_steps, size_threshold)
+    D = tl.size
+    idx, samp = greedy_encode(tl, ts, np.zeros(D, np.float32), np.ones(D, np.float32), starts,
+                              n_bits_per_step, n_steps, seed, rho, 0, nthreads)
+    return destandardise(samp, p_loc, p_scale), idx, starts

@@ -1,0 +1,271 @@
+"""GPU parity tests: libcwq.so (gfx950 kernels) against the CPU oracle.
+
+Bar: bit-exact.  Indices are compared as integers; samples as float32 bit
+patterns (the north star allows 1e-5 on samples; we require equality).
+The oracle itself is pinned as described in oracle/cwq_oracle.c (Random123
+KATs, glibc libm, reference bit-string examples); parity against TensorFlow
+is unpinned (the reference cannot run here).
+"""
+import hashlib
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import GOLDEN
+
+pytestmark = pytest.mark.gpu
+
+N23 = 1 << 23
+
+
+@pytest.fixture(scope="module")
+def cwq(cwqlib):
+    assert torch.cuda.is_available(), "GPU tests need a ROCm device"
+    import compression_without_quantization_amd as C
+    return C
+
+
+def _u32(a):
+    return np.ascontiguousarray(np.asarray(a, np.float32)).view(np.uint32)
+
+
+def _assert_bits_equal(got, want, what):
+    g, w = _u32(got), _u32(want)
+    bad = np.nonzero(g != w)[0]
+    assert bad.size == 0, f"{what}: {bad.size} of {w.size} differ, first at {bad[:8]}"
+
+
+# ---------------------------------------------------------------------------
+# transcendentals: device restatement vs host glibc, full 2^23 domains
+# ---------------------------------------------------------------------------
+def test_device_box_muller_exhaustive(cwq, cwqlib, oracle):
+    dev = torch.device("cuda")
+    rad = torch.empty(N23, dtype=torch.float32, device=dev)
+    sn = torch.empty_like(rad)
+    cs = torch.empty_like(rad)
+    rc = cwqlib.cwq_selftest_bm_tables(0, N23, rad.data_ptr(), sn.data_ptr(), cs.data_ptr(),
+                                       torch.cuda.current_stream().cuda_stream)
+    assert rc == 0
+    torch.cuda.synchronize()
+    _assert_bits_equal(rad.cpu().numpy(), oracle.bm_radius_table(0, N23), "radius")
+    ws, wc = oracle.bm_sincos_table(0, N23)
+    _assert_bits_equal(sn.cpu().numpy(), ws, "sin")
+    _assert_bits_equal(cs.cpu().numpy(), wc, "cos")
+    t = json.load(open(os.path.join(GOLDEN, "bm_tables.json")))
+    assert hashlib.sha256(rad.cpu().numpy().tobytes()).hexdigest() == t["radius_sha256"]
+
+
+def test_device_logf_all_positive_floats_strided(cwq, cwqlib, oracle):
+    # every 61st positive float (35M values incl. subnormals) + specials
+    bits = np.arange(0, 0x7f800001, 61, dtype=np.uint32)
+    x = np.concatenate([bits.view(np.float32),
+                        np.array([0, 1, np.inf, -1, -0.0, np.nan, 1e-45], np.float32)])
+    want = oracle.logf_table(x)
+    xd = torch.from_numpy(x).cuda()
+    out = torch.empty_like(xd)
+    assert cwqlib.cwq_selftest_logf(xd.data_ptr(), x.size, out.data_ptr(),
+                                    torch.cuda.current_stream().cuda_stream) == 0
+    got = out.cpu().numpy()
+    nan = np.isnan(want) & np.isnan(got)
+    _assert_bits_equal(got[~nan], want[~nan], "logf")
+
+
+# ---------------------------------------------------------------------------
+# RNG (misc.py:3-17)
+# ---------------------------------------------------------------------------
+@pytest.mark.parametrize("d,n,seed", [(1, 33, 42000), (7, 1001, -5), (32, 65536, 123457),
+                                      (13, 4097, 2147483647)])
+def test_stateless_normal_sample(cwq, oracle, d, n, seed):
+    rng = np.random.default_rng(d)
+    loc = rng.standard_normal(d).astype(np.float32)
+    scale = rng.uniform(0.1, 3, d).astype(np.float32)
+    got = cwq.stateless_normal_sample(loc, scale, n, seed)
+    want = oracle.stateless_normal_sample(loc, scale, n, seed)
+    _assert_bits_equal(got, want, "stateless_normal_sample")
+
+
+# ---------------------------------------------------------------------------
+# coder vs golden fixtures
+# ---------------------------------------------------------------------------
+GOLDEN_CASES = ["oracle_c1.npz", "oracle_c4_slice.npz", "oracle_multistep.npz",
+                "oracle_odd_d.npz", "oracle_c5_slice.npz"]
+
+
+@pytest.mark.parametrize("name", GOLDEN_CASES)
+def test_encode_decode_golden(cwq, golden, name):
+    g = golden(name)
+    off = g["block_off"]
+    args = (int(g["n_bits"]), int(g["n_steps"]), int(g["seed"]))
+    kw = dict(rho=float(g["rho"]), block_id_base=int(g["block_id_base"]))
+    idx, sample = cwq.encode_blocks(g["t_loc"], g["t_scale"], g["p_loc"], g["p_scale"], *args,
+                                    block_off=off, **kw)
+    assert np.array_equal(idx.cpu().numpy(), g["idx"])
+    _assert_bits_equal(sample.cpu().numpy(), g["sample"], name + " sample")
+    d = np.diff(off)
+    if (d == d[0]).all():  # uniform entry point too
+        idx2, sample2 = cwq.encode_blocks(g["t_loc"], g["t_scale"], g["p_loc"], g["p_scale"],
+                                          *args, block_dim=int(d[0]), **kw)
+        assert np.array_equal(idx2.cpu().numpy(), g["idx"])
+        _assert_bits_equal(sample2.cpu().numpy(), g["sample"], name + " uniform")
+    dec = cwq.decode_blocks(g["idx"], g["p_loc"], g["p_scale"], *args, block_off=off, **kw)
+    _assert_bits_equal(dec.cpu().numpy(), g["sample"], name + " decode")
+
+
+# ---------------------------------------------------------------------------
+# coder vs oracle on random configurations (edge cases of the reference)
+# ---------------------------------------------------------------------------
+CASES = [
+    # nb, d, bits, n_steps, rho, seed, base
+    (5, 1, 0, 1, 1.0, 42, 0),        # 2^0 = one candidate
+    (9, 3, 1, 2, 1.0, -3, 7),        # odd d, tiny N, negative seed
+    (4, 8, 4, 1, 1.0, 42, 0),        # C1 shape
+    (3, 5, 10, 4, 0.7, 99, 2),       # multi-step, rho
+    (17, 32, 8, 1, 1.0, 2147483, 0),  # 1000*seed wraps int32
+    (2, 33, 12, 2, 1.3, 5, 0),       # d > 32, Eigen tail, split tiles
+    (6, 12, 9, 1, 1.0, 0, 123),
+    (1, 64, 14, 1, 1.0, 42, 0),
+]
+
+
+@pytest.mark.parametrize("case", CASES)
+def test_encode_vs_oracle(cwq, oracle, case):
+    nb, d, bits, n_steps, rho, seed, base = case
+    from compression_without_quantization_amd.synthetic import make_blocks
+    b = make_blocks(nb, d, max(bits, 2), seed=1000 + nb * d + bits)
+    tl, ts, pl, ps = (b[k].reshape(-1) for k in ("post_loc", "post_scale", "prior_loc",
+                                                 "prior_scale"))
+    off = np.arange(nb + 1) * d
+    wi, ws = oracle.greedy_encode(tl, ts, pl, ps, off, bits, n_steps, seed, rho, base)
+    gi, gs = cwq.encode_blocks(tl, ts, pl, ps, bits, n_steps, seed, rho=rho, block_off=off,
+                               block_id_base=base)
+    assert np.array_equal(gi.cpu().numpy(), wi)
+    _assert_bits_equal(gs.cpu().numpy(), ws, f"sample {case}")
+    dec = cwq.decode_blocks(wi, pl, ps, bits, n_steps, seed, rho=rho, block_off=off,
+                            block_id_base=base)
+    _assert_bits_equal(dec.cpu().numpy(), ws, f"decode {case}")
+
+
+def test_ragged_blocks_with_empty_groups(cwq, oracle):
+    rng = np.random.default_rng(4)
+    sizes = [0, 3, 1, 0, 17, 8, 5, 0, 40, 2]
+    off = np.concatenate([[0], np.cumsum(sizes)])
+    D = int(off[-1])
+    tl = rng.standard_normal(D).astype(np.float32)
+    ts = rng.uniform(0.2, 1.0, D).astype(np.float32)
+    pl = np.zeros(D, np.float32)
+    ps = np.ones(D, np.float32)
+    wi, ws = oracle.greedy_encode(tl, ts, pl, ps, off, 8, 1, 42)
+    gi, gs = cwq.encode_blocks(tl, ts, pl, ps, 8, 1, 42, block_off=off)
+    assert np.array_equal(gi.cpu().numpy(), wi)
+    assert (wi[np.array(sizes) == 0] == 0).all()  # empty group -> index 0
+    _assert_bits_equal(gs.cpu().numpy(), ws, "ragged")
+
+
+# ---------------------------------------------------------------------------
+# reference surface
+# ---------------------------------------------------------------------------
+def test_code_greedy_sample_api(cwq, oracle):
+    rng = np.random.default_rng(8)
+    d = 11
+    t_loc = rng.standard_normal(d).astype(np.float32)
+    t_scale = rng.uniform(0.3, 0.9, d).astype(np.float32)
+    p_loc = (0.1 * rng.standard_normal(d)).astype(np.float32)
+    p_scale = rng.uniform(0.8, 1.2, d).astype(np.float32)
+    best, code = cwq.code_greedy_sample(t_loc, t_scale, p_loc, p_scale, 7, 3, 17)
+    wi, ws = oracle.code_greedy_sample(t_loc, t_scale, p_loc, p_scale, 7, 3, 17)
+    assert code == ''.join(cwq.to_bit_string(int(i), 7) for i in wi)
+    _assert_bits_equal(best, ws, "code_greedy_sample")
+    dec = cwq.decode_greedy_sample(code, p_loc, p_scale, 7, 3, 17)
+    _assert_bits_equal(dec, ws, "decode_greedy_sample")
+    # torch in -> torch out, same values
+    tb, tcode = cwq.code_greedy_sample(*(torch.from_numpy(a).cuda() for a in
+                                         (t_loc, t_scale, p_loc, p_scale)), 7, 3, 17)
+    assert isinstance(tb, torch.Tensor) and tb.is_cuda and tcode == code
+
+
+def test_encode_decode_convenience(cwq, oracle):
+    from compression_without_quantization_amd.synthetic import make_blocks
+    b = make_blocks(20, 16, 10)
+    idx, samp = cwq.encode(b["prior_loc"], b["prior_scale"], b["post_loc"], b["post_scale"],
+                           42, 10)
+    assert idx.shape == (20,) and samp.shape == (20, 16)
+    off = np.arange(21) * 16
+    wi, ws = oracle.greedy_encode(b["post_loc"], b["post_scale"], b["prior_loc"],
+                                  b["prior_scale"], off, 10, 1, 42)
+    assert np.array_equal(idx, wi[:, 0])
+    _assert_bits_equal(samp.reshape(-1), ws, "encode()")
+    bitcode = cwq.indices_to_bitcode(idx, 10)
+    for arg in (idx, bitcode):
+        dec = cwq.decode(arg, b["prior_loc"], b["prior_scale"], 42, 10)
+        _assert_bits_equal(dec.reshape(-1), ws, "decode()")
+
+
+def test_grouped_golden(cwq, golden):
+    g = golden("oracle_grouped.npz")
+    cwq.coded_greedy_sampler.VERBOSE = False
+    target = cwq.Normal(g["q_loc"], g["q_scale"])
+    proposal = cwq.Normal(g["p_loc"], g["p_scale"])
+    sample, bitcode, starts = cwq.code_grouped_greedy_sample(None, target, proposal, 1, 8, 42)
+    assert starts == [int(v) for v in g["starts"]]
+    assert bitcode == cwq.indices_to_bitcode(g["idx"], 8)
+    _assert_bits_equal(sample, g["sample"], "grouped sample")
+    dec = cwq.decode_grouped_greedy_sample(None, bitcode, starts, proposal, 8, 1, 42)
+    _assert_bits_equal(dec, g["sample"], "grouped decode")
+    assert starts[-1] == g["p_loc"].size  # caller's list not mutated
+
+
+def test_grouped_dtype_errors(cwq):
+    t = cwq.Normal(np.zeros(4, np.float64), np.ones(4, np.float64))
+    p = cwq.Normal(np.zeros(4, np.float32), np.ones(4, np.float32))
+    with pytest.raises(Exception, match="Target datatype must be float32!"):
+        cwq.code_grouped_greedy_sample(None, t, p, 1, 8, 42)
+    with pytest.raises(Exception, match="Proposal datatype must be float32!"):
+        cwq.code_grouped_greedy_sample(None, p, t, 1, 8, 42)
+    with pytest.raises(Exception, match="Proposal datatype must be float32!"):
+        cwq.decode_grouped_greedy_sample(None, "0" * 8, [0], t, 8, 1, 42)
+
+
+# ---------------------------------------------------------------------------
+# full-size configurations: oracle on a sample + size-independent properties
+# ---------------------------------------------------------------------------
+def test_c2_image_grouped_full(cwq, oracle):
+    """C2: one 512x768 image's level-1 latents (196,608 dims) at 8 bits/group."""
+    from compression_without_quantization_amd.synthetic import make_latents
+    q_loc, q_scale, p_loc, p_scale = make_latents(32 * 48 * 128, seed=5)
+    cwq.coded_greedy_sampler.VERBOSE = False
+    sample, bitcode, starts = cwq.code_grouped_greedy_sample(
+        None, cwq.Normal(q_loc, q_scale), cwq.Normal(p_loc, p_scale), 1, 8, 42)
+    ws, wi, wst = oracle.code_grouped_greedy_sample(q_loc, q_scale, p_loc, p_scale, 1, 8, 42,
+                                                    cwq.group_size_threshold(12))
+    assert starts == wst
+    assert bitcode == cwq.indices_to_bitcode(wi, 8)
+    _assert_bits_equal(sample, ws, "C2 sample")
+    dec = cwq.decode_grouped_greedy_sample(None, bitcode, starts, cwq.Normal(p_loc, p_scale),
+                                           8, 1, 42)
+    _assert_bits_equal(dec, ws, "C2 decode")
+
+
+def test_c4_full_size_roundtrip_and_sample(cwq, oracle):
+    """C4: 10^6 blocks x d=32 at 16 bits.  Round trip on all blocks; oracle on 48."""
+    from compression_without_quantization_amd.synthetic import make_blocks
+    nb, d, bits = 1_000_000, 32, 16
+    b = make_blocks(nb, d, bits)
+    dev = torch.device("cuda")
+    t = {k: torch.from_numpy(v.reshape(-1)).to(dev) for k, v in b.items()}
+    idx, sample = cwq.encode_blocks(t["post_loc"], t["post_scale"], t["prior_loc"],
+                                    t["prior_scale"], bits, 1, 42, block_dim=d)
+    dec = cwq.decode_blocks(idx, t["prior_loc"], t["prior_scale"], bits, 1, 42, block_dim=d)
+    assert torch.equal(dec.view(torch.int32), sample.view(torch.int32))
+    idx_h = idx.cpu().numpy().reshape(-1)
+    assert idx_h.min() >= 0 and idx_h.max() < (1 << bits)
+    pick = np.random.default_rng(0).choice(nb, 48, replace=False)
+    for g in pick:
+        s = slice(g * d, (g + 1) * d)
+        wi, ws = oracle.code_greedy_sample(b["post_loc"][g], b["post_scale"][g],
+                                           b["prior_loc"][g], b["prior_scale"][g], bits, 1,
+                                           42 + int(g))
+        assert wi[0] == idx_h[g], f"block {g}"
+        _assert_bits_equal(sample[s].cpu().numpy(), ws, f"block {g}")
