@@ -17,6 +17,7 @@ namespace {
 thread_local char g_err[512] = {0};
 thread_local void* g_ev_start = nullptr;
 thread_local void* g_ev_stop = nullptr;
+thread_local int g_prune = 1;
 
 int fail(int code, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
 int fail(int code, const char* fmt, ...) {
@@ -108,6 +109,7 @@ int encode_impl(const float* t_loc, const float* t_scale, const float* p_loc,
   a.n_cand = (int64_t)1 << n_bits;
   choose_tiling(nb, a.n_cand, &a.tiles_per_block, &a.cand_per_tile);
   a.n_steps = n_steps;
+  a.prune = g_prune;
   a.seed = seed;
   a.rho = rho;
   a.block_id_base = block_id_base;
@@ -271,6 +273,11 @@ int cwq_profile_set_eval_events(void* start_event, void* stop_event) {
     return fail(CWQ_ERR_INVALID, "give both events or neither");
   g_ev_start = start_event;
   g_ev_stop = stop_event;
+  return ok();
+}
+
+int cwq_set_pruning(int enable) {
+  g_prune = enable ? 1 : 0;
   return ok();
 }
 

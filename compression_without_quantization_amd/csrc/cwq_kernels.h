@@ -18,6 +18,7 @@ struct EncodeArgs {
   int64_t tiles_per_block;
   int64_t cand_per_tile;     // multiple of 256
   int n_steps;
+  int prune;                 // 1: use the pruned kernel where it applies
   int32_t seed;
   float rho;
   int64_t block_id_base;

@@ -170,6 +170,211 @@ __global__ void __launch_bounds__(256) k_encode_eval(
 }
 
 // ---------------------------------------------------------------------------
+// Pruned encoder for uniform blocks, D % 8 == 0, D <= 64 (the C1/C4/C5 shapes).
+//
+// Same result as k_encode_eval, less work: a candidate whose log-density can
+// no longer reach the best value already found in this tile is dropped before
+// its remaining dims are generated.  Rows are still evaluated in natural dim
+// order, one Philox block (4 dims) per step, so the lane's Eigen partial sums
+// stay exact and a candidate that survives all D dims yields its exact value.
+//
+// Drop rule ("pruning bound"): after the first 4q dims with float
+// running sum s, candidate n is dropped iff
+//     s + 2^-14 |s| + B_q  <  tau
+// where tau is the exact value of a candidate already completed in this tile
+// and B_q >= sum_{j>=4q} f(M_j) + 2^-14 K_q (+ float evaluation margin), with
+// M_j = -c_j the maximum of the float log-density of dim j, f(x) = x+g|x|,
+// g >= gamma_{D-1} + gamma_{4q}.  This bounds the float Eigen-order sum of
+// every completion of the row from above, so a dropped candidate's value is
+// strictly below tau: it can be neither the argmax nor a tie.
+//
+// Lanes keep one candidate each and refill from a per-wave counter with
+// ballot/mbcnt when theirs completes or is dropped, so waves stay full even
+// though candidates stop after different numbers of dims.
+// ---------------------------------------------------------------------------
+constexpr float kPruneC1 = 0x1p-14f;
+
+__device__ __forceinline__ uint32_t ord_f32(float v) {
+  const uint32_t b = f2u(v);
+  return (b & 0x80000000u) ? ~b : (b | 0x80000000u);
+}
+__device__ __forceinline__ float unord_f32(uint32_t o) {
+  return u2f((o & 0x80000000u) ? (o & 0x7fffffffu) : ~o);
+}
+__device__ __forceinline__ float wave_max_f32(float v) {
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) v = fmaxf(v, __shfl_xor(v, off, 64));
+  return v;
+}
+__device__ __forceinline__ float round_up_f32(double b) {
+  if (!(b == b) || b > 3.0e38 || b < -3.0e38) return __builtin_inff();  // never prune
+  float f = (float)b;
+  if ((double)f < b) {
+    const uint32_t u = f2u(f);
+    f = (f >= 0.0f) ? u2f(f == 0.0f ? 1u : u + 1u) : u2f(u - 1u);
+  }
+  return f;
+}
+
+template <bool STEP0>
+__device__ __forceinline__ float cand_logprob(float z, float ls, float ss, float mu, float sg,
+                                              float cc, float bb) {
+  float s = ss * z;  // misc.py:14
+  s = ls + s;        // misc.py:15
+  const float tv = STEP0 ? s : bb + s;
+  return log_prob(tv, mu, sg, cc);
+}
+
+template <int D, bool STEP0>
+__global__ void __launch_bounds__(256) k_encode_prune(
+    const float* __restrict__ t_loc, const float* __restrict__ t_scale,
+    const float* __restrict__ loc_s, const float* __restrict__ scale_s,
+    const float* __restrict__ lognorm, const float* __restrict__ best, int64_t ntiles,
+    int64_t tiles_per_block, int64_t cand_per_tile, int64_t n_cand, int32_t seed,
+    int64_t block_id_base, int32_t step, unsigned long long* __restrict__ keys) {
+  static_assert(D % 8 == 0 && D >= 8 && D <= 64, "pruned path: D % 8 == 0, D <= 64");
+  constexpr int G = D / 4;
+  constexpr int NF = STEP0 ? 5 : 6;
+  __shared__ double logtab[32];
+  __shared__ float4 cst[G * NF];
+  __shared__ float bnd[G + 1];
+  __shared__ uint32_t tau_ord;
+  __shared__ unsigned long long wkey[4];
+  fill_logtab(logtab);
+  const uint32_t wv = wave_id();
+  const uint32_t lane = threadIdx.x & 63u;
+
+  for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const int64_t g = tile / tiles_per_block;
+    const int64_t tt = tile - g * tiles_per_block;
+    const int64_t off = g * D;
+    const int64_t n0 = tt * cand_per_tile;
+    const int64_t n1 = (n0 + cand_per_tile < n_cand) ? n0 + cand_per_tile : n_cand;
+    const PhiloxStream st =
+        generate_key(step_seed(block_seed(seed, block_id_base + g), step), 42);
+
+    // stage this block's per-dim constants: cst[q*NF + f] = field f of dims 4q..4q+3
+    if (threadIdx.x < D) {
+      const int j = threadIdx.x, q = j >> 2, w = j & 3;
+      float* c = reinterpret_cast<float*>(cst);
+      c[(q * NF + 0) * 4 + w] = loc_s[off + j];
+      c[(q * NF + 1) * 4 + w] = scale_s[off + j];
+      c[(q * NF + 2) * 4 + w] = t_loc[off + j];
+      c[(q * NF + 3) * 4 + w] = t_scale[off + j];
+      c[(q * NF + 4) * 4 + w] = lognorm[off + j];
+      if (!STEP0) c[(q * NF + 5) * 4 + w] = best[off + j];
+    }
+    __syncthreads();
+    if (threadIdx.x <= G) {  // thread q computes the drop bound after q groups
+      const int qb = threadIdx.x;
+      const float* c = reinterpret_cast<const float*>(cst);
+      double rf = 0.0, k = 0.0, asum = 0.0;
+#pragma unroll 1
+      for (int j = 0; j < D; ++j) {
+        const double mj = -(double)c[((j >> 2) * NF + 4) * 4 + (j & 3)];  // M_j = -c_j
+        const double aj = __builtin_fabs(mj);
+        asum += aj;
+        if (j >= 4 * qb)
+          rf += mj + 0x1p-17 * aj;
+        else
+          k += aj + mj;
+      }
+      const double b = rf + 0x1p-14 * k + 0x1p-20 * (__builtin_fabs(rf) + asum) + 0x1p-126;
+      bnd[qb] = round_up_f32(b);
+      if (qb == 0) tau_ord = ord_f32(-__builtin_inff());
+    }
+    __syncthreads();
+
+    // this wave's contiguous share of the tile's candidates
+    const int64_t per_wave = (n1 - n0 + 3) / 4;
+    const int64_t w0 = n0 + (int64_t)wv * per_wave;
+    const int64_t w1 = (w0 + per_wave < n1) ? w0 + per_wave : n1;
+    int64_t wnext = w0 + 64;
+    int64_t n = w0 + lane;
+    bool active = n < w1;
+    int q = 0;
+    float s = 0.0f;
+    float pa0 = 0.f, pa1 = 0.f, pa2 = 0.f, pa3 = 0.f;  // p[0..3]
+    float pb0 = 0.f, pb1 = 0.f, pb2 = 0.f, pb3 = 0.f;  // p[4..7]
+    float tau = -__builtin_inff();
+    uint64_t bestk = 0;
+    uint32_t iter = 0;
+
+    while (__ballot(active) != 0ull) {
+      const uint32_t grp = (uint32_t)n * (uint32_t)G + (uint32_t)q;
+      const U4 x = philox10(grp, 0u, st.c2, st.c3, st.k0, st.k1);
+      float z0, z1, z2, z3;
+      box_muller(x.x, x.y, logtab, z0, z1);
+      box_muller(x.z, x.w, logtab, z2, z3);
+      const float4* cq = cst + q * NF;
+      const float4 ls = cq[0], ss = cq[1], mu = cq[2], sg = cq[3], cc = cq[4];
+      const float4 bb = STEP0 ? float4{0.f, 0.f, 0.f, 0.f} : cq[NF - 1];
+      const float L0 = cand_logprob<STEP0>(z0, ls.x, ss.x, mu.x, sg.x, cc.x, bb.x);
+      const float L1 = cand_logprob<STEP0>(z1, ls.y, ss.y, mu.y, sg.y, cc.y, bb.y);
+      const float L2 = cand_logprob<STEP0>(z2, ls.z, ss.z, mu.z, sg.z, cc.z, bb.z);
+      const float L3 = cand_logprob<STEP0>(z3, ls.w, ss.w, mu.w, sg.w, cc.w, bb.w);
+      // Eigen partials: dim 4q+w feeds p[(4q+w) & 7] = (q odd ? pB : pA)[w]
+      const bool odd = (q & 1) != 0;
+      const float a0 = (odd ? pb0 : pa0) + L0;
+      const float a1 = (odd ? pb1 : pa1) + L1;
+      const float a2 = (odd ? pb2 : pa2) + L2;
+      const float a3 = (odd ? pb3 : pa3) + L3;
+      pa0 = odd ? pa0 : a0;
+      pa1 = odd ? pa1 : a1;
+      pa2 = odd ? pa2 : a2;
+      pa3 = odd ? pa3 : a3;
+      pb0 = odd ? a0 : pb0;
+      pb1 = odd ? a1 : pb1;
+      pb2 = odd ? a2 : pb2;
+      pb3 = odd ? a3 : pb3;
+      s = s + L0;
+      s = s + L1;
+      s = s + L2;
+      s = s + L3;
+      q += 1;
+      const bool complete = (q == G);
+      const float lhs = (s + __builtin_fabsf(s) * kPruneC1) + bnd[q];
+      const bool prune = !complete && (lhs < tau);
+      if (complete && active) {
+        const float q0 = pa0 + pb0, q1 = pa1 + pb1, q2 = pa2 + pb2, q3 = pa3 + pb3;
+        const float v = 0.0f + ((q0 + q2) + (q1 + q3));
+        const uint64_t k = argmax_key(v, (uint32_t)n);
+        bestk = k > bestk ? k : bestk;
+        tau = fmaxf(tau, v);
+      }
+      const bool done = complete || prune || !active;
+      const uint64_t m = __ballot(done);
+      const uint32_t rank =
+          __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+      if (done) {
+        n = wnext + rank;
+        q = 0;
+        s = 0.0f;
+        pa0 = pa1 = pa2 = pa3 = 0.f;
+        pb0 = pb1 = pb2 = pb3 = 0.f;
+      }
+      wnext += (int64_t)__builtin_popcountll(m);
+      active = n < w1;
+      if (((++iter) & 15u) == 0u) {  // share tau across the workgroup's waves
+        const float tm = wave_max_f32(tau);
+        if (lane == 0) atomicMax(&tau_ord, ord_f32(tm));
+        tau = fmaxf(tau, unord_f32(__atomic_load_n(&tau_ord, __ATOMIC_RELAXED)));
+      }
+    }
+
+    bestk = wave_max_u64(bestk);
+    if (lane == 0) wkey[wv] = bestk;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      uint64_t mk = wkey[0];
+      for (int i = 1; i < 4; ++i) mk = wkey[i] > mk ? wkey[i] : mk;
+      if (mk) atomicMax(&keys[g], (unsigned long long)mk);
+    }
+    __syncthreads();
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Encoder, end of a step: index -> out_idx; best += winning candidate (:63).
 // One wave per block.
 // ---------------------------------------------------------------------------
@@ -369,8 +574,33 @@ static void launch_eval_t(const EncodeArgs& a, int step, hipStream_t stream) {
                      a.block_id_base, step, a.keys);
 }
 
+template <int D, bool STEP0>
+static void launch_prune_t(const EncodeArgs& a, int step, hipStream_t stream) {
+  const int64_t ntiles = a.nb * a.tiles_per_block;
+  const unsigned grid = (unsigned)(ntiles < (1LL << 30) ? ntiles : (1LL << 30));
+  hipLaunchKernelGGL((k_encode_prune<D, STEP0>), dim3(grid), dim3(256), 0, stream, a.t_loc,
+                     a.t_scale, a.loc_s, a.scale_s, a.lognorm, a.out_sample, ntiles,
+                     a.tiles_per_block, a.cand_per_tile, a.n_cand, a.seed, a.block_id_base, step,
+                     a.keys);
+}
+
 template <bool STEP0>
 static void launch_eval_dc(const EncodeArgs& a, int step, hipStream_t stream) {
+  // pruned path: uniform D % 8 == 0, D <= 64, Philox block index n*D/4 < 2^32
+  if (a.block_off == nullptr && a.prune && a.ud % 8 == 0 && a.ud >= 8 && a.ud <= 64 &&
+      a.n_cand * (a.ud / 4) <= (1LL << 32)) {
+    switch (a.ud) {
+      case 8: return launch_prune_t<8, STEP0>(a, step, stream);
+      case 16: return launch_prune_t<16, STEP0>(a, step, stream);
+      case 24: return launch_prune_t<24, STEP0>(a, step, stream);
+      case 32: return launch_prune_t<32, STEP0>(a, step, stream);
+      case 40: return launch_prune_t<40, STEP0>(a, step, stream);
+      case 48: return launch_prune_t<48, STEP0>(a, step, stream);
+      case 56: return launch_prune_t<56, STEP0>(a, step, stream);
+      case 64: return launch_prune_t<64, STEP0>(a, step, stream);
+      default: break;
+    }
+  }
   if (a.block_off == nullptr) {
     switch (a.ud) {
       case 8: return launch_eval_t<8, STEP0>(a, step, stream);

@@ -147,6 +147,11 @@ int cwq_selftest_logf(const float* x, int64_t n, float* out, void* stream);
  * one, so the caller can time the dominant kernel alone.  NULL, NULL clears. */
 int cwq_profile_set_eval_events(void* start_event, void* stop_event);
 
+/* Candidate pruning (DESIGN.md "pruning bound") is on by default for uniform
+ * blocks with d % 8 == 0, d <= 64; it never changes results.  0 turns it off
+ * for this host thread (A/B timing and tests). */
+int cwq_set_pruning(int enable);
+
 #ifdef __cplusplus
 }
 #endif

@@ -269,3 +269,64 @@ def test_c4_full_size_roundtrip_and_sample(cwq, oracle):
                                            42 + int(g))
         assert wi[0] == idx_h[g], f"block {g}"
         _assert_bits_equal(sample[s].cpu().numpy(), ws, f"block {g}")
+
+
+# ---------------------------------------------------------------------------
+# pruned encoder (uniform d % 8 == 0): same results as the unpruned kernel and
+# the oracle, including adversarial inputs where the bound is tight or useless
+# ---------------------------------------------------------------------------
+def _uniform_encode(cwq, cwqlib, tl, ts, pl, ps, d, bits, n_steps, seed, rho, prune):
+    cwqlib.cwq_set_pruning(1 if prune else 0)
+    try:
+        i, s = cwq.encode_blocks(tl, ts, pl, ps, bits, n_steps, seed, rho=rho, block_dim=d)
+        torch.cuda.synchronize()
+        return i.cpu().numpy(), s.cpu().numpy()
+    finally:
+        cwqlib.cwq_set_pruning(1)
+
+
+@pytest.mark.parametrize("d,bits,n_steps,nb,rho", [
+    (8, 4, 1, 64, 1.0), (8, 12, 1, 16, 1.0), (16, 14, 1, 8, 1.0), (24, 10, 2, 12, 1.0),
+    (32, 16, 1, 6, 1.0), (32, 9, 3, 10, 0.8), (40, 11, 1, 8, 1.0), (64, 13, 1, 4, 1.0),
+    (16, 20, 1, 1, 1.0)])
+def test_pruned_matches_unpruned_and_oracle(cwq, cwqlib, oracle, d, bits, n_steps, nb, rho):
+    from compression_without_quantization_amd.synthetic import make_blocks
+    b = make_blocks(nb, d, bits, seed=77 + d + bits)
+    tl, ts, pl, ps = (b[k].reshape(-1) for k in ("post_loc", "post_scale", "prior_loc",
+                                                 "prior_scale"))
+    i1, s1 = _uniform_encode(cwq, cwqlib, tl, ts, pl, ps, d, bits, n_steps, 42, rho, True)
+    i0, s0 = _uniform_encode(cwq, cwqlib, tl, ts, pl, ps, d, bits, n_steps, 42, rho, False)
+    assert np.array_equal(i1, i0)
+    _assert_bits_equal(s1, s0, "pruned vs unpruned")
+    if (1 << bits) * d * nb <= (1 << 22):
+        wi, ws = oracle.greedy_encode(tl, ts, pl, ps, np.arange(nb + 1) * d, bits, n_steps, 42,
+                                      rho)
+        assert np.array_equal(i1, wi)
+        _assert_bits_equal(s1, ws, "pruned vs oracle")
+
+
+@pytest.mark.parametrize("kind", ["posterior_is_prior", "tiny_scales", "huge_scales",
+                                  "inf_scale", "zero_scale", "mixed_sign_norm"])
+def test_pruned_adversarial(cwq, cwqlib, oracle, kind):
+    rng = np.random.default_rng(hash(kind) % 1000)
+    nb, d, bits = 6, 16, 10
+    pl = rng.standard_normal(nb * d).astype(np.float32)
+    ps = rng.uniform(0.5, 2, nb * d).astype(np.float32)
+    tl = pl.copy()
+    ts = ps.copy()
+    if kind == "tiny_scales":      # huge deficits, normaliser M_j >> 0
+        ts = (ps * 1e-6).astype(np.float32)
+        tl = (pl + 0.1 * ps * rng.standard_normal(nb * d)).astype(np.float32)
+    elif kind == "huge_scales":    # flat target: everything is a near-tie
+        ts = (ps * 1e6).astype(np.float32)
+    elif kind == "inf_scale":
+        ts[3] = np.inf
+    elif kind == "zero_scale":
+        ts[5] = 0.0
+        tl[5] = pl[5]
+    elif kind == "mixed_sign_norm":  # some c_j < 0 (M_j > 0), some > 0
+        ts = np.where(rng.uniform(size=nb * d) < 0.5, 0.05, 3.0).astype(np.float32)
+    i1, s1 = _uniform_encode(cwq, cwqlib, tl, ts, pl, ps, d, bits, 1, 42, 1.0, True)
+    wi, ws = oracle.greedy_encode(tl, ts, pl, ps, np.arange(nb + 1) * d, bits, 1, 42)
+    assert np.array_equal(i1, wi)
+    _assert_bits_equal(s1, ws, kind)
