@@ -9,7 +9,8 @@ parity tests use blocks of the configured shape:
              sum_j 0.5 (t_loc^2 + t_scale^2 - 1 - 2 ln t_scale) equals K nats
              (K = kl_bits*ln2 - 1, the reference's n_nats_per_group,
              coded_greedy_sampler.py:226; C1 uses K = 4 ln2 exactly);
-             blocks whose RHS is <= 0 are redrawn.
+             blocks whose scale part alone exceeds K get their log-scale
+             deviations shrunk until it takes K/2.
   posterior  post_loc = p_loc + p_scale * t_loc, post_scale = p_scale * t_scale
 
 Generator: numpy PCG64(20261015) unless a seed is given.
@@ -35,14 +36,22 @@ def make_blocks(nb, d, kl_bits, seed=DEFAULT_SEED, exact_kl=False, chunk=1 << 16
         p_scale = rng.uniform(0.5, 2.0, (n, d))
         t_scale = rng.uniform(0.3, 0.9, (n, d))
         m = rng.standard_normal((n, d))
-        while True:
+        rhs = 2 * K - np.sum(t_scale ** 2 - 1 - 2 * np.log(t_scale), axis=1)
+        bad = rhs <= 0
+        if bad.any():
+            # the scale part alone exceeds K (large d, small K): shrink the
+            # log-scale deviations of those blocks so it uses K/2 nats
+            ls = np.log(t_scale[bad])
+            lo = np.zeros(ls.shape[0])
+            hi = np.ones(ls.shape[0])
+            for _ in range(60):
+                lam = 0.5 * (lo + hi)
+                f = np.sum(np.exp(2 * lam[:, None] * ls) - 1 - 2 * lam[:, None] * ls, axis=1)
+                over = f > K
+                hi = np.where(over, lam, hi)
+                lo = np.where(over, lo, lam)
+            t_scale[bad] = np.exp(lo[:, None] * ls)
             rhs = 2 * K - np.sum(t_scale ** 2 - 1 - 2 * np.log(t_scale), axis=1)
-            bad = (rhs <= 0) | (np.sum(m ** 2, axis=1) == 0)
-            if not bad.any():
-                break
-            k = int(bad.sum())
-            t_scale[bad] = rng.uniform(0.3, 0.9, (k, d))
-            m[bad] = rng.standard_normal((k, d))
         alpha = np.sqrt(rhs / np.sum(m ** 2, axis=1))
         t_loc = alpha[:, None] * m
         out["prior_loc"][b0:b0 + n] = p_loc
