@@ -290,6 +290,14 @@ int cwq_selftest_bm_tables(uint32_t m0, int64_t count, float* radius, float* sin
   return ok();
 }
 
+int cwq_selftest_div(const float* a, const float* b, int64_t n, float* out, void* stream) {
+  if (n < 0 || (n > 0 && (!a || !b || !out)))
+    return fail(CWQ_ERR_INVALID, "cwq_selftest_div: bad arguments");
+  hipError_t e = cwq::launch_selftest_div(a, b, n, out, (hipStream_t)stream);
+  if (e != hipSuccess) return hip_fail(e, "cwq_selftest_div");
+  return ok();
+}
+
 int cwq_selftest_logf(const float* x, int64_t n, float* out, void* stream) {
   if (n < 0 || (n > 0 && (!x || !out)))
     return fail(CWQ_ERR_INVALID, "cwq_selftest_logf: bad arguments");

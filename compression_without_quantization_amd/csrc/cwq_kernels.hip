@@ -44,6 +44,99 @@ __device__ __forceinline__ uint64_t wave_max_u64(uint64_t v) {
   return v;
 }
 
+// ---------------------------------------------------------------------------
+// Device-tuned arithmetic.  Same results as the portable restatement in
+// cwq_math.h (the Box-Muller pieces are verified exhaustively on the GPU by
+// tests/test_gpu.py via cwq_selftest_bm_tables), fewer instructions:
+//   * Philox: the two 3-input XORs of a round are one v_bitop3_b32 each.
+//   * sqrt for the Box-Muller radius: the argument -2 logf(u1) lies in
+//     [2.4e-7, 32.3] (normal, finite), so the correctly rounded sqrt is
+//     v_sqrt_f32 plus the two one-ulp corrections, without the denormal
+//     scaling and special-case fixups of the general sequence.
+//   * angle: Uint32ToFloat(x1) = m * 2^-23 exactly, so
+//     RN64(2pi * U) = RN64((2pi * 2^-23) * m) and m converts exactly.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ U4 philox10_dev(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
+                                           uint32_t k0, uint32_t k1) {
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    const uint64_t p0 = (uint64_t)kPhiloxM0 * c0;
+    const uint64_t p1 = (uint64_t)kPhiloxM1 * c2;
+    const uint32_t n0 = __builtin_amdgcn_bitop3_b32((uint32_t)(p1 >> 32), c1, k0, 0x96);
+    const uint32_t n2 = __builtin_amdgcn_bitop3_b32((uint32_t)(p0 >> 32), c3, k1, 0x96);
+    c1 = (uint32_t)p1;
+    c3 = (uint32_t)p0;
+    c0 = n0;
+    c2 = n2;
+    k0 += kPhiloxW0;
+    k1 += kPhiloxW1;
+  }
+  return U4{c0, c1, c2, c3};
+}
+
+__device__ __forceinline__ U4 philox_block_dev(const PhiloxStream& s, uint64_t grp) {
+  return philox10_dev((uint32_t)grp, (uint32_t)(grp >> 32), s.c2, s.c3, s.k0, s.k1);
+}
+
+__device__ __forceinline__ float sqrt_cr_bm(float x) {
+  const float s = __builtin_amdgcn_sqrtf(x);
+  const float sd = u2f(f2u(s) - 1u);
+  const float su = u2f(f2u(s) + 1u);
+  const float rd = __builtin_fmaf(-sd, s, x);
+  const float ru = __builtin_fmaf(-su, s, x);
+  const float t = (rd <= 0.0f) ? sd : s;
+  return (ru > 0.0f) ? su : t;
+}
+
+__device__ __forceinline__ float bm_radius_dev(uint32_t x0, const double* logtab) {
+  float u1 = uint32_to_float(x0);
+  u1 = u1 < 1.0e-7f ? 1.0e-7f : u1;
+  return sqrt_cr_bm(-2.0f * logf_core(u1, logtab));
+}
+
+__device__ __forceinline__ float bm_angle_dev(uint32_t x1) {
+  return (float)((double)(x1 & 0x7fffffu) * 0x1.921fb54442d18p-21);
+}
+
+__device__ __forceinline__ void box_muller_dev(uint32_t x0, uint32_t x1, const double* logtab,
+                                               float& f0, float& f1) {
+  const float u2 = bm_radius_dev(x0, logtab);
+  float s, c;
+  sincosf_pos(bm_angle_dev(x1), s, c);
+  f0 = s * u2;
+  f1 = c * u2;
+}
+
+__device__ __forceinline__ F4 normal4_dev(const PhiloxStream& s, uint64_t grp,
+                                          const double* logtab) {
+  const U4 x = philox_block_dev(s, grp);
+  F4 z;
+  box_muller_dev(x.x, x.y, logtab, z.a, z.b);
+  box_muller_dev(x.z, x.w, logtab, z.c, z.d);
+  return z;
+}
+
+// Correctly rounded a / b for 2^-60 <= |a| <= 2^60 (or a == 0) and
+// 2^-60 <= b <= 2^60, given y = RN(1/b).  q0 = RN(a y) is within 2 ulps;
+// one residual step brings q1 within 1 ulp; with q1 within 1 ulp and y within
+// half an ulp of 1/b, the residual b*q1 - a is exact and the final fused step
+// rounds to RN(a/b) (Markstein's theorem).  The ranges keep
+// every intermediate normal.  Callers route other operands to IEEE division.
+__device__ __forceinline__ float div_rn_markstein(float a, float b, float y) {
+  const float q0 = a * y;
+  const float r0 = __builtin_fmaf(-b, q0, a);
+  const float q1 = __builtin_fmaf(r0, y, q0);
+  const float r1 = __builtin_fmaf(-b, q1, a);
+  return __builtin_fmaf(r1, y, q1);
+}
+__device__ __forceinline__ bool markstein_ok(float a) {
+  const float m = __builtin_fabsf(a);
+  return (m >= 0x1p-60f && m <= 0x1p60f) || m == 0.0f;
+}
+__device__ __forceinline__ bool markstein_ok_den(float b) {
+  return b >= 0x1p-60f && b <= 0x1p60f;
+}
+
 struct BlockSpan {
   int64_t off;
   int64_t d;
@@ -102,7 +195,7 @@ __device__ __forceinline__ float eval_row(const PhiloxStream& st, uint64_t kbase
 
   auto elem = [&](int64_t e) -> float {
     const int w = (align + (int)(e & 3)) & 3;  // wave-uniform
-    if (w == 0 || e == 0) z = normal4(st, (kbase + (uint64_t)e) >> 2, logtab);
+    if (w == 0 || e == 0) z = normal4_dev(st, (kbase + (uint64_t)e) >> 2, logtab);
     const float zz = w == 0 ? z.a : (w == 1 ? z.b : (w == 2 ? z.c : z.d));
     float s = scale_s[e] * zz;  // misc.py:14
     s = loc_s[e] + s;           // misc.py:15
@@ -216,13 +309,17 @@ __device__ __forceinline__ float round_up_f32(double b) {
   return f;
 }
 
+// best + (loc_s + scale_s z) - mu  (misc.py:14-15, coded_greedy_sampler.py:57, TFP _z numerator)
 template <bool STEP0>
-__device__ __forceinline__ float cand_logprob(float z, float ls, float ss, float mu, float sg,
-                                              float cc, float bb) {
+__device__ __forceinline__ float cand_diff(float z, float ls, float ss, float mu, float bb) {
   float s = ss * z;  // misc.py:14
   s = ls + s;        // misc.py:15
   const float tv = STEP0 ? s : bb + s;
-  return log_prob(tv, mu, sg, cc);
+  return tv - mu;
+}
+__device__ __forceinline__ float lp_from_z(float z, float cc) {
+  const float u = -0.5f * (z * z);
+  return u - cc;
 }
 
 template <int D, bool STEP0>
@@ -234,7 +331,7 @@ __global__ void __launch_bounds__(256) k_encode_prune(
     int64_t block_id_base, int32_t step, unsigned long long* __restrict__ keys) {
   static_assert(D % 8 == 0 && D >= 8 && D <= 64, "pruned path: D % 8 == 0, D <= 64");
   constexpr int G = D / 4;
-  constexpr int NF = STEP0 ? 5 : 6;
+  constexpr int NF = STEP0 ? 6 : 7;  // loc_s, scale_s, mu, sigma, c, 1/sigma[, best]
   __shared__ double logtab[32];
   __shared__ float4 cst[G * NF];
   __shared__ float bnd[G + 1];
@@ -254,17 +351,21 @@ __global__ void __launch_bounds__(256) k_encode_prune(
         generate_key(step_seed(block_seed(seed, block_id_base + g), step), 42);
 
     // stage this block's per-dim constants: cst[q*NF + f] = field f of dims 4q..4q+3
+    int den_ok = 1;
     if (threadIdx.x < D) {
       const int j = threadIdx.x, q = j >> 2, w = j & 3;
       float* c = reinterpret_cast<float*>(cst);
+      const float sgj = t_scale[off + j];
       c[(q * NF + 0) * 4 + w] = loc_s[off + j];
       c[(q * NF + 1) * 4 + w] = scale_s[off + j];
       c[(q * NF + 2) * 4 + w] = t_loc[off + j];
-      c[(q * NF + 3) * 4 + w] = t_scale[off + j];
+      c[(q * NF + 3) * 4 + w] = sgj;
       c[(q * NF + 4) * 4 + w] = lognorm[off + j];
-      if (!STEP0) c[(q * NF + 5) * 4 + w] = best[off + j];
+      c[(q * NF + 5) * 4 + w] = 1.0f / sgj;
+      if (!STEP0) c[(q * NF + 6) * 4 + w] = best[off + j];
+      den_ok = markstein_ok_den(sgj) ? 1 : 0;
     }
-    __syncthreads();
+    const bool fastdiv = __syncthreads_and(den_ok) != 0;
     if (threadIdx.x <= G) {  // thread q computes the drop bound after q groups
       const int qb = threadIdx.x;
       const float* c = reinterpret_cast<const float*>(cst);
@@ -302,17 +403,34 @@ __global__ void __launch_bounds__(256) k_encode_prune(
 
     while (__ballot(active) != 0ull) {
       const uint32_t grp = (uint32_t)n * (uint32_t)G + (uint32_t)q;
-      const U4 x = philox10(grp, 0u, st.c2, st.c3, st.k0, st.k1);
+      const U4 x = philox10_dev(grp, 0u, st.c2, st.c3, st.k0, st.k1);
       float z0, z1, z2, z3;
-      box_muller(x.x, x.y, logtab, z0, z1);
-      box_muller(x.z, x.w, logtab, z2, z3);
+      box_muller_dev(x.x, x.y, logtab, z0, z1);
+      box_muller_dev(x.z, x.w, logtab, z2, z3);
       const float4* cq = cst + q * NF;
-      const float4 ls = cq[0], ss = cq[1], mu = cq[2], sg = cq[3], cc = cq[4];
-      const float4 bb = STEP0 ? float4{0.f, 0.f, 0.f, 0.f} : cq[NF - 1];
-      const float L0 = cand_logprob<STEP0>(z0, ls.x, ss.x, mu.x, sg.x, cc.x, bb.x);
-      const float L1 = cand_logprob<STEP0>(z1, ls.y, ss.y, mu.y, sg.y, cc.y, bb.y);
-      const float L2 = cand_logprob<STEP0>(z2, ls.z, ss.z, mu.z, sg.z, cc.z, bb.z);
-      const float L3 = cand_logprob<STEP0>(z3, ls.w, ss.w, mu.w, sg.w, cc.w, bb.w);
+      const float4 ls = cq[0], ss = cq[1], mu = cq[2], sg = cq[3], cc = cq[4], ry = cq[5];
+      const float4 bb = STEP0 ? float4{0.f, 0.f, 0.f, 0.f} : cq[6];
+      const float d0 = cand_diff<STEP0>(z0, ls.x, ss.x, mu.x, bb.x);
+      const float d1 = cand_diff<STEP0>(z1, ls.y, ss.y, mu.y, bb.y);
+      const float d2 = cand_diff<STEP0>(z2, ls.z, ss.z, mu.z, bb.z);
+      const float d3 = cand_diff<STEP0>(z3, ls.w, ss.w, mu.w, bb.w);
+      float y0, y1, y2, y3;  // _z(x) = (x - loc) / scale, correctly rounded
+      if (fastdiv && markstein_ok(d0) && markstein_ok(d1) && markstein_ok(d2) &&
+          markstein_ok(d3)) {
+        y0 = div_rn_markstein(d0, sg.x, ry.x);
+        y1 = div_rn_markstein(d1, sg.y, ry.y);
+        y2 = div_rn_markstein(d2, sg.z, ry.z);
+        y3 = div_rn_markstein(d3, sg.w, ry.w);
+      } else {
+        y0 = d0 / sg.x;
+        y1 = d1 / sg.y;
+        y2 = d2 / sg.z;
+        y3 = d3 / sg.w;
+      }
+      const float L0 = lp_from_z(y0, cc.x);
+      const float L1 = lp_from_z(y1, cc.y);
+      const float L2 = lp_from_z(y2, cc.z);
+      const float L3 = lp_from_z(y3, cc.w);
       // Eigen partials: dim 4q+w feeds p[(4q+w) & 7] = (q odd ? pB : pA)[w]
       const bool odd = (q & 1) != 0;
       const float a0 = (odd ? pb0 : pa0) + L0;
@@ -397,7 +515,7 @@ __global__ void __launch_bounds__(256) k_encode_finalize(
         generate_key(step_seed(block_seed(seed, block_id_base + g), step), 42);
     for (int64_t j = lane; j < sp.d; j += 64) {
       const uint64_t k = (uint64_t)idx * (uint64_t)sp.d + (uint64_t)j;
-      const F4 z = normal4(st, k >> 2, logtab);
+      const F4 z = normal4_dev(st, k >> 2, logtab);
       const uint32_t w = (uint32_t)(k & 3u);
       const float zz = w == 0 ? z.a : (w == 1 ? z.b : (w == 2 ? z.c : z.d));
       float s = scale_s[sp.off + j] * zz;
@@ -435,7 +553,7 @@ __global__ void __launch_bounds__(256) k_decode(
         }
         const PhiloxStream st = generate_key(step_seed(sg, i), 42);
         const uint64_t k = (uint64_t)n * (uint64_t)sp.d + (uint64_t)j;
-        const F4 z = normal4(st, k >> 2, logtab);
+        const F4 z = normal4_dev(st, k >> 2, logtab);
         const uint32_t w = (uint32_t)(k & 3u);
         const float zz = w == 0 ? z.a : (w == 1 ? z.b : (w == 2 ? z.c : z.d));
         float s = ss * zz;
@@ -459,7 +577,7 @@ __global__ void __launch_bounds__(256) k_stateless_normal_sample(
   const int64_t ngrp = (total + 3) >> 2;
   for (int64_t G = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; G < ngrp;
        G += (int64_t)gridDim.x * blockDim.x) {
-    const F4 z = normal4(st, (uint64_t)G, logtab);
+    const F4 z = normal4_dev(st, (uint64_t)G, logtab);
     const float zz[4] = {z.a, z.b, z.c, z.d};
 #pragma unroll
     for (int w = 0; w < 4; ++w) {
@@ -528,9 +646,9 @@ __global__ void __launch_bounds__(256) k_selftest_bm(uint32_t m0, int64_t count,
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < count;
        i += (int64_t)gridDim.x * blockDim.x) {
     const uint32_t m = m0 + (uint32_t)i;
-    rad[i] = bm_radius(m, logtab);
+    rad[i] = bm_radius_dev(m, logtab);
     float s, c;
-    sincosf_pos(bm_angle(m), s, c);
+    sincosf_pos(bm_angle_dev(m), s, c);
     sn[i] = s;
     cs[i] = c;
   }
@@ -541,6 +659,16 @@ __global__ void __launch_bounds__(256) k_selftest_logf(const float* __restrict__
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x)
     out[i] = logf_full(x[i], kLogTabConst);
+}
+
+__global__ void __launch_bounds__(256) k_selftest_div(const float* __restrict__ a,
+                                                      const float* __restrict__ b, int64_t n,
+                                                      float* __restrict__ out) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const float y = 1.0f / b[i];
+    out[i] = div_rn_markstein(a[i], b[i], y);
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -698,6 +826,14 @@ hipError_t launch_selftest_bm(uint32_t m0, int64_t count, float* rad, float* sn,
   if (count <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_selftest_bm, dim3(grid_for(count, 256, 65536)), dim3(256), 0, stream, m0,
                      count, rad, sn, cs);
+  return hipGetLastError();
+}
+
+hipError_t launch_selftest_div(const float* a, const float* b, int64_t n, float* out,
+                               hipStream_t stream) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_selftest_div, dim3(grid_for(n, 256, 65536)), dim3(256), 0, stream, a, b, n,
+                     out);
   return hipGetLastError();
 }
 

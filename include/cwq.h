@@ -140,6 +140,10 @@ int64_t cwq_group_starts(const float* kl, int64_t D, int64_t size_threshold, dou
 int cwq_selftest_bm_tables(uint32_t m0, int64_t count, float* radius, float* sin_out,
                            float* cos_out, void* stream);
 int cwq_selftest_logf(const float* x, int64_t n, float* out, void* stream);
+/* out[i] = the device's fast correctly-rounded quotient a[i] / b[i]
+ * (Markstein sequence with y = RN(1/b); only valid in the ranges documented in
+ * DESIGN.md -- the test feeds it exactly those). */
+int cwq_selftest_div(const float* a, const float* b, int64_t n, float* out, void* stream);
 
 /* Profiling hook (bench.py): when set, every later encode call made by this
  * host thread records hipEvent_t `start_event` on its stream right before its

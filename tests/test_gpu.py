@@ -330,3 +330,37 @@ def test_pruned_adversarial(cwq, cwqlib, oracle, kind):
     wi, ws = oracle.greedy_encode(tl, ts, pl, ps, np.arange(nb + 1) * d, bits, 1, 42)
     assert np.array_equal(i1, wi)
     _assert_bits_equal(s1, ws, kind)
+
+
+def test_device_fast_division_correctly_rounded(cwq, cwqlib):
+    """The 5-op quotient used by the pruned kernel equals IEEE a/b on its
+    documented domain: 2^-60 <= |a| <= 2^60 (or 0), 2^-60 <= b <= 2^60."""
+    rng = np.random.default_rng(11)
+    n = 1 << 24
+    parts = []
+    for _ in range(6):
+        # random significands, exponents spread over the whole domain
+        a = (rng.uniform(1, 2, n) * np.exp2(rng.integers(-60, 60, n))).astype(np.float32)
+        a *= np.where(rng.uniform(size=n) < 0.5, -1, 1).astype(np.float32)
+        b = (rng.uniform(1, 2, n) * np.exp2(rng.integers(-60, 60, n))).astype(np.float32)
+        parts.append((a, b))
+    # adversarial: b = 1 +- k ulp, a = near multiples of b; b = powers of two
+    k = rng.integers(1, 1 << 20, n)
+    b = (np.float32(1) + k.astype(np.float32) * np.float32(2 ** -23)).astype(np.float32)
+    m = rng.integers(1, 1 << 24, n).astype(np.float64)
+    a = (m * b.astype(np.float64) * (1 + rng.integers(-3, 4, n) * 2.0 ** -24)).astype(np.float32)
+    parts.append((a, b))
+    parts.append((rng.uniform(-4, 4, n).astype(np.float32),
+                  np.exp2(rng.integers(-60, 61, n)).astype(np.float32)))
+    parts.append((np.zeros(1024, np.float32), rng.uniform(0.1, 9, 1024).astype(np.float32)))
+    for a, b in parts:
+        ad = torch.from_numpy(a).cuda()
+        bd = torch.from_numpy(b).cuda()
+        out = torch.empty_like(ad)
+        assert cwqlib.cwq_selftest_div(ad.data_ptr(), bd.data_ptr(), a.size, out.data_ptr(),
+                                       torch.cuda.current_stream().cuda_stream) == 0
+        want = (a / b).astype(np.float32)
+        got = out.cpu().numpy()
+        got = np.where(a == 0, np.abs(got), got)  # sign of a zero quotient is irrelevant
+        want = np.where(a == 0, np.abs(want), want)
+        _assert_bits_equal(got, want, "fast division")
