@@ -8,7 +8,9 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libcwq.so")
+# CWQ_LIB_PATH selects another build of the same library (tools/variants.sh
+# A/B-times compile-time tuning variants this way); default is the in-tree one.
+LIB_PATH = os.environ.get("CWQ_LIB_PATH") or os.path.join(_HERE, "libcwq.so")
 
 c_int = ctypes.c_int
 c_i32 = ctypes.c_int32

@@ -286,6 +286,12 @@ __global__ void __launch_bounds__(256) k_encode_eval(
 // though candidates stop after different numbers of dims.
 // ---------------------------------------------------------------------------
 constexpr float kPruneC1 = 0x1p-14f;
+#ifndef CWQ_PRUNE_MIN_WAVES
+#define CWQ_PRUNE_MIN_WAVES 1  // waves/SIMD the register allocator must allow
+#endif
+#ifndef CWQ_TAU_SHARE_MASK
+#define CWQ_TAU_SHARE_MASK 15u  // share tau across the workgroup every 16 units
+#endif
 
 __device__ __forceinline__ uint32_t ord_f32(float v) {
   const uint32_t b = f2u(v);
@@ -323,7 +329,7 @@ __device__ __forceinline__ float lp_from_z(float z, float cc) {
 }
 
 template <int D, bool STEP0>
-__global__ void __launch_bounds__(256) k_encode_prune(
+__global__ void __launch_bounds__(256, CWQ_PRUNE_MIN_WAVES) k_encode_prune(
     const float* __restrict__ t_loc, const float* __restrict__ t_scale,
     const float* __restrict__ loc_s, const float* __restrict__ scale_s,
     const float* __restrict__ lognorm, const float* __restrict__ best, int64_t ntiles,
@@ -473,7 +479,7 @@ __global__ void __launch_bounds__(256) k_encode_prune(
       }
       wnext += (int64_t)__builtin_popcountll(m);
       active = n < w1;
-      if (((++iter) & 15u) == 0u) {  // share tau across the workgroup's waves
+      if (((++iter) & CWQ_TAU_SHARE_MASK) == 0u) {  // share tau across the workgroup's waves
         const float tm = wave_max_f32(tau);
         if (lane == 0) atomicMax(&tau_ord, ord_f32(tm));
         tau = fmaxf(tau, unord_f32(__atomic_load_n(&tau_ord, __ATOMIC_RELAXED)));

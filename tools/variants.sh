@@ -1,0 +1,26 @@
+#!/bin/bash
+# Build compile-time tuning variants of libcwq.so into tools/variants/ and
+# time each on the C4 bench (run on the GPU box).  Usage: tools/variants.sh build|run
+set -e
+cd "$(dirname "$0")/.."
+CSRC=compression_without_quantization_amd/csrc
+OUT=tools/variants
+FLAGS="--offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -fno-fast-math -fPIC -shared"
+declare -A V=(
+  [base]=""
+  [w6]="-DCWQ_PRUNE_MIN_WAVES=6"
+  [w8]="-DCWQ_PRUNE_MIN_WAVES=8"
+  [tau4]="-DCWQ_TAU_SHARE_MASK=3u"
+)
+if [ "$1" = build ]; then
+  mkdir -p $OUT
+  for k in "${!V[@]}"; do
+    hipcc $FLAGS ${V[$k]} -o $OUT/libcwq_$k.so $CSRC/cwq_kernels.hip $CSRC/cwq_capi.hip &
+  done
+  wait
+else
+  for k in $(echo "${!V[@]}" | tr ' ' '\n' | sort); do
+    echo "== $k ${V[$k]}"
+    CWQ_LIB_PATH=$PWD/$OUT/libcwq_$k.so timeout -k 10 300 python -u bench.py --no-cpu --no-e2e --steps 2 --warmup 1 | python -c "import json,sys; d=json.loads(sys.stdin.read()); print(d['value'], d['roofline']['kernel_ms'])"
+  done
+fi
