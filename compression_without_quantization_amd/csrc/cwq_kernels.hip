@@ -266,24 +266,34 @@ __global__ void __launch_bounds__(256) k_encode_eval(
 // Pruned encoder for uniform blocks, D % 8 == 0, D <= 64 (the C1/C4/C5 shapes).
 //
 // Same result as k_encode_eval, less work: a candidate whose log-density can
-// no longer reach the best value already found in this tile is dropped before
-// its remaining dims are generated.  Rows are still evaluated in natural dim
-// order, one Philox block (4 dims) per step, so the lane's Eigen partial sums
-// stay exact and a candidate that survives all D dims yields its exact value.
+// no longer reach a value already achieved in this tile is dropped before its
+// remaining dims are generated.
 //
-// Drop rule ("pruning bound"): after the first 4q dims with float
-// running sum s, candidate n is dropped iff
-//     s + 2^-14 |s| + B_q  <  tau
-// where tau is the exact value of a candidate already completed in this tile
-// and B_q >= sum_{j>=4q} f(M_j) + 2^-14 K_q (+ float evaluation margin), with
-// M_j = -c_j the maximum of the float log-density of dim j, f(x) = x+g|x|,
-// g >= gamma_{D-1} + gamma_{4q}.  This bounds the float Eigen-order sum of
-// every completion of the row from above, so a dropped candidate's value is
-// strictly below tau: it can be neither the argmax nor a tie.
+// Order: each block's D/4 Philox groups are visited in decreasing order of
+// their expected log-density deficit under the proposal shard (the dims that
+// discriminate most first), one group (4 dims, one Philox block) per step.
+//
+// Drop rule ("pruning bound"): after the first k visited groups,
+// with float running sum s of their log-densities, candidate n is dropped iff
+//     s + 2^-14 |s| + B_k  <  tau
+// where B_k >= sum_{unvisited j} f(M_j) + 2^-14 K_k (+ float evaluation
+// margin), M_j = -c_j is the largest value the float log-density of dim j can
+// take, f(x) = x + g|x| with g >= gamma_{D-1} + gamma_{D}, and K_k sums
+// |M_j| + M_j over the visited dims.  The left side bounds from above the
+// float Eigen-order value of every completion of the row; tau is a lower
+// bound of the exact value of a candidate already completed in this tile.  So
+// a dropped candidate is strictly worse than an existing one: neither the
+// argmax nor a tie.
+//
+// Completion: after all groups, s brackets the exact value within
+// [s - 2^-14|s| - L, s + 2^-14|s| + B_D].  Candidates whose upper end reaches
+// tau go to an LDS survivor list; at the end of the tile the survivors whose
+// upper end reaches the final tau are re-evaluated exactly (natural order,
+// Eigen summation, eval_row) and only those produce argmax keys.
 //
 // Lanes keep one candidate each and refill from a per-wave counter with
 // ballot/mbcnt when theirs completes or is dropped, so waves stay full even
-// though candidates stop after different numbers of dims.
+// though candidates stop after different numbers of groups.
 // ---------------------------------------------------------------------------
 constexpr float kPruneC1 = 0x1p-14f;
 #ifndef CWQ_PRUNE_MIN_WAVES
@@ -291,6 +301,9 @@ constexpr float kPruneC1 = 0x1p-14f;
 #endif
 #ifndef CWQ_TAU_SHARE_MASK
 #define CWQ_TAU_SHARE_MASK 15u  // share tau across the workgroup every 16 units
+#endif
+#ifndef CWQ_SURVIVOR_CAP
+#define CWQ_SURVIVOR_CAP 1024
 #endif
 
 __device__ __forceinline__ uint32_t ord_f32(float v) {
@@ -305,8 +318,9 @@ __device__ __forceinline__ float wave_max_f32(float v) {
   for (int off = 32; off >= 1; off >>= 1) v = fmaxf(v, __shfl_xor(v, off, 64));
   return v;
 }
+// smallest float >= b (+inf for non-finite b: such a bound never drops anything)
 __device__ __forceinline__ float round_up_f32(double b) {
-  if (!(b == b) || b > 3.0e38 || b < -3.0e38) return __builtin_inff();  // never prune
+  if (!(b == b) || b > 3.0e38 || b < -3.0e38) return __builtin_inff();
   float f = (float)b;
   if ((double)f < b) {
     const uint32_t u = f2u(f);
@@ -339,9 +353,16 @@ __global__ void __launch_bounds__(256, CWQ_PRUNE_MIN_WAVES) k_encode_prune(
   constexpr int G = D / 4;
   constexpr int NF = STEP0 ? 6 : 7;  // loc_s, scale_s, mu, sigma, c, 1/sigma[, best]
   __shared__ double logtab[32];
-  __shared__ float4 cst[G * NF];
-  __shared__ float bnd[G + 1];
+  __shared__ float4 cst[G * NF];     // constants of the k-th visited group
+  __shared__ int2 meta[G];           // {Philox group of visit k, bits of B_{k+1}}
+  __shared__ float dscore[D];
+  __shared__ float gscore[G];
+  __shared__ int gpos[G];
+  __shared__ float lowc;             // L: lower-end constant of a completed row
   __shared__ uint32_t tau_ord;
+  __shared__ uint32_t sq_cnt;
+  __shared__ uint32_t sq_n[CWQ_SURVIVOR_CAP];
+  __shared__ float sq_ub[CWQ_SURVIVOR_CAP];
   __shared__ unsigned long long wkey[4];
   fill_logtab(logtab);
   const uint32_t wv = wave_id();
@@ -356,41 +377,78 @@ __global__ void __launch_bounds__(256, CWQ_PRUNE_MIN_WAVES) k_encode_prune(
     const PhiloxStream st =
         generate_key(step_seed(block_seed(seed, block_id_base + g), step), 42);
 
-    // stage this block's per-dim constants: cst[q*NF + f] = field f of dims 4q..4q+3
+    // (a) per-dim constants into registers; expected deficit of dim j under the
+    //     proposal shard: E[0.5((T - mu)/sigma)^2], T ~ N(best + loc_s, scale_s^2)
+    float fj[7] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     int den_ok = 1;
     if (threadIdx.x < D) {
-      const int j = threadIdx.x, q = j >> 2, w = j & 3;
-      float* c = reinterpret_cast<float*>(cst);
+      const int j = threadIdx.x;
       const float sgj = t_scale[off + j];
-      c[(q * NF + 0) * 4 + w] = loc_s[off + j];
-      c[(q * NF + 1) * 4 + w] = scale_s[off + j];
-      c[(q * NF + 2) * 4 + w] = t_loc[off + j];
-      c[(q * NF + 3) * 4 + w] = sgj;
-      c[(q * NF + 4) * 4 + w] = lognorm[off + j];
-      c[(q * NF + 5) * 4 + w] = 1.0f / sgj;
-      if (!STEP0) c[(q * NF + 6) * 4 + w] = best[off + j];
+      fj[0] = loc_s[off + j];
+      fj[1] = scale_s[off + j];
+      fj[2] = t_loc[off + j];
+      fj[3] = sgj;
+      fj[4] = lognorm[off + j];
+      fj[5] = 1.0f / sgj;
+      if (!STEP0) fj[6] = best[off + j];
       den_ok = markstein_ok_den(sgj) ? 1 : 0;
+      const float m = (STEP0 ? fj[0] : fj[6] + fj[0]) - fj[2];
+      float e = 0.5f * (fj[1] * fj[1] + m * m) * (fj[5] * fj[5]);
+      dscore[j] = (e == e) ? e : -1.0f;
     }
     const bool fastdiv = __syncthreads_and(den_ok) != 0;
-    if (threadIdx.x <= G) {  // thread q computes the drop bound after q groups
-      const int qb = threadIdx.x;
-      const float* c = reinterpret_cast<const float*>(cst);
-      double rf = 0.0, k = 0.0, asum = 0.0;
-#pragma unroll 1
-      for (int j = 0; j < D; ++j) {
-        const double mj = -(double)c[((j >> 2) * NF + 4) * 4 + (j & 3)];  // M_j = -c_j
-        const double aj = __builtin_fabs(mj);
-        asum += aj;
-        if (j >= 4 * qb)
-          rf += mj + 0x1p-17 * aj;
-        else
-          k += aj + mj;
-      }
-      const double b = rf + 0x1p-14 * k + 0x1p-20 * (__builtin_fabs(rf) + asum) + 0x1p-126;
-      bnd[qb] = round_up_f32(b);
-      if (qb == 0) tau_ord = ord_f32(-__builtin_inff());
+    // (b) group scores, (c) visit order: rank by decreasing score, ties by index
+    if (threadIdx.x < G) {
+      const int q = threadIdx.x;
+      gscore[q] = ((dscore[4 * q] + dscore[4 * q + 1]) + dscore[4 * q + 2]) + dscore[4 * q + 3];
     }
     __syncthreads();
+    if (threadIdx.x < G) {
+      const int q = threadIdx.x;
+      const float sq = gscore[q];
+      int r = 0;
+      for (int q2 = 0; q2 < G; ++q2) {
+        const float s2 = gscore[q2];
+        r += (s2 > sq || (s2 == sq && q2 < q)) ? 1 : 0;
+      }
+      gpos[q] = r;
+    }
+    __syncthreads();
+    // (d) constants in visit order
+    if (threadIdx.x < D) {
+      const int j = threadIdx.x, k = gpos[j >> 2], w = j & 3;
+      float* c = reinterpret_cast<float*>(cst);
+#pragma unroll
+      for (int f = 0; f < NF; ++f) c[(k * NF + f) * 4 + w] = fj[f];
+      if (w == 0) meta[k].x = j >> 2;
+    }
+    __syncthreads();
+    // (e) drop bounds: thread k computes B_k for the first k visited groups
+    if (threadIdx.x <= G) {
+      const int kb = threadIdx.x;
+      const float* c = reinterpret_cast<const float*>(cst);
+      double rf = 0.0, kk = 0.0, asum = 0.0;
+#pragma unroll 1
+      for (int p = 0; p < D; ++p) {  // p = 4 * (visit position) + w
+        const double mj = -(double)c[((p >> 2) * NF + 4) * 4 + (p & 3)];  // M_j = -c_j
+        const double aj = __builtin_fabs(mj);
+        asum += aj;
+        if (p >= 4 * kb)
+          rf += mj + 0x1p-17 * aj;
+        else
+          kk += aj + mj;
+      }
+      const double marg = 0x1p-20 * (__builtin_fabs(rf) + asum) + 0x1p-126;
+      const float bk = round_up_f32(rf + 0x1p-14 * kk + marg);
+      if (kb >= 1) meta[kb - 1].y = (int)f2u(bk);
+      if (kb == G) lowc = round_up_f32(0x1p-14 * kk + marg);
+      if (kb == 0) {
+        tau_ord = ord_f32(-__builtin_inff());
+        sq_cnt = 0u;
+      }
+    }
+    __syncthreads();
+    const float lc = lowc;
 
     // this wave's contiguous share of the tile's candidates
     const int64_t per_wave = (n1 - n0 + 3) / 4;
@@ -399,21 +457,20 @@ __global__ void __launch_bounds__(256, CWQ_PRUNE_MIN_WAVES) k_encode_prune(
     int64_t wnext = w0 + 64;
     int64_t n = w0 + lane;
     bool active = n < w1;
-    int q = 0;
+    int k = 0;
     float s = 0.0f;
-    float pa0 = 0.f, pa1 = 0.f, pa2 = 0.f, pa3 = 0.f;  // p[0..3]
-    float pb0 = 0.f, pb1 = 0.f, pb2 = 0.f, pb3 = 0.f;  // p[4..7]
     float tau = -__builtin_inff();
     uint64_t bestk = 0;
     uint32_t iter = 0;
 
     while (__ballot(active) != 0ull) {
-      const uint32_t grp = (uint32_t)n * (uint32_t)G + (uint32_t)q;
+      const int2 mt = meta[k];
+      const uint32_t grp = (uint32_t)n * (uint32_t)G + (uint32_t)mt.x;
       const U4 x = philox10_dev(grp, 0u, st.c2, st.c3, st.k0, st.k1);
       float z0, z1, z2, z3;
       box_muller_dev(x.x, x.y, logtab, z0, z1);
       box_muller_dev(x.z, x.w, logtab, z2, z3);
-      const float4* cq = cst + q * NF;
+      const float4* cq = cst + k * NF;
       const float4 ls = cq[0], ss = cq[1], mu = cq[2], sg = cq[3], cc = cq[4], ry = cq[5];
       const float4 bb = STEP0 ? float4{0.f, 0.f, 0.f, 0.f} : cq[6];
       const float d0 = cand_diff<STEP0>(z0, ls.x, ss.x, mu.x, bb.x);
@@ -433,38 +490,28 @@ __global__ void __launch_bounds__(256, CWQ_PRUNE_MIN_WAVES) k_encode_prune(
         y2 = d2 / sg.z;
         y3 = d3 / sg.w;
       }
-      const float L0 = lp_from_z(y0, cc.x);
-      const float L1 = lp_from_z(y1, cc.y);
-      const float L2 = lp_from_z(y2, cc.z);
-      const float L3 = lp_from_z(y3, cc.w);
-      // Eigen partials: dim 4q+w feeds p[(4q+w) & 7] = (q odd ? pB : pA)[w]
-      const bool odd = (q & 1) != 0;
-      const float a0 = (odd ? pb0 : pa0) + L0;
-      const float a1 = (odd ? pb1 : pa1) + L1;
-      const float a2 = (odd ? pb2 : pa2) + L2;
-      const float a3 = (odd ? pb3 : pa3) + L3;
-      pa0 = odd ? pa0 : a0;
-      pa1 = odd ? pa1 : a1;
-      pa2 = odd ? pa2 : a2;
-      pa3 = odd ? pa3 : a3;
-      pb0 = odd ? a0 : pb0;
-      pb1 = odd ? a1 : pb1;
-      pb2 = odd ? a2 : pb2;
-      pb3 = odd ? a3 : pb3;
-      s = s + L0;
-      s = s + L1;
-      s = s + L2;
-      s = s + L3;
-      q += 1;
-      const bool complete = (q == G);
-      const float lhs = (s + __builtin_fabsf(s) * kPruneC1) + bnd[q];
-      const bool prune = !complete && (lhs < tau);
-      if (complete && active) {
-        const float q0 = pa0 + pb0, q1 = pa1 + pb1, q2 = pa2 + pb2, q3 = pa3 + pb3;
-        const float v = 0.0f + ((q0 + q2) + (q1 + q3));
-        const uint64_t k = argmax_key(v, (uint32_t)n);
-        bestk = k > bestk ? k : bestk;
-        tau = fmaxf(tau, v);
+      s = s + lp_from_z(y0, cc.x);
+      s = s + lp_from_z(y1, cc.y);
+      s = s + lp_from_z(y2, cc.z);
+      s = s + lp_from_z(y3, cc.w);
+      k += 1;
+      const bool complete = (k == G);
+      const float as = __builtin_fabsf(s) * kPruneC1;
+      const float upper = (s + as) + u2f((uint32_t)mt.y);
+      const bool prune = !complete && (upper < tau);
+      if (complete && active && upper >= tau) {  // may be the best: keep it
+        tau = fmaxf(tau, (s - as) - lc);
+        const uint32_t slot = atomicAdd(&sq_cnt, 1u);
+        if (slot < CWQ_SURVIVOR_CAP) {
+          sq_n[slot] = (uint32_t)n;
+          sq_ub[slot] = upper;
+        } else {  // list full (near-ties everywhere): evaluate exactly now
+          const float v = eval_row<D, STEP0>(st, (uint64_t)n * D, D, 0, loc_s + off,
+                                             scale_s + off, t_loc + off, t_scale + off,
+                                             lognorm + off, STEP0 ? nullptr : best + off, logtab);
+          const uint64_t kv = argmax_key(v, (uint32_t)n);
+          bestk = kv > bestk ? kv : bestk;
+        }
       }
       const bool done = complete || prune || !active;
       const uint64_t m = __ballot(done);
@@ -472,10 +519,8 @@ __global__ void __launch_bounds__(256, CWQ_PRUNE_MIN_WAVES) k_encode_prune(
           __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
       if (done) {
         n = wnext + rank;
-        q = 0;
+        k = 0;
         s = 0.0f;
-        pa0 = pa1 = pa2 = pa3 = 0.f;
-        pb0 = pb1 = pb2 = pb3 = 0.f;
       }
       wnext += (int64_t)__builtin_popcountll(m);
       active = n < w1;
@@ -483,6 +528,25 @@ __global__ void __launch_bounds__(256, CWQ_PRUNE_MIN_WAVES) k_encode_prune(
         const float tm = wave_max_f32(tau);
         if (lane == 0) atomicMax(&tau_ord, ord_f32(tm));
         tau = fmaxf(tau, unord_f32(__atomic_load_n(&tau_ord, __ATOMIC_RELAXED)));
+      }
+    }
+
+    // exact evaluation of the survivors that can still reach the final tau
+    {
+      const float tm = wave_max_f32(tau);
+      if (lane == 0) atomicMax(&tau_ord, ord_f32(tm));
+    }
+    __syncthreads();
+    const float tau_final = unord_f32(tau_ord);
+    const uint32_t nsurv = sq_cnt < CWQ_SURVIVOR_CAP ? sq_cnt : CWQ_SURVIVOR_CAP;
+    for (uint32_t i = threadIdx.x; i < nsurv; i += blockDim.x) {
+      if (sq_ub[i] >= tau_final) {
+        const uint32_t nn = sq_n[i];
+        const float v = eval_row<D, STEP0>(st, (uint64_t)nn * D, D, 0, loc_s + off,
+                                           scale_s + off, t_loc + off, t_scale + off,
+                                           lognorm + off, STEP0 ? nullptr : best + off, logtab);
+        const uint64_t kv = argmax_key(v, nn);
+        bestk = kv > bestk ? kv : bestk;
       }
     }
 
@@ -515,7 +579,9 @@ __global__ void __launch_bounds__(256) k_encode_finalize(
   for (int64_t g = (int64_t)blockIdx.x * 4 + wv; g < nb; g += (int64_t)gridDim.x * 4) {
     const BlockSpan sp = block_span(block_off, ud, g);
     const uint64_t key = keys[g];
-    const uint32_t idx = key ? argmax_key_index(key) : 0u;
+    // ArgMaxTupleReducer starts at (index 0, lowest()) and only a value strictly
+    // above lowest() replaces it: a winning key at the clamp level means index 0
+    const uint32_t idx = (key >> 32) > kArgmaxClampOrd ? argmax_key_index(key) : 0u;
     if (lane == 0) out_idx[g * n_steps + step] = (int32_t)idx;
     const PhiloxStream st =
         generate_key(step_seed(block_seed(seed, block_id_base + g), step), 42);

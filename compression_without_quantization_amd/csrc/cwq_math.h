@@ -282,6 +282,8 @@ CWQ_HD uint64_t argmax_key(float v, uint32_t idx) {
   uint32_t o = (b & 0x80000000u) ? ~b : (b | 0x80000000u);
   return ((uint64_t)o << 32) | (uint64_t)(0xFFFFFFFFu - idx);
 }
+// ord(lowest()): keys at this level carry no information about the index.
+constexpr uint32_t kArgmaxClampOrd = 0x00800000u;
 CWQ_HD uint32_t argmax_key_index(uint64_t key) {
   return 0xFFFFFFFFu - (uint32_t)(key & 0xFFFFFFFFull);
 }

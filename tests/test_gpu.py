@@ -306,7 +306,8 @@ def test_pruned_matches_unpruned_and_oracle(cwq, cwqlib, oracle, d, bits, n_step
 
 
 @pytest.mark.parametrize("kind", ["posterior_is_prior", "tiny_scales", "huge_scales",
-                                  "inf_scale", "zero_scale", "mixed_sign_norm"])
+                                  "inf_scale", "zero_scale", "mixed_sign_norm", "nan_scale",
+                                  "nan_loc_one_dim"])
 def test_pruned_adversarial(cwq, cwqlib, oracle, kind):
     rng = np.random.default_rng(sum(map(ord, kind)))
     nb, d, bits = 6, 16, 10
@@ -324,6 +325,10 @@ def test_pruned_adversarial(cwq, cwqlib, oracle, kind):
     elif kind == "zero_scale":
         ts[5] = 0.0
         tl[5] = pl[5]
+    elif kind == "nan_scale":      # every candidate's value is NaN -> index 0
+        ts[:] = np.nan
+    elif kind == "nan_loc_one_dim":  # NaN in one dim of every other block
+        tl[7::32] = np.nan
     elif kind == "mixed_sign_norm":  # some c_j < 0 (M_j > 0), some > 0
         ts = np.where(rng.uniform(size=nb * d) < 0.5, 0.05, 3.0).astype(np.float32)
     i1, s1 = _uniform_encode(cwq, cwqlib, tl, ts, pl, ps, d, bits, 1, 42, 1.0, True)
