@@ -12,7 +12,7 @@
 //     /lib/x86_64-linux-gnu/libm.so.6 (.rodata of __logf_data and
 //     __sincosf_table), and the Box-Muller domains (2^23 inputs each) are
 //     verified exhaustively against that libm by tests/test_math_exhaustive.py
-//     (host) and tests/test_gpu_math.py (device).
+//     (host) and tests/test_gpu.py (device, via cwq_selftest_bm_tables).
 //   * TFP (<=0.7) Normal.log_prob and the Eigen inner-dim sum order (A.5, A.6).
 //
 // Compile with -ffp-contract=off: every fused multiply-add below is explicit.
@@ -55,8 +55,8 @@ CWQ_HD void philox_round(uint32_t& c0, uint32_t& c1, uint32_t& c2, uint32_t& c3,
   c2 = n2;
 }
 
-// Ten rounds, nine key bumps.  The key schedule is passed pre-bumped when the
-// caller can hoist it (uniform per block/step): see PhiloxKeySched.
+// Ten rounds; the key bump after the last round is dead code (the compiler
+// drops it).  When the key is uniform the bumped keys live in SGPRs.
 CWQ_HD U4 philox10(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0,
                    uint32_t k1) {
 #pragma unroll
