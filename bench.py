@@ -107,12 +107,19 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
+    ndev = torch.cuda.device_count()
+    dev = torch.device("cuda", local_rank % ndev)
+    torch.cuda.set_device(dev)
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=dev)
+        # RCCL when every rank owns a GPU (the data path itself has no collective:
+        # only the start/stop barriers and the max-reduce of the step time use
+        # it); gloo when ranks share one device (a rehearsal on a 1-GPU box)
+        if ndev >= world:
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
 
     nb, d, bits, n_steps, desc = CONFIGS[args.config]
     if args.blocks:
@@ -157,7 +164,8 @@ def main():
     _lib.check(lib.cwq_profile_set_eval_events(None, None), "events")
     elapsed = t1 - t0
     if dist:
-        e = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        e = torch.tensor([elapsed], dtype=torch.float64,
+                         device=dev if dist.get_backend() == "nccl" else "cpu")
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
         elapsed = float(e.item())
     eval_ms = float(np.mean([a.elapsed_time(b) for a, b in events]))
