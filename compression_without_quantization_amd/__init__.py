@@ -4,12 +4,17 @@ Public surface mirrors the reference's code/coded_greedy_sampler.py,
 code/misc.py and code/binary_io.py (bit-string helpers); every sample is
 computed by the gfx950 kernels in libcwq.so (see include/cwq.h).
 """
-from .binary_io import (bitcode_to_indices, from_bit_string, indices_to_bitcode,
-                        to_bit_string)
+from .binary_io import (bitcode_to_indices, elias_delta_code, elias_delta_decode,
+                        from_bit_string, indices_to_bitcode, to_bit_string)
 from .coded_greedy_sampler import (Normal, code_greedy_sample, code_grouped_greedy_sample,
                                    decode, decode_blocks, decode_greedy_sample,
                                    decode_grouped_greedy_sample, encode, encode_blocks,
                                    encode_workspace_bytes, group_size_threshold, group_starts)
+from .coded_importance_sampler import (code_grouped_importance_sample,
+                                       code_importance_sample,
+                                       decode_grouped_importance_sample,
+                                       decode_importance_sample, importance_decode_blocks,
+                                       importance_encode_blocks)
 from .misc import stateless_normal_sample
 from .parallel import gather_indices, shard_range
 
@@ -18,5 +23,8 @@ __all__ = [
     "decode_grouped_greedy_sample", "encode", "decode", "encode_blocks", "decode_blocks",
     "encode_workspace_bytes", "group_starts", "group_size_threshold",
     "stateless_normal_sample", "to_bit_string", "from_bit_string", "indices_to_bitcode",
-    "bitcode_to_indices", "shard_range", "gather_indices",
+    "bitcode_to_indices", "shard_range", "gather_indices", "elias_delta_code",
+    "elias_delta_decode", "code_importance_sample", "decode_importance_sample",
+    "code_grouped_importance_sample", "decode_grouped_importance_sample",
+    "importance_encode_blocks", "importance_decode_blocks",
 ]

@@ -39,6 +39,13 @@ SIGNATURES = {
     "cwq_kl_normal_normal": (c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp]),
     "cwq_destandardise": (c_int, [c_vp, c_vp, c_vp, c_i64, c_vp, c_vp]),
     "cwq_group_starts": (c_i64, [c_vp, c_i64, c_i64, c_f64, c_vp, c_i64]),
+    "cwq_importance_workspace_size": (c_size, [c_i64, c_i64]),
+    "cwq_importance_encode": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i32,
+                                      c_i64, c_vp, c_vp, c_vp, c_size, c_vp]),
+    "cwq_importance_decode": (c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i32, c_i64, c_vp,
+                                      c_vp]),
+    "cwq_importance_group_starts": (c_i64, [c_vp, c_i64, c_i64, c_f64, c_vp, c_i64]),
+    "cwq_importance_plan": (c_int, [c_vp, c_vp, c_i64, c_vp]),
     "cwq_selftest_bm_tables": (c_int, [ctypes.c_uint32, c_i64, c_vp, c_vp, c_vp, c_vp]),
     "cwq_selftest_logf": (c_int, [c_vp, c_i64, c_vp, c_vp]),
     "cwq_selftest_div": (c_int, [c_vp, c_vp, c_i64, c_vp, c_vp]),

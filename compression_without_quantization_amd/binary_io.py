@@ -70,3 +70,35 @@ def bitcode_to_indices(bitcode, num_bits, count):
     bits = bits.reshape(count, num_bits)
     weights = (np.int64(1) << np.arange(num_bits, dtype=np.int64))
     return (bits * weights[None, :]).sum(axis=1)
+
+
+def elias_delta_code(x):
+    """binary_io.py:7-21 -- Elias-delta code of x >= 1 as a '0'/'1' string.
+
+    n = floor(log2 x) and l = floor(log2(n + 1)) are evaluated exactly as the
+    reference does (np.log ratio in float64); for x < 2^31 that equals the
+    bit length (pinned by tests/test_importance.py).
+    """
+    x = int(x)
+    lg2 = np.log(2)
+    n = int(np.floor(np.log(x) / lg2).astype(np.int32))
+    l = int(np.floor(np.log(n + 1) / lg2).astype(np.int32))
+    length_length_code = ''.join(["0"] * l)
+    length_code = to_bit_string(n + 1, l + 1)[::-1]
+    num_code = to_bit_string(x, n + 1)[::-1][1:]
+    return length_length_code + length_code + num_code
+
+
+def elias_delta_decode(x):
+    """binary_io.py:23-39 -- decode one Elias-delta code at the start of x
+    (bytes or str).  Returns (num, code_length)."""
+    if isinstance(x, str):
+        x = x.encode("ascii")
+    l = 0
+    while x[l] == 48:  # '0'
+        l += 1
+    x = x[l:]
+    n_plus_one = from_bit_string(x[:l + 1][::-1])
+    x = x[l + 1:]
+    num = from_bit_string(x[:n_plus_one - 1][::-1] + b"1")
+    return num, 2 * l + n_plus_one

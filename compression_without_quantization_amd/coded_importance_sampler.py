@@ -1,0 +1,300 @@
+"""Coded importance sampler -- code/coded_importance_sampler.py on the gfx950 kernels.
+
+  code_importance_sample            (:29-79)
+  decode_importance_sample          (:82-109)
+  code_grouped_importance_sample    (:112-274)
+  decode_grouped_importance_sample  (:277-363)
+
+Candidate scoring runs in libcwq.so (cwq_importance_encode).  Host code keeps
+only the reference's per-group bookkeeping: the sequential partition
+(cwq_importance_group_starts), the per-group candidate count
+ceil(exp(sum KL)) (cwq_importance_plan), Elias-delta strings and the
+quint16 outlier packing.
+
+Deliberate differences from the TF1 reference:
+  * the reference draws the outlier dims' target sample with an unseeded
+    `target.sample()` (:150, non-deterministic); here it
+    is the stateless draw x = q_loc + q_scale * z, z ~ stateless_normal([D],
+    seed=[seed - 1, 42]) (seed - 1 is never a group's seed), so encoding is
+    reproducible;
+  * decode_grouped_importance_sample does not append to the caller's list
+    (:294 mutates it);
+  * results are concrete values; `sess` is accepted and ignored.
+"""
+import numpy as np
+import torch
+
+from . import _lib
+from .binary_io import elias_delta_code, elias_delta_decode
+from .coded_greedy_sampler import _device_of, _f32, _is_float32, _like_input, _ptr
+
+VERBOSE = True
+QUANT_MIN, QUANT_MAX = -30.0, 30.0
+
+
+def _stream(dev):
+    return torch.cuda.current_stream(dev).cuda_stream
+
+
+def importance_group_size_threshold(max_group_size_bits):
+    """Smallest s with np.log(s + 1) / np.log(2) > max_group_size_bits (:185-187)."""
+    bits = max_group_size_bits
+    s = max(int(2 ** bits) - 3, 0)
+    while s > 0 and np.log(s + 1) / np.log(2) > bits:
+        s -= 1
+    while not (np.log(s + 1) / np.log(2) > bits):
+        s += 1
+    return s
+
+
+def importance_group_starts(kl_divs, n_bits_per_group, max_group_size_bits=4):
+    """coded_importance_sampler.py:164-203 -> group start list with D appended."""
+    kl = np.ascontiguousarray(np.asarray(kl_divs, dtype=np.float32).reshape(-1))
+    D = kl.size
+    n_nats = n_bits_per_group * np.log(2) - 1
+    cap = D + 2
+    starts = np.empty(cap, dtype=np.int64)
+    n = _lib.load().cwq_importance_group_starts(
+        kl.ctypes.data if D else None, D, importance_group_size_threshold(max_group_size_bits),
+        float(n_nats), starts.ctypes.data, cap)
+    _lib.check(n, "cwq_importance_group_starts")
+    return [int(v) for v in starts[:n]]
+
+
+def num_samples_plan(kl_divs, starts):
+    """:48-51 per group: int32(ceil(exp(reduce_sum(kl)))) (host bookkeeping)."""
+    kl = np.ascontiguousarray(np.asarray(kl_divs, dtype=np.float32).reshape(-1))
+    st = np.ascontiguousarray(np.asarray(starts, dtype=np.int64).reshape(-1))
+    ng = st.size - 1
+    out = np.empty(max(ng, 1), dtype=np.int64)
+    _lib.check(_lib.load().cwq_importance_plan(kl.ctypes.data if kl.size else None,
+                                               st.ctypes.data, ng, out.ctypes.data),
+               "cwq_importance_plan")
+    return out[:ng]
+
+
+def _kl(dev, a_loc, a_scale, b_loc, b_scale):
+    n = a_loc.numel()
+    out = torch.empty(n, dtype=torch.float32, device=dev)
+    _lib.check(_lib.load().cwq_kl_normal_normal(_ptr(a_loc), _ptr(a_scale), _ptr(b_loc),
+                                                _ptr(b_scale), n, _ptr(out), _stream(dev)),
+               "cwq_kl_normal_normal")
+    return out
+
+
+def importance_encode_blocks(t_loc, t_scale, p_loc, p_scale, block_off, n_samples, seed,
+                             block_id_base=0):
+    """cwq_importance_encode over CSR groups.  Returns (index int64 [nb], sample f32 [D])."""
+    lib = _lib.load()
+    dev = _device_of(t_loc, t_scale, p_loc, p_scale)
+    tl, ts, pl, ps = (_f32(x, dev, w) for x, w in ((t_loc, "t_loc"), (t_scale, "t_scale"),
+                                                   (p_loc, "p_loc"), (p_scale, "p_scale")))
+    D = tl.numel()
+    offs = torch.as_tensor(np.asarray(block_off, dtype=np.int64)).to(dev)
+    nb = offs.numel() - 1
+    ns = torch.as_tensor(np.asarray(n_samples, dtype=np.int64)).to(dev)
+    idx = torch.empty(max(nb, 0), dtype=torch.int64, device=dev)
+    sample = torch.empty(D, dtype=torch.float32, device=dev)
+    need = int(lib.cwq_importance_workspace_size(nb, D))
+    ws = torch.empty(max(need, 1), dtype=torch.uint8, device=dev)
+    seed32 = int(np.int32(np.uint32(int(seed) & 0xFFFFFFFF)))
+    _lib.check(lib.cwq_importance_encode(_ptr(tl), _ptr(ts), _ptr(pl), _ptr(ps), offs.data_ptr(),
+                                         _ptr(ns), nb, D, seed32, int(block_id_base), _ptr(idx),
+                                         _ptr(sample), ws.data_ptr(), ws.numel(), _stream(dev)),
+               "cwq_importance_encode")
+    return idx, sample
+
+
+def importance_decode_blocks(index, p_loc, p_scale, block_off, seed, block_id_base=0):
+    """cwq_importance_decode over CSR groups.  Returns sample f32 [D]."""
+    lib = _lib.load()
+    dev = _device_of(index, p_loc, p_scale)
+    pl, ps = _f32(p_loc, dev, "p_loc"), _f32(p_scale, dev, "p_scale")
+    D = pl.numel()
+    offs = torch.as_tensor(np.asarray(block_off, dtype=np.int64)).to(dev)
+    nb = offs.numel() - 1
+    ix = torch.as_tensor(np.asarray(index.cpu() if isinstance(index, torch.Tensor) else index,
+                                    dtype=np.int64)).to(dev)
+    out = torch.empty(D, dtype=torch.float32, device=dev)
+    seed32 = int(np.int32(np.uint32(int(seed) & 0xFFFFFFFF)))
+    _lib.check(lib.cwq_importance_decode(_ptr(ix), _ptr(pl), _ptr(ps), offs.data_ptr(), nb, D,
+                                         seed32, int(block_id_base), _ptr(out), _stream(dev)),
+               "cwq_importance_decode")
+    return out
+
+
+# ---------------------------------------------------------------------------
+# reference surface
+# ---------------------------------------------------------------------------
+def code_importance_sample(t_loc, t_scale, p_loc, p_scale, n_coding_bits, seed,
+                           return_index_only=False):
+    """:29-79.  Returns (best_sample [1, d], index + 1) or (best_sample, Elias code)."""
+    dev = _device_of(t_loc, t_scale, p_loc, p_scale)
+    tl, ts, pl, ps = (_f32(x, dev, "input") for x in (t_loc, t_scale, p_loc, p_scale))
+    d = tl.numel()
+    kl = _kl(dev, tl, ts, pl, ps).cpu().numpy()
+    n = num_samples_plan(kl, [0, d])
+    idx, sample = importance_encode_blocks(tl, ts, pl, ps, [0, d], n, seed)
+    index = int(idx[0].item())
+    best = _like_input(sample.reshape(1, d), t_loc)
+    if return_index_only:
+        return best, index + 1
+    return best, elias_delta_code(index + 1)
+
+
+def decode_importance_sample(sample_index, p_loc, p_scale, seed, use_index=False):
+    """:82-109.  use_index: sample_index is index + 1 -> samples[-1:].  Otherwise
+    sample_index is an Elias-delta string/bytes -> (samples[-1:], code_length,
+    index, samples) with samples the index + 1 candidates."""
+    from .misc import stateless_normal_sample
+    dev = _device_of(p_loc, p_scale)
+    pl, ps = _f32(p_loc, dev, "p_loc"), _f32(p_scale, dev, "p_scale")
+    d = pl.numel()
+    if use_index:
+        index = int(sample_index) - 1
+        row = importance_decode_blocks([index], pl, ps, [0, d], seed)
+        return _like_input(row.reshape(1, d), p_loc)
+    num, code_length = elias_delta_decode(sample_index)
+    index = num - 1
+    samples = stateless_normal_sample(pl, ps, index + 1, seed)
+    return (_like_input(samples[-1:].reshape(1, d), p_loc), code_length, index,
+            _like_input(samples.reshape(index + 1, d), p_loc))
+
+
+def quantize_quint16(x, mn=QUANT_MIN, mx=QUANT_MAX):
+    """tf.quantization.quantize(x, mn, mx, tf.quint16) (MIN_COMBINED, float32):
+    uint16((clamp(x) - mn) * float32(65535 / (mx - mn)) + 0.5f)."""
+    x = np.asarray(x, dtype=np.float32)
+    scale = np.float32((65535.0 - 0.0) / (float(mx) - float(mn)))
+    v = np.maximum(np.minimum(x, np.float32(mx)), np.float32(mn))
+    t = (v - np.float32(mn)) * scale
+    t = t + np.float32(0.5)
+    return t.astype(np.uint16)
+
+
+def dequantize_quint16(q, mn=QUANT_MIN, mx=QUANT_MAX):
+    """tf.quantization.dequantize(q, mn, mx) for quint16 (MIN_COMBINED, float32)."""
+    sf = np.float32((np.float32(mx) - np.float32(mn)) / np.float32(65535.0))
+    return (np.asarray(q, dtype=np.uint16).astype(np.float32) * sf + np.float32(mn)).astype(
+        np.float32)
+
+
+def _outlier_target_draw(dev, q_loc, q_scale, seed):
+    from .misc import stateless_normal_sample
+    s = int(np.int32(np.uint32((int(seed) - 1) & 0xFFFFFFFF)))
+    return stateless_normal_sample(q_loc, q_scale, 1, s).reshape(-1)
+
+
+def code_grouped_importance_sample(sess, target, proposal, seed, n_bits_per_group,
+                                   max_group_size_bits=4, dim_kl_bit_limit=12,
+                                   return_group_indices_only=False, return_indices=False,
+                                   return_indices_only=False):
+    """:112-274.  Returns (sample np.float32 [D], bitcode str | indices,
+    group_start_indices np.ndarray, outlier_extras (indices int64, quint16))."""
+    if not _is_float32(target.loc) or not _is_float32(target.scale):
+        raise Exception("Target datatype must be float32!")
+    if not _is_float32(proposal.loc) or not _is_float32(proposal.scale):
+        raise Exception("Proposal datatype must be float32!")
+    lib = _lib.load()
+    dev = _device_of(target.loc, target.scale, proposal.loc, proposal.scale)
+    q_loc, q_scale = _f32(target.loc, dev, "target.loc"), _f32(target.scale, dev, "target.scale")
+    p_loc, p_scale = _f32(proposal.loc, dev, "proposal.loc"), _f32(proposal.scale, dev,
+                                                                   "proposal.scale")
+    D = p_loc.numel()
+    zeros = torch.zeros(D, dtype=torch.float32, device=dev)
+    ones = torch.ones(D, dtype=torch.float32, device=dev)
+    # :137-138 standardise
+    t_loc = torch.empty(D, dtype=torch.float32, device=dev)
+    t_scale = torch.empty(D, dtype=torch.float32, device=dev)
+    _lib.check(lib.cwq_standardise(_ptr(q_loc), _ptr(q_scale), _ptr(p_loc), _ptr(p_scale), D,
+                                   _ptr(t_loc), _ptr(t_scale), _stream(dev)), "cwq_standardise")
+    # :142 kl_bits = KL(target || proposal) / ln 2 (float32)
+    kl_bits = _kl(dev, q_loc, q_scale, p_loc, p_scale).cpu().numpy() / np.float32(np.log(2))
+    keep = kl_bits <= dim_kl_bit_limit
+    keep_d = torch.from_numpy(keep).to(dev)
+    t_loc = torch.where(keep_d, t_loc, zeros)                      # :144
+    t_scale = torch.where(keep_d, t_scale, ones)                   # :145
+    outlier_indices = np.nonzero(~keep)[0].astype(np.int64)       # :148
+    target_samples = _outlier_target_draw(dev, q_loc, q_scale, seed)  # :150 (see docstring)
+    outlier_samples = quantize_quint16(
+        target_samples.cpu().numpy()[outlier_indices])           # :153-156
+    outlier_extras = (outlier_indices, outlier_samples)
+    # :160-163 KL of the standardised target vs N(0, 1)
+    kl_divs = _kl(dev, t_loc, t_scale, zeros, ones).cpu().numpy()
+    if VERBOSE:
+        total_kl_bits = np.sum(kl_divs) / np.log(2)
+        print("Total KL to split up: {:.2f} bits, "
+              "maximum bits per group: {}, "
+              "estimated number of groups: {},"
+              "coding {} dimensions".format(total_kl_bits, n_bits_per_group,
+                                            total_kl_bits // n_bits_per_group + 1, D))
+    starts = importance_group_starts(kl_divs, n_bits_per_group, max_group_size_bits)
+    group_start_indices = np.array(starts)
+    if return_group_indices_only:
+        return group_start_indices, _group_kls(kl_divs, starts)
+    n_samples = num_samples_plan(kl_divs, starts)
+    idx, sample = importance_encode_blocks(t_loc, t_scale, zeros, ones, starts, n_samples, seed)
+    indices = tuple(int(v) + 1 for v in idx.cpu().numpy())
+    if return_indices_only:
+        return indices
+    out = torch.empty(D, dtype=torch.float32, device=dev)         # :265 rescale
+    _lib.check(lib.cwq_destandardise(_ptr(sample), _ptr(p_loc), _ptr(p_scale), D, _ptr(out),
+                                     _stream(dev)), "cwq_destandardise")
+    sample_h = np.where(keep, out.cpu().numpy(), target_samples.cpu().numpy())  # :267
+    sample_h = sample_h.astype(np.float32)
+    if return_indices:
+        return sample_h, indices, group_start_indices, outlier_extras
+    bitcode = ''.join(elias_delta_code(i) for i in indices)
+    return sample_h, bitcode, group_start_indices, outlier_extras
+
+
+def _group_kls(kl_divs, starts):
+    """The reference's group_kls list (:192): the running group KL in bits at
+    every boundary (print-only in the coder)."""
+    out = []
+    cur = np.float32(0)
+    for a, b in zip(starts[:-1], starts[1:]):
+        out.append(cur / np.log(2))
+        cur = np.float32(0)
+        for v in np.asarray(kl_divs, np.float32)[a:b]:
+            cur = np.float32(cur + v)
+    return out
+
+
+def decode_grouped_importance_sample(sess, bitcode, group_start_indices, proposal,
+                                     n_bits_per_group, seed, outlier_indices, outlier_samples,
+                                     use_indices=False):
+    """:277-363.  group_start_indices WITHOUT the trailing D (the reference
+    appends it, :294).  Returns np.float32 [D]."""
+    if not _is_float32(proposal.loc) or not _is_float32(proposal.scale):
+        raise Exception("Proposal datatype must be float32!")
+    lib = _lib.load()
+    dev = _device_of(proposal.loc, proposal.scale)
+    p_loc, p_scale = _f32(proposal.loc, dev, "proposal.loc"), _f32(proposal.scale, dev,
+                                                                   "proposal.scale")
+    D = p_loc.numel()
+    starts = [int(s) for s in np.asarray(group_start_indices).reshape(-1)] + [D]
+    G = len(starts) - 1
+    if use_indices:
+        index = [int(bitcode[i]) - 1 for i in range(G)]
+    else:
+        code = bitcode.encode("ascii") if isinstance(bitcode, str) else bytes(bitcode)
+        index = []
+        for _ in range(G):                                          # :325-336
+            if not code:
+                raise ValueError("bitcode exhausted before the last group")
+            num, codelength = elias_delta_decode(code)
+            index.append(num - 1)
+            code = code[codelength:]
+    zeros = torch.zeros(D, dtype=torch.float32, device=dev)
+    ones = torch.ones(D, dtype=torch.float32, device=dev)
+    sample = importance_decode_blocks(index, zeros, ones, starts, seed)
+    out = torch.empty(D, dtype=torch.float32, device=dev)          # :347 rescale
+    _lib.check(lib.cwq_destandardise(_ptr(sample), _ptr(p_loc), _ptr(p_scale), D, _ptr(out),
+                                     _stream(dev)), "cwq_destandardise")
+    sample_h = out.cpu().numpy()
+    # :351-361 dequantise outliers and put them back where the update is non-zero
+    deq = dequantize_quint16(outlier_samples)
+    updates = np.zeros(D, dtype=np.float32)
+    updates[np.asarray(outlier_indices, dtype=np.int64).reshape(-1)] = deq
+    return np.where(updates == 0, sample_h, updates).astype(np.float32)

@@ -7,6 +7,7 @@
 #include <stdint.h>
 #include <stdarg.h>
 #include <stdio.h>
+#include <math.h>
 #include <string.h>
 
 #include "../../include/cwq.h"
@@ -71,6 +72,47 @@ void choose_tiling(int64_t nb, int64_t n_cand, int64_t* tiles_per_block, int64_t
   if (cpt < 256) cpt = 256;
   *cand_per_tile = cpt;
   *tiles_per_block = (n_cand + cpt - 1) / cpt;
+}
+
+// Eigen 3.3 AVX inner-dim sum order, host side.
+float eigen_sum(const float* x, int64_t d) {
+  const int64_t vec = (d / 8) * 8;
+  float p[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  for (int64_t j = 0; j < vec; j += 8)
+    for (int l = 0; l < 8; ++l) p[l] = p[l] + x[j + l];
+  float t = 0.0f;
+  for (int64_t j = vec; j < d; ++j) t = t + x[j];
+  const float q0 = p[0] + p[4], q1 = p[1] + p[5], q2 = p[2] + p[6], q3 = p[3] + p[7];
+  return t + ((q0 + q2) + (q1 + q3));
+}
+
+// coded_greedy_sampler.py:207-252 (strict=false) and
+// coded_importance_sampler.py:178-203 (strict=true).
+int64_t group_starts_impl(const float* kl, int64_t D, int64_t size_threshold, double n_nats,
+                          int64_t* starts, int64_t cap, bool strict) {
+  if (D < 0 || (D > 0 && !kl) || !starts || cap < 2)
+    return fail(CWQ_ERR_INVALID, "group starts: bad arguments");
+  int64_t ns = 0;
+  starts[ns++] = 0;
+  int64_t cur_size = 0;
+  float cur_kl = 0.0f;  // numpy float32 scalar accumulator
+  for (int64_t i = 0; i < D; ++i) {
+    const float s = cur_kl + kl[i];  // float32 + float32
+    const bool over = strict ? ((double)s > n_nats) : ((double)s >= n_nats);
+    if (cur_size >= size_threshold || over || i == D - 1) {
+      if (ns >= cap) return fail(CWQ_ERR_INVALID, "group starts: cap too small");
+      starts[ns++] = i;
+      cur_size = 1;
+      cur_kl = kl[i];
+    } else {
+      cur_kl = s;
+      cur_size += 1;
+    }
+  }
+  if (ns >= cap) return fail(CWQ_ERR_INVALID, "group starts: cap too small");
+  starts[ns++] = D;
+  ok();
+  return ns;
 }
 
 int check_common(int n_bits, int n_steps, int64_t nb) {
@@ -243,29 +285,64 @@ int cwq_destandardise(const float* sample, const float* p_loc, const float* p_sc
 
 int64_t cwq_group_starts(const float* kl, int64_t D, int64_t size_threshold, double n_nats,
                          int64_t* starts, int64_t cap) {
-  if (D < 0 || (D > 0 && !kl) || !starts || cap < 2)
-    return fail(CWQ_ERR_INVALID, "cwq_group_starts: bad arguments");
-  int64_t ns = 0;
-  starts[ns++] = 0;
-  int64_t cur_size = 0;
-  float cur_kl = 0.0f;  // numpy float32 scalar accumulator (:224, :243)
-  for (int64_t i = 0; i < D; ++i) {
-    const float s = cur_kl + kl[i];  // float32 + float32
-    // :230-234  group_bits >= max bits | f32 sum (as f64) >= n_nats | last dim
-    if (cur_size >= size_threshold || (double)s >= n_nats || i == D - 1) {
-      if (ns >= cap) return fail(CWQ_ERR_INVALID, "cwq_group_starts: cap too small");
-      starts[ns++] = i;
-      cur_size = 1;
-      cur_kl = kl[i];
-    } else {
-      cur_kl = s;
-      cur_size += 1;
-    }
+  return group_starts_impl(kl, D, size_threshold, n_nats, starts, cap, false);
+}
+
+int64_t cwq_importance_group_starts(const float* kl, int64_t D, int64_t size_threshold,
+                                    double n_nats, int64_t* starts, int64_t cap) {
+  return group_starts_impl(kl, D, size_threshold, n_nats, starts, cap, true);
+}
+
+int cwq_importance_plan(const float* kl, const int64_t* starts, int64_t ng, int64_t* n_samples) {
+  if (ng < 0 || (ng > 0 && (!kl || !starts || !n_samples)))
+    return fail(CWQ_ERR_INVALID, "cwq_importance_plan: bad arguments");
+  for (int64_t g = 0; g < ng; ++g) {
+    const int64_t a = starts[g], b = starts[g + 1];
+    if (b < a) return fail(CWQ_ERR_INVALID, "cwq_importance_plan: starts not sorted");
+    const float total = eigen_sum(kl + a, b - a);            // tf.reduce_sum(kls)
+    const float e = ceilf(expf(total));                       // tf.math.ceil(tf.exp(.))
+    n_samples[g] = (int64_t)(int32_t)(e == e && e < 2147483648.0f ? e : -2147483648.0f);
   }
-  if (ns >= cap) return fail(CWQ_ERR_INVALID, "cwq_group_starts: cap too small");
-  starts[ns++] = D;  // :252
-  ok();
-  return ns;
+  return ok();
+}
+
+size_t cwq_importance_workspace_size(int64_t nb, int64_t total_dims) {
+  if (nb < 0 || total_dims < 0) return 0;
+  return cwq::importance_workspace_size(nb, total_dims);
+}
+
+int cwq_importance_encode(const float* t_loc, const float* t_scale, const float* p_loc,
+                          const float* p_scale, const int64_t* block_off,
+                          const int64_t* n_samples, int64_t nb, int64_t total_dims, int32_t seed,
+                          int64_t block_id_base, int64_t* out_index, float* out_sample,
+                          void* workspace, size_t workspace_bytes, void* stream) {
+  if (nb < 0 || total_dims < 0) return fail(CWQ_ERR_INVALID, "negative size");
+  if (nb > 0 && (!block_off || !n_samples || !out_index))
+    return fail(CWQ_ERR_INVALID, "null pointer");
+  if (total_dims > 0 && (!t_loc || !t_scale || !p_loc || !p_scale || !out_sample))
+    return fail(CWQ_ERR_INVALID, "null pointer");
+  const size_t need = cwq::importance_workspace_size(nb, total_dims);
+  if (workspace_bytes < need || (need && !workspace))
+    return fail(CWQ_ERR_WORKSPACE, "workspace %zu bytes < required %zu", workspace_bytes, need);
+  hipError_t e = cwq::launch_importance_encode(t_loc, t_scale, p_loc, p_scale, block_off,
+                                               n_samples, nb, total_dims, seed, block_id_base,
+                                               out_index, out_sample, workspace,
+                                               (hipStream_t)stream);
+  if (e != hipSuccess) return hip_fail(e, "cwq_importance_encode");
+  return ok();
+}
+
+int cwq_importance_decode(const int64_t* index, const float* p_loc, const float* p_scale,
+                          const int64_t* block_off, int64_t nb, int64_t total_dims, int32_t seed,
+                          int64_t block_id_base, float* out_sample, void* stream) {
+  if (nb < 0 || total_dims < 0) return fail(CWQ_ERR_INVALID, "negative size");
+  if (nb > 0 && (!block_off || !index)) return fail(CWQ_ERR_INVALID, "null pointer");
+  if (total_dims > 0 && (!p_loc || !p_scale || !out_sample))
+    return fail(CWQ_ERR_INVALID, "null pointer");
+  hipError_t e = cwq::launch_importance_decode(index, p_loc, p_scale, block_off, nb, seed,
+                                               block_id_base, out_sample, (hipStream_t)stream);
+  if (e != hipSuccess) return hip_fail(e, "cwq_importance_decode");
+  return ok();
 }
 
 int cwq_profile_set_eval_events(void* start_event, void* stop_event) {

@@ -1,0 +1,199 @@
+// cwq_device.h -- device helpers shared by the gfx950 kernels (greedy and
+// importance coders): LDS log table, wave reductions, block spans, the
+// device-tuned Philox / Box-Muller / division, and the Eigen-order row
+// evaluator.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "cwq_math.h"
+
+namespace cwq {
+
+static __constant__ double kLogTabConst[32] = CWQ_LOGF_TAB_INIT;
+
+__device__ __forceinline__ void fill_logtab(double* lds) {
+  if (threadIdx.x < 32) lds[threadIdx.x] = kLogTabConst[threadIdx.x];
+  __syncthreads();
+}
+
+__device__ __forceinline__ uint32_t wave_id() {
+  return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+}
+
+__device__ __forceinline__ uint64_t wave_max_u64(uint64_t v) {
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) {
+    uint64_t o = __shfl_xor(v, off, 64);
+    v = o > v ? o : v;
+  }
+  return v;
+}
+
+// ---------------------------------------------------------------------------
+// Device-tuned arithmetic.  Same results as the portable restatement in
+// cwq_math.h (the Box-Muller pieces are verified exhaustively on the GPU by
+// tests/test_gpu.py via cwq_selftest_bm_tables), fewer instructions:
+//   * Philox: the two 3-input XORs of a round are one v_bitop3_b32 each.
+//   * sqrt for the Box-Muller radius: the argument -2 logf(u1) lies in
+//     [2.4e-7, 32.3] (normal, finite), so the correctly rounded sqrt is
+//     v_sqrt_f32 plus the two one-ulp corrections, without the denormal
+//     scaling and special-case fixups of the general sequence.
+//   * angle: Uint32ToFloat(x1) = m * 2^-23 exactly, so
+//     RN64(2pi * U) = RN64((2pi * 2^-23) * m) and m converts exactly.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ U4 philox10_dev(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
+                                           uint32_t k0, uint32_t k1) {
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    const uint64_t p0 = (uint64_t)kPhiloxM0 * c0;
+    const uint64_t p1 = (uint64_t)kPhiloxM1 * c2;
+    const uint32_t n0 = __builtin_amdgcn_bitop3_b32((uint32_t)(p1 >> 32), c1, k0, 0x96);
+    const uint32_t n2 = __builtin_amdgcn_bitop3_b32((uint32_t)(p0 >> 32), c3, k1, 0x96);
+    c1 = (uint32_t)p1;
+    c3 = (uint32_t)p0;
+    c0 = n0;
+    c2 = n2;
+    k0 += kPhiloxW0;
+    k1 += kPhiloxW1;
+  }
+  return U4{c0, c1, c2, c3};
+}
+
+__device__ __forceinline__ U4 philox_block_dev(const PhiloxStream& s, uint64_t grp) {
+  return philox10_dev((uint32_t)grp, (uint32_t)(grp >> 32), s.c2, s.c3, s.k0, s.k1);
+}
+
+__device__ __forceinline__ float sqrt_cr_bm(float x) {
+  const float s = __builtin_amdgcn_sqrtf(x);
+  const float sd = u2f(f2u(s) - 1u);
+  const float su = u2f(f2u(s) + 1u);
+  const float rd = __builtin_fmaf(-sd, s, x);
+  const float ru = __builtin_fmaf(-su, s, x);
+  const float t = (rd <= 0.0f) ? sd : s;
+  return (ru > 0.0f) ? su : t;
+}
+
+__device__ __forceinline__ float bm_radius_dev(uint32_t x0, const double* logtab) {
+  float u1 = uint32_to_float(x0);
+  u1 = u1 < 1.0e-7f ? 1.0e-7f : u1;
+  return sqrt_cr_bm(-2.0f * logf_core(u1, logtab));
+}
+
+__device__ __forceinline__ float bm_angle_dev(uint32_t x1) {
+  return (float)((double)(x1 & 0x7fffffu) * 0x1.921fb54442d18p-21);
+}
+
+__device__ __forceinline__ void box_muller_dev(uint32_t x0, uint32_t x1, const double* logtab,
+                                               float& f0, float& f1) {
+  const float u2 = bm_radius_dev(x0, logtab);
+  float s, c;
+  sincosf_pos(bm_angle_dev(x1), s, c);
+  f0 = s * u2;
+  f1 = c * u2;
+}
+
+__device__ __forceinline__ F4 normal4_dev(const PhiloxStream& s, uint64_t grp,
+                                          const double* logtab) {
+  const U4 x = philox_block_dev(s, grp);
+  F4 z;
+  box_muller_dev(x.x, x.y, logtab, z.a, z.b);
+  box_muller_dev(x.z, x.w, logtab, z.c, z.d);
+  return z;
+}
+
+// Correctly rounded a / b for 2^-60 <= |a| <= 2^60 (or a == 0) and
+// 2^-60 <= b <= 2^60, given y = RN(1/b).  q0 = RN(a y) is within 2 ulps;
+// one residual step brings q1 within 1 ulp; with q1 within 1 ulp and y within
+// half an ulp of 1/b, the residual b*q1 - a is exact and the final fused step
+// rounds to RN(a/b) (Markstein's theorem).  The ranges keep
+// every intermediate normal.  Callers route other operands to IEEE division.
+__device__ __forceinline__ float div_rn_markstein(float a, float b, float y) {
+  const float q0 = a * y;
+  const float r0 = __builtin_fmaf(-b, q0, a);
+  const float q1 = __builtin_fmaf(r0, y, q0);
+  const float r1 = __builtin_fmaf(-b, q1, a);
+  return __builtin_fmaf(r1, y, q1);
+}
+__device__ __forceinline__ bool markstein_ok(float a) {
+  const float m = __builtin_fabsf(a);
+  return (m >= 0x1p-60f && m <= 0x1p60f) || m == 0.0f;
+}
+__device__ __forceinline__ bool markstein_ok_den(float b) {
+  return b >= 0x1p-60f && b <= 0x1p60f;
+}
+
+struct BlockSpan {
+  int64_t off;
+  int64_t d;
+};
+
+__device__ __forceinline__ BlockSpan block_span(const int64_t* __restrict__ block_off,
+                                                int64_t ud, int64_t g) {
+  if (block_off == nullptr) return BlockSpan{g * ud, ud};
+  int64_t a = block_off[g];
+  int64_t b = block_off[g + 1];
+  return BlockSpan{a, b - a};
+}
+
+__device__ __forceinline__ int32_t block_seed(int32_t seed, int64_t block_id) {
+  return (int32_t)((uint32_t)seed + (uint32_t)block_id);
+}
+
+__device__ __forceinline__ uint32_t ord_f32(float v) {
+  const uint32_t b = f2u(v);
+  return (b & 0x80000000u) ? ~b : (b | 0x80000000u);
+}
+__device__ __forceinline__ float unord_f32(uint32_t o) {
+  return u2f((o & 0x80000000u) ? (o & 0x7fffffffu) : ~o);
+}
+__device__ __forceinline__ float wave_max_f32(float v) {
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) v = fmaxf(v, __shfl_xor(v, off, 64));
+  return v;
+}
+// smallest float >= b (+inf for non-finite b: such a bound never drops anything)
+__device__ __forceinline__ float round_up_f32(double b) {
+  if (!(b == b) || b > 3.0e38 || b < -3.0e38) return __builtin_inff();
+  float f = (float)b;
+  if ((double)f < b) {
+    const uint32_t u = f2u(f);
+    f = (f >= 0.0f) ? u2f(f == 0.0f ? 1u : u + 1u) : u2f(u - 1u);
+  }
+  return f;
+}
+
+template <int DC, class ElemF>
+__device__ __forceinline__ float eval_row_f(const PhiloxStream& st, uint64_t kbase, int64_t d_rt,
+                                            int align_rt, const double* logtab, ElemF&& val) {
+  const int64_t d = DC > 0 ? (int64_t)DC : d_rt;
+  const int align = (DC > 0 && (DC % 4) == 0) ? 0 : align_rt;
+  const int64_t vec = d & ~(int64_t)7;
+  float p[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  F4 z = {0.f, 0.f, 0.f, 0.f};
+
+  auto elem = [&](int64_t e) -> float {
+    const int w = (align + (int)(e & 3)) & 3;  // wave-uniform
+    if (w == 0 || e == 0) z = normal4_dev(st, (kbase + (uint64_t)e) >> 2, logtab);
+    const float zz = w == 0 ? z.a : (w == 1 ? z.b : (w == 2 ? z.c : z.d));
+    return val(e, zz);
+  };
+
+  for (int64_t j = 0; j < vec; j += 8) {
+#pragma unroll
+    for (int l = 0; l < 8; ++l) p[l] = p[l] + elem(j + l);
+  }
+  float t = 0.0f;
+  for (int64_t j = vec; j < d; ++j) t = t + elem(j);
+  const float q0 = p[0] + p[4], q1 = p[1] + p[5], q2 = p[2] + p[6], q3 = p[3] + p[7];
+  return t + ((q0 + q2) + (q1 + q3));
+}
+
+static inline unsigned grid_for(int64_t work, int64_t per_block, unsigned cap) {
+  int64_t g = (work + per_block - 1) / per_block;
+  if (g < 1) g = 1;
+  if (g > cap) g = cap;
+  return (unsigned)g;
+}
+
+}  // namespace cwq

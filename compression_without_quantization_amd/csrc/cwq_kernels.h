@@ -50,6 +50,17 @@ hipError_t launch_kl(const float* q_loc, const float* q_scale, const float* p_lo
 hipError_t launch_destandardise(const float* sample, const float* p_loc, const float* p_scale,
                                 int64_t n, float* out, hipStream_t stream);
 
+size_t importance_workspace_size(int64_t nb, int64_t total_dims);
+hipError_t launch_importance_encode(const float* t_loc, const float* t_scale, const float* p_loc,
+                                    const float* p_scale, const int64_t* block_off,
+                                    const int64_t* n_samples, int64_t nb, int64_t total_dims,
+                                    int32_t seed, int64_t block_id_base, int64_t* out_index,
+                                    float* out_sample, void* workspace, hipStream_t stream);
+hipError_t launch_importance_decode(const int64_t* index, const float* p_loc,
+                                    const float* p_scale, const int64_t* block_off, int64_t nb,
+                                    int32_t seed, int64_t block_id_base, float* out_sample,
+                                    hipStream_t stream);
+
 hipError_t launch_selftest_bm(uint32_t m0, int64_t count, float* rad, float* sn, float* cs,
                               hipStream_t stream);
 hipError_t launch_selftest_div(const float* a, const float* b, int64_t n, float* out,

@@ -132,6 +132,39 @@ int cwq_destandardise(const float* sample, const float* p_loc, const float* p_sc
 int64_t cwq_group_starts(const float* kl, int64_t D, int64_t size_threshold, double n_nats,
                          int64_t* starts, int64_t cap);
 
+/* ---- Importance sampler (code/coded_importance_sampler.py) ------------- */
+/* Workspace bytes for cwq_importance_encode. */
+size_t cwq_importance_workspace_size(int64_t nb, int64_t total_dims);
+
+/* code_importance_sample (:29-79) for nb CSR groups at once.  Group g draws
+ * n_samples[g] (device int64) candidates x = p_loc + p_scale*z from the
+ * stateless stream with seed (seed + block_id_base + g) -- the group seed
+ * itself (:55, :243) -- scores sum_j log q(x_j) - log p(x_j) (:60) and writes
+ * the 0-based argmax out_index[g] (device int64; the reference codes
+ * index + 1 with Elias-delta) and that candidate into out_sample. */
+int cwq_importance_encode(const float* t_loc, const float* t_scale, const float* p_loc,
+                          const float* p_scale, const int64_t* block_off,
+                          const int64_t* n_samples, int64_t nb, int64_t total_dims, int32_t seed,
+                          int64_t block_id_base, int64_t* out_index, float* out_sample,
+                          void* workspace, size_t workspace_bytes, void* stream);
+
+/* decode_importance_sample (:82-109): the last of index+1 samples, i.e. row
+ * `index` of group g's stream. */
+int cwq_importance_decode(const int64_t* index, const float* p_loc, const float* p_scale,
+                          const int64_t* block_off, int64_t nb, int64_t total_dims, int32_t seed,
+                          int64_t block_id_base, float* out_sample, void* stream);
+
+/* HOST (:178-203): the importance coder's partition; as cwq_group_starts but
+ * with the reference's strict comparisons (`group_bits > max bits`,
+ * `kl_sum > n_nats`).  size_threshold: the smallest s with
+ * np.log(s + 1) / np.log(2) > max_group_size_bits. */
+int64_t cwq_importance_group_starts(const float* kl, int64_t D, int64_t size_threshold,
+                                    double n_nats, int64_t* starts, int64_t cap);
+
+/* HOST (:48-51): n_samples[g] = int32(ceil(expf(sum of group g's float32 KLs in
+ * Eigen inner-dim order))), for groups [starts[g], starts[g+1]) of HOST kl. */
+int cwq_importance_plan(const float* kl, const int64_t* starts, int64_t ng, int64_t* n_samples);
+
 /* Diagnostics (used by the parity tests): evaluate the device restatement of
  * the Box-Muller transcendentals for the 23-bit mantissas m0 .. m0+count-1:
  *   radius[i] = sqrtf(-2 logf(max(m*2^-23, 1e-7f)))    (BoxMullerFloat u2)

@@ -464,3 +464,135 @@ CWQO_API void cwqo_logf_table(const float* x, int64_t n, float* out) {
 #endif
   for (int64_t i = 0; i < n; ++i) out[i] = logf(x[i]);
 }
+
+/* ------------------------------------------------------------------------ */
+/* Importance sampler (code/coded_importance_sampler.py).                    */
+/* ------------------------------------------------------------------------ */
+/* :48-51 num_samples = int32(ceil(exp(reduce_sum(KL(target || proposal)))))
+ * (float32 KL per dim, Eigen-order sum, glibc expf, ceilf). */
+CWQO_API int64_t cwqo_importance_num_samples(const float* t_loc, const float* t_scale,
+                                             const float* p_loc, const float* p_scale,
+                                             int64_t d) {
+  float* kl = (float*)malloc((size_t)(d > 0 ? d : 1) * sizeof(float));
+  if (!kl) return -1;
+  cwqo_kl_normal_normal(t_loc, t_scale, p_loc, p_scale, d, kl);
+  float total = cwqo_eigen_rowsum(kl, d);
+  free(kl);
+  float e = ceilf(expf(total));
+  return (int64_t)(int32_t)e;
+}
+
+/* Given per-dim KLs and group starts (group g = [s[g], s[g+1])), the same
+ * count per group from the precomputed KLs. */
+CWQO_API void cwqo_importance_plan(const float* kl, const int64_t* starts, int64_t ng,
+                                   int64_t* n_samples) {
+  for (int64_t g = 0; g < ng; ++g) {
+    float total = cwqo_eigen_rowsum(kl + starts[g], starts[g + 1] - starts[g]);
+    n_samples[g] = (int64_t)(int32_t)ceilf(expf(total));
+  }
+}
+
+/* code_importance_sample for ONE block (:29-79): samples = stateless_normal_sample(
+ * p_loc, p_scale, num_samples, seed) (note: `seed` itself, not 1000*seed+i);
+ * weights = reduce_sum(target.log_prob(x) - proposal.log_prob(x), axis=1);
+ * index = argmax.  Writes the 0-based index and best_sample [d]. */
+CWQO_API int cwqo_importance_encode_block(const float* t_loc, const float* t_scale,
+                                          const float* p_loc, const float* p_scale, int64_t d,
+                                          int32_t seed, int64_t n_samples, int64_t* out_index,
+                                          float* out_sample) {
+  if (d < 0 || n_samples < 1) return -1;
+  size_t db = (size_t)(d > 0 ? d : 1) * sizeof(float);
+  float* ct = (float*)malloc(db);
+  float* cp = (float*)malloc(db);
+  float* row = (float*)malloc(db);
+  if (!ct || !cp || !row) { free(ct); free(cp); free(row); return -2; }
+  for (int64_t j = 0; j < d; ++j) {
+    ct[j] = cwqo_log_normalization(t_scale[j]);
+    cp[j] = cwqo_log_normalization(p_scale[j]);
+  }
+  normal_stream st;
+  memset(&st, 0, sizeof(st));
+  cwqo_generate_key(seed, 42, st.key, st.ctr);
+  int64_t best_idx = 0;
+  float best_val = -FLT_MAX;
+  for (int64_t n = 0; n < n_samples; ++n) {
+    for (int64_t j = 0; j < d; ++j) {
+      float z = stream_normal(&st, (uint64_t)(n * d + j));
+      float x = p_scale[j] * z;  /* misc.py:14 */
+      x = p_loc[j] + x;          /* misc.py:15 */
+      float lt = log_prob_c(x, t_loc[j], t_scale[j], ct[j]);
+      float lp = log_prob_c(x, p_loc[j], p_scale[j], cp[j]);
+      row[j] = lt - lp;          /* :60 */
+    }
+    float v = cwqo_eigen_rowsum(row, d);
+    if (v > best_val) { best_val = v; best_idx = n; }
+  }
+  for (int64_t j = 0; j < d; ++j) {
+    float z = stream_normal(&st, (uint64_t)(best_idx * d + j));
+    float x = p_scale[j] * z;
+    out_sample[j] = p_loc[j] + x; /* :63 samples[index] */
+  }
+  *out_index = best_idx;
+  free(ct); free(cp); free(row);
+  return 0;
+}
+
+/* decode_importance_sample (:82-109): the last of index+1 samples = row index. */
+CWQO_API void cwqo_importance_decode_block(int64_t index, const float* p_loc,
+                                           const float* p_scale, int64_t d, int32_t seed,
+                                           float* out_sample) {
+  normal_stream st;
+  memset(&st, 0, sizeof(st));
+  cwqo_generate_key(seed, 42, st.key, st.ctr);
+  for (int64_t j = 0; j < d; ++j) {
+    float z = stream_normal(&st, (uint64_t)(index * d + j));
+    float x = p_scale[j] * z;
+    out_sample[j] = p_loc[j] + x;
+  }
+}
+
+/* Batched over CSR groups with per-group counts; group g uses seed+base+g (:243). */
+CWQO_API int cwqo_importance_encode(const float* t_loc, const float* t_scale, const float* p_loc,
+                                    const float* p_scale, const int64_t* block_off, int64_t nb,
+                                    const int64_t* n_samples, int32_t seed,
+                                    int64_t block_id_base, int64_t* out_index,
+                                    float* out_sample, int nthreads) {
+  int err = 0;
+#ifdef _OPENMP
+  if (nthreads > 0) omp_set_num_threads(nthreads);
+#pragma omp parallel for schedule(dynamic, 1) reduction(| : err)
+#endif
+  for (int64_t g = 0; g < nb; ++g) {
+    int64_t o = block_off[g], d = block_off[g + 1] - block_off[g];
+    int32_t sg = (int32_t)((uint32_t)seed + (uint32_t)(block_id_base + g));
+    if (cwqo_importance_encode_block(t_loc + o, t_scale + o, p_loc + o, p_scale + o, d, sg,
+                                     n_samples[g], out_index + g, out_sample + o))
+      err |= 1;
+  }
+  return err ? -1 : 0;
+}
+
+/* tf.quantization.quantize(x, -30, 30, tf.quint16) (MIN_COMBINED, unsigned fast
+ * path): cast<uint16>((clamp(x) - min) * scale + 0.5f), scale = float(65535/60). */
+CWQO_API void cwqo_quantize_quint16(const float* x, int64_t n, float mn, float mx,
+                                    uint16_t* out) {
+  float scale = (float)((65535.0 - 0.0) / ((double)mx - (double)mn));
+  for (int64_t i = 0; i < n; ++i) {
+    float v = x[i] < mx ? x[i] : mx;   /* cwiseMin(max_range) */
+    v = v > mn ? v : mn;               /* cwiseMax(min_range) */
+    float t = (v - mn) * scale;
+    t = t + 0.5f;
+    out[i] = (uint16_t)t;
+  }
+}
+
+/* tf.quantization.dequantize(q, -30, 30) for quint16 (MIN_COMBINED):
+ * q * ((max - min) / 65535) + min, float32. */
+CWQO_API void cwqo_dequantize_quint16(const uint16_t* q, int64_t n, float mn, float mx,
+                                      float* out) {
+  float sf = (mx - mn) / 65535.0f;
+  for (int64_t i = 0; i < n; ++i) {
+    float t = (float)q[i] * sf;
+    out[i] = t + mn;
+  }
+}

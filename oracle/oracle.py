@@ -55,6 +55,13 @@ def lib():
             "cwqo_group_starts": (i64, [vp, i64, i64, f64, vp, i64]),
             "cwqo_destandardise": (None, [vp, vp, vp, i64, vp]),
             "cwqo_num_threads": (ci, []),
+            "cwqo_importance_num_samples": (i64, [vp, vp, vp, vp, i64]),
+            "cwqo_importance_plan": (None, [vp, vp, i64, vp]),
+            "cwqo_importance_encode_block": (ci, [vp, vp, vp, vp, i64, i32, i64, vp, vp]),
+            "cwqo_importance_decode_block": (None, [i64, vp, vp, i64, i32, vp]),
+            "cwqo_importance_encode": (ci, [vp, vp, vp, vp, vp, i64, vp, i32, i64, vp, vp, ci]),
+            "cwqo_quantize_quint16": (None, [vp, i64, f32, f32, vp]),
+            "cwqo_dequantize_quint16": (None, [vp, i64, f32, f32, vp]),
         }
         for name, (res, args) in sig.items():
             fn = getattr(L, name)
@@ -219,3 +226,100 @@ def code_grouped_greedy_sample(q_loc, q_scale, p_loc, p_scale, n_steps, n_bits_p
     idx, samp = greedy_encode(tl, ts, np.zeros(D, np.float32), np.ones(D, np.float32), starts,
                               n_bits_per_step, n_steps, seed, rho, 0, nthreads)
     return destandardise(samp, p_loc, p_scale), idx, starts
+
+
+# --------------------------------------------------------------------------
+# importance sampler (code/coded_importance_sampler.py)
+# --------------------------------------------------------------------------
+def importance_num_samples(t_loc, t_scale, p_loc, p_scale):
+    tl, ts, pl, ps = map(_f32, (t_loc, t_scale, p_loc, p_scale))
+    return int(lib().cwqo_importance_num_samples(_p(tl), _p(ts), _p(pl), _p(ps), tl.size))
+
+
+def importance_plan(kl, starts):
+    k = _f32(kl)
+    st = np.ascontiguousarray(np.asarray(starts, dtype=np.int64))
+    out = np.zeros(max(st.size - 1, 1), dtype=np.int64)
+    lib().cwqo_importance_plan(_p(k), _p(st), st.size - 1, _p(out))
+    return out[:st.size - 1]
+
+
+def importance_encode(t_loc, t_scale, p_loc, p_scale, block_off, n_samples, seed,
+                      block_id_base=0, nthreads=0):
+    tl, ts, pl, ps = map(_f32, (t_loc, t_scale, p_loc, p_scale))
+    off = np.ascontiguousarray(np.asarray(block_off, dtype=np.int64))
+    ns = np.ascontiguousarray(np.asarray(n_samples, dtype=np.int64))
+    nb = off.size - 1
+    idx = np.zeros(max(nb, 1), dtype=np.int64)
+    sample = np.zeros(tl.size, dtype=np.float32)
+    rc = lib().cwqo_importance_encode(_p(tl), _p(ts), _p(pl), _p(ps), _p(off), nb, _p(ns),
+                                      int(seed), int(block_id_base), _p(idx), _p(sample),
+                                      int(nthreads))
+    assert rc == 0, rc
+    return idx[:nb], sample
+
+
+def importance_decode_block(index, p_loc, p_scale, seed):
+    pl, ps = _f32(p_loc), _f32(p_scale)
+    out = np.zeros(pl.size, dtype=np.float32)
+    lib().cwqo_importance_decode_block(int(index), _p(pl), _p(ps), pl.size, int(seed), _p(out))
+    return out
+
+
+def quantize_quint16(x, mn=-30.0, mx=30.0):
+    v = _f32(x)
+    out = np.zeros(v.size, dtype=np.uint16)
+    lib().cwqo_quantize_quint16(_p(v), v.size, float(mn), float(mx), _p(out))
+    return out
+
+
+def dequantize_quint16(q, mn=-30.0, mx=30.0):
+    qq = np.ascontiguousarray(np.asarray(q, dtype=np.uint16))
+    out = np.zeros(qq.size, dtype=np.float32)
+    lib().cwqo_dequantize_quint16(_p(qq), qq.size, float(mn), float(mx), _p(out))
+    return out
+
+
+def importance_group_starts(kl, n_bits_per_group, max_group_size_bits):
+    """coded_importance_sampler.py:178-203, transcribed (strict comparisons)."""
+    kl = np.asarray(kl, np.float32)
+    starts = [0]
+    cur_size = 0
+    cur_kl = 0
+    n_nats = n_bits_per_group * np.log(2) - 1
+    D = kl.size
+    for idx in range(D):
+        group_bits = np.log(cur_size + 1) / np.log(2)
+        if group_bits > max_group_size_bits or cur_kl + kl[idx] > n_nats or idx == D - 1:
+            starts.append(idx)
+            cur_size = 1
+            cur_kl = kl[idx]
+        else:
+            cur_kl += kl[idx]
+            cur_size += 1
+    return starts + [D]
+
+
+def code_grouped_importance_sample(q_loc, q_scale, p_loc, p_scale, seed, n_bits_per_group,
+                                   max_group_size_bits=4, dim_kl_bit_limit=12, nthreads=0):
+    """Whole grouped importance pipeline (:112-274) on the CPU, with the same
+    deterministic outlier draw as the product (stateless seed [seed-1, 42]).
+    Returns (sample [D], indices (index+1) list, starts list, (outlier idx, quint16))."""
+    ql, qs, pl, ps = map(_f32, (q_loc, q_scale, p_loc, p_scale))
+    D = ql.size
+    tl, ts = standardise(ql, qs, pl, ps)
+    kl_bits = kl_normal_normal(ql, qs, pl, ps) / np.float32(np.log(2))
+    keep = kl_bits <= dim_kl_bit_limit
+    tl = np.where(keep, tl, np.float32(0)).astype(np.float32)
+    ts = np.where(keep, ts, np.float32(1)).astype(np.float32)
+    out_idx = np.nonzero(~keep)[0].astype(np.int64)
+    s1 = int(np.int32(np.uint32((int(seed) - 1) & 0xFFFFFFFF)))
+    target_samples = stateless_normal_sample(ql, qs, 1, s1).reshape(-1)
+    out_q = quantize_quint16(target_samples[out_idx])
+    zeros, ones = np.zeros(D, np.float32), np.ones(D, np.float32)
+    kl_divs = kl_normal_normal(tl, ts, zeros, ones)
+    starts = importance_group_starts(kl_divs, n_bits_per_group, max_group_size_bits)
+    ns = importance_plan(kl_divs, starts)
+    idx, samp = importance_encode(tl, ts, zeros, ones, starts, ns, seed, 0, nthreads)
+    sample = np.where(keep, destandardise(samp, pl, ps), target_samples).astype(np.float32)
+    return sample, [int(i) + 1 for i in idx], starts, (out_idx, out_q)
