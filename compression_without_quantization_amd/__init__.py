@@ -5,7 +5,9 @@ code/misc.py and code/binary_io.py (bit-string helpers); every sample is
 computed by the gfx950 kernels in libcwq.so (see include/cwq.h).
 """
 from .binary_io import (bitcode_to_indices, elias_delta_code, elias_delta_decode,
-                        from_bit_string, indices_to_bitcode, to_bit_string)
+                        from_bit_string, indices_to_bitcode, read_bin_code, to_bit_string,
+                        write_bin_code)
+from .coding import ArithmeticCoder
 from .coded_greedy_sampler import (Normal, code_greedy_sample, code_grouped_greedy_sample,
                                    decode, decode_blocks, decode_greedy_sample,
                                    decode_grouped_greedy_sample, encode, encode_blocks,
@@ -26,5 +28,6 @@ __all__ = [
     "bitcode_to_indices", "shard_range", "gather_indices", "elias_delta_code",
     "elias_delta_decode", "code_importance_sample", "decode_importance_sample",
     "code_grouped_importance_sample", "decode_grouped_importance_sample",
-    "importance_encode_blocks", "importance_decode_blocks",
+    "importance_encode_blocks", "importance_decode_blocks", "ArithmeticCoder",
+    "write_bin_code", "read_bin_code",
 ]

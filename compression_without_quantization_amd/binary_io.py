@@ -102,3 +102,83 @@ def elias_delta_decode(x):
     x = x[l + 1:]
     num = from_bit_string(x[:n_plus_one - 1][::-1] + b"1")
     return num, 2 * l + n_plus_one
+
+
+# ---------------------------------------------------------------------------
+# .miracle container (binary_io.py:69-197)
+# ---------------------------------------------------------------------------
+def _pack_bits(bits):
+    """'0'/'1' string -> bytes, MSB first, zero padded to a byte (:76-78)."""
+    if len(bits) % 8:
+        bits = bits + "0" * (8 - len(bits) % 8)
+    if not bits:
+        return b""
+    a = np.frombuffer(bits.encode("ascii"), dtype=np.uint8) - ord("0")
+    return np.packbits(a).tobytes()
+
+
+def write_bin_code(code, path, extras=None, extra_var_bits=None, var_length_extras=None,
+                   var_length_bits=None):
+    """binary_io.py:69-133: 4-byte big-endian extras, 16-bit-length variable
+    bit strings, 16-bit-length + 8-bit-width integer lists, then the message
+    bits, each section packed MSB-first with zero padding."""
+    if var_length_extras is not None:
+        if var_length_bits is None or len(var_length_extras) != len(var_length_bits):
+            raise Exception("Each var length extra needs to have a bitlength associated!")
+    out = bytearray()
+    if extras is not None:
+        for extra in extras:
+            extra = int(extra)
+            eb = []
+            for _ in range(4):
+                eb.append(extra % 256)
+                extra = extra // 256
+            out += bytes(eb[::-1])
+    if extra_var_bits is not None:
+        for bits in extra_var_bits:
+            bits = ''.join(bits)
+            out += bytes([len(bits) // 256, len(bits) % 256])
+            out += _pack_bits(bits)
+    if var_length_extras is not None:
+        for extra, extra_bit_size in zip(var_length_extras, var_length_bits):
+            extra = list(extra)
+            out += bytes([len(extra) // 256, len(extra) % 256])
+            out += bytes([extra_bit_size])
+            out += _pack_bits(''.join(to_bit_string(int(item), extra_bit_size)
+                                      for item in extra))
+    out += _pack_bits(''.join(code))
+    with open(path, "wb") as f:
+        f.write(bytes(out))
+
+
+def read_bin_code(path, num_extras=0, num_extra_var_bits=0, num_var_length_extras=0,
+                  extras_bytes=4, extra_bytes=2):
+    """binary_io.py:135-197 -> (remaining message bits incl. padding, extras,
+    extra_var_bits, var_length_extras)."""
+    with open(path, "rb") as f:
+        raw = np.frombuffer(f.read(), dtype=np.uint8)
+    compressed = (np.unpackbits(raw) + ord("0")).tobytes().decode("ascii") if raw.size else ""
+    extra_bits = compressed[:num_extras * extras_bytes * 8]
+    compressed = compressed[num_extras * extras_bytes * 8:]
+    extras = [int('0b' + extra_bits[s:s + extras_bytes * 8], 2)
+              for s in range(0, num_extras * extras_bytes * 8, extras_bytes * 8)]
+    extra_var_bits = []
+    for _ in range(num_extra_var_bits):
+        bits_length = int('0b' + compressed[:extra_bytes * 8], 2)
+        compressed = compressed[extra_bytes * 8:]
+        bytes_to_read = bits_length // 8 + (1 if bits_length % 8 else 0)
+        extra_var_bits.append(compressed[:bits_length])
+        compressed = compressed[bytes_to_read * 8:]
+    var_length_extras = []
+    for _ in range(num_var_length_extras):
+        extra_length = int('0b' + compressed[:extra_bytes * 8], 2)
+        extra_bit_size = int('0b' + compressed[extra_bytes * 8:(extra_bytes + 1) * 8], 2)
+        compressed = compressed[(extra_bytes + 1) * 8:]
+        bytes_to_read = extra_bit_size * extra_length // 8
+        if extra_bit_size * extra_length % 8 != 0:
+            bytes_to_read += 1
+        extra = [from_bit_string(compressed[s:s + extra_bit_size])
+                 for s in range(0, bytes_to_read * 8, extra_bit_size)]
+        compressed = compressed[bytes_to_read * 8:]
+        var_length_extras.append(extra[:extra_length])
+    return compressed, extras, extra_var_bits, var_length_extras

@@ -1,0 +1,179 @@
+// cwq_ac.cpp -- integer arithmetic coder, the native-code equivalent of the
+// reference's only compiled component, code/coding.pyx:27-310 (SURVEY.md
+// 8(f) row 3).  Host code: the coder is a serial integer renormalisation
+// loop with nothing to parallelise, so it stays on the CPU.
+//
+// Semantics follow coding.pyx exactly:
+//   * C[i] = sum_{k<i} P[k], D[i] = C[i] + P[i], R = D[K-1] (:35-55);
+//   * interval update high = low + (width*D[s]) // R, low = low + (width*C[s]) // R
+//     with the old `low` in both (:85-89);
+//   * renormalisation on `high < half` / `low > half` (strict, as written,
+//     :92-109), middle rescaling on `low > quarter && high < 3 quarter`
+//     (:112-115), pending bits `s`, final emission (:118-123);
+//   * decoding (:129-216) stops at symbol 0 (EOF) and returns it too.
+// decode_fast's AVL search (:220-310, data_structures.py:188-215) is a binary
+// search here: the symbol containing z is the last j with
+// (width*C[j]) // R <= z - low, which is what the linear decoder (:162-181)
+// finds as well.  Products are formed in 128-bit integers, so no count
+// total can overflow (the reference's int64 arithmetic would for R > 2^31).
+#include <stdint.h>
+#include <stddef.h>
+
+#include <vector>
+
+#include "../../include/cwq.h"
+#include "cwq_kernels.h"
+
+namespace {
+
+typedef __int128 i128;
+
+struct Model {
+  std::vector<int64_t> C, D;
+  int64_t R = 0;
+};
+
+bool build_model(const int64_t* counts, int64_t K, Model* m) {
+  if (K <= 0 || !counts) return false;
+  m->C.resize((size_t)K);
+  m->D.resize((size_t)K);
+  int64_t c = 0;
+  for (int64_t i = 0; i < K; ++i) {
+    if (counts[i] < 0) return false;
+    m->C[(size_t)i] = c;
+    c += counts[i];
+    m->D[(size_t)i] = c;
+  }
+  m->R = c;
+  return c > 0;
+}
+
+inline int64_t scale(int64_t width, int64_t x, int64_t R) {
+  return (int64_t)(((i128)width * (i128)x) / (i128)R);  // non-negative: floor == trunc
+}
+
+}  // namespace
+
+extern "C" {
+
+int64_t cwq_ac_encode(const int64_t* counts, int64_t K, int precision, const int64_t* message,
+                      int64_t n, char* out_bits, int64_t cap) {
+  Model m;
+  if (precision < 3 || precision > 62 || n < 0 || (n > 0 && !message) || !build_model(counts, K, &m))
+    return cwq::set_error(CWQ_ERR_INVALID, "cwq_ac_encode: bad counts/precision/message");
+  const int64_t whole = (int64_t)1 << precision;
+  const int64_t half = (int64_t)1 << (precision - 1);
+  const int64_t quarter = (int64_t)1 << (precision - 2);
+  int64_t low = 0, high = whole;
+  int64_t s = 0;
+  int64_t nbits = 0;
+  auto emit = [&](char b) -> bool {
+    if (out_bits) {
+      if (nbits >= cap) return false;
+      out_bits[nbits] = b;
+    }
+    ++nbits;
+    return true;
+  };
+  for (int64_t k = 0; k < n; ++k) {
+    const int64_t sym = message[k];
+    if (sym < 0 || sym >= K)
+      return cwq::set_error(CWQ_ERR_INVALID, "cwq_ac_encode: symbol outside [0, K)");
+    const int64_t width = high - low;
+    high = low + scale(width, m.D[(size_t)sym], m.R);
+    low = low + scale(width, m.C[(size_t)sym], m.R);
+    while (high < half || low > half) {
+      if (high < half) {
+        if (!emit('0')) return cwq::set_error(CWQ_ERR_CAPACITY, "cwq_ac_encode: cap");
+        for (; s > 0; --s)
+          if (!emit('1')) return cwq::set_error(CWQ_ERR_CAPACITY, "cwq_ac_encode: cap");
+        low *= 2;
+        high *= 2;
+      } else {
+        if (!emit('1')) return cwq::set_error(CWQ_ERR_CAPACITY, "cwq_ac_encode: cap");
+        for (; s > 0; --s)
+          if (!emit('0')) return cwq::set_error(CWQ_ERR_CAPACITY, "cwq_ac_encode: cap");
+        low = (low - half) * 2;
+        high = (high - half) * 2;
+      }
+    }
+    while (low > quarter && high < 3 * quarter) {
+      s += 1;
+      low = (low - quarter) * 2;
+      high = (high - quarter) * 2;
+    }
+  }
+  s += 1;
+  const char first = (low <= quarter) ? '0' : '1';
+  const char rest = (low <= quarter) ? '1' : '0';
+  if (!emit(first)) return cwq::set_error(CWQ_ERR_CAPACITY, "cwq_ac_encode: cap");
+  for (; s > 0; --s)
+    if (!emit(rest)) return cwq::set_error(CWQ_ERR_CAPACITY, "cwq_ac_encode: cap");
+  cwq::set_error(CWQ_OK, "");
+  return nbits;
+}
+
+int64_t cwq_ac_decode(const int64_t* counts, int64_t K, int precision, const char* bits,
+                      int64_t nbits, int64_t* out_msg, int64_t cap) {
+  Model m;
+  if (precision < 3 || precision > 62 || nbits < 0 || (nbits > 0 && !bits) || !out_msg ||
+      !build_model(counts, K, &m))
+    return cwq::set_error(CWQ_ERR_INVALID, "cwq_ac_decode: bad counts/precision/bits");
+  const int64_t whole = (int64_t)1 << precision;
+  const int64_t half = (int64_t)1 << (precision - 1);
+  const int64_t quarter = (int64_t)1 << (precision - 2);
+  int64_t low = 0, high = whole;
+  int64_t z = 0;
+  int64_t i = 0;
+  while (i < precision && i < nbits) {
+    if (bits[i] == '1') z += (int64_t)1 << (precision - i - 1);
+    ++i;
+  }
+  int64_t nout = 0;
+  for (;;) {
+    const int64_t width = high - low;
+    const int64_t target = z - low;
+    // last j with scale(width, C[j]) <= target
+    int64_t lo = 0, hi = K;  // invariant: answer in [lo, hi)
+    if (target < 0) return cwq::set_error(CWQ_ERR_INVALID, "cwq_ac_decode: corrupt code");
+    while (hi - lo > 1) {
+      const int64_t mid = (lo + hi) >> 1;
+      if (scale(width, m.C[(size_t)mid], m.R) <= target) lo = mid; else hi = mid;
+    }
+    const int64_t j = lo;
+    const int64_t high_ = low + scale(width, m.D[(size_t)j], m.R);
+    const int64_t low_ = low + scale(width, m.C[(size_t)j], m.R);
+    if (!(low_ <= z && z < high_))  // corrupt code (the reference loops forever)
+      return cwq::set_error(CWQ_ERR_INVALID, "cwq_ac_decode: corrupt code");
+    if (nout >= cap) return cwq::set_error(CWQ_ERR_CAPACITY, "cwq_ac_decode: cap");
+    out_msg[nout++] = j;
+    high = high_;
+    low = low_;
+    if (j == 0) {  // EOF symbol
+      cwq::set_error(CWQ_OK, "");
+      return nout;
+    }
+    while (high < half || low > half) {
+      if (high < half) {
+        low *= 2;
+        high *= 2;
+        z *= 2;
+      } else {
+        low = (low - half) * 2;
+        high = (high - half) * 2;
+        z = (z - half) * 2;
+      }
+      if (i < nbits && bits[i] == '1') z += 1;
+      ++i;
+    }
+    while (low > quarter && high < 3 * quarter) {
+      low = (low - quarter) * 2;
+      high = (high - quarter) * 2;
+      z = (z - quarter) * 2;
+      if (i < nbits && bits[i] == '1') z += 1;
+      ++i;
+    }
+  }
+}
+
+}  // extern "C"

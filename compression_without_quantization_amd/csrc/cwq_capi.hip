@@ -171,6 +171,10 @@ int encode_impl(const float* t_loc, const float* t_scale, const float* p_loc,
 
 }  // namespace
 
+namespace cwq {
+int set_error(int code, const char* msg) { return fail(code, "%s", msg); }
+}  // namespace cwq
+
 extern "C" {
 
 int cwq_version(void) { return (0 << 16) | 1; }

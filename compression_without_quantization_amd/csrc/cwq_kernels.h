@@ -5,6 +5,9 @@
 
 namespace cwq {
 
+// Records `msg` for cwq_last_error() (thread-local) and returns `code`.
+int set_error(int code, const char* msg);
+
 struct EncodeArgs {
   const float* t_loc;
   const float* t_scale;

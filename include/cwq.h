@@ -53,6 +53,7 @@ extern "C" {
 #define CWQ_ERR_INVALID (-1)   /* bad argument (sizes, bits, null pointer) */
 #define CWQ_ERR_HIP (-2)       /* HIP runtime error (launch, memset) */
 #define CWQ_ERR_WORKSPACE (-3) /* workspace too small */
+#define CWQ_ERR_CAPACITY (-4)  /* output buffer too small (retry with a larger one) */
 
 #define CWQ_MAX_BITS_PER_STEP 30
 
@@ -164,6 +165,22 @@ int64_t cwq_importance_group_starts(const float* kl, int64_t D, int64_t size_thr
 /* HOST (:48-51): n_samples[g] = int32(ceil(expf(sum of group g's float32 KLs in
  * Eigen inner-dim order))), for groups [starts[g], starts[g+1]) of HOST kl. */
 int cwq_importance_plan(const float* kl, const int64_t* starts, int64_t ng, int64_t* n_samples);
+
+/* ---- Arithmetic coder (code/coding.pyx:27-310), HOST functions ---------- */
+/* ArithmeticCoder(P, precision).encode(message): writes the code as '0'/'1'
+ * chars to out_bits (if non-null, at most cap) and returns the number of bits
+ * (or a negative error).  counts: P[K] (non-negative, sum > 0); message
+ * symbols in [0, K) and, as the reference's callers do, ending with the EOF
+ * symbol 0.  precision in [3, 62] (the reference uses 32). */
+int64_t cwq_ac_encode(const int64_t* counts, int64_t K, int precision, const int64_t* message,
+                      int64_t n, char* out_bits, int64_t cap);
+
+/* .decode / .decode_fast (:129-310): decodes until the EOF symbol 0 and
+ * returns the number of symbols written to out_msg (EOF included),
+ * CWQ_ERR_CAPACITY if cap is too small, or CWQ_ERR_INVALID for a corrupt code
+ * (where the reference would loop forever). */
+int64_t cwq_ac_decode(const int64_t* counts, int64_t K, int precision, const char* bits,
+                      int64_t nbits, int64_t* out_msg, int64_t cap);
 
 /* Diagnostics (used by the parity tests): evaluate the device restatement of
  * the Box-Muller transcendentals for the 23-bit mantissas m0 .. m0+count-1:

@@ -1,0 +1,81 @@
+"""CPU tests: the C++ arithmetic coder (code/coding.pyx equivalent) against a
+line-by-line Python restatement, and the .miracle container (binary_io.py:69-197)."""
+import numpy as np
+import pytest
+
+from compression_without_quantization_amd import ArithmeticCoder, read_bin_code, write_bin_code
+from compression_without_quantization_amd import to_bit_string
+from oracle.arithmetic_coder import ArithmeticCoderRef
+
+
+def _message(rng, P, n):
+    p = np.asarray(P, float)
+    p[0] = 0
+    p /= p.sum()
+    msg = list(rng.choice(len(P), size=n, p=p)) + [0]  # callers append EOF (pln.py:515)
+    return [int(m) for m in msg]
+
+
+@pytest.mark.parametrize("case", range(6))
+def test_ac_matches_reference_restatement(cwqlib, case):
+    rng = np.random.default_rng(case)
+    K = [2, 5, 16, 300, 4096, 64][case]
+    P = rng.integers(1, 1000, K)
+    if case == 5:
+        P = np.ones(K, np.int64)
+        P[3] = 10 ** 6          # very skewed: many symbols per bit
+    n = [50, 500, 2000, 3000, 2000, 3000][case]
+    msg = _message(rng, P, n)
+    ref = ArithmeticCoderRef(P)
+    want = ref.encode(msg)
+    ac = ArithmeticCoder(P, precision=32)
+    got = ac.encode(msg)
+    assert got == want
+    assert ac.decode_fast(got) == msg
+    assert ac.decode(''.join(got)) == msg
+    if n <= 500:
+        assert ref.decode(want) == msg
+
+
+def test_ac_precision_and_empty(cwqlib):
+    P = np.array([3, 1, 1, 5])
+    for prec in (16, 24, 32, 40):
+        ac = ArithmeticCoder(P, precision=prec)
+        ref = ArithmeticCoderRef(P, precision=prec)
+        msg = [1, 2, 3, 3, 1, 0]
+        assert ac.encode(msg) == ref.encode(msg)
+        assert ac.decode_fast(ac.encode(msg)) == msg
+    assert ArithmeticCoder(P).encode([0]) == ArithmeticCoderRef(P).encode([0])
+
+
+def test_ac_rejects_corrupt(cwqlib):
+    from compression_without_quantization_amd._lib import CwqError
+    ac = ArithmeticCoder(np.array([1, 5, 5]))
+    with pytest.raises(CwqError):
+        ac.encode([3, 0])
+
+
+def test_bin_code_roundtrip_and_layout(tmp_path):
+    rng = np.random.default_rng(7)
+    code = ''.join(rng.choice(['0', '1'], 1003))
+    extras = [42, 1, 14, 20, 20, 1003, 77, 32, 48, 8, 12]
+    evb = [''.join(rng.choice(['0', '1'], 37)), ''.join(rng.choice(['0', '1'], 16))]
+    vle = [[3, 17, 255, 0, 9], [65535, 1, 2]]
+    vlb = [8, 16]
+    p = tmp_path / "x.miracle"
+    write_bin_code(code, str(p), extras=extras, extra_var_bits=evb, var_length_extras=vle,
+                   var_length_bits=vlb)
+    raw = p.read_bytes()
+    # layout: 11 x 4-byte big-endian extras first
+    assert raw[:4] == (42).to_bytes(4, "big") and raw[20:24] == (1003).to_bytes(4, "big")
+    # 16-bit length then MSB-first packed bits
+    assert raw[44:46] == bytes([0, 37])
+    assert raw[46] == int(evb[0][:8], 2)
+    msg, ex, vb, vl = read_bin_code(str(p), num_extras=11, num_extra_var_bits=2,
+                                    num_var_length_extras=2)
+    assert ex == extras and vb == evb and vl == vle
+    assert msg[:len(code)] == code and set(msg[len(code):]) <= {"0"} and len(msg) % 8 == 0
+    # items are LSB-first bit strings (to_bit_string) inside the packed stream
+    assert to_bit_string(3, 8) == "11000000"
+    with pytest.raises(Exception, match="bitlength associated"):
+        write_bin_code("1", str(p), var_length_extras=[[1]], var_length_bits=None)

@@ -15,7 +15,7 @@ declare -A V=(
 if [ "$1" = build ]; then
   mkdir -p $OUT
   for k in "${!V[@]}"; do
-    hipcc $FLAGS ${V[$k]} -o $OUT/libcwq_$k.so $CSRC/cwq_kernels.hip $CSRC/cwq_importance.hip $CSRC/cwq_capi.hip &
+    hipcc $FLAGS ${V[$k]} -o $OUT/libcwq_$k.so $CSRC/cwq_kernels.hip $CSRC/cwq_importance.hip $CSRC/cwq_capi.hip $CSRC/cwq_ac.cpp &
   done
   wait
 else
