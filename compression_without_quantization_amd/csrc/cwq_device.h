@@ -115,9 +115,11 @@ __device__ __forceinline__ float div_rn_markstein(float a, float b, float y) {
   const float r1 = __builtin_fmaf(-b, q1, a);
   return __builtin_fmaf(r1, y, q1);
 }
+// 2^-60 <= |a| < 2^60 (biased exponent 67..186) or a == +-0, branch-free.
 __device__ __forceinline__ bool markstein_ok(float a) {
-  const float m = __builtin_fabsf(a);
-  return (m >= 0x1p-60f && m <= 0x1p60f) || m == 0.0f;
+  const uint32_t u = f2u(a);
+  const uint32_t e = ((u >> 23) & 0xffu) - 67u;  // wraps below 2^-60
+  return (e < 120u) | ((u << 1) == 0u);
 }
 __device__ __forceinline__ bool markstein_ok_den(float b) {
   return b >= 0x1p-60f && b <= 0x1p60f;

@@ -308,8 +308,9 @@ __global__ void __launch_bounds__(256, CWQ_PRUNE_MIN_WAVES) k_encode_prune(
       const float d2 = cand_diff<STEP0>(z2, ls.z, ss.z, mu.z, bb.z);
       const float d3 = cand_diff<STEP0>(z3, ls.w, ss.w, mu.w, bb.w);
       float y0, y1, y2, y3;  // _z(x) = (x - loc) / scale, correctly rounded
-      if (fastdiv && markstein_ok(d0) && markstein_ok(d1) && markstein_ok(d2) &&
-          markstein_ok(d3)) {
+      const bool ok = fastdiv & markstein_ok(d0) & markstein_ok(d1) & markstein_ok(d2) &
+                      markstein_ok(d3);
+      if (ok) {
         y0 = div_rn_markstein(d0, sg.x, ry.x);
         y1 = div_rn_markstein(d1, sg.y, ry.y);
         y2 = div_rn_markstein(d2, sg.z, ry.z);

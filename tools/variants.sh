@@ -10,7 +10,7 @@ declare -A V=(
   [base]=""
   [w6]="-DCWQ_PRUNE_MIN_WAVES=6"
   [w8]="-DCWQ_PRUNE_MIN_WAVES=8"
-  [tau4]="-DCWQ_TAU_SHARE_MASK=3u"
+
 )
 if [ "$1" = build ]; then
   mkdir -p $OUT
