@@ -73,6 +73,8 @@ def load():
             "(python -c 'import __graft_entry__ as g; g.build()')")
     lib = ctypes.CDLL(LIB_PATH)
     for name, (res, args) in SIGNATURES.items():
+        if os.environ.get("CWQ_LIB_PATH") and not hasattr(lib, name):
+            continue  # an older tuning build (tools/variants.sh) may lack newer entry points
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args

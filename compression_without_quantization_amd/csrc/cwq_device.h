@@ -116,10 +116,16 @@ __device__ __forceinline__ float div_rn_markstein(float a, float b, float y) {
   return __builtin_fmaf(r1, y, q1);
 }
 // 2^-60 <= |a| < 2^60 (biased exponent 67..186) or a == +-0, branch-free.
-__device__ __forceinline__ bool markstein_ok(float a) {
-  const uint32_t u = f2u(a);
-  const uint32_t e = ((u >> 23) & 0xffu) - 67u;  // wraps below 2^-60
-  return (e < 120u) | ((u << 1) == 0u);
+// True when all four numerators lie in [2^-60, 2^60].  Exact zeros fail
+// too (they are rare, and the caller's IEEE fallback handles them), which lets
+// the test be two 3-input min/max ops and two compares.  A NaN numerator may
+// pass: both division paths then yield NaN, which the score clamps anyway.
+__device__ __forceinline__ bool markstein_ok4(float a, float b, float c, float d) {
+  const float ma = __builtin_fabsf(a), mb = __builtin_fabsf(b);
+  const float mc = __builtin_fabsf(c), md = __builtin_fabsf(d);
+  const float hi = __builtin_fmaxf(__builtin_fmaxf(ma, mb), __builtin_fmaxf(mc, md));
+  const float lo = __builtin_fminf(__builtin_fminf(ma, mb), __builtin_fminf(mc, md));
+  return (hi <= 0x1p60f) & (lo >= 0x1p-60f);
 }
 __device__ __forceinline__ bool markstein_ok_den(float b) {
   return b >= 0x1p-60f && b <= 0x1p60f;

@@ -307,19 +307,21 @@ __global__ void __launch_bounds__(256, CWQ_PRUNE_MIN_WAVES) k_encode_prune(
       const float d1 = cand_diff<STEP0>(z1, ls.y, ss.y, mu.y, bb.y);
       const float d2 = cand_diff<STEP0>(z2, ls.z, ss.z, mu.z, bb.z);
       const float d3 = cand_diff<STEP0>(z3, ls.w, ss.w, mu.w, bb.w);
-      float y0, y1, y2, y3;  // _z(x) = (x - loc) / scale, correctly rounded
-      const bool ok = fastdiv & markstein_ok(d0) & markstein_ok(d1) & markstein_ok(d2) &
-                      markstein_ok(d3);
-      if (ok) {
-        y0 = div_rn_markstein(d0, sg.x, ry.x);
-        y1 = div_rn_markstein(d1, sg.y, ry.y);
-        y2 = div_rn_markstein(d2, sg.z, ry.z);
-        y3 = div_rn_markstein(d3, sg.w, ry.w);
-      } else {
-        y0 = d0 / sg.x;
-        y1 = d1 / sg.y;
-        y2 = d2 / sg.z;
-        y3 = d3 / sg.w;
+      // fast correctly rounded quotients; lanes whose operands leave the
+      // Markstein ranges (never, for sane inputs) redo them with IEEE division
+      // inside a wave-uniform branch, so the common path issues no fallback.
+      float y0 = div_rn_markstein(d0, sg.x, ry.x);
+      float y1 = div_rn_markstein(d1, sg.y, ry.y);
+      float y2 = div_rn_markstein(d2, sg.z, ry.z);
+      float y3 = div_rn_markstein(d3, sg.w, ry.w);
+      const bool ok = fastdiv & markstein_ok4(d0, d1, d2, d3);
+      if (__builtin_expect(__ballot(!ok) != 0ull, 0)) {
+        if (!ok) {
+          y0 = d0 / sg.x;
+          y1 = d1 / sg.y;
+          y2 = d2 / sg.z;
+          y3 = d3 / sg.w;
+        }
       }
       s = s + lp_from_z(y0, cc.x);
       s = s + lp_from_z(y1, cc.y);

@@ -10,11 +10,14 @@ declare -A V=(
   [base]=""
   [w6]="-DCWQ_PRUNE_MIN_WAVES=6"
   [w8]="-DCWQ_PRUNE_MIN_WAVES=8"
+  [old_9368822]=prebuilt
+  [old_9a56617]=prebuilt
 
 )
 if [ "$1" = build ]; then
   mkdir -p $OUT
   for k in "${!V[@]}"; do
+    [ "${V[$k]}" = prebuilt ] && continue  # built by hand from an older commit
     hipcc $FLAGS ${V[$k]} -o $OUT/libcwq_$k.so $CSRC/cwq_kernels.hip $CSRC/cwq_importance.hip $CSRC/cwq_capi.hip $CSRC/cwq_ac.cpp &
   done
   wait
