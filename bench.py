@@ -56,6 +56,8 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
+    ap.add_argument("--prune-mode", type=int, default=2, choices=(0, 1, 2),
+                    help="0 unpruned, 1 exact pruning, 2 pruning + screening (default)")
     return ap.parse_args()
 
 
@@ -132,6 +134,8 @@ def main():
     out_sample = torch.empty(nb * d, dtype=torch.float32, device=dev)
     ws = torch.empty(C.encode_workspace_bytes(nb, nb * d), dtype=torch.uint8, device=dev)
     lib = _lib.load()
+    if hasattr(lib, "cwq_set_pruning"):
+        lib.cwq_set_pruning(args.prune_mode)
 
     def step():
         C.encode_blocks(t["post_loc"], t["post_scale"], t["prior_loc"], t["prior_scale"], bits,

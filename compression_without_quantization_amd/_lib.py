@@ -49,6 +49,7 @@ SIGNATURES = {
     "cwq_ac_encode": (c_i64, [c_vp, c_i64, c_int, c_vp, c_i64, c_vp, c_i64]),
     "cwq_ac_decode": (c_i64, [c_vp, c_i64, c_int, c_vp, c_i64, c_vp, c_i64]),
     "cwq_selftest_bm_tables": (c_int, [ctypes.c_uint32, c_i64, c_vp, c_vp, c_vp, c_vp]),
+    "cwq_selftest_screen_tables": (c_int, [ctypes.c_uint32, c_i64, c_vp, c_vp, c_vp, c_vp]),
     "cwq_selftest_logf": (c_int, [c_vp, c_i64, c_vp, c_vp]),
     "cwq_selftest_div": (c_int, [c_vp, c_vp, c_i64, c_vp, c_vp]),
     "cwq_profile_set_eval_events": (c_int, [c_vp, c_vp]),

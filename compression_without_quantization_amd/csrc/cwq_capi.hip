@@ -18,7 +18,7 @@ namespace {
 thread_local char g_err[512] = {0};
 thread_local void* g_ev_start = nullptr;
 thread_local void* g_ev_stop = nullptr;
-thread_local int g_prune = 1;
+thread_local int g_prune = 2;  // 0 off, 1 exact pruning, 2 + screening
 
 int fail(int code, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
 int fail(int code, const char* fmt, ...) {
@@ -357,8 +357,8 @@ int cwq_profile_set_eval_events(void* start_event, void* stop_event) {
   return ok();
 }
 
-int cwq_set_pruning(int enable) {
-  g_prune = enable ? 1 : 0;
+int cwq_set_pruning(int enable) {  // mode, see include/cwq.h
+  g_prune = enable < 0 ? 0 : (enable > 2 ? 2 : enable);
   return ok();
 }
 
@@ -368,6 +368,16 @@ int cwq_selftest_bm_tables(uint32_t m0, int64_t count, float* radius, float* sin
     return fail(CWQ_ERR_INVALID, "cwq_selftest_bm_tables: bad arguments");
   hipError_t e = cwq::launch_selftest_bm(m0, count, radius, sin_out, cos_out, (hipStream_t)stream);
   if (e != hipSuccess) return hip_fail(e, "cwq_selftest_bm_tables");
+  return ok();
+}
+
+int cwq_selftest_screen_tables(uint32_t m0, int64_t count, float* radius, float* sin_out,
+                               float* cos_out, void* stream) {
+  if (count < 0 || (count > 0 && (!radius || !sin_out || !cos_out)))
+    return fail(CWQ_ERR_INVALID, "cwq_selftest_screen_tables: bad arguments");
+  hipError_t e =
+      cwq::launch_selftest_screen(m0, count, radius, sin_out, cos_out, (hipStream_t)stream);
+  if (e != hipSuccess) return hip_fail(e, "cwq_selftest_screen_tables");
   return ok();
 }
 

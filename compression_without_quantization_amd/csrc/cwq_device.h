@@ -93,6 +93,31 @@ __device__ __forceinline__ void box_muller_dev(uint32_t x0, uint32_t x1, const d
   f1 = c * u2;
 }
 
+// Screening Box-Muller (approximate).  The hardware transcendentals
+// v_log_f32 / v_sqrt_f32 / v_sin_f32 / v_cos_f32 (sin and cos take the angle in
+// revolutions, so U = Uint32ToFloat(x1) needs no scaling or range reduction).
+// Used ONLY by the pruned encoder's screening pass, which turns the value into
+// rigorous bounds: the largest deviation from the exact pair over every
+// possible input (2^23 each) is a measured constant, kScreenEr / kScreenEs,
+// re-checked exhaustively on the GPU by tests/test_gpu.py.
+__device__ __forceinline__ float bm_radius_screen(uint32_t x0) {
+  float u1 = uint32_to_float(x0);
+  u1 = u1 < 1.0e-7f ? 1.0e-7f : u1;
+  return __builtin_amdgcn_sqrtf(-0x1.62e430p+0f * __builtin_amdgcn_logf(u1));  // -2 ln2 log2(u1)
+}
+__device__ __forceinline__ void bm_sincos_screen(uint32_t x1, float& s, float& c) {
+  const float U = uint32_to_float(x1);
+  s = __builtin_amdgcn_sinf(U);
+  c = __builtin_amdgcn_cosf(U);
+}
+__device__ __forceinline__ void box_muller_screen(uint32_t x0, uint32_t x1, float& f0, float& f1) {
+  const float u2 = bm_radius_screen(x0);
+  float s, c;
+  bm_sincos_screen(x1, s, c);
+  f0 = s * u2;
+  f1 = c * u2;
+}
+
 __device__ __forceinline__ F4 normal4_dev(const PhiloxStream& s, uint64_t grp,
                                           const double* logtab) {
   const U4 x = philox_block_dev(s, grp);

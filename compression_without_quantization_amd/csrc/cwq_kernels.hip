@@ -17,6 +17,8 @@
 //     normals in registers (Philox -> Box-Muller -> shard -> log-prob) and
 //     accumulates them in the Eigen AVX summation order.
 #include <hip/hip_runtime.h>
+
+#include <type_traits>
 #include <stdint.h>
 
 #include "cwq_device.h"
@@ -172,23 +174,53 @@ __device__ __forceinline__ float lp_from_z(float z, float cc) {
   return u - cc;
 }
 
+// Screening pass ("screening bound").  On tiles whose constants
+// pass the range gate below, the drop decisions are taken on cheap
+// approximations instead of exact values: z~ from the hardware
+// transcendentals (|z~ - z| <= kScreenEz for every Philox output), and per dim
+//     m_j = max(|ss_j z~ + off_j| R1_j - Q1_j, 0)  <=  |y_j| / sqrt(2),
+// y_j the exact standardised value, so -m_j^2 - c_j bounds the exact float
+// log-density from above.  With s = float sum of -m_j^2 over the visited dims
+// (all terms <= 0), every completion of the row has an exact Eigen-order value
+//     E  <=  (1 - 2^-14) s + Bs,    Bs ~ sum_j M_j (+ rounding margins),
+// and a completed row has E >= (1 + 2^-12) s + As - Pq sqrt(-s) (the lower
+// end feeds tau).  Survivors are re-evaluated exactly as in the exact pass,
+// so the screening arithmetic never reaches the output.
+constexpr float kScreenC1 = 1.0f - 0x1p-14f;
+constexpr float kScreenC2 = 1.0f + 0x1p-12f;
+// measured maxima over all 2^23 inputs (tools/screen_err.py, re-checked by
+// tests/test_gpu.py): |r~ - r| <= 4.77e-7, |sin~ - sin|, |cos~ - cos| <= 2.99e-7
+constexpr double kScreenEr = 1.0e-6;
+constexpr double kScreenEs = 6.0e-7;
+constexpr double kScreenRmax = 5.68;  // r <= sqrt(-2 ln 1e-7) = 5.6777
+// |RN(s~ r~) - RN(s r)| <= (1 + Es) Er + Rmax Es + 2^-23 (Rmax + Er)
+constexpr double kScreenEz =
+    (1.0 + kScreenEs) * kScreenEr + kScreenRmax * kScreenEs + 0x1p-23 * (kScreenRmax + kScreenEr);
+constexpr double kScreenZm = 5.7;     // bound on |z| and |z~|
+
+__device__ __forceinline__ float round_dn_f32(double b) { return -round_up_f32(-b); }
+
 template <int D, bool STEP0>
 __global__ void __launch_bounds__(256, CWQ_PRUNE_MIN_WAVES) k_encode_prune(
     const float* __restrict__ t_loc, const float* __restrict__ t_scale,
     const float* __restrict__ loc_s, const float* __restrict__ scale_s,
     const float* __restrict__ lognorm, const float* __restrict__ best, int64_t ntiles,
     int64_t tiles_per_block, int64_t cand_per_tile, int64_t n_cand, int32_t seed,
-    int64_t block_id_base, int32_t step, unsigned long long* __restrict__ keys) {
+    int64_t block_id_base, int32_t step, int allow_screen, unsigned long long* __restrict__ keys) {
   static_assert(D % 8 == 0 && D >= 8 && D <= 64, "pruned path: D % 8 == 0, D <= 64");
   constexpr int G = D / 4;
   constexpr int NF = STEP0 ? 6 : 7;  // loc_s, scale_s, mu, sigma, c, 1/sigma[, best]
+  constexpr int NS = 4;              // screening: scale_s, off, R1, Q1
   __shared__ double logtab[32];
   __shared__ float4 cst[G * NF];     // constants of the k-th visited group
+  __shared__ float4 scst[G * NS];    // screening constants of the k-th visited group
   __shared__ int2 meta[G];           // {Philox group of visit k, bits of B_{k+1}}
   __shared__ float dscore[D];
+  __shared__ float dP[D];            // screening: P_j (lower-end slack per dim)
   __shared__ float gscore[G];
   __shared__ int gpos[G];
   __shared__ float lowc;             // L: lower-end constant of a completed row
+  __shared__ float scr_b, scr_a, scr_pq;  // screening: Bs, As, Pq
   __shared__ uint32_t tau_ord;
   __shared__ uint32_t sq_cnt;
   __shared__ uint32_t sq_n[CWQ_SURVIVOR_CAP];
@@ -210,7 +242,8 @@ __global__ void __launch_bounds__(256, CWQ_PRUNE_MIN_WAVES) k_encode_prune(
     // (a) per-dim constants into registers; expected deficit of dim j under the
     //     proposal shard: E[0.5((T - mu)/sigma)^2], T ~ N(best + loc_s, scale_s^2)
     float fj[7] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    int den_ok = 1;
+    float sj[NS] = {0.f, 0.f, 0.f, 0.f};
+    int den_ok = 1, scr_ok = 1;
     if (threadIdx.x < D) {
       const int j = threadIdx.x;
       const float sgj = t_scale[off + j];
@@ -225,8 +258,35 @@ __global__ void __launch_bounds__(256, CWQ_PRUNE_MIN_WAVES) k_encode_prune(
       const float m = (STEP0 ? fj[0] : fj[6] + fj[0]) - fj[2];
       float e = 0.5f * (fj[1] * fj[1] + m * m) * (fj[5] * fj[5]);
       dscore[j] = (e == e) ? e : -1.0f;
+      // screening constants (see kScreen* above and DESIGN.md)
+      const double ssa = __builtin_fabs((double)fj[1]), lsa = __builtin_fabs((double)fj[0]);
+      const double mua = __builtin_fabs((double)fj[2]);
+      const double bba = STEP0 ? 0.0 : __builtin_fabs((double)fj[6]);
+      const double zs = kScreenZm * ssa;
+      const double mag = bba + lsa + zs + mua;
+      // rounding of the exact chain RN(RN(RN(bb +) RN(ls + RN(ss z))) - mu)
+      const double rho = 0x1p-24 * 1.0001 * (zs + (lsa + zs) + (STEP0 ? 0.0 : bba + lsa + zs) + mag);
+      const double offd = (STEP0 ? 0.0 : (double)fj[6]) + (double)fj[0] - (double)fj[2];
+      const double delta =
+          (rho + ssa * kScreenEz + 0x1p-24 * __builtin_fabs(offd) + 0x1p-48 * mag) * (1.0 + 0x1p-20) +
+          0x1p-140;
+      const double sig = (double)sgj;
+      double q1 = delta / sig * 0.70710678118654757 * (1.0 + 0x1p-20);
+      q1 = q1 > 0x1p-30 ? q1 : 0x1p-30;
+      sj[0] = fj[1];
+      sj[1] = (float)offd;
+      sj[2] = round_dn_f32((1.0 / sig) * (1.0 - 0x1p-23) * 0.7071067601131229 * (1.0 - 0x1p-22));
+      sj[3] = round_up_f32(q1);
+      const float pj = round_up_f32(2.0001 * (double)sj[3]);
+      dP[j] = pj;
+      const float cj = fj[4];
+      scr_ok = (den_ok && mag <= 0x1p100 && mag / sig <= 0x1p60 && sj[3] <= 0x1p60f &&
+                pj <= 0x1p60f && cj - cj == 0.0f)
+                   ? 1
+                   : 0;
     }
     const bool fastdiv = __syncthreads_and(den_ok) != 0;
+    const bool scr_all = __syncthreads_and(scr_ok) != 0;
     // (b) group scores, (c) visit order: rank by decreasing score, ties by index
     if (threadIdx.x < G) {
       const int q = threadIdx.x;
@@ -250,28 +310,46 @@ __global__ void __launch_bounds__(256, CWQ_PRUNE_MIN_WAVES) k_encode_prune(
       float* c = reinterpret_cast<float*>(cst);
 #pragma unroll
       for (int f = 0; f < NF; ++f) c[(k * NF + f) * 4 + w] = fj[f];
+      float* sc = reinterpret_cast<float*>(scst);
+#pragma unroll
+      for (int f = 0; f < NS; ++f) sc[(k * NS + f) * 4 + w] = sj[f];
       if (w == 0) meta[k].x = j >> 2;
     }
     __syncthreads();
-    // (e) drop bounds: thread k computes B_k for the first k visited groups
-    if (threadIdx.x <= G) {
+    // (e) drop bounds: thread k computes B_k for the first k visited groups;
+    //     thread G + 1 the screening constants
+    if (threadIdx.x <= G + 1) {
       const int kb = threadIdx.x;
       const float* c = reinterpret_cast<const float*>(cst);
-      double rf = 0.0, kk = 0.0, asum = 0.0;
+      double rf = 0.0, kk = 0.0, asum = 0.0, msum = 0.0, kall = 0.0, p2 = 0.0, pmax = 0.0;
 #pragma unroll 1
       for (int p = 0; p < D; ++p) {  // p = 4 * (visit position) + w
         const double mj = -(double)c[((p >> 2) * NF + 4) * 4 + (p & 3)];  // M_j = -c_j
         const double aj = __builtin_fabs(mj);
         asum += aj;
+        msum += mj;
+        kall += aj + mj;
         if (p >= 4 * kb)
           rf += mj + 0x1p-17 * aj;
         else
           kk += aj + mj;
+        if (kb == G + 1) {
+          const double pj = (double)dP[p];
+          p2 += pj * pj;
+          pmax = pj > pmax ? pj : pmax;
+        }
       }
       const double marg = 0x1p-20 * (__builtin_fabs(rf) + asum) + 0x1p-126;
-      const float bk = round_up_f32(rf + 0x1p-14 * kk + marg);
-      if (kb >= 1) meta[kb - 1].y = (int)f2u(bk);
-      if (kb == G) lowc = round_up_f32(0x1p-14 * kk + marg);
+      if (kb <= G) {
+        const float bk = round_up_f32(rf + 0x1p-14 * kk + marg);
+        if (kb >= 1) meta[kb - 1].y = (int)f2u(bk);
+        if (kb == G) lowc = round_up_f32(0x1p-14 * kk + marg);
+      } else {
+        const double sl = 0x1p-14 * (__builtin_fabs(msum) + asum + kall) + 0x1p-126;
+        scr_b = round_up_f32(msum + sl);
+        scr_a = round_dn_f32(msum - sl - 1.01 * p2);
+        scr_pq = round_up_f32(2.01 * pmax * __builtin_sqrt((double)D));
+      }
       if (kb == 0) {
         tau_ord = ord_f32(-__builtin_inff());
         sq_cnt = 0u;
@@ -279,6 +357,9 @@ __global__ void __launch_bounds__(256, CWQ_PRUNE_MIN_WAVES) k_encode_prune(
     }
     __syncthreads();
     const float lc = lowc;
+    const bool screen = allow_screen && scr_all && scr_b - scr_b == 0.0f &&
+                        scr_a - scr_a == 0.0f && scr_pq - scr_pq == 0.0f;
+    const float sB = scr_b, sA = scr_a, sPq = scr_pq;
 
     // this wave's contiguous share of the tile's candidates
     const int64_t per_wave = (n1 - n0 + 3) / 4;
@@ -293,76 +374,104 @@ __global__ void __launch_bounds__(256, CWQ_PRUNE_MIN_WAVES) k_encode_prune(
     uint64_t bestk = 0;
     uint32_t iter = 0;
 
-    while (__ballot(active) != 0ull) {
-      const int2 mt = meta[k];
-      const uint32_t grp = (uint32_t)n * (uint32_t)G + (uint32_t)mt.x;
-      const U4 x = philox10_dev(grp, 0u, st.c2, st.c3, st.k0, st.k1);
-      float z0, z1, z2, z3;
-      box_muller_dev(x.x, x.y, logtab, z0, z1);
-      box_muller_dev(x.z, x.w, logtab, z2, z3);
-      const float4* cq = cst + k * NF;
-      const float4 ls = cq[0], ss = cq[1], mu = cq[2], sg = cq[3], cc = cq[4], ry = cq[5];
-      const float4 bb = STEP0 ? float4{0.f, 0.f, 0.f, 0.f} : cq[6];
-      const float d0 = cand_diff<STEP0>(z0, ls.x, ss.x, mu.x, bb.x);
-      const float d1 = cand_diff<STEP0>(z1, ls.y, ss.y, mu.y, bb.y);
-      const float d2 = cand_diff<STEP0>(z2, ls.z, ss.z, mu.z, bb.z);
-      const float d3 = cand_diff<STEP0>(z3, ls.w, ss.w, mu.w, bb.w);
-      // fast correctly rounded quotients; lanes whose operands leave the
-      // Markstein ranges (never, for sane inputs) redo them with IEEE division
-      // inside a wave-uniform branch, so the common path issues no fallback.
-      float y0 = div_rn_markstein(d0, sg.x, ry.x);
-      float y1 = div_rn_markstein(d1, sg.y, ry.y);
-      float y2 = div_rn_markstein(d2, sg.z, ry.z);
-      float y3 = div_rn_markstein(d3, sg.w, ry.w);
-      const bool ok = fastdiv & markstein_ok4(d0, d1, d2, d3);
-      if (__builtin_expect(__ballot(!ok) != 0ull, 0)) {
-        if (!ok) {
-          y0 = d0 / sg.x;
-          y1 = d1 / sg.y;
-          y2 = d2 / sg.z;
-          y3 = d3 / sg.w;
+    auto pass = [&](auto screen_tag) {
+      constexpr bool SCREEN = decltype(screen_tag)::value;
+      while (__ballot(active) != 0ull) {
+        const int2 mt = meta[k];
+        const uint32_t grp = (uint32_t)n * (uint32_t)G + (uint32_t)mt.x;
+        const U4 x = philox10_dev(grp, 0u, st.c2, st.c3, st.k0, st.k1);
+        float z0, z1, z2, z3;
+        float upper;
+        if constexpr (SCREEN) {
+          box_muller_screen(x.x, x.y, z0, z1);
+          box_muller_screen(x.z, x.w, z2, z3);
+          const float4* cq = scst + k * NS;
+          const float4 ss = cq[0], of = cq[1], r1 = cq[2], q1 = cq[3];
+          const float m0 = fmaxf(__builtin_fmaf(__builtin_fabsf(__builtin_fmaf(ss.x, z0, of.x)), r1.x, -q1.x), 0.0f);
+          const float m1 = fmaxf(__builtin_fmaf(__builtin_fabsf(__builtin_fmaf(ss.y, z1, of.y)), r1.y, -q1.y), 0.0f);
+          const float m2 = fmaxf(__builtin_fmaf(__builtin_fabsf(__builtin_fmaf(ss.z, z2, of.z)), r1.z, -q1.z), 0.0f);
+          const float m3 = fmaxf(__builtin_fmaf(__builtin_fabsf(__builtin_fmaf(ss.w, z3, of.w)), r1.w, -q1.w), 0.0f);
+          s = __builtin_fmaf(-m0, m0, s);
+          s = __builtin_fmaf(-m1, m1, s);
+          s = __builtin_fmaf(-m2, m2, s);
+          s = __builtin_fmaf(-m3, m3, s);
+          upper = __builtin_fmaf(s, kScreenC1, sB);
+        } else {
+          box_muller_dev(x.x, x.y, logtab, z0, z1);
+          box_muller_dev(x.z, x.w, logtab, z2, z3);
+          const float4* cq = cst + k * NF;
+          const float4 ls = cq[0], ss = cq[1], mu = cq[2], sg = cq[3], cc = cq[4], ry = cq[5];
+          const float4 bb = STEP0 ? float4{0.f, 0.f, 0.f, 0.f} : cq[6];
+          const float d0 = cand_diff<STEP0>(z0, ls.x, ss.x, mu.x, bb.x);
+          const float d1 = cand_diff<STEP0>(z1, ls.y, ss.y, mu.y, bb.y);
+          const float d2 = cand_diff<STEP0>(z2, ls.z, ss.z, mu.z, bb.z);
+          const float d3 = cand_diff<STEP0>(z3, ls.w, ss.w, mu.w, bb.w);
+          // fast correctly rounded quotients; lanes whose operands leave the
+          // Markstein ranges (never, for sane inputs) redo them with IEEE division
+          // inside a wave-uniform branch, so the common path issues no fallback.
+          float y0 = div_rn_markstein(d0, sg.x, ry.x);
+          float y1 = div_rn_markstein(d1, sg.y, ry.y);
+          float y2 = div_rn_markstein(d2, sg.z, ry.z);
+          float y3 = div_rn_markstein(d3, sg.w, ry.w);
+          const bool ok = fastdiv & markstein_ok4(d0, d1, d2, d3);
+          if (__builtin_expect(__ballot(!ok) != 0ull, 0)) {
+            if (!ok) {
+              y0 = d0 / sg.x;
+              y1 = d1 / sg.y;
+              y2 = d2 / sg.z;
+              y3 = d3 / sg.w;
+            }
+          }
+          s = s + lp_from_z(y0, cc.x);
+          s = s + lp_from_z(y1, cc.y);
+          s = s + lp_from_z(y2, cc.z);
+          s = s + lp_from_z(y3, cc.w);
+          upper = (s + __builtin_fabsf(s) * kPruneC1) + u2f((uint32_t)mt.y);
+        }
+        k += 1;
+        const bool complete = (k == G);
+        const bool prune = !complete && (upper < tau);
+        if (complete && active && upper >= tau) {  // may be the best: keep it
+          float lower;
+          if constexpr (SCREEN)
+            lower = __builtin_fmaf(s, kScreenC2, sA) - sPq * __builtin_sqrtf(-s);
+          else
+            lower = (s - __builtin_fabsf(s) * kPruneC1) - lc;
+          tau = fmaxf(tau, lower);
+          const uint32_t slot = atomicAdd(&sq_cnt, 1u);
+          if (slot < CWQ_SURVIVOR_CAP) {
+            sq_n[slot] = (uint32_t)n;
+            sq_ub[slot] = upper;
+          } else {  // list full (near-ties everywhere): evaluate exactly now
+            const float v = eval_row<D, STEP0>(st, (uint64_t)n * D, D, 0, loc_s + off,
+                                               scale_s + off, t_loc + off, t_scale + off,
+                                               lognorm + off, STEP0 ? nullptr : best + off, logtab);
+            const uint64_t kv = argmax_key(v, (uint32_t)n);
+            bestk = kv > bestk ? kv : bestk;
+          }
+        }
+        const bool done = complete || prune || !active;
+        const uint64_t m = __ballot(done);
+        const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                        __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+        if (done) {
+          n = wnext + rank;
+          k = 0;
+          s = 0.0f;
+        }
+        wnext += (int64_t)__builtin_popcountll(m);
+        active = n < w1;
+        if (((++iter) & CWQ_TAU_SHARE_MASK) == 0u) {  // share tau across the workgroup's waves
+          const float tm = wave_max_f32(tau);
+          if (lane == 0) atomicMax(&tau_ord, ord_f32(tm));
+          tau = fmaxf(tau, unord_f32(__atomic_load_n(&tau_ord, __ATOMIC_RELAXED)));
         }
       }
-      s = s + lp_from_z(y0, cc.x);
-      s = s + lp_from_z(y1, cc.y);
-      s = s + lp_from_z(y2, cc.z);
-      s = s + lp_from_z(y3, cc.w);
-      k += 1;
-      const bool complete = (k == G);
-      const float as = __builtin_fabsf(s) * kPruneC1;
-      const float upper = (s + as) + u2f((uint32_t)mt.y);
-      const bool prune = !complete && (upper < tau);
-      if (complete && active && upper >= tau) {  // may be the best: keep it
-        tau = fmaxf(tau, (s - as) - lc);
-        const uint32_t slot = atomicAdd(&sq_cnt, 1u);
-        if (slot < CWQ_SURVIVOR_CAP) {
-          sq_n[slot] = (uint32_t)n;
-          sq_ub[slot] = upper;
-        } else {  // list full (near-ties everywhere): evaluate exactly now
-          const float v = eval_row<D, STEP0>(st, (uint64_t)n * D, D, 0, loc_s + off,
-                                             scale_s + off, t_loc + off, t_scale + off,
-                                             lognorm + off, STEP0 ? nullptr : best + off, logtab);
-          const uint64_t kv = argmax_key(v, (uint32_t)n);
-          bestk = kv > bestk ? kv : bestk;
-        }
-      }
-      const bool done = complete || prune || !active;
-      const uint64_t m = __ballot(done);
-      const uint32_t rank =
-          __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-      if (done) {
-        n = wnext + rank;
-        k = 0;
-        s = 0.0f;
-      }
-      wnext += (int64_t)__builtin_popcountll(m);
-      active = n < w1;
-      if (((++iter) & CWQ_TAU_SHARE_MASK) == 0u) {  // share tau across the workgroup's waves
-        const float tm = wave_max_f32(tau);
-        if (lane == 0) atomicMax(&tau_ord, ord_f32(tm));
-        tau = fmaxf(tau, unord_f32(__atomic_load_n(&tau_ord, __ATOMIC_RELAXED)));
-      }
-    }
+    };
+    if (screen)
+      pass(std::true_type{});
+    else
+      pass(std::false_type{});
 
     // exact evaluation of the survivors that can still reach the final tau
     {
@@ -559,6 +668,21 @@ __global__ void __launch_bounds__(256) k_selftest_bm(uint32_t m0, int64_t count,
   }
 }
 
+__global__ void __launch_bounds__(256) k_selftest_screen(uint32_t m0, int64_t count,
+                                                         float* __restrict__ rad,
+                                                         float* __restrict__ sn,
+                                                         float* __restrict__ cs) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < count;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const uint32_t m = m0 + (uint32_t)i;
+    rad[i] = bm_radius_screen(m);
+    float s, c;
+    bm_sincos_screen(m, s, c);
+    sn[i] = s;
+    cs[i] = c;
+  }
+}
+
 __global__ void __launch_bounds__(256) k_selftest_logf(const float* __restrict__ x, int64_t n,
                                                        float* __restrict__ out) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
@@ -608,7 +732,7 @@ static void launch_prune_t(const EncodeArgs& a, int step, hipStream_t stream) {
   hipLaunchKernelGGL((k_encode_prune<D, STEP0>), dim3(grid), dim3(256), 0, stream, a.t_loc,
                      a.t_scale, a.loc_s, a.scale_s, a.lognorm, a.out_sample, ntiles,
                      a.tiles_per_block, a.cand_per_tile, a.n_cand, a.seed, a.block_id_base, step,
-                     a.keys);
+                     a.prune >= 2 ? 1 : 0, a.keys);
 }
 
 template <bool STEP0>
@@ -725,6 +849,14 @@ hipError_t launch_selftest_bm(uint32_t m0, int64_t count, float* rad, float* sn,
   if (count <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_selftest_bm, dim3(grid_for(count, 256, 65536)), dim3(256), 0, stream, m0,
                      count, rad, sn, cs);
+  return hipGetLastError();
+}
+
+hipError_t launch_selftest_screen(uint32_t m0, int64_t count, float* rad, float* sn, float* cs,
+                                  hipStream_t stream) {
+  if (count <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_selftest_screen, dim3(grid_for(count, 256, 65536)), dim3(256), 0, stream,
+                     m0, count, rad, sn, cs);
   return hipGetLastError();
 }
 

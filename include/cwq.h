@@ -190,6 +190,11 @@ int64_t cwq_ac_decode(const int64_t* counts, int64_t K, int precision, const cha
 int cwq_selftest_bm_tables(uint32_t m0, int64_t count, float* radius, float* sin_out,
                            float* cos_out, void* stream);
 int cwq_selftest_logf(const float* x, int64_t n, float* out, void* stream);
+/* The pruned encoder's screening approximations of the same three tables
+ * (hardware v_log/v_sqrt/v_sin/v_cos).  The tests bound their deviation from
+ * the exact tables by the constants the screening bounds are built on. */
+int cwq_selftest_screen_tables(uint32_t m0, int64_t count, float* radius, float* sin_out,
+                               float* cos_out, void* stream);
 /* out[i] = the device's fast correctly-rounded quotient a[i] / b[i]
  * (Markstein sequence with y = RN(1/b); only valid in the ranges documented in
  * DESIGN.md -- the test feeds it exactly those). */
@@ -202,9 +207,12 @@ int cwq_selftest_div(const float* a, const float* b, int64_t n, float* out, void
 int cwq_profile_set_eval_events(void* start_event, void* stop_event);
 
 /* Candidate pruning (DESIGN.md "pruning bound") is on by default for uniform
- * blocks with d % 8 == 0, d <= 64; it never changes results.  0 turns it off
- * for this host thread (A/B timing and tests). */
-int cwq_set_pruning(int enable);
+ * blocks with d % 8 == 0, d <= 64; it never changes results.  Modes for this
+ * host thread (A/B timing and tests): 0 = off (every candidate scored
+ * exactly), 1 = pruning on exact values, 2 (default) = pruning with the
+ * screening pass (DESIGN.md "screening bound") where a tile's constants allow
+ * it, exact pruning elsewhere. */
+int cwq_set_pruning(int mode);
 
 #ifdef __cplusplus
 }

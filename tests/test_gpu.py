@@ -275,14 +275,15 @@ def test_c4_full_size_roundtrip_and_sample(cwq, oracle):
 # pruned encoder (uniform d % 8 == 0): same results as the unpruned kernel and
 # the oracle, including adversarial inputs where the bound is tight or useless
 # ---------------------------------------------------------------------------
-def _uniform_encode(cwq, cwqlib, tl, ts, pl, ps, d, bits, n_steps, seed, rho, prune):
-    cwqlib.cwq_set_pruning(1 if prune else 0)
+def _uniform_encode(cwq, cwqlib, tl, ts, pl, ps, d, bits, n_steps, seed, rho, mode):
+    """mode: 0 unpruned, 1 pruning on exact values, 2 pruning with screening."""
+    cwqlib.cwq_set_pruning(int(mode))
     try:
         i, s = cwq.encode_blocks(tl, ts, pl, ps, bits, n_steps, seed, rho=rho, block_dim=d)
         torch.cuda.synchronize()
         return i.cpu().numpy(), s.cpu().numpy()
     finally:
-        cwqlib.cwq_set_pruning(1)
+        cwqlib.cwq_set_pruning(2)
 
 
 @pytest.mark.parametrize("d,bits,n_steps,nb,rho", [
@@ -294,10 +295,11 @@ def test_pruned_matches_unpruned_and_oracle(cwq, cwqlib, oracle, d, bits, n_step
     b = make_blocks(nb, d, bits, seed=77 + d + bits)
     tl, ts, pl, ps = (b[k].reshape(-1) for k in ("post_loc", "post_scale", "prior_loc",
                                                  "prior_scale"))
-    i1, s1 = _uniform_encode(cwq, cwqlib, tl, ts, pl, ps, d, bits, n_steps, 42, rho, True)
-    i0, s0 = _uniform_encode(cwq, cwqlib, tl, ts, pl, ps, d, bits, n_steps, 42, rho, False)
-    assert np.array_equal(i1, i0)
-    _assert_bits_equal(s1, s0, "pruned vs unpruned")
+    i0, s0 = _uniform_encode(cwq, cwqlib, tl, ts, pl, ps, d, bits, n_steps, 42, rho, 0)
+    for mode in (1, 2):
+        i1, s1 = _uniform_encode(cwq, cwqlib, tl, ts, pl, ps, d, bits, n_steps, 42, rho, mode)
+        assert np.array_equal(i1, i0), f"mode {mode}"
+        _assert_bits_equal(s1, s0, f"pruned (mode {mode}) vs unpruned")
     if (1 << bits) * d * nb <= (1 << 22):
         wi, ws = oracle.greedy_encode(tl, ts, pl, ps, np.arange(nb + 1) * d, bits, n_steps, 42,
                                       rho)
@@ -307,8 +309,9 @@ def test_pruned_matches_unpruned_and_oracle(cwq, cwqlib, oracle, d, bits, n_step
 
 @pytest.mark.parametrize("kind", ["posterior_is_prior", "tiny_scales", "huge_scales",
                                   "inf_scale", "zero_scale", "mixed_sign_norm", "nan_scale",
-                                  "nan_loc_one_dim"])
-def test_pruned_adversarial(cwq, cwqlib, oracle, kind):
+                                  "nan_loc_one_dim", "far_locs", "huge_locs", "tiny_locs"])
+@pytest.mark.parametrize("mode", [1, 2])
+def test_pruned_adversarial(cwq, cwqlib, oracle, kind, mode):
     rng = np.random.default_rng(sum(map(ord, kind)))
     nb, d, bits = 6, 16, 10
     pl = rng.standard_normal(nb * d).astype(np.float32)
@@ -331,10 +334,46 @@ def test_pruned_adversarial(cwq, cwqlib, oracle, kind):
         tl[7::32] = np.nan
     elif kind == "mixed_sign_norm":  # some c_j < 0 (M_j > 0), some > 0
         ts = np.where(rng.uniform(size=nb * d) < 0.5, 0.05, 3.0).astype(np.float32)
-    i1, s1 = _uniform_encode(cwq, cwqlib, tl, ts, pl, ps, d, bits, 1, 42, 1.0, True)
+    elif kind == "far_locs":       # |loc| >> scale: the float rounding of loc + scale z dominates
+        pl = (3.0e4 + pl).astype(np.float32)
+        tl = (pl + 0.3 * ps * rng.standard_normal(nb * d)).astype(np.float32)
+        ts = (0.01 * ps).astype(np.float32)
+    elif kind == "huge_locs":      # outside the screening gate: exact pruning for these tiles
+        pl = (1.0e35 * np.sign(pl)).astype(np.float32)
+        tl = pl.copy()
+        ts = (ps * 1e33).astype(np.float32)
+        ps = (ps * 1e33).astype(np.float32)
+    elif kind == "tiny_locs":      # values near zero: subnormal-range differences
+        pl = (pl * 1e-30).astype(np.float32)
+        ps = (ps * 1e-30).astype(np.float32)
+        tl = (pl + 0.5 * ps * rng.standard_normal(nb * d)).astype(np.float32)
+        ts = (0.7 * ps).astype(np.float32)
+    i1, s1 = _uniform_encode(cwq, cwqlib, tl, ts, pl, ps, d, bits, 1, 42, 1.0, mode)
     wi, ws = oracle.greedy_encode(tl, ts, pl, ps, np.arange(nb + 1) * d, bits, 1, 42)
     assert np.array_equal(i1, wi)
     _assert_bits_equal(s1, ws, kind)
+
+
+def test_screen_tables_within_bounds(cwq, cwqlib):
+    """The screening pass's Box-Muller approximations (hardware v_log/v_sqrt/
+    v_sin/v_cos) stay within the constants its bounds are built on
+    (kScreenEr, kScreenEs, kScreenRmax in csrc/cwq_kernels.hip), over all 2^23
+    inputs of each."""
+    k_er, k_es, k_rmax = 1.0e-6, 6.0e-7, 5.68
+    dev = torch.device("cuda")
+    t = [torch.empty(N23, dtype=torch.float32, device=dev) for _ in range(6)]
+    st = torch.cuda.current_stream().cuda_stream
+    assert cwqlib.cwq_selftest_bm_tables(0, N23, t[0].data_ptr(), t[1].data_ptr(),
+                                         t[2].data_ptr(), st) == 0
+    assert cwqlib.cwq_selftest_screen_tables(0, N23, t[3].data_ptr(), t[4].data_ptr(),
+                                             t[5].data_ptr(), st) == 0
+    torch.cuda.synchronize()
+    a = [x.cpu().numpy().astype(np.float64) for x in t]
+    assert np.isfinite(a[3]).all() and np.isfinite(a[4]).all() and np.isfinite(a[5]).all()
+    assert np.abs(a[3] - a[0]).max() <= k_er
+    assert np.abs(a[4] - a[1]).max() <= k_es
+    assert np.abs(a[5] - a[2]).max() <= k_es
+    assert a[0].max() <= k_rmax and a[3].max() <= k_rmax
 
 
 def test_device_fast_division_correctly_rounded(cwq, cwqlib):
