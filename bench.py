@@ -216,12 +216,14 @@ def main():
             traffic = tj.get("hbm_bytes_per_launch")
     roofline = {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                "kernel": "k_encode_eval", "kernel_ms": round(eval_ms, 3),
+                "kernel": (f"k_encode_prune<{d},true>" if args.prune_mode and d % 8 == 0
+                           and 8 <= d <= 64 else "k_encode_eval"),
+                "kernel_ms": round(eval_ms, 3),
                 "algorithmic_bytes_per_launch": bytes_per_launch,
                 "compute_bound": {"unit": "candidate-dims/s",
                                   "achieved": cand_dims / (eval_ms * 1e-3),
-                                  "note": "VALU-bound path (Philox + glibc-exact Box-Muller "
-                                          "+ log-pdf); see DESIGN.md"}}
+                                  "note": "VALU-bound path (Philox + Box-Muller; pruned with "
+                                          "the screening pass, survivors exact); see DESIGN.md"}}
 
     cpu = None
     parity = None

@@ -381,6 +381,14 @@ int cwq_selftest_screen_tables(uint32_t m0, int64_t count, float* radius, float*
   return ok();
 }
 
+int cwq_debug_prune_stats(unsigned long long* out72, int flags) {
+  if (!out72) return fail(CWQ_ERR_INVALID, "cwq_debug_prune_stats: null output");
+  const int r = cwq::prune_stats(out72, flags);
+  if (r < 0) return fail(CWQ_ERR_HIP, "cwq_debug_prune_stats: symbol copy failed");
+  cwq::set_error(CWQ_OK, "");
+  return r;
+}
+
 int cwq_selftest_div(const float* a, const float* b, int64_t n, float* out, void* stream) {
   if (n < 0 || (n > 0 && (!a || !b || !out)))
     return fail(CWQ_ERR_INVALID, "cwq_selftest_div: bad arguments");

@@ -152,7 +152,7 @@ __global__ void __launch_bounds__(256) k_encode_eval(
 // ---------------------------------------------------------------------------
 constexpr float kPruneC1 = 0x1p-14f;
 #ifndef CWQ_PRUNE_MIN_WAVES
-#define CWQ_PRUNE_MIN_WAVES 1  // waves/SIMD the register allocator must allow
+#define CWQ_PRUNE_MIN_WAVES 6  // waves/SIMD the register allocator must allow (tools/variants.sh)
 #endif
 #ifndef CWQ_TAU_SHARE_MASK
 #define CWQ_TAU_SHARE_MASK 15u  // share tau across the workgroup every 16 units
@@ -178,16 +178,21 @@ __device__ __forceinline__ float lp_from_z(float z, float cc) {
 // pass the range gate below, the drop decisions are taken on cheap
 // approximations instead of exact values: z~ from the hardware
 // transcendentals (|z~ - z| <= kScreenEz for every Philox output), and per dim
-//     m_j = max(|ss_j z~ + off_j| R1_j - Q1_j, 0)  <=  |y_j| / sqrt(2),
-// y_j the exact standardised value, so -m_j^2 - c_j bounds the exact float
-// log-density from above.  With s = float sum of -m_j^2 over the visited dims
-// (all terms <= 0), every completion of the row has an exact Eigen-order value
-//     E  <=  (1 - 2^-14) s + Bs,    Bs ~ sum_j M_j (+ rounding margins),
-// and a completed row has E >= (1 + 2^-12) s + As - Pq sqrt(-s) (the lower
-// end feeds tau).  Survivors are re-evaluated exactly as in the exact pass,
-// so the screening arithmetic never reaches the output.
+//     a_j = RN(sA_j z~ + sB_j),  sA_j ~ ss_j K_j,  sB_j ~ (best + loc_s - mu)_j K_j,
+// K_j = sqrt(phi (1 - 2^-24) / 2) / sigma_j, with the guarantee
+//     0.5 y_j^2 (1 - 2^-24)  >=  a_j^2 - C_j
+// for the exact standardised value y_j (C_j a tiny per-dim constant).  With s
+// the float sum of -a_j^2 over the visited dims, every completion of the row
+// has an exact Eigen-order value
+//     E  <=  (1 - 2^-14) s + Bs_k,    Bs_k ~ sum_j M_j + sum_{visited} C_j,
+// and a completed row has E >= (1 + 2^-13) s + As - Pq sqrt(-s), which
+// feeds tau.  Survivors are re-evaluated exactly as in the exact pass, so the
+// screening arithmetic never reaches the output.
 constexpr float kScreenC1 = 1.0f - 0x1p-14f;
-constexpr float kScreenC2 = 1.0f + 0x1p-12f;
+constexpr float kScreenC2 = 1.0f + 0x1p-13f;
+constexpr double kScreenEps = 0x1p-15;  // split of the additive error: (x-A)^2 >= (1-e)x^2 - (1/e-1)A^2
+constexpr double kScreenPhi = (1.0 - kScreenEps) * (1.0 - 0x1p-21);
+constexpr double kScreenKappa = 0.7070958018530696;  // sqrt(phi (1 - 2^-24) / 2), rounded down
 // measured maxima over all 2^23 inputs (tools/screen_err.py, re-checked by
 // tests/test_gpu.py): |r~ - r| <= 4.77e-7, |sin~ - sin|, |cos~ - cos| <= 2.99e-7
 constexpr double kScreenEr = 1.0e-6;
@@ -200,6 +205,17 @@ constexpr double kScreenZm = 5.7;     // bound on |z| and |z~|
 
 __device__ __forceinline__ float round_dn_f32(double b) { return -round_up_f32(-b); }
 
+#ifdef CWQ_PRUNE_STATS
+// tuning builds only (tools/prune_stats.py): [0..64] candidates finished after
+// k units, [65] completed rows, [66] survivors pushed, [67] screened tiles
+__device__ unsigned long long g_prune_stats[72];
+// "oracle tau" experiment: each tile's best key is saved; with g_seed_tau set
+// the next launch starts every tile at the exact best value of the last one
+constexpr int kDbgBlocks = 1 << 20;
+__device__ unsigned long long g_dbg_best[kDbgBlocks];
+__device__ int g_seed_tau;
+#endif
+
 template <int D, bool STEP0>
 __global__ void __launch_bounds__(256, CWQ_PRUNE_MIN_WAVES) k_encode_prune(
     const float* __restrict__ t_loc, const float* __restrict__ t_scale,
@@ -210,17 +226,18 @@ __global__ void __launch_bounds__(256, CWQ_PRUNE_MIN_WAVES) k_encode_prune(
   static_assert(D % 8 == 0 && D >= 8 && D <= 64, "pruned path: D % 8 == 0, D <= 64");
   constexpr int G = D / 4;
   constexpr int NF = STEP0 ? 6 : 7;  // loc_s, scale_s, mu, sigma, c, 1/sigma[, best]
-  constexpr int NS = 4;              // screening: scale_s, off, R1, Q1
+  constexpr int NS = 2;              // screening: sA, sB
   __shared__ double logtab[32];
   __shared__ float4 cst[G * NF];     // constants of the k-th visited group
   __shared__ float4 scst[G * NS];    // screening constants of the k-th visited group
   __shared__ int2 meta[G];           // {Philox group of visit k, bits of B_{k+1}}
   __shared__ float dscore[D];
-  __shared__ float dP[D];            // screening: P_j (lower-end slack per dim)
+  __shared__ float dA[D];            // screening: A_j (additive error, a units)
+  __shared__ float dC[D];            // screening: C_j
   __shared__ float gscore[G];
   __shared__ int gpos[G];
   __shared__ float lowc;             // L: lower-end constant of a completed row
-  __shared__ float scr_b, scr_a, scr_pq;  // screening: Bs, As, Pq
+  __shared__ float scr_a, scr_pq;    // screening: As, Pq
   __shared__ uint32_t tau_ord;
   __shared__ uint32_t sq_cnt;
   __shared__ uint32_t sq_n[CWQ_SURVIVOR_CAP];
@@ -231,6 +248,11 @@ __global__ void __launch_bounds__(256, CWQ_PRUNE_MIN_WAVES) k_encode_prune(
   const uint32_t lane = threadIdx.x & 63u;
 
   for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    // thread index re-derived per tile behind an opaque move: the per-thread
+    // addresses below are then recomputed (cheap) instead of hoisted out of the
+    // tile loop and spilled under the 6-waves/SIMD register budget
+    uint32_t tid = threadIdx.x;
+    asm volatile("" : "+v"(tid));
     const int64_t g = tile / tiles_per_block;
     const int64_t tt = tile - g * tiles_per_block;
     const int64_t off = g * D;
@@ -239,13 +261,40 @@ __global__ void __launch_bounds__(256, CWQ_PRUNE_MIN_WAVES) k_encode_prune(
     const PhiloxStream st =
         generate_key(step_seed(block_seed(seed, block_id_base + g), step), 42);
 
-    // (a) per-dim constants into registers; expected deficit of dim j under the
-    //     proposal shard: E[0.5((T - mu)/sigma)^2], T ~ N(best + loc_s, scale_s^2)
-    float fj[7] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    float sj[NS] = {0.f, 0.f, 0.f, 0.f};
+    // (a) expected deficit of dim j under the proposal shard:
+    //     E[0.5((T - mu)/sigma)^2], T ~ N(best + loc_s, scale_s^2)
+    if (tid < D) {
+      const int j = tid;
+      const float ls = loc_s[off + j], ss = scale_s[off + j], mu = t_loc[off + j];
+      const float rs = 1.0f / t_scale[off + j];
+      const float m = (STEP0 ? ls : best[off + j] + ls) - mu;
+      float e = 0.5f * (ss * ss + m * m) * (rs * rs);
+      dscore[j] = (e == e) ? e : -1.0f;
+    }
+    __syncthreads();
+    // (b) group scores, (c) visit order: rank by decreasing score, ties by index
+    if (tid < G) {
+      const int q = tid;
+      gscore[q] = ((dscore[4 * q] + dscore[4 * q + 1]) + dscore[4 * q + 2]) + dscore[4 * q + 3];
+    }
+    __syncthreads();
+    if (tid < G) {
+      const int q = tid;
+      const float sq = gscore[q];
+      int r = 0;
+      for (int q2 = 0; q2 < G; ++q2) {
+        const float s2 = gscore[q2];
+        r += (s2 > sq || (s2 == sq && q2 < q)) ? 1 : 0;
+      }
+      gpos[q] = r;
+      meta[r].x = q;
+    }
+    __syncthreads();
+    // (d) constants in visit order (reloaded: nothing is held across the syncs)
     int den_ok = 1, scr_ok = 1;
-    if (threadIdx.x < D) {
-      const int j = threadIdx.x;
+    if (tid < D) {
+      const int j = tid, k = gpos[j >> 2], w = j & 3;
+      float fj[7];
       const float sgj = t_scale[off + j];
       fj[0] = loc_s[off + j];
       fj[1] = scale_s[off + j];
@@ -253,11 +302,11 @@ __global__ void __launch_bounds__(256, CWQ_PRUNE_MIN_WAVES) k_encode_prune(
       fj[3] = sgj;
       fj[4] = lognorm[off + j];
       fj[5] = 1.0f / sgj;
-      if (!STEP0) fj[6] = best[off + j];
+      fj[6] = STEP0 ? 0.0f : best[off + j];
+      float* c = reinterpret_cast<float*>(cst);
+#pragma unroll
+      for (int f = 0; f < NF; ++f) c[(k * NF + f) * 4 + w] = fj[f];
       den_ok = markstein_ok_den(sgj) ? 1 : 0;
-      const float m = (STEP0 ? fj[0] : fj[6] + fj[0]) - fj[2];
-      float e = 0.5f * (fj[1] * fj[1] + m * m) * (fj[5] * fj[5]);
-      dscore[j] = (e == e) ? e : -1.0f;
       // screening constants (see kScreen* above and DESIGN.md)
       const double ssa = __builtin_fabs((double)fj[1]), lsa = __builtin_fabs((double)fj[0]);
       const double mua = __builtin_fabs((double)fj[2]);
@@ -267,61 +316,35 @@ __global__ void __launch_bounds__(256, CWQ_PRUNE_MIN_WAVES) k_encode_prune(
       // rounding of the exact chain RN(RN(RN(bb +) RN(ls + RN(ss z))) - mu)
       const double rho = 0x1p-24 * 1.0001 * (zs + (lsa + zs) + (STEP0 ? 0.0 : bba + lsa + zs) + mag);
       const double offd = (STEP0 ? 0.0 : (double)fj[6]) + (double)fj[0] - (double)fj[2];
-      const double delta =
-          (rho + ssa * kScreenEz + 0x1p-24 * __builtin_fabs(offd) + 0x1p-48 * mag) * (1.0 + 0x1p-20) +
-          0x1p-140;
       const double sig = (double)sgj;
-      double q1 = delta / sig * 0.70710678118654757 * (1.0 + 0x1p-20);
-      q1 = q1 > 0x1p-30 ? q1 : 0x1p-30;
-      sj[0] = fj[1];
-      sj[1] = (float)offd;
-      sj[2] = round_dn_f32((1.0 / sig) * (1.0 - 0x1p-23) * 0.7071067601131229 * (1.0 - 0x1p-22));
-      sj[3] = round_up_f32(q1);
-      const float pj = round_up_f32(2.0001 * (double)sj[3]);
-      dP[j] = pj;
+      const double kq = kScreenKappa / sig;
+      const float sa = (float)((double)fj[1] * kq);
+      const float sb = (float)(offd * kq);
+      float* sc = reinterpret_cast<float*>(scst);
+      sc[(k * NS + 0) * 4 + w] = sa;
+      sc[(k * NS + 1) * 4 + w] = sb;
+      const double a0 = (kq * (rho + ssa * kScreenEz) +
+                         kq * 0x1p-24 * 1.0001 * (zs + __builtin_fabs(offd))) * (1.0 + 0x1p-20) +
+                        0x1p-140;
+      const float cdim = round_up_f32((1.0 / kScreenEps - 1.0) * a0 * a0 / kScreenPhi * (1.0 + 0x1p-20));
+      dA[j] = round_up_f32(a0 * 1.0001);
+      dC[j] = cdim;
       const float cj = fj[4];
-      scr_ok = (den_ok && mag <= 0x1p100 && mag / sig <= 0x1p60 && sj[3] <= 0x1p60f &&
-                pj <= 0x1p60f && cj - cj == 0.0f)
+      scr_ok = (den_ok && mag <= 0x1p100 && mag / sig <= 0x1p50 && cdim <= 0x1p60f &&
+                sa - sa == 0.0f && sb - sb == 0.0f && cj - cj == 0.0f)
                    ? 1
                    : 0;
     }
     const bool fastdiv = __syncthreads_and(den_ok) != 0;
     const bool scr_all = __syncthreads_and(scr_ok) != 0;
-    // (b) group scores, (c) visit order: rank by decreasing score, ties by index
-    if (threadIdx.x < G) {
-      const int q = threadIdx.x;
-      gscore[q] = ((dscore[4 * q] + dscore[4 * q + 1]) + dscore[4 * q + 2]) + dscore[4 * q + 3];
-    }
-    __syncthreads();
-    if (threadIdx.x < G) {
-      const int q = threadIdx.x;
-      const float sq = gscore[q];
-      int r = 0;
-      for (int q2 = 0; q2 < G; ++q2) {
-        const float s2 = gscore[q2];
-        r += (s2 > sq || (s2 == sq && q2 < q)) ? 1 : 0;
-      }
-      gpos[q] = r;
-    }
-    __syncthreads();
-    // (d) constants in visit order
-    if (threadIdx.x < D) {
-      const int j = threadIdx.x, k = gpos[j >> 2], w = j & 3;
-      float* c = reinterpret_cast<float*>(cst);
-#pragma unroll
-      for (int f = 0; f < NF; ++f) c[(k * NF + f) * 4 + w] = fj[f];
-      float* sc = reinterpret_cast<float*>(scst);
-#pragma unroll
-      for (int f = 0; f < NS; ++f) sc[(k * NS + f) * 4 + w] = sj[f];
-      if (w == 0) meta[k].x = j >> 2;
-    }
-    __syncthreads();
-    // (e) drop bounds: thread k computes B_k for the first k visited groups;
-    //     thread G + 1 the screening constants
-    if (threadIdx.x <= G + 1) {
-      const int kb = threadIdx.x;
+    // (e) drop bounds: thread k computes B_k for the first k visited groups
+    //     (exact or screening form); thread G + 1 the screening constants
+    const bool screen = allow_screen && scr_all;
+    if (tid <= G + 1) {
+      const int kb = tid;
       const float* c = reinterpret_cast<const float*>(cst);
-      double rf = 0.0, kk = 0.0, asum = 0.0, msum = 0.0, kall = 0.0, p2 = 0.0, pmax = 0.0;
+      double rf = 0.0, kk = 0.0, asum = 0.0, msum = 0.0, kall = 0.0, cvis = 0.0, a2 = 0.0,
+             amax = 0.0;
 #pragma unroll 1
       for (int p = 0; p < D; ++p) {  // p = 4 * (visit position) + w
         const double mj = -(double)c[((p >> 2) * NF + 4) * 4 + (p & 3)];  // M_j = -c_j
@@ -329,37 +352,44 @@ __global__ void __launch_bounds__(256, CWQ_PRUNE_MIN_WAVES) k_encode_prune(
         asum += aj;
         msum += mj;
         kall += aj + mj;
-        if (p >= 4 * kb)
+        if (p >= 4 * kb) {
           rf += mj + 0x1p-17 * aj;
-        else
+        } else {
           kk += aj + mj;
-        if (kb == G + 1) {
-          const double pj = (double)dP[p];
-          p2 += pj * pj;
-          pmax = pj > pmax ? pj : pmax;
+          if (screen) cvis += (double)dC[(meta[p >> 2].x << 2) + (p & 3)];
+        }
+        if (screen && kb == G + 1) {
+          const double av = (double)dA[p];
+          a2 += av * av;
+          amax = av > amax ? av : amax;
         }
       }
       const double marg = 0x1p-20 * (__builtin_fabs(rf) + asum) + 0x1p-126;
+      const double sl = 0x1p-14 * (__builtin_fabs(msum) + asum + kall) + 0x1p-126;
       if (kb <= G) {
-        const float bk = round_up_f32(rf + 0x1p-14 * kk + marg);
+        const float bk = screen ? round_up_f32(msum + cvis * (1.0 + 0x1p-20) + sl)
+                                : round_up_f32(rf + 0x1p-14 * kk + marg);
         if (kb >= 1) meta[kb - 1].y = (int)f2u(bk);
         if (kb == G) lowc = round_up_f32(0x1p-14 * kk + marg);
-      } else {
-        const double sl = 0x1p-14 * (__builtin_fabs(msum) + asum + kall) + 0x1p-126;
-        scr_b = round_up_f32(msum + sl);
-        scr_a = round_dn_f32(msum - sl - 1.01 * p2);
-        scr_pq = round_up_f32(2.01 * pmax * __builtin_sqrt((double)D));
+      } else if (screen) {
+        scr_a = round_dn_f32(msum - sl - 1.01 * a2 * (1.0 + 0x1p-11));
+        scr_pq = round_up_f32(2.01 * amax * __builtin_sqrt((double)D) * (1.0 + 0x1p-11));
       }
       if (kb == 0) {
         tau_ord = ord_f32(-__builtin_inff());
+#ifdef CWQ_PRUNE_STATS
+        if (g_seed_tau && g < kDbgBlocks && (g_dbg_best[g] >> 32) > kArgmaxClampOrd)
+          tau_ord = (uint32_t)(g_dbg_best[g] >> 32);
+#endif
         sq_cnt = 0u;
       }
     }
     __syncthreads();
     const float lc = lowc;
-    const bool screen = allow_screen && scr_all && scr_b - scr_b == 0.0f &&
-                        scr_a - scr_a == 0.0f && scr_pq - scr_pq == 0.0f;
-    const float sB = scr_b, sA = scr_a, sPq = scr_pq;
+#ifdef CWQ_PRUNE_STATS
+    const float tau_seed = unord_f32(tau_ord);
+#endif
+    const float sA = scr_a, sPq = scr_pq;
 
     // this wave's contiguous share of the tile's candidates
     const int64_t per_wave = (n1 - n0 + 3) / 4;
@@ -371,6 +401,9 @@ __global__ void __launch_bounds__(256, CWQ_PRUNE_MIN_WAVES) k_encode_prune(
     int k = 0;
     float s = 0.0f;
     float tau = -__builtin_inff();
+#ifdef CWQ_PRUNE_STATS
+    tau = tau_seed;
+#endif
     uint64_t bestk = 0;
     uint32_t iter = 0;
 
@@ -386,16 +419,16 @@ __global__ void __launch_bounds__(256, CWQ_PRUNE_MIN_WAVES) k_encode_prune(
           box_muller_screen(x.x, x.y, z0, z1);
           box_muller_screen(x.z, x.w, z2, z3);
           const float4* cq = scst + k * NS;
-          const float4 ss = cq[0], of = cq[1], r1 = cq[2], q1 = cq[3];
-          const float m0 = fmaxf(__builtin_fmaf(__builtin_fabsf(__builtin_fmaf(ss.x, z0, of.x)), r1.x, -q1.x), 0.0f);
-          const float m1 = fmaxf(__builtin_fmaf(__builtin_fabsf(__builtin_fmaf(ss.y, z1, of.y)), r1.y, -q1.y), 0.0f);
-          const float m2 = fmaxf(__builtin_fmaf(__builtin_fabsf(__builtin_fmaf(ss.z, z2, of.z)), r1.z, -q1.z), 0.0f);
-          const float m3 = fmaxf(__builtin_fmaf(__builtin_fabsf(__builtin_fmaf(ss.w, z3, of.w)), r1.w, -q1.w), 0.0f);
-          s = __builtin_fmaf(-m0, m0, s);
-          s = __builtin_fmaf(-m1, m1, s);
-          s = __builtin_fmaf(-m2, m2, s);
-          s = __builtin_fmaf(-m3, m3, s);
-          upper = __builtin_fmaf(s, kScreenC1, sB);
+          const float4 sa = cq[0], sb = cq[1];
+          const float a0 = __builtin_fmaf(sa.x, z0, sb.x);
+          const float a1 = __builtin_fmaf(sa.y, z1, sb.y);
+          const float a2 = __builtin_fmaf(sa.z, z2, sb.z);
+          const float a3 = __builtin_fmaf(sa.w, z3, sb.w);
+          s = __builtin_fmaf(-a0, a0, s);
+          s = __builtin_fmaf(-a1, a1, s);
+          s = __builtin_fmaf(-a2, a2, s);
+          s = __builtin_fmaf(-a3, a3, s);
+          upper = __builtin_fmaf(s, kScreenC1, u2f((uint32_t)mt.y));
         } else {
           box_muller_dev(x.x, x.y, logtab, z0, z1);
           box_muller_dev(x.z, x.w, logtab, z2, z3);
@@ -451,6 +484,11 @@ __global__ void __launch_bounds__(256, CWQ_PRUNE_MIN_WAVES) k_encode_prune(
           }
         }
         const bool done = complete || prune || !active;
+#ifdef CWQ_PRUNE_STATS
+        if (active && (complete || prune)) atomicAdd(&g_prune_stats[k], 1ull);
+        if (active && complete) atomicAdd(&g_prune_stats[65], 1ull);
+        if (active && complete && upper >= tau) atomicAdd(&g_prune_stats[66], 1ull);
+#endif
         const uint64_t m = __ballot(done);
         const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
                                                         __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
@@ -468,6 +506,9 @@ __global__ void __launch_bounds__(256, CWQ_PRUNE_MIN_WAVES) k_encode_prune(
         }
       }
     };
+#ifdef CWQ_PRUNE_STATS
+    if (screen && tid == 0) atomicAdd(&g_prune_stats[67], 1ull);
+#endif
     if (screen)
       pass(std::true_type{});
     else
@@ -481,7 +522,7 @@ __global__ void __launch_bounds__(256, CWQ_PRUNE_MIN_WAVES) k_encode_prune(
     __syncthreads();
     const float tau_final = unord_f32(tau_ord);
     const uint32_t nsurv = sq_cnt < CWQ_SURVIVOR_CAP ? sq_cnt : CWQ_SURVIVOR_CAP;
-    for (uint32_t i = threadIdx.x; i < nsurv; i += blockDim.x) {
+    for (uint32_t i = tid; i < nsurv; i += blockDim.x) {
       if (sq_ub[i] >= tau_final) {
         const uint32_t nn = sq_n[i];
         const float v = eval_row<D, STEP0>(st, (uint64_t)nn * D, D, 0, loc_s + off,
@@ -495,10 +536,13 @@ __global__ void __launch_bounds__(256, CWQ_PRUNE_MIN_WAVES) k_encode_prune(
     bestk = wave_max_u64(bestk);
     if (lane == 0) wkey[wv] = bestk;
     __syncthreads();
-    if (threadIdx.x == 0) {
+    if (tid == 0) {
       uint64_t mk = wkey[0];
       for (int i = 1; i < 4; ++i) mk = wkey[i] > mk ? wkey[i] : mk;
       if (mk) atomicMax(&keys[g], (unsigned long long)mk);
+#ifdef CWQ_PRUNE_STATS
+      if (!g_seed_tau && g < kDbgBlocks) g_dbg_best[g] = mk;
+#endif
     }
     __syncthreads();
   }
@@ -727,8 +771,15 @@ static void launch_eval_t(const EncodeArgs& a, int step, hipStream_t stream) {
 
 template <int D, bool STEP0>
 static void launch_prune_t(const EncodeArgs& a, int step, hipStream_t stream) {
+  // persistent-style grid: 256 CUs x 6 resident workgroups x 64; each workgroup
+  // loops over tiles (per-workgroup setup, e.g. register spill slots written
+  // once at entry, is paid thousands of times less often than one per tile)
+#ifndef CWQ_PRUNE_GRID
+#define CWQ_PRUNE_GRID (256 * 6 * 64)
+#endif
+  constexpr int64_t kPruneGrid = CWQ_PRUNE_GRID;
   const int64_t ntiles = a.nb * a.tiles_per_block;
-  const unsigned grid = (unsigned)(ntiles < (1LL << 30) ? ntiles : (1LL << 30));
+  const unsigned grid = (unsigned)(ntiles < kPruneGrid ? ntiles : kPruneGrid);
   hipLaunchKernelGGL((k_encode_prune<D, STEP0>), dim3(grid), dim3(256), 0, stream, a.t_loc,
                      a.t_scale, a.loc_s, a.scale_s, a.lognorm, a.out_sample, ntiles,
                      a.tiles_per_block, a.cand_per_tile, a.n_cand, a.seed, a.block_id_base, step,
@@ -858,6 +909,27 @@ hipError_t launch_selftest_screen(uint32_t m0, int64_t count, float* rad, float*
   hipLaunchKernelGGL(k_selftest_screen, dim3(grid_for(count, 256, 65536)), dim3(256), 0, stream,
                      m0, count, rad, sn, cs);
   return hipGetLastError();
+}
+
+int prune_stats(unsigned long long* out72, int reset) {
+#ifdef CWQ_PRUNE_STATS
+  if (hipMemcpyFromSymbol(out72, HIP_SYMBOL(g_prune_stats), sizeof(unsigned long long) * 72) !=
+      hipSuccess)
+    return -1;
+  if (reset & 6) {
+    const int v = (reset & 2) ? 1 : 0;
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_seed_tau), &v, sizeof(int)) != hipSuccess) return -1;
+  }
+  if (reset & 1) {
+    static const unsigned long long zero[72] = {0};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_prune_stats), zero, sizeof(zero)) != hipSuccess) return -1;
+  }
+  return 1;
+#else
+  for (int i = 0; i < 72; ++i) out72[i] = 0;
+  (void)reset;
+  return 0;
+#endif
 }
 
 hipError_t launch_selftest_div(const float* a, const float* b, int64_t n, float* out,

@@ -200,6 +200,15 @@ int cwq_selftest_screen_tables(uint32_t m0, int64_t count, float* radius, float*
  * DESIGN.md -- the test feeds it exactly those). */
 int cwq_selftest_div(const float* a, const float* b, int64_t n, float* out, void* stream);
 
+/* Tuning counters of the pruned encoder, filled only by builds compiled with
+ * -DCWQ_PRUNE_STATS (tools/prune_stats.py); returns 1 there, 0 (and zeros)
+ * otherwise.  out72[k] = candidates finished after k units (k <= 64),
+ * [65] completed rows, [66] survivors pushed, [67] tiles on the screening pass.
+ * flags: bit 0 resets the counters; bit 1 / bit 2 switch the "oracle tau"
+ * experiment on / off (later launches start each tile at the best value the
+ * last launch found for it). */
+int cwq_debug_prune_stats(unsigned long long* out72, int flags);
+
 /* Profiling hook (bench.py): when set, every later encode call made by this
  * host thread records hipEvent_t `start_event` on its stream right before its
  * first candidate-scoring (eval) launch and `stop_event` right after its last

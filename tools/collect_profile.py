@@ -1,0 +1,40 @@
+"""Turn tools/profile.sh output into the committed evidence under profiles/.
+Usage: python tools/collect_profile.py TAG CONFIG BLOCKS KERNEL_SUBSTR ALG_BYTES"""
+import csv, glob, json, os, shutil, sys
+
+tag, config, blocks, ksub, alg = sys.argv[1], sys.argv[2], int(sys.argv[3]), sys.argv[4], int(sys.argv[5])
+root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+src = os.path.join(root, "gpurun_out", "prof_" + tag)
+dst = os.path.join(root, "profiles")
+
+
+def one(pattern):
+    f = sorted(glob.glob(os.path.join(src, pattern), recursive=True))
+    assert f, pattern
+    return f[0]
+
+
+shutil.copy(one("trace/**/*kernel_stats.csv"), os.path.join(dst, f"{tag}_kernel_stats.csv"))
+shutil.copy(one("trace/**/*kernel_trace.csv"), os.path.join(dst, f"{tag}_kernel_trace.csv"))
+vals = {}
+for pas in ("fetch", "write", "valu"):
+    f = one(f"{pas}/**/*counter_collection.csv")
+    shutil.copy(f, os.path.join(dst, f"{tag}_pmc_{pas}.csv"))
+    with open(f) as fh:
+        for row in csv.DictReader(fh):
+            if ksub in row["Kernel_Name"]:
+                vals.setdefault(row["Counter_Name"], 0.0)
+                vals[row["Counter_Name"]] += float(row["Counter_Value"])
+fetch_kb, write_kb = vals["FETCH_SIZE"], vals["WRITE_SIZE"]
+hbm = int((2 * fetch_kb + write_kb) * 1024)
+out = {"config": config, "blocks": blocks, "kernel": ksub, "FETCH_SIZE_kB": fetch_kb,
+       "WRITE_SIZE_kB": write_kb, "hbm_bytes_per_launch": hbm,
+       "algorithmic_bytes_per_launch": alg,
+       "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes of "
+                 "`python3 bench.py --steps 1 --warmup 0 --no-cpu --no-e2e` (one eval launch "
+                 "each); bytes = (2*FETCH_SIZE + WRITE_SIZE) * 1024 per MI355X_MICROARCH.md",
+       "valu": {k: vals.get(k) for k in ("SQ_ACTIVE_INST_VALU", "SQ_WAVE_CYCLES",
+                                         "SQ_BUSY_CYCLES", "GRBM_GUI_ACTIVE")}}
+with open(os.path.join(dst, f"traffic_{config}.json"), "w") as fh:
+    json.dump(out, fh, indent=1)
+print(json.dumps(out, indent=1))

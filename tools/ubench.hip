@@ -73,6 +73,35 @@ __global__ void k_cvt_f64(float* out, float a) {
   float s = 0; for (int i = 0; i < CH; ++i) s += x[i]; out[blockIdx.x * blockDim.x + threadIdx.x] = s;
 }
 
+#define UNARY_KERNEL(NAME, EXPR)                                                        \
+  __global__ void NAME(float* out, float a) {                                           \
+    float x[CH]; for (int i = 0; i < CH; ++i) x[i] = (threadIdx.x + i + 1) * 1e-3f;     \
+    for (int it = 0; it < ITERS; ++it)                                                  \
+      _Pragma("unroll") for (int i = 0; i < CH; ++i) { float v = x[i]; x[i] = (EXPR) + a; } \
+    float s = 0; for (int i = 0; i < CH; ++i) s += x[i];                                \
+    out[blockIdx.x * blockDim.x + threadIdx.x] = s;                                     \
+  }
+UNARY_KERNEL(k_log_f32, __builtin_amdgcn_logf(v))
+UNARY_KERNEL(k_sin_f32, __builtin_amdgcn_sinf(v))
+UNARY_KERNEL(k_cos_f32, __builtin_amdgcn_cosf(v))
+UNARY_KERNEL(k_rsq_f32, __builtin_amdgcn_rsqf(v))
+UNARY_KERNEL(k_exp_f32, __builtin_amdgcn_exp2f(v))
+// one v_sin per 4 independent f32 FMAs: does the transcendental overlap?
+__global__ void k_sin_mix(float* out, float a) {
+  float x[CH], y[CH];
+  for (int i = 0; i < CH; ++i) { x[i] = (threadIdx.x + i + 1) * 1e-3f; y[i] = x[i] + 1.f; }
+  for (int it = 0; it < ITERS; ++it)
+#pragma unroll
+    for (int i = 0; i < CH; ++i) {
+      x[i] = __builtin_amdgcn_sinf(x[i]);
+      y[i] = __builtin_fmaf(y[i], a, 0.5f);
+      y[i] = __builtin_fmaf(y[i], a, 0.25f);
+      y[i] = __builtin_fmaf(y[i], a, 0.125f);
+      y[i] = __builtin_fmaf(y[i], a, 0.0625f);
+    }
+  float s = 0; for (int i = 0; i < CH; ++i) s += x[i] + y[i]; out[blockIdx.x * blockDim.x + threadIdx.x] = s;
+}
+
 template <typename K, typename T>
 void run(const char* name, K k, T arg, int ops_per_iter_per_chain) {
   void* out; hipMalloc(&out, 256 * 8192 * 8);
@@ -99,5 +128,11 @@ int main() {
   run("xor+shr+add", k_xor, 0xD2511F53u, 3);
   run("sqrt+add", k_sqrt_f32, 1.0f, 2);
   run("cvt64+cvt32", k_cvt_f64, 1.0f, 2);
+  run("log+add", k_log_f32, 1.0f, 2);
+  run("sin+add", k_sin_f32, 0.001f, 2);
+  run("cos+add", k_cos_f32, 0.001f, 2);
+  run("rsq+add", k_rsq_f32, 1.0f, 2);
+  run("exp2+add", k_exp_f32, -1.0f, 2);
+  run("sin+4fma", k_sin_mix, 0.999f, 5);
   return 0;
 }

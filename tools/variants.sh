@@ -8,11 +8,10 @@ OUT=tools/variants
 FLAGS="--offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -fno-fast-math -fPIC -shared"
 declare -A V=(
   [base]=""
-  [w6]="-DCWQ_PRUNE_MIN_WAVES=6"
-  [w8]="-DCWQ_PRUNE_MIN_WAVES=8"
-  [old_9368822]=prebuilt
-  [old_9a56617]=prebuilt
-
+  [w7]="-DCWQ_PRUNE_MIN_WAVES=7"
+  [g4]="-DCWQ_PRUNE_GRID=6144"
+  [gfull]="-DCWQ_PRUNE_GRID=1073741824"
+  [stats]="-DCWQ_PRUNE_STATS"
 )
 if [ "$1" = build ]; then
   mkdir -p $OUT
@@ -23,6 +22,7 @@ if [ "$1" = build ]; then
   wait
 else
   for k in $(echo "${!V[@]}" | tr ' ' '\n' | sort); do
+    [ "$k" = stats ] && continue  # counters only: tools/prune_stats.py
     echo "== $k ${V[$k]}"
     CWQ_LIB_PATH=$PWD/$OUT/libcwq_$k.so timeout -k 10 300 python -u bench.py --no-cpu --no-e2e --steps 2 --warmup 1 $BENCH_ARGS | python -c "import json,sys; d=json.loads(sys.stdin.read()); print(d['value'], d['roofline']['kernel_ms'])"
   done
