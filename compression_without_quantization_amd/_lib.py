@@ -51,6 +51,7 @@ SIGNATURES = {
     "cwq_selftest_bm_tables": (c_int, [ctypes.c_uint32, c_i64, c_vp, c_vp, c_vp, c_vp]),
     "cwq_selftest_screen_tables": (c_int, [ctypes.c_uint32, c_i64, c_vp, c_vp, c_vp, c_vp]),
     "cwq_selftest_logf": (c_int, [c_vp, c_i64, c_vp, c_vp]),
+    "cwq_selftest_wave_max": (c_int, [c_vp, c_i64, c_vp, c_vp]),
     "cwq_selftest_div": (c_int, [c_vp, c_vp, c_i64, c_vp, c_vp]),
     "cwq_debug_prune_stats": (c_int, [c_vp, c_int]),
     "cwq_profile_set_eval_events": (c_int, [c_vp, c_vp]),

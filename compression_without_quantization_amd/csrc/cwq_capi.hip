@@ -389,6 +389,14 @@ int cwq_debug_prune_stats(unsigned long long* out72, int flags) {
   return r;
 }
 
+int cwq_selftest_wave_max(const float* x, int64_t n_waves, float* out, void* stream) {
+  if (n_waves < 0 || n_waves > (1LL << 31) || (n_waves > 0 && (!x || !out)))
+    return fail(CWQ_ERR_INVALID, "cwq_selftest_wave_max: bad arguments");
+  hipError_t e = cwq::launch_selftest_wave_max(x, n_waves, out, (hipStream_t)stream);
+  if (e != hipSuccess) return hip_fail(e, "cwq_selftest_wave_max");
+  return ok();
+}
+
 int cwq_selftest_div(const float* a, const float* b, int64_t n, float* out, void* stream) {
   if (n < 0 || (n > 0 && (!a || !b || !out)))
     return fail(CWQ_ERR_INVALID, "cwq_selftest_div: bad arguments");

@@ -180,10 +180,23 @@ __device__ __forceinline__ uint32_t ord_f32(float v) {
 __device__ __forceinline__ float unord_f32(uint32_t o) {
   return u2f((o & 0x80000000u) ? (o & 0x7fffffffu) : ~o);
 }
+// Wave-wide max with GFX9 DPP (quad perms, row mirrors, row_bcast:15/31):
+// six v_max_f32_dpp and one readlane.  Requires a full exec mask.
+template <int CTRL, int ROW_MASK>
+__device__ __forceinline__ float dpp_max_step(float v) {
+  const int ninf = (int)0xff800000u;  // -inf: identity for the rows DPP leaves unwritten
+  const int o = __builtin_amdgcn_update_dpp(ninf, __builtin_bit_cast(int, v), CTRL, ROW_MASK, 0xf,
+                                            false);
+  return fmaxf(v, __builtin_bit_cast(float, o));
+}
 __device__ __forceinline__ float wave_max_f32(float v) {
-#pragma unroll
-  for (int off = 32; off >= 1; off >>= 1) v = fmaxf(v, __shfl_xor(v, off, 64));
-  return v;
+  v = dpp_max_step<0xb1, 0xf>(v);   // quad_perm [1,0,3,2]
+  v = dpp_max_step<0x4e, 0xf>(v);   // quad_perm [2,3,0,1]
+  v = dpp_max_step<0x141, 0xf>(v);  // row_half_mirror
+  v = dpp_max_step<0x140, 0xf>(v);  // row_mirror: every lane holds its row's max
+  v = dpp_max_step<0x142, 0xa>(v);  // row_bcast:15 into rows 1, 3
+  v = dpp_max_step<0x143, 0xc>(v);  // row_bcast:31 into rows 2, 3: lane 63 holds the max
+  return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 63));
 }
 // smallest float >= b (+inf for non-finite b: such a bound never drops anything)
 __device__ __forceinline__ float round_up_f32(double b) {

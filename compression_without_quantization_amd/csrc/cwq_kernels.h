@@ -69,6 +69,7 @@ hipError_t launch_selftest_bm(uint32_t m0, int64_t count, float* rad, float* sn,
 hipError_t launch_selftest_screen(uint32_t m0, int64_t count, float* rad, float* sn, float* cs,
                                   hipStream_t stream);
 int prune_stats(unsigned long long* out72, int reset);
+hipError_t launch_selftest_wave_max(const float* x, int64_t nw, float* out, hipStream_t stream);
 hipError_t launch_selftest_div(const float* a, const float* b, int64_t n, float* out,
                                hipStream_t stream);
 hipError_t launch_selftest_logf(const float* x, int64_t n, float* out, hipStream_t stream);

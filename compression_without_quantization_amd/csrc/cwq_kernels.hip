@@ -467,7 +467,7 @@ __global__ void __launch_bounds__(256, CWQ_PRUNE_MIN_WAVES) k_encode_prune(
         if (complete && active && upper >= tau) {  // may be the best: keep it
           float lower;
           if constexpr (SCREEN)
-            lower = __builtin_fmaf(s, kScreenC2, sA) - sPq * __builtin_sqrtf(-s);
+            lower = __builtin_fmaf(s, kScreenC2, sA) - sPq * __builtin_amdgcn_sqrtf(-s);  // ~1 ulp: inside Pq's 0.4% slack
           else
             lower = (s - __builtin_fabsf(s) * kPruneC1) - lc;
           tau = fmaxf(tau, lower);
@@ -476,6 +476,9 @@ __global__ void __launch_bounds__(256, CWQ_PRUNE_MIN_WAVES) k_encode_prune(
             sq_n[slot] = (uint32_t)n;
             sq_ub[slot] = upper;
           } else {  // list full (near-ties everywhere): evaluate exactly now
+#ifdef CWQ_PRUNE_STATS
+            atomicAdd(&g_prune_stats[69], 1ull);
+#endif
             const float v = eval_row<D, STEP0>(st, (uint64_t)n * D, D, 0, loc_s + off,
                                                scale_s + off, t_loc + off, t_scale + off,
                                                lognorm + off, STEP0 ? nullptr : best + off, logtab);
@@ -524,6 +527,9 @@ __global__ void __launch_bounds__(256, CWQ_PRUNE_MIN_WAVES) k_encode_prune(
     const uint32_t nsurv = sq_cnt < CWQ_SURVIVOR_CAP ? sq_cnt : CWQ_SURVIVOR_CAP;
     for (uint32_t i = tid; i < nsurv; i += blockDim.x) {
       if (sq_ub[i] >= tau_final) {
+#ifdef CWQ_PRUNE_STATS
+        atomicAdd(&g_prune_stats[68], 1ull);
+#endif
         const uint32_t nn = sq_n[i];
         const float v = eval_row<D, STEP0>(st, (uint64_t)nn * D, D, 0, loc_s + off,
                                            scale_s + off, t_loc + off, t_scale + off,
@@ -725,6 +731,16 @@ __global__ void __launch_bounds__(256) k_selftest_screen(uint32_t m0, int64_t co
     sn[i] = s;
     cs[i] = c;
   }
+}
+
+// out[w] = max over the 64 inputs of wave w (wave_max_f32, the DPP reduction
+// the pruned kernel shares tau with)
+__global__ void __launch_bounds__(256) k_selftest_wave_max(const float* __restrict__ x, int64_t nw,
+                                                           float* __restrict__ out) {
+  const int64_t w = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const float v = w < nw ? x[w * 64 + (threadIdx.x & 63)] : -__builtin_inff();
+  const float m = wave_max_f32(v);
+  if (w < nw && (threadIdx.x & 63) == 0) out[w] = m;
 }
 
 __global__ void __launch_bounds__(256) k_selftest_logf(const float* __restrict__ x, int64_t n,
@@ -930,6 +946,13 @@ int prune_stats(unsigned long long* out72, int reset) {
   (void)reset;
   return 0;
 #endif
+}
+
+hipError_t launch_selftest_wave_max(const float* x, int64_t nw, float* out, hipStream_t stream) {
+  if (nw <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_selftest_wave_max, dim3((unsigned)((nw + 3) / 4)), dim3(256), 0, stream, x,
+                     nw, out);
+  return hipGetLastError();
 }
 
 hipError_t launch_selftest_div(const float* a, const float* b, int64_t n, float* out,

@@ -199,11 +199,15 @@ int cwq_selftest_screen_tables(uint32_t m0, int64_t count, float* radius, float*
  * (Markstein sequence with y = RN(1/b); only valid in the ranges documented in
  * DESIGN.md -- the test feeds it exactly those). */
 int cwq_selftest_div(const float* a, const float* b, int64_t n, float* out, void* stream);
+/* out[w] = max(x[64 w .. 64 w + 63]): the wave-wide DPP max the pruned encoder
+ * shares its threshold with. */
+int cwq_selftest_wave_max(const float* x, int64_t n_waves, float* out, void* stream);
 
 /* Tuning counters of the pruned encoder, filled only by builds compiled with
  * -DCWQ_PRUNE_STATS (tools/prune_stats.py); returns 1 there, 0 (and zeros)
  * otherwise.  out72[k] = candidates finished after k units (k <= 64),
- * [65] completed rows, [66] survivors pushed, [67] tiles on the screening pass.
+ * [65] completed rows, [66] survivors pushed, [67] tiles on the screening pass,
+ * [68] survivors re-evaluated exactly at tile end, [69] in-loop exact evaluations.
  * flags: bit 0 resets the counters; bit 1 / bit 2 switch the "oracle tau"
  * experiment on / off (later launches start each tile at the best value the
  * last launch found for it). */

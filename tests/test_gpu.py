@@ -376,6 +376,26 @@ def test_screen_tables_within_bounds(cwq, cwqlib):
     assert a[0].max() <= k_rmax and a[3].max() <= k_rmax
 
 
+def test_device_wave_max(cwq, cwqlib):
+    """The DPP wave-wide max (tau sharing in the pruned kernel) on random waves,
+    with -inf, ties and the maximum in every lane position."""
+    rng = np.random.default_rng(5)
+    nw = 4096
+    x = rng.standard_normal((nw, 64)).astype(np.float32)
+    x[:64, :] = -np.inf
+    for w in range(64):
+        x[64 + w, w] = 100.0                 # max in lane w
+        x[128 + w, :] = -np.inf
+        x[128 + w, w] = -5.0                 # single finite lane
+    x[300, :] = 3.0                          # all equal
+    xd = torch.from_numpy(x).cuda()
+    out = torch.empty(nw, dtype=torch.float32, device="cuda")
+    assert cwqlib.cwq_selftest_wave_max(xd.data_ptr(), nw, out.data_ptr(),
+                                        torch.cuda.current_stream().cuda_stream) == 0
+    torch.cuda.synchronize()
+    assert np.array_equal(out.cpu().numpy(), x.max(axis=1))
+
+
 def test_device_fast_division_correctly_rounded(cwq, cwqlib):
     """The 5-op quotient used by the pruned kernel equals IEEE a/b on its
     documented domain: 2^-60 <= |a| <= 2^60 (or 0), 2^-60 <= b <= 2^60."""

@@ -43,3 +43,5 @@ for k in range(1, 65):
         print(f"  finished after {k:2d} units: {hist[k] / ncand:.5f}")
 print(f"completed rows {a[65]:.0f} ({a[65] / nb:.2f}/block), survivors pushed {a[66]:.0f} "
       f"({a[66] / nb:.2f}/block), screened tiles {a[67]:.0f}")
+print(f"survivors re-evaluated exactly {a[68]:.0f} ({a[68] / nb:.2f}/block), "
+      f"in-loop exact evaluations (list full) {a[69]:.0f}")
