@@ -36,6 +36,15 @@ GROUPED = {
     "c3": (24, [32 * 48 * 128, 8 * 12 * 24], 8,
            "C3: 24 images x (196,608 + 2,304) dims, both ladder levels, 8 bits/group"),
 }
+IMPORTANCE = {
+    # name: (images, latent dims, n_bits_per_group, max_group_size_bits, dim_kl_bit_limit, desc)
+    "i1": (1, 32 * 48 * 128, 20, 4, 16,
+           "I1: one image's PLN level-1 latents (196,608 dims), grouped importance coder, "
+           "20 bits/group, groups <= 15 dims (miracle_arguments.py:177-183)"),
+    "i2": (24, 8 * 12 * 24, 20, 2, 16,
+           "I2: 24 images' PLN level-2 latents (2,304 dims each), grouped importance coder, "
+           "20 bits/group, groups <= 3 dims (miracle_arguments.py:168-174)"),
+}
 CONFIGS = {
     # name: (blocks per GPU, block dim, kl bits, n_steps, description)
     "c4": (1_000_000, 32, 16, 1, "C4: 1e6 blocks x d=32, KL=16 bits (2^16 candidates/block)"),
@@ -51,7 +60,8 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--config", default="c4", choices=sorted(CONFIGS) + sorted(GROUPED))
+    ap.add_argument("--config", default="c4",
+                    choices=sorted(CONFIGS) + sorted(GROUPED) + sorted(IMPORTANCE))
     ap.add_argument("--blocks", type=int, default=0, help="override blocks per GPU")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu", action="store_true")
@@ -102,10 +112,82 @@ def grouped_main(args):
     print(json.dumps(line), flush=True)
 
 
+def importance_main(args):
+    """I1/I2: the grouped importance pipeline per image
+    (code_grouped_importance_sample): standardise + KL on the GPU, host
+    grouping and N_g plan, the tiled candidate kernel, Elias-delta bitcode and
+    quint16 outliers.  Synthetic PLN-like latents."""
+    import compression_without_quantization_amd.coded_importance_sampler as I
+    from compression_without_quantization_amd.synthetic import make_latents
+    I.VERBOSE = False
+    n_img, D, nbits, gbits, kl_lim, desc = IMPORTANCE[args.config]
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    lat = []
+    for i in range(n_img):
+        q_loc, q_scale, p_loc, p_scale = make_latents(D, seed=5000 + i)
+        lat.append((C.Normal(torch.from_numpy(q_loc).to(dev), torch.from_numpy(q_scale).to(dev)),
+                    C.Normal(torch.from_numpy(p_loc).to(dev), torch.from_numpy(p_scale).to(dev))))
+
+    def step():
+        return [I.code_grouped_importance_sample(None, t, p, 42, nbits, max_group_size_bits=gbits,
+                                                 dim_kl_bit_limit=kl_lim) for t, p in lat]
+    for _ in range(args.warmup):
+        res = step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        res = step()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    # work: sum over groups of N_g * d_g candidate-dims (the plan the coder used)
+    cand_dims = 0
+    for (t, p), r in zip(lat, res):
+        starts = np.asarray(r[2], dtype=np.int64)
+        cand_dims += _importance_work(t, p, starts, kl_lim, dev)
+    groups = sum(len(r[2]) - 1 for r in res)
+    bitlen = sum(len(r[1]) for r in res)
+    line = {"metric": "images coded/s (grouped importance pipeline)",
+            "value": n_img * args.steps / el, "unit": "images/s", "n_gpus": 1,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": el / args.steps * 1e3,
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+            "data": "synthetic PLN-like latents",
+            "config": {"workload": desc, "groups_per_step": groups, "bits_per_step": bitlen,
+                       "groups_per_s": groups * args.steps / el,
+                       "candidate_dims_per_step": cand_dims,
+                       "candidate_dims_per_s": cand_dims * args.steps / el}}
+    print(json.dumps(line), flush=True)
+
+
+def _importance_work(target, proposal, starts, kl_lim, dev):
+    """sum_g N_g d_g for the plan code_grouped_importance_sample used."""
+    import compression_without_quantization_amd.coded_importance_sampler as I
+    lib = _lib.load()
+    D = proposal.loc.numel()
+    t_loc = torch.empty(D, dtype=torch.float32, device=dev)
+    t_scale = torch.empty(D, dtype=torch.float32, device=dev)
+    f = lambda x: x.contiguous().float()
+    tl, ts, pl, ps = f(target.loc), f(target.scale), f(proposal.loc), f(proposal.scale)
+    _lib.check(lib.cwq_standardise(tl.data_ptr(), ts.data_ptr(), pl.data_ptr(), ps.data_ptr(), D,
+                                   t_loc.data_ptr(), t_scale.data_ptr(),
+                                   torch.cuda.current_stream(dev).cuda_stream), "standardise")
+    kl_bits = I._kl(dev, tl, ts, pl, ps).cpu().numpy() / np.float32(np.log(2))
+    keep = torch.from_numpy(kl_bits <= kl_lim).to(dev)
+    t_loc = torch.where(keep, t_loc, torch.zeros_like(t_loc))
+    t_scale = torch.where(keep, t_scale, torch.ones_like(t_scale))
+    z, o = torch.zeros_like(t_loc), torch.ones_like(t_loc)
+    kl = I._kl(dev, t_loc, t_scale, z, o).cpu().numpy()
+    n = I.num_samples_plan(kl, starts)
+    sizes = np.diff(starts)
+    return int((np.maximum(n, 1) * sizes).sum())
+
+
 def main():
     args = parse()
     if args.config in GROUPED:
         return grouped_main(args)
+    if args.config in IMPORTANCE:
+        return importance_main(args)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
@@ -247,15 +329,34 @@ def main():
         n = min(nb, 2 * nthr)
         dt, wi, wsm = run(n)
         if dt < args.cpu_seconds / 4 and n < nb:
-            n = int(min(nb, max(n, n * args.cpu_seconds / max(dt, 1e-3))))
+            rate = n / max(dt, 1e-3)
+            n = int(min(nb, max(n, rate * args.cpu_seconds)))
+            if n < min(nb, 10_000) and min(nb, 10_000) / rate <= 30.0:
+                n = min(nb, 10_000)     # the first 10^4 blocks where that fits 30 s
             n = max(nthr, (n // nthr) * nthr)
             dt, wi, wsm = run(n)
         mism_idx = int((wi != idx_h[:n]).sum())
         mism_smp = int((wsm.view(np.uint32) != samp_h[:n * d].view(np.uint32)).sum())
+        # 1-core figure on a short sample
+        n1 = max(1, min(n, int(max(1.0, n / dt / nthr * 3.0))))
+        off1 = np.arange(n1 + 1, dtype=np.int64) * d
+        c0 = time.perf_counter()
+        O.greedy_encode(host["post_loc"].reshape(-1)[:n1 * d], host["post_scale"].reshape(-1)[:n1 * d],
+                        host["prior_loc"].reshape(-1)[:n1 * d], host["prior_scale"].reshape(-1)[:n1 * d],
+                        off1, bits, n_steps, seed, 1.0, block_id_base, 1)
+        dt1 = time.perf_counter() - c0
+        model = ""
+        try:
+            with open("/proc/cpuinfo") as f:
+                model = next((ln.split(":", 1)[1].strip() for ln in f if ln.startswith("model name")), "")
+        except OSError:
+            pass
         cpu = {"value": n / dt, "unit": "blocks/s", "cores": nthr, "kind": "port",
                "sample": f"first {n} blocks of the same {args.config} workload "
                          f"({n * (1 << bits) * d:.3g} candidate-dims, {dt:.1f} s), "
-                         "oracle/cwq_oracle.c OpenMP over blocks"}
+                         "oracle/cwq_oracle.c OpenMP over blocks",
+               "one_core_value": n1 / dt1, "one_core_sample": f"first {n1} blocks, {dt1:.1f} s",
+               "cpu_model": model}
         parity = {"blocks_checked": n, "index_mismatches": mism_idx,
                   "sample_word_mismatches": mism_smp}
 

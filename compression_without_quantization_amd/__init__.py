@@ -5,6 +5,7 @@ code/misc.py and code/binary_io.py (bit-string helpers); every sample is
 computed by the gfx950 kernels in libcwq.so (see include/cwq.h).
 """
 from .binary_io import (bitcode_to_indices, elias_delta_code, elias_delta_decode,
+                        elias_delta_code_many, elias_delta_decode_many,
                         from_bit_string, indices_to_bitcode, read_bin_code, to_bit_string,
                         write_bin_code)
 from .coding import ArithmeticCoder
@@ -26,7 +27,8 @@ __all__ = [
     "encode_workspace_bytes", "group_starts", "group_size_threshold",
     "stateless_normal_sample", "to_bit_string", "from_bit_string", "indices_to_bitcode",
     "bitcode_to_indices", "shard_range", "gather_indices", "elias_delta_code",
-    "elias_delta_decode", "code_importance_sample", "decode_importance_sample",
+    "elias_delta_decode", "elias_delta_code_many", "elias_delta_decode_many",
+    "code_importance_sample", "decode_importance_sample",
     "code_grouped_importance_sample", "decode_grouped_importance_sample",
     "importance_encode_blocks", "importance_decode_blocks", "ArithmeticCoder",
     "write_bin_code", "read_bin_code",

@@ -104,6 +104,41 @@ def elias_delta_decode(x):
     return num, 2 * l + n_plus_one
 
 
+def elias_delta_code_many(values):
+    """''.join(elias_delta_code(v) for v in values), in one native call
+    (cwq_elias_delta_encode).  Values >= 2^30, where the reference's float64
+    formulas are not proven equal to the bit lengths, take the Python path."""
+    from . import _lib
+    x = np.ascontiguousarray(np.asarray(values, dtype=np.int64).reshape(-1))
+    if x.size == 0:
+        return ''
+    if x.min() < 1 or x.max() >= (1 << 30):
+        return ''.join(elias_delta_code(int(v)) for v in x)
+    lib = _lib.load()
+    n = _lib.check(lib.cwq_elias_delta_encode(x.ctypes.data, x.size, None, 0), "elias encode")
+    buf = np.empty(n, dtype=np.uint8)
+    _lib.check(lib.cwq_elias_delta_encode(x.ctypes.data, x.size, buf.ctypes.data, n),
+               "elias encode")
+    return buf.tobytes().decode('ascii')
+
+
+def elias_delta_decode_many(bitcode, count):
+    """Parse ``count`` concatenated Elias-delta codes from the start of
+    ``bitcode`` (str or bytes).  Returns (values int64 [count], chars consumed).
+    Raises ValueError when the code runs out (cwq_elias_delta_decode)."""
+    from . import _lib
+    raw = bitcode.encode('ascii') if isinstance(bitcode, str) else bytes(bitcode)
+    out = np.empty(max(int(count), 0), dtype=np.int64)
+    if count <= 0:
+        return out, 0
+    lib = _lib.load()
+    r = lib.cwq_elias_delta_decode(raw, len(raw), int(count), out.ctypes.data)
+    if r < 0:
+        raise ValueError("bitcode exhausted or corrupt: " +
+                         lib.cwq_last_error().decode("utf-8", "replace"))
+    return out, int(r)
+
+
 # ---------------------------------------------------------------------------
 # .miracle container (binary_io.py:69-197)
 # ---------------------------------------------------------------------------

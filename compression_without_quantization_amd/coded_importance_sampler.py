@@ -25,7 +25,8 @@ import numpy as np
 import torch
 
 from . import _lib
-from .binary_io import elias_delta_code, elias_delta_decode
+from .binary_io import (elias_delta_code, elias_delta_code_many, elias_delta_decode,
+                        elias_delta_decode_many)
 from .coded_greedy_sampler import _device_of, _f32, _is_float32, _like_input, _ptr
 
 VERBOSE = True
@@ -244,7 +245,7 @@ def code_grouped_importance_sample(sess, target, proposal, seed, n_bits_per_grou
     sample_h = sample_h.astype(np.float32)
     if return_indices:
         return sample_h, indices, group_start_indices, outlier_extras
-    bitcode = ''.join(elias_delta_code(i) for i in indices)
+    bitcode = elias_delta_code_many(indices)
     return sample_h, bitcode, group_start_indices, outlier_extras
 
 
@@ -278,14 +279,8 @@ def decode_grouped_importance_sample(sess, bitcode, group_start_indices, proposa
     if use_indices:
         index = [int(bitcode[i]) - 1 for i in range(G)]
     else:
-        code = bitcode.encode("ascii") if isinstance(bitcode, str) else bytes(bitcode)
-        index = []
-        for _ in range(G):                                          # :325-336
-            if not code:
-                raise ValueError("bitcode exhausted before the last group")
-            num, codelength = elias_delta_decode(code)
-            index.append(num - 1)
-            code = code[codelength:]
+        nums, _ = elias_delta_decode_many(bitcode, G)               # :325-336
+        index = [int(v) - 1 for v in nums]
     zeros = torch.zeros(D, dtype=torch.float32, device=dev)
     ones = torch.ones(D, dtype=torch.float32, device=dev)
     sample = importance_decode_blocks(index, zeros, ones, starts, seed)

@@ -176,4 +176,55 @@ int64_t cwq_ac_decode(const int64_t* counts, int64_t K, int precision, const cha
   }
 }
 
+// Elias-delta strings for the importance sampler's indices (binary_io.py:7-39),
+// vectorised: the reference's float64 formulas n = floor(log2 x),
+// l = floor(log2(n + 1)) equal the bit lengths for 1 <= x < 2^30
+// (tests/test_importance.py); larger x is rejected so the caller can fall back.
+int64_t cwq_elias_delta_encode(const int64_t* x, int64_t n, char* out, int64_t cap) {
+  if (n < 0 || (n > 0 && !x)) return cwq::set_error(CWQ_ERR_INVALID, "cwq_elias_delta_encode: bad arguments");
+  int64_t pos = 0;
+  for (int64_t i = 0; i < n; ++i) {
+    const int64_t v = x[i];
+    if (v < 1 || v >= ((int64_t)1 << 30))
+      return cwq::set_error(CWQ_ERR_INVALID, "cwq_elias_delta_encode: value outside [1, 2^30)");
+    const int nb = 63 - __builtin_clzll((unsigned long long)v);          // n = floor(log2 v)
+    const int l = 63 - __builtin_clzll((unsigned long long)(nb + 1));    // floor(log2(n + 1))
+    const int64_t len = (int64_t)l + (l + 1) + nb;
+    if (out) {
+      if (pos + len > cap) return cwq::set_error(CWQ_ERR_CAPACITY, "cwq_elias_delta_encode: cap");
+      char* o = out + pos;
+      for (int k = 0; k < l; ++k) *o++ = '0';
+      for (int k = l; k >= 0; --k) *o++ = (char)('0' + (((nb + 1) >> k) & 1));  // n+1, MSB first
+      for (int k = nb - 1; k >= 0; --k) *o++ = (char)('0' + ((v >> k) & 1));     // v without its top bit
+    }
+    pos += len;
+  }
+  cwq::set_error(CWQ_OK, "");
+  return pos;
+}
+
+int64_t cwq_elias_delta_decode(const char* bits, int64_t nbits, int64_t count, int64_t* out) {
+  if (nbits < 0 || count < 0 || (nbits > 0 && !bits) || (count > 0 && !out))
+    return cwq::set_error(CWQ_ERR_INVALID, "cwq_elias_delta_decode: bad arguments");
+  int64_t pos = 0;
+  for (int64_t i = 0; i < count; ++i) {
+    int l = 0;
+    while (pos + l < nbits && bits[pos + l] == '0') ++l;
+    if (l > 30 || pos + 2 * l + 1 > nbits)
+      return cwq::set_error(CWQ_ERR_INVALID, "cwq_elias_delta_decode: code exhausted or corrupt");
+    pos += l;
+    int64_t np1 = 0;
+    for (int k = 0; k <= l; ++k) np1 = (np1 << 1) | (bits[pos + k] == '1');
+    pos += l + 1;
+    if (np1 < 1 || np1 > 31 || pos + (np1 - 1) > nbits)
+      return cwq::set_error(CWQ_ERR_INVALID, "cwq_elias_delta_decode: code exhausted or corrupt");
+    int64_t v = 1;
+    for (int64_t k = 0; k < np1 - 1; ++k) v = (v << 1) | (bits[pos + k] == '1');
+    pos += np1 - 1;
+    out[i] = v;
+  }
+  cwq::set_error(CWQ_OK, "");
+  return pos;
+}
+
 }  // extern "C"

@@ -330,8 +330,8 @@ int cwq_importance_encode(const float* t_loc, const float* t_scale, const float*
     return fail(CWQ_ERR_WORKSPACE, "workspace %zu bytes < required %zu", workspace_bytes, need);
   hipError_t e = cwq::launch_importance_encode(t_loc, t_scale, p_loc, p_scale, block_off,
                                                n_samples, nb, total_dims, seed, block_id_base,
-                                               out_index, out_sample, workspace,
-                                               (hipStream_t)stream);
+                                               g_prune >= 2 ? 1 : 0, out_index, out_sample,
+                                               workspace, (hipStream_t)stream);
   if (e != hipSuccess) return hip_fail(e, "cwq_importance_encode");
   return ok();
 }

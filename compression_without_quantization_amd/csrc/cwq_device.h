@@ -118,6 +118,25 @@ __device__ __forceinline__ void box_muller_screen(uint32_t x0, uint32_t x1, floa
   f1 = c * u2;
 }
 
+// Error constants of the screening Box-Muller, shared by both screening passes.
+// measured maxima over all 2^23 inputs (tools/screen_err.py, re-checked by
+// tests/test_gpu.py): |r~ - r| <= 4.77e-7, |sin~ - sin|, |cos~ - cos| <= 2.99e-7
+constexpr double kScreenEr = 1.0e-6;
+constexpr double kScreenEs = 6.0e-7;
+constexpr double kScreenRmax = 5.68;  // r <= sqrt(-2 ln 1e-7) = 5.6777
+// |RN(s~ r~) - RN(s r)| <= (1 + Es) Er + Rmax Es + 2^-23 (Rmax + Er)
+constexpr double kScreenEz =
+    (1.0 + kScreenEs) * kScreenEr + kScreenRmax * kScreenEs + 0x1p-23 * (kScreenRmax + kScreenEr);
+constexpr double kScreenZm = 5.7;     // bound on |z| and |z~|
+
+__device__ __forceinline__ F4 normal4_screen(const PhiloxStream& s, uint64_t grp) {
+  const U4 x = philox_block_dev(s, grp);
+  F4 z;
+  box_muller_screen(x.x, x.y, z.a, z.b);
+  box_muller_screen(x.z, x.w, z.c, z.d);
+  return z;
+}
+
 __device__ __forceinline__ F4 normal4_dev(const PhiloxStream& s, uint64_t grp,
                                           const double* logtab) {
   const U4 x = philox_block_dev(s, grp);
@@ -208,6 +227,7 @@ __device__ __forceinline__ float round_up_f32(double b) {
   }
   return f;
 }
+__device__ __forceinline__ float round_dn_f32(double b) { return -round_up_f32(-b); }
 
 template <int DC, class ElemF>
 __device__ __forceinline__ float eval_row_f(const PhiloxStream& st, uint64_t kbase, int64_t d_rt,

@@ -18,7 +18,11 @@
 
 namespace cwq {
 
-constexpr int64_t kImpCandPerTile = 4096;
+constexpr int64_t kImpCandPerTile = 16384;
+constexpr int kImpScreenMaxD = 256;   // screening pass: per-dim constants live in LDS
+#ifndef CWQ_IMP_SURVIVOR_CAP
+#define CWQ_IMP_SURVIVOR_CAP 1024
+#endif
 
 __global__ void __launch_bounds__(256) k_imp_prep(const float* __restrict__ t_scale,
                                                   const float* __restrict__ p_scale, int64_t n,
@@ -32,9 +36,11 @@ __global__ void __launch_bounds__(256) k_imp_prep(const float* __restrict__ t_sc
 }
 
 // tprefix[g] = sum_{h<g} ceil(max(N_h,1) / cpt); tprefix[nb] = total tiles.
+// Also resets the per-group shared screening threshold gtau[g].
 __global__ void __launch_bounds__(1024) k_imp_tiles(const int64_t* __restrict__ n_samples,
                                                     int64_t nb, int64_t cpt,
-                                                    int64_t* __restrict__ tprefix) {
+                                                    int64_t* __restrict__ tprefix,
+                                                    uint32_t* __restrict__ gtau) {
   __shared__ int64_t part[1024];
   const int64_t chunk = (nb + 1023) / 1024;
   const int64_t g0 = threadIdx.x * chunk;
@@ -43,6 +49,7 @@ __global__ void __launch_bounds__(1024) k_imp_tiles(const int64_t* __restrict__ 
   for (int64_t g = g0; g < g1; ++g) {
     const int64_t n = n_samples[g] > 1 ? n_samples[g] : 1;
     sum += (n + cpt - 1) / cpt;
+    gtau[g] = ord_f32(-__builtin_inff());
   }
   part[threadIdx.x] = sum;
   __syncthreads();
@@ -64,14 +71,91 @@ __global__ void __launch_bounds__(1024) k_imp_tiles(const int64_t* __restrict__ 
   }
 }
 
+// Screening row value: sum_j (A_j z_j + B_j) z_j + C_j over the candidate's
+// dims, z from the hardware-transcendental Box-Muller ("screening
+// the importance sampler").  `align` = (kbase mod 4) must be wave-uniform.
+__device__ __forceinline__ float screen_row_imp(const PhiloxStream& st, uint64_t kbase, int64_t d,
+                                                int align, const float4* __restrict__ coef) {
+  float s = 0.0f;
+  F4 z = {0.f, 0.f, 0.f, 0.f};
+  for (int64_t e = 0; e < d; ++e) {
+    const int w = (align + (int)(e & 3)) & 3;  // wave-uniform
+    if (w == 0 || e == 0) z = normal4_screen(st, (kbase + (uint64_t)e) >> 2);
+    const float zz = w == 0 ? z.a : (w == 1 ? z.b : (w == 2 ? z.c : z.d));
+    const float4 c = coef[e];
+    s = s + __builtin_fmaf(__builtin_fmaf(c.x, zz, c.y), zz, c.z);
+  }
+  return s;
+}
+
+// Per-dim screening constants and error bound (host-free, in double).  The
+// exact term is t = RN(lt - lq), lt = RN(RN(-0.5 RN(yt^2)) - ct),
+// yt = RN(RN(x - tl) / ts), lq likewise with (pl, ps, cp), x = RN(pl + RN(ps z)).
+// In real arithmetic t(z) = A z^2 + B z + C with a = ps/ts, b = (pl - tl)/ts,
+// A = (1 - a^2)/2, B = -a b, C = cp - ct - b^2/2.  Returns false if the dim
+// must not be screened.
+struct ImpScreenDim {
+  float A, B, C, err, mag;
+};
+__device__ __forceinline__ bool imp_screen_dim(float tl, float ts, float pl, float ps, float ct,
+                                               float cp, ImpScreenDim& o) {
+  if (!(ts >= 0x1p-60f && ts <= 0x1p60f && ps >= 0x1p-60f && ps <= 0x1p60f)) return false;
+  if (!(tl - tl == 0.0f && pl - pl == 0.0f && ct - ct == 0.0f && cp - cp == 0.0f)) return false;
+  const double u = 0x1p-24, r = 1.0001, Zm = kScreenZm, Ez = kScreenEz;
+  const double dtl = tl, dts = ts, dpl = pl, dps = ps, dct = ct, dcp = cp;
+  // rounding of the exact chain, bounded with |z| <= Zm
+  const double m1 = __builtin_fabs(dps) * Zm;
+  const double mx = __builtin_fabs(dpl) + m1;
+  const double ex = u * (m1 + mx) * r;
+  const double mdt = mx + __builtin_fabs(dtl), mdq = mx + __builtin_fabs(dpl);
+  const double Myt = mdt / dts * (1.0 + 4.0 * u), Myq = mdq / dps * (1.0 + 4.0 * u);
+  const double eyt = ((ex + u * mdt) / dts + u * Myt) * r;
+  const double eyq = ((ex + u * mdq) / dps + u * Myq) * r;
+  const double lt_mag = 0.5 * Myt * Myt + __builtin_fabs(dct);
+  const double lq_mag = 0.5 * Myq * Myq + __builtin_fabs(dcp);
+  const double rho = (0.5 * (2.0 * Myt * eyt + eyt * eyt + u * Myt * Myt) + u * lt_mag +
+                      0.5 * (2.0 * Myq * eyq + eyq * eyq + u * Myq * Myq) + u * lq_mag +
+                      u * (lt_mag + lq_mag)) * r;
+  // the real quadratic and its float coefficients
+  const double a = dps / dts, b = (dpl - dtl) / dts;
+  const double A = 0.5 * (1.0 - a * a), B = -a * b, C = dcp - dct - 0.5 * b * b;
+  o.A = (float)A;
+  o.B = (float)B;
+  o.C = (float)C;
+  const double dA = __builtin_fabs((double)o.A - A) + 0x1p-50 * (1.0 + a * a);
+  const double dB = __builtin_fabs((double)o.B - B) + 0x1p-50 * __builtin_fabs(a * b);
+  const double dC = __builtin_fabs((double)o.C - C) +
+                    0x1p-50 * (__builtin_fabs(dcp) + __builtin_fabs(dct) + b * b);
+  const double fA = __builtin_fabs((double)o.A), fB = __builtin_fabs((double)o.B);
+  const double fC = __builtin_fabs((double)o.C);
+  const double h1 = fA * Zm + fB;  // |A z + B|
+  const double horner = dA * Zm * Zm + dB * Zm + dC + Zm * u * h1 * r + u * (h1 * Zm * r + fC);
+  // z~ vs z: |t(z) - t(z~)| <= max|t'| Ez + |A| Ez^2
+  const double slope = 2.0 * __builtin_fabs(A) * Zm + __builtin_fabs(B);
+  const double e = (rho + slope * Ez + __builtin_fabs(A) * Ez * Ez + horner) * (1.0 + 0x1p-20) +
+                   0x1p-140;
+  o.err = round_up_f32(e);
+  o.mag = round_up_f32(lt_mag + lq_mag + e);  // bounds |t| and |t~|
+  return o.err - o.err == 0.0f && o.mag - o.mag == 0.0f && o.A - o.A == 0.0f &&
+         o.B - o.B == 0.0f && o.C - o.C == 0.0f;
+}
+
 __global__ void __launch_bounds__(256) k_imp_eval(
     const float* __restrict__ t_loc, const float* __restrict__ t_scale,
     const float* __restrict__ p_loc, const float* __restrict__ p_scale,
     const float* __restrict__ lnt, const float* __restrict__ lnp,
     const int64_t* __restrict__ block_off, const int64_t* __restrict__ n_samples, int64_t nb,
     const int64_t* __restrict__ tprefix, int64_t cpt, int32_t seed, int64_t block_id_base,
-    unsigned long long* __restrict__ keys) {
+    int allow_screen, uint32_t* __restrict__ gtau, unsigned long long* __restrict__ keys) {
   __shared__ double logtab[32];
+  __shared__ float4 coef[kImpScreenMaxD];   // A, B, C per dim (screening)
+  __shared__ float derr[kImpScreenMaxD];    // per-dim error bound
+  __shared__ float dmag[kImpScreenMaxD];    // per-dim magnitude bound
+  __shared__ float etot_sh;
+  __shared__ uint32_t tau_ord;
+  __shared__ uint32_t sq_cnt;
+  __shared__ uint32_t sq_n[CWQ_IMP_SURVIVOR_CAP];
+  __shared__ float sq_up[CWQ_IMP_SURVIVOR_CAP];
   __shared__ unsigned long long wkey[4];
   fill_logtab(logtab);
   const uint32_t wv = wave_id();
@@ -79,6 +163,8 @@ __global__ void __launch_bounds__(256) k_imp_eval(
   const int64_t total = tprefix[nb];
 
   for (int64_t tile = blockIdx.x; tile < total; tile += gridDim.x) {
+    uint32_t tid = threadIdx.x;
+    asm volatile("" : "+v"(tid));
     // group of this tile: last g with tprefix[g] <= tile
     int64_t lo = 0, hi = nb;  // tprefix[lo] <= tile < tprefix[hi]
     while (hi - lo > 1) {
@@ -99,24 +185,101 @@ __global__ void __launch_bounds__(256) k_imp_eval(
     const float* ps = p_scale + off;
     const float* ct = lnt + off;
     const float* cp = lnp + off;
+    auto exact_row = [&](int64_t n) -> float {
+      return eval_row_f<0>(st, (uint64_t)n * (uint64_t)d, d, (int)(((uint64_t)n * d) & 3u), logtab,
+                           [&](int64_t e, float zz) -> float {
+                             float x = ps[e] * zz;  // misc.py:14
+                             x = pl[e] + x;         // misc.py:15
+                             const float lt = log_prob(x, tl[e], ts[e], ct[e]);
+                             const float lq = log_prob(x, pl[e], ps[e], cp[e]);
+                             return lt - lq;        // :60
+                           });
+    };
+
+    // screening gate and constants
+    int ok = (allow_screen && d >= 1 && d <= kImpScreenMaxD) ? 1 : 0;
+    if (ok && tid < d) {
+      ImpScreenDim o;
+      ok = imp_screen_dim(tl[tid], ts[tid], pl[tid], ps[tid], ct[tid], cp[tid], o) ? 1 : 0;
+      coef[tid] = float4{o.A, o.B, o.C, 0.0f};
+      derr[tid] = o.err;
+      dmag[tid] = o.mag;
+    }
+    const bool screen = __syncthreads_and(ok) != 0;
+    if (screen && tid == 0) {
+      double es = 0.0, ms = 0.0;
+      for (int64_t j = 0; j < d; ++j) {
+        es += (double)derr[j];
+        ms += (double)dmag[j];
+      }
+      // |screened sum - exact Eigen-order sum| <= sum err_j + 2 gamma_d sum mag_j
+      const double gam = 1.01 * (double)d * 0x1p-24;
+      const double et = (es + 2.0 * gam * ms) * (1.0 + 0x1p-20) + 0x1p-126;
+      etot_sh = et < 1.0e3 ? round_up_f32(et) : __builtin_inff();
+      tau_ord = ord_f32(-__builtin_inff());
+      sq_cnt = 0u;
+    }
+    __syncthreads();
+    const float E = etot_sh;
 
     uint64_t bestk = 0;
-    for (int64_t n = n0 + 4 * (int64_t)lane + wv; n < n1; n += 256) {
-      const float v = eval_row_f<0>(st, (uint64_t)n * (uint64_t)d, d, align, logtab,
-                                    [&](int64_t e, float zz) -> float {
-                                      float x = ps[e] * zz;  // misc.py:14
-                                      x = pl[e] + x;         // misc.py:15
-                                      const float lt = log_prob(x, tl[e], ts[e], ct[e]);
-                                      const float lq = log_prob(x, pl[e], ps[e], cp[e]);
-                                      return lt - lq;        // :60
-                                    });
-      const uint64_t k = argmax_key(v, (uint32_t)n);
-      bestk = k > bestk ? k : bestk;
+    if (screen && E - E == 0.0f) {
+      float tau = -__builtin_inff();
+      for (int64_t n = n0 + 4 * (int64_t)lane + wv; n < n1; n += 256) {
+        const float sh = screen_row_imp(st, (uint64_t)n * (uint64_t)d, d, align, coef);
+        const float slack = E + __builtin_fabsf(sh) * 0x1p-22f;
+        const float up = sh + slack;
+        if (up >= tau) {  // may be the best: keep it
+          tau = fmaxf(tau, sh - slack);
+          const uint32_t slot = atomicAdd(&sq_cnt, 1u);
+          if (slot < CWQ_IMP_SURVIVOR_CAP) {
+            sq_n[slot] = (uint32_t)(n - n0);
+            sq_up[slot] = up;
+          } else {  // list full: evaluate exactly now
+            const uint64_t k = argmax_key(exact_row(n), (uint32_t)n);
+            bestk = k > bestk ? k : bestk;
+          }
+        }
+      }
+      {
+        const float tm = wave_max_f32(tau);
+        if (lane == 0) atomicMax(&tau_ord, ord_f32(tm));
+      }
+      __syncthreads();
+      // this tile's threshold, raised by what other tiles of the group published
+      if (tid == 0) {
+        const uint32_t mine = tau_ord;
+        const uint32_t prev = atomicMax(&gtau[g], mine);
+        tau_ord = prev > mine ? prev : mine;
+      }
+      __syncthreads();
+      const float tau_final = unord_f32(tau_ord);
+      const uint32_t ns = sq_cnt < CWQ_IMP_SURVIVOR_CAP ? sq_cnt : CWQ_IMP_SURVIVOR_CAP;
+      for (uint32_t i = tid; i < ns; i += blockDim.x) {
+        if (sq_up[i] >= tau_final) {
+          const int64_t n = n0 + (int64_t)sq_n[i];
+          const uint64_t k = argmax_key(exact_row(n), (uint32_t)n);
+          bestk = k > bestk ? k : bestk;
+        }
+      }
+    } else {
+      for (int64_t n = n0 + 4 * (int64_t)lane + wv; n < n1; n += 256) {
+        const float v = eval_row_f<0>(st, (uint64_t)n * (uint64_t)d, d, align, logtab,
+                                      [&](int64_t e, float zz) -> float {
+                                        float x = ps[e] * zz;  // misc.py:14
+                                        x = pl[e] + x;         // misc.py:15
+                                        const float lt = log_prob(x, tl[e], ts[e], ct[e]);
+                                        const float lq = log_prob(x, pl[e], ps[e], cp[e]);
+                                        return lt - lq;        // :60
+                                      });
+        const uint64_t k = argmax_key(v, (uint32_t)n);
+        bestk = k > bestk ? k : bestk;
+      }
     }
     bestk = wave_max_u64(bestk);
     if (lane == 0) wkey[wv] = bestk;
     __syncthreads();
-    if (threadIdx.x == 0) {
+    if (tid == 0) {
       uint64_t m = wkey[0];
       for (int i = 1; i < 4; ++i) m = wkey[i] > m ? wkey[i] : m;
       if (m) atomicMax(&keys[g], (unsigned long long)m);
@@ -166,14 +329,16 @@ __global__ void __launch_bounds__(256) k_imp_rows(
 
 size_t importance_workspace_size(int64_t nb, int64_t total_dims) {
   auto up = [](size_t v) { return (v + 255) / 256 * 256; };
-  return up((size_t)nb * 8) + up((size_t)(nb + 1) * 8) + 2 * up((size_t)total_dims * 4);
+  return up((size_t)nb * 8) + up((size_t)(nb + 1) * 8) + 2 * up((size_t)total_dims * 4) +
+         up((size_t)nb * 4);
 }
 
 hipError_t launch_importance_encode(const float* t_loc, const float* t_scale, const float* p_loc,
                                     const float* p_scale, const int64_t* block_off,
                                     const int64_t* n_samples, int64_t nb, int64_t total_dims,
-                                    int32_t seed, int64_t block_id_base, int64_t* out_index,
-                                    float* out_sample, void* workspace, hipStream_t stream) {
+                                    int32_t seed, int64_t block_id_base, int allow_screen,
+                                    int64_t* out_index, float* out_sample, void* workspace,
+                                    hipStream_t stream) {
   if (nb <= 0) return hipSuccess;
   auto up = [](size_t v) { return (v + 255) / 256 * 256; };
   char* w = (char*)workspace;
@@ -181,16 +346,17 @@ hipError_t launch_importance_encode(const float* t_loc, const float* t_scale, co
   int64_t* tprefix = (int64_t*)(w + up((size_t)nb * 8));
   float* lnt = (float*)(w + up((size_t)nb * 8) + up((size_t)(nb + 1) * 8));
   float* lnp = lnt + up((size_t)total_dims * 4) / 4;
+  uint32_t* gtau = (uint32_t*)((char*)lnp + up((size_t)total_dims * 4));
   hipError_t e = hipMemsetAsync(keys, 0, (size_t)nb * 8, stream);
   if (e != hipSuccess) return e;
   if (total_dims > 0)
     hipLaunchKernelGGL(k_imp_prep, dim3(grid_for(total_dims, 256, 65536)), dim3(256), 0, stream,
                        t_scale, p_scale, total_dims, lnt, lnp);
   hipLaunchKernelGGL(k_imp_tiles, dim3(1), dim3(1024), 0, stream, n_samples, nb,
-                     kImpCandPerTile, tprefix);
+                     kImpCandPerTile, tprefix, gtau);
   hipLaunchKernelGGL(k_imp_eval, dim3(256 * 16), dim3(256), 0, stream, t_loc, t_scale, p_loc,
                      p_scale, lnt, lnp, block_off, n_samples, nb, tprefix, kImpCandPerTile, seed,
-                     block_id_base, keys);
+                     block_id_base, allow_screen, gtau, keys);
   hipLaunchKernelGGL(k_imp_rows, dim3(grid_for(nb, 4, 65536)), dim3(256), 0, stream,
                      (const unsigned long long*)keys, (const int64_t*)nullptr, p_loc, p_scale,
                      block_off, nb, seed, block_id_base, out_index, out_sample);

@@ -57,8 +57,9 @@ size_t importance_workspace_size(int64_t nb, int64_t total_dims);
 hipError_t launch_importance_encode(const float* t_loc, const float* t_scale, const float* p_loc,
                                     const float* p_scale, const int64_t* block_off,
                                     const int64_t* n_samples, int64_t nb, int64_t total_dims,
-                                    int32_t seed, int64_t block_id_base, int64_t* out_index,
-                                    float* out_sample, void* workspace, hipStream_t stream);
+                                    int32_t seed, int64_t block_id_base, int allow_screen,
+                                    int64_t* out_index, float* out_sample, void* workspace,
+                                    hipStream_t stream);
 hipError_t launch_importance_decode(const int64_t* index, const float* p_loc,
                                     const float* p_scale, const int64_t* block_off, int64_t nb,
                                     int32_t seed, int64_t block_id_base, float* out_sample,

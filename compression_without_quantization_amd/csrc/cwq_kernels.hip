@@ -193,17 +193,7 @@ constexpr float kScreenC2 = 1.0f + 0x1p-13f;
 constexpr double kScreenEps = 0x1p-15;  // split of the additive error: (x-A)^2 >= (1-e)x^2 - (1/e-1)A^2
 constexpr double kScreenPhi = (1.0 - kScreenEps) * (1.0 - 0x1p-21);
 constexpr double kScreenKappa = 0.7070958018530696;  // sqrt(phi (1 - 2^-24) / 2), rounded down
-// measured maxima over all 2^23 inputs (tools/screen_err.py, re-checked by
-// tests/test_gpu.py): |r~ - r| <= 4.77e-7, |sin~ - sin|, |cos~ - cos| <= 2.99e-7
-constexpr double kScreenEr = 1.0e-6;
-constexpr double kScreenEs = 6.0e-7;
-constexpr double kScreenRmax = 5.68;  // r <= sqrt(-2 ln 1e-7) = 5.6777
-// |RN(s~ r~) - RN(s r)| <= (1 + Es) Er + Rmax Es + 2^-23 (Rmax + Er)
-constexpr double kScreenEz =
-    (1.0 + kScreenEs) * kScreenEr + kScreenRmax * kScreenEs + 0x1p-23 * (kScreenRmax + kScreenEr);
-constexpr double kScreenZm = 5.7;     // bound on |z| and |z~|
 
-__device__ __forceinline__ float round_dn_f32(double b) { return -round_up_f32(-b); }
 
 #ifdef CWQ_PRUNE_STATS
 // tuning builds only (tools/prune_stats.py): [0..64] candidates finished after

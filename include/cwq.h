@@ -182,6 +182,16 @@ int64_t cwq_ac_encode(const int64_t* counts, int64_t K, int precision, const int
 int64_t cwq_ac_decode(const int64_t* counts, int64_t K, int precision, const char* bits,
                       int64_t nbits, int64_t* out_msg, int64_t cap);
 
+/* Elias-delta codes of the importance sampler's index + 1 values
+ * (code/binary_io.py:7-39), concatenated.  Host memory.  encode writes the
+ * '0'/'1' chars of x[0..n) to out (NULL: only count) and returns their
+ * number; values must lie in [1, 2^30) (CWQ_ERR_INVALID otherwise, where the
+ * reference's float64 log formulas may differ from the bit lengths).  decode
+ * parses `count` codes from bits[0..nbits) into out and returns the chars
+ * consumed (coded_importance_sampler.py:325-336). */
+int64_t cwq_elias_delta_encode(const int64_t* x, int64_t n, char* out, int64_t cap);
+int64_t cwq_elias_delta_decode(const char* bits, int64_t nbits, int64_t count, int64_t* out);
+
 /* Diagnostics (used by the parity tests): evaluate the device restatement of
  * the Box-Muller transcendentals for the 23-bit mantissas m0 .. m0+count-1:
  *   radius[i] = sqrtf(-2 logf(max(m*2^-23, 1e-7f)))    (BoxMullerFloat u2)
@@ -224,7 +234,8 @@ int cwq_profile_set_eval_events(void* start_event, void* stop_event);
  * host thread (A/B timing and tests): 0 = off (every candidate scored
  * exactly), 1 = pruning on exact values, 2 (default) = pruning with the
  * screening pass (DESIGN.md "screening bound") where a tile's constants allow
- * it, exact pruning elsewhere. */
+ * it, exact pruning elsewhere.  Mode 2 also turns on the importance sampler's
+ * screening pass; modes 0 and 1 score its candidates exactly. */
 int cwq_set_pruning(int mode);
 
 #ifdef __cplusplus

@@ -509,3 +509,64 @@ def test_importance_grouped_golden(cwq, golden):
                                                 proposal, 20, int(g["seed"]), oi, oq,
                                                 use_indices=True)
     _assert_bits_equal(dec2, dec, "use_indices decode")
+
+
+# ---------------------------------------------------------------------------
+# importance sampler screening pass: the screened encoder must
+# give the same indices and samples as the exact one, also where the bound is
+# loose (tiny target scales), useless (all ties) or gated off (huge values)
+# ---------------------------------------------------------------------------
+def _importance_modes(cwq, cwqlib, tl, ts, pl, ps, off, ns, seed):
+    out = []
+    for mode in (0, 2):
+        cwqlib.cwq_set_pruning(mode)
+        try:
+            i, s = cwq.importance_encode_blocks(tl, ts, pl, ps, off, ns, seed)
+            torch.cuda.synchronize()
+            out.append((i.cpu().numpy(), s.cpu().numpy()))
+        finally:
+            cwqlib.cwq_set_pruning(2)
+    return out
+
+
+@pytest.mark.parametrize("kind", ["pln_like", "tiny_target", "wide_target", "ties",
+                                  "huge_values", "far_means", "long_rows"])
+def test_importance_screening_matches_exact(cwq, cwqlib, oracle, kind):
+    rng = np.random.default_rng(sum(map(ord, kind)))
+    sizes = [15, 3, 1, 7, 15, 4, 12, 2, 9, 15]
+    if kind == "long_rows":
+        sizes = [64, 200, 33, 256, 300]   # 300 > the screening LDS limit: exact fallback
+    off = np.concatenate([[0], np.cumsum(sizes)])
+    D = int(off[-1])
+    tl = (rng.standard_normal(D) * 0.7).astype(np.float32)
+    ts = rng.uniform(0.3, 0.95, D).astype(np.float32)
+    pl = np.zeros(D, np.float32)
+    ps = np.ones(D, np.float32)
+    if kind == "tiny_target":
+        ts = rng.uniform(1e-4, 1e-3, D).astype(np.float32)
+        tl = (rng.standard_normal(D) * 1e-3).astype(np.float32)
+    elif kind == "wide_target":     # sigma_q > sigma_p: the log ratio is convex in z
+        ts = rng.uniform(1.0, 3.0, D).astype(np.float32)
+    elif kind == "ties":            # target == proposal: every score is 0, index 0 wins
+        tl[:] = 0.0
+        ts[:] = 1.0
+    elif kind == "huge_values":
+        pl = (rng.standard_normal(D) * 1e20).astype(np.float32)
+        ps = rng.uniform(1e18, 1e19, D).astype(np.float32)
+        tl = pl.copy()
+        ts = (ps * 0.5).astype(np.float32)
+    elif kind == "far_means":
+        pl = (3.0e4 + rng.standard_normal(D)).astype(np.float32)
+        ps = rng.uniform(0.5, 2.0, D).astype(np.float32)
+        tl = (pl + 0.5 * ps * rng.standard_normal(D)).astype(np.float32)
+        ts = (ps * rng.uniform(0.3, 0.9, D)).astype(np.float32)
+    ns = np.array([min(int(x), 50_000) for x in
+                   rng.integers(1, 60_000, len(sizes))], dtype=np.int64)
+    ns[2] = 1
+    (i0, s0), (i2, s2) = _importance_modes(cwq, cwqlib, tl, ts, pl, ps, off, ns, 77)
+    assert np.array_equal(i0, i2), kind
+    _assert_bits_equal(s2, s0, f"importance screened vs exact ({kind})")
+    if kind in ("pln_like", "ties", "wide_target"):
+        wi, ws = oracle.importance_encode(tl, ts, pl, ps, off, ns, 77)
+        assert np.array_equal(i2, wi)
+        _assert_bits_equal(s2, ws, f"importance vs oracle ({kind})")

@@ -117,3 +117,24 @@ def test_oracle_importance_argmax_brute_force(oracle):
     assert idx[0] == int(np.argmax(sums))
     assert np.array_equal(sample, cand[idx[0]])
     assert np.array_equal(oracle.importance_decode_block(idx[0], pl, ps, seed), sample)
+
+
+def test_elias_many_matches_per_value(cwqlib):
+    """The native batch coder (cwq_elias_delta_encode/decode) equals the
+    per-value restatement of binary_io.py:7-39 and parses its own output."""
+    from compression_without_quantization_amd.binary_io import (
+        elias_delta_code, elias_delta_code_many, elias_delta_decode_many)
+    rng = np.random.default_rng(8)
+    xs = np.concatenate([np.arange(1, 5000), rng.integers(1, 2 ** 30, 5000),
+                         [2 ** k for k in range(30)], [2 ** k - 1 for k in range(1, 31)]])
+    want = ''.join(elias_delta_code(int(v)) for v in xs)
+    got = elias_delta_code_many(xs)
+    assert got == want
+    back, used = elias_delta_decode_many(got + "0101", xs.size)
+    assert used == len(got) and np.array_equal(back, xs)
+    # values past 2^30 take the per-value path
+    big = [2 ** 30, 2 ** 30 + 5, 7]
+    assert elias_delta_code_many(big) == ''.join(elias_delta_code(v) for v in big)
+    with pytest.raises(ValueError):
+        elias_delta_decode_many(got[:-3], xs.size)
+    assert elias_delta_code_many([]) == ''
