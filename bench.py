@@ -290,12 +290,14 @@ def main():
     cand_dims = nb * n_steps * (1 << bits) * d
     achieved = bytes_per_launch / (eval_ms * 1e-3) / 1e9
     traffic = None
+    valu = None
     tf = os.path.join(REPO, "profiles", f"traffic_{args.config}.json")
     if os.path.exists(tf):
         with open(tf) as f:
             tj = json.load(f)
         if tj.get("blocks") == nb:
             traffic = tj.get("hbm_bytes_per_launch")
+            valu = tj.get("valu")
     roofline = {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                 "kernel": (f"k_encode_prune<{d},true>" if args.prune_mode and d % 8 == 0
@@ -305,7 +307,11 @@ def main():
                 "compute_bound": {"unit": "candidate-dims/s",
                                   "achieved": cand_dims / (eval_ms * 1e-3),
                                   "note": "VALU-bound path (Philox + Box-Muller; pruned with "
-                                          "the screening pass, survivors exact); see DESIGN.md"}}
+                                          "the screening pass, survivors exact); see DESIGN.md",
+                                  "valu_issue_frac": (valu or {}).get("valu_issue_frac"),
+                                  "valu_source": "profiles/traffic_%s.json (rocprofv3 --pmc "
+                                                 "SQ_INSTS_VALU GRBM_GUI_ACTIVE)" % args.config
+                                                 if valu else None}}
 
     cpu = None
     parity = None

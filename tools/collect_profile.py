@@ -33,8 +33,15 @@ out = {"config": config, "blocks": blocks, "kernel": ksub, "FETCH_SIZE_kB": fetc
        "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes of "
                  "`python3 bench.py --steps 1 --warmup 0 --no-cpu --no-e2e` (one eval launch "
                  "each); bytes = (2*FETCH_SIZE + WRITE_SIZE) * 1024 per MI355X_MICROARCH.md",
-       "valu": {k: vals.get(k) for k in ("SQ_ACTIVE_INST_VALU", "SQ_WAVE_CYCLES",
-                                         "SQ_BUSY_CYCLES", "GRBM_GUI_ACTIVE")}}
+       "valu": {k: vals.get(k) for k in ("SQ_INSTS_VALU", "SQ_INSTS_SALU",
+                                         "SQ_ACTIVE_INST_VALU", "GRBM_GUI_ACTIVE")}}
+v = out["valu"]
+if v.get("SQ_INSTS_VALU") and v.get("GRBM_GUI_ACTIVE"):
+    # a wave64 VALU instruction occupies its SIMD32 for 2 cycles (MI355X_MICROARCH.md);
+    # GRBM_GUI_ACTIVE sums the 8 XCDs' busy cycles
+    cycles = v["GRBM_GUI_ACTIVE"] / 8.0
+    v["kernel_cycles"] = cycles
+    v["valu_issue_frac"] = 2.0 * v["SQ_INSTS_VALU"] / (1024.0 * cycles)
 with open(os.path.join(dst, f"traffic_{config}.json"), "w") as fh:
     json.dump(out, fh, indent=1)
 print(json.dumps(out, indent=1))
