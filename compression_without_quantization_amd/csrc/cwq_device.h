@@ -76,7 +76,7 @@ __device__ __forceinline__ float sqrt_cr_bm(float x) {
 
 __device__ __forceinline__ float bm_radius_dev(uint32_t x0, const double* logtab) {
   float u1 = uint32_to_float(x0);
-  u1 = u1 < 1.0e-7f ? 1.0e-7f : u1;
+  u1 = fmaxf(u1, 1.0e-7f);  // == (u1 < 1e-7f ? 1e-7f : u1): u1 is never NaN
   return sqrt_cr_bm(-2.0f * logf_core(u1, logtab));
 }
 
@@ -96,14 +96,18 @@ __device__ __forceinline__ void box_muller_dev(uint32_t x0, uint32_t x1, const d
 // Screening Box-Muller (approximate).  The hardware transcendentals
 // v_log_f32 / v_sqrt_f32 / v_sin_f32 / v_cos_f32 (sin and cos take the angle in
 // revolutions, so U = Uint32ToFloat(x1) needs no scaling or range reduction).
-// Used ONLY by the pruned encoder's screening pass, which turns the value into
-// rigorous bounds: the largest deviation from the exact pair over every
-// possible input (2^23 each) is a measured constant, kScreenEr / kScreenEs,
-// re-checked exhaustively on the GPU by tests/test_gpu.py.
-__device__ __forceinline__ float bm_radius_screen(uint32_t x0) {
-  float u1 = uint32_to_float(x0);
-  u1 = u1 < 1.0e-7f ? 1.0e-7f : u1;
-  return __builtin_amdgcn_sqrtf(-0x1.62e430p+0f * __builtin_amdgcn_logf(u1));  // -2 ln2 log2(u1)
+// Used ONLY by the screening passes, which turn the values into rigorous
+// bounds: the largest deviation from the exact pair over every possible input
+// (2^23 each) is a measured constant, kScreenEr / kScreenEs, re-checked
+// exhaustively on the GPU by tests/test_gpu.py.
+//
+// The radius is carried without its constant factor: q~ = sqrt(-log2 u1) =
+// r~ / sqrt(2 ln 2), and box_muller_screen returns z~ / sqrt(2 ln 2); callers
+// fold kSqrt2Ln2 into their per-dim constants (one multiply less per pair).
+constexpr double kSqrt2Ln2 = 1.1774100225154747;  // sqrt(2 ln 2)
+__device__ __forceinline__ float bm_qradius_screen(uint32_t x0) {
+  const float u1 = fmaxf(uint32_to_float(x0), 1.0e-7f);
+  return __builtin_amdgcn_sqrtf(-__builtin_amdgcn_logf(u1));
 }
 __device__ __forceinline__ void bm_sincos_screen(uint32_t x1, float& s, float& c) {
   const float U = uint32_to_float(x1);
@@ -111,20 +115,20 @@ __device__ __forceinline__ void bm_sincos_screen(uint32_t x1, float& s, float& c
   c = __builtin_amdgcn_cosf(U);
 }
 __device__ __forceinline__ void box_muller_screen(uint32_t x0, uint32_t x1, float& f0, float& f1) {
-  const float u2 = bm_radius_screen(x0);
+  const float q = bm_qradius_screen(x0);
   float s, c;
   bm_sincos_screen(x1, s, c);
-  f0 = s * u2;
-  f1 = c * u2;
+  f0 = s * q;
+  f1 = c * q;
 }
 
 // Error constants of the screening Box-Muller, shared by both screening passes.
 // measured maxima over all 2^23 inputs (tools/screen_err.py, re-checked by
-// tests/test_gpu.py): |r~ - r| <= 4.77e-7, |sin~ - sin|, |cos~ - cos| <= 2.99e-7
+// tests/test_gpu.py): |sqrt(2 ln 2) q~ - r| <= 5.82e-7, |sin~ - sin|, |cos~ - cos| <= 2.99e-7
 constexpr double kScreenEr = 1.0e-6;
 constexpr double kScreenEs = 6.0e-7;
 constexpr double kScreenRmax = 5.68;  // r <= sqrt(-2 ln 1e-7) = 5.6777
-// |RN(s~ r~) - RN(s r)| <= (1 + Es) Er + Rmax Es + 2^-23 (Rmax + Er)
+// |sqrt(2 ln 2) RN(s~ q~) - RN(s r)| <= (1 + Es) Er + Rmax Es + 2^-23 (Rmax + Er)
 constexpr double kScreenEz =
     (1.0 + kScreenEs) * kScreenEr + kScreenRmax * kScreenEs + 0x1p-23 * (kScreenRmax + kScreenEr);
 constexpr double kScreenZm = 5.7;     // bound on |z| and |z~|

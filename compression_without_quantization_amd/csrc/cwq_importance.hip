@@ -116,20 +116,23 @@ __device__ __forceinline__ bool imp_screen_dim(float tl, float ts, float pl, flo
   const double rho = (0.5 * (2.0 * Myt * eyt + eyt * eyt + u * Myt * Myt) + u * lt_mag +
                       0.5 * (2.0 * Myq * eyq + eyq * eyq + u * Myq * Myq) + u * lq_mag +
                       u * (lt_mag + lq_mag)) * r;
-  // the real quadratic and its float coefficients
+  // the real quadratic in z and its float coefficients in z' = z / sqrt(2 ln 2)
+  // (the screening Box-Muller's output): A' = 2 ln2 A, B' = sqrt(2 ln 2) B
   const double a = dps / dts, b = (dpl - dtl) / dts;
   const double A = 0.5 * (1.0 - a * a), B = -a * b, C = dcp - dct - 0.5 * b * b;
-  o.A = (float)A;
-  o.B = (float)B;
+  const double A1 = A * (kSqrt2Ln2 * kSqrt2Ln2), B1 = B * kSqrt2Ln2;
+  const double Zq = Zm / kSqrt2Ln2 * (1.0 + 4.0 * u);  // bound on |z'|
+  o.A = (float)A1;
+  o.B = (float)B1;
   o.C = (float)C;
-  const double dA = __builtin_fabs((double)o.A - A) + 0x1p-50 * (1.0 + a * a);
-  const double dB = __builtin_fabs((double)o.B - B) + 0x1p-50 * __builtin_fabs(a * b);
+  const double dA = __builtin_fabs((double)o.A - A1) + 0x1p-50 * (1.0 + a * a) * 1.4;
+  const double dB = __builtin_fabs((double)o.B - B1) + 0x1p-50 * __builtin_fabs(a * b) * 1.2;
   const double dC = __builtin_fabs((double)o.C - C) +
                     0x1p-50 * (__builtin_fabs(dcp) + __builtin_fabs(dct) + b * b);
   const double fA = __builtin_fabs((double)o.A), fB = __builtin_fabs((double)o.B);
   const double fC = __builtin_fabs((double)o.C);
-  const double h1 = fA * Zm + fB;  // |A z + B|
-  const double horner = dA * Zm * Zm + dB * Zm + dC + Zm * u * h1 * r + u * (h1 * Zm * r + fC);
+  const double h1 = fA * Zq + fB;  // |A' z' + B'|
+  const double horner = dA * Zq * Zq + dB * Zq + dC + Zq * u * h1 * r + u * (h1 * Zq * r + fC);
   // z~ vs z: |t(z) - t(z~)| <= max|t'| Ez + |A| Ez^2
   const double slope = 2.0 * __builtin_fabs(A) * Zm + __builtin_fabs(B);
   const double e = (rho + slope * Ez + __builtin_fabs(A) * Ez * Ez + horner) * (1.0 + 0x1p-20) +

@@ -308,7 +308,7 @@ __global__ void __launch_bounds__(256, CWQ_PRUNE_MIN_WAVES) k_encode_prune(
       const double offd = (STEP0 ? 0.0 : (double)fj[6]) + (double)fj[0] - (double)fj[2];
       const double sig = (double)sgj;
       const double kq = kScreenKappa / sig;
-      const float sa = (float)((double)fj[1] * kq);
+      const float sa = (float)((double)fj[1] * kq * kSqrt2Ln2);  // z~ arrives / sqrt(2 ln 2)
       const float sb = (float)(offd * kq);
       float* sc = reinterpret_cast<float*>(scst);
       sc[(k * NS + 0) * 4 + w] = sa;
@@ -715,7 +715,7 @@ __global__ void __launch_bounds__(256) k_selftest_screen(uint32_t m0, int64_t co
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < count;
        i += (int64_t)gridDim.x * blockDim.x) {
     const uint32_t m = m0 + (uint32_t)i;
-    rad[i] = bm_radius_screen(m);
+    rad[i] = bm_qradius_screen(m);  // r~ / sqrt(2 ln 2)
     float s, c;
     bm_sincos_screen(m, s, c);
     sn[i] = s;

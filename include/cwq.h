@@ -200,9 +200,10 @@ int64_t cwq_elias_delta_decode(const char* bits, int64_t nbits, int64_t count, i
 int cwq_selftest_bm_tables(uint32_t m0, int64_t count, float* radius, float* sin_out,
                            float* cos_out, void* stream);
 int cwq_selftest_logf(const float* x, int64_t n, float* out, void* stream);
-/* The pruned encoder's screening approximations of the same three tables
- * (hardware v_log/v_sqrt/v_sin/v_cos).  The tests bound their deviation from
- * the exact tables by the constants the screening bounds are built on. */
+/* The screening passes' approximations of the same three tables (hardware
+ * v_log/v_sqrt/v_sin/v_cos); radius[i] holds r~ / sqrt(2 ln 2), the form the
+ * kernels carry.  The tests bound their deviation from the exact tables by the
+ * constants the screening bounds are built on. */
 int cwq_selftest_screen_tables(uint32_t m0, int64_t count, float* radius, float* sin_out,
                                float* cos_out, void* stream);
 /* out[i] = the device's fast correctly-rounded quotient a[i] / b[i]

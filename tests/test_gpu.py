@@ -370,6 +370,7 @@ def test_screen_tables_within_bounds(cwq, cwqlib):
     torch.cuda.synchronize()
     a = [x.cpu().numpy().astype(np.float64) for x in t]
     assert np.isfinite(a[3]).all() and np.isfinite(a[4]).all() and np.isfinite(a[5]).all()
+    a[3] = a[3] * np.sqrt(2.0 * np.log(2.0))    # the table holds r~ / sqrt(2 ln 2)
     assert np.abs(a[3] - a[0]).max() <= k_er
     assert np.abs(a[4] - a[1]).max() <= k_es
     assert np.abs(a[5] - a[2]).max() <= k_es

@@ -14,6 +14,7 @@ assert lib.cwq_selftest_bm_tables(0, N, t[0].data_ptr(), t[1].data_ptr(), t[2].d
 assert lib.cwq_selftest_screen_tables(0, N, t[3].data_ptr(), t[4].data_ptr(), t[5].data_ptr(), st) == 0
 torch.cuda.synchronize()
 a = [x.cpu().numpy().astype(np.float64) for x in t]
+a[3] = a[3] * np.sqrt(2.0 * np.log(2.0))   # the screen table holds r~ / sqrt(2 ln 2)
 er = np.abs(a[3] - a[0]); es = np.abs(a[4] - a[1]); ec = np.abs(a[5] - a[2])
 print("Er max %.6g at m=%d (r=%.6g)" % (er.max(), er.argmax(), a[0][er.argmax()]))
 print("Es max %.6g at m=%d" % (es.max(), es.argmax()))
