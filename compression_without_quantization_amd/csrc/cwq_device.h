@@ -110,9 +110,11 @@ __device__ __forceinline__ float bm_qradius_screen(uint32_t x0) {
   return __builtin_amdgcn_sqrtf(-__builtin_amdgcn_logf(u1));
 }
 __device__ __forceinline__ void bm_sincos_screen(uint32_t x1, float& s, float& c) {
-  const float U = uint32_to_float(x1);
-  s = __builtin_amdgcn_sinf(U);
-  c = __builtin_amdgcn_cosf(U);
+  // 1 + U (exact, in [1, 2)): sin/cos in revolutions are 1-periodic, so the
+  // "- 1.0f" of Uint32ToFloat is not needed here (the error table covers it)
+  const float V = u2f((x1 & 0x7fffffu) | 0x3f800000u);
+  s = __builtin_amdgcn_sinf(V);
+  c = __builtin_amdgcn_cosf(V);
 }
 __device__ __forceinline__ void box_muller_screen(uint32_t x0, uint32_t x1, float& f0, float& f1) {
   const float q = bm_qradius_screen(x0);
