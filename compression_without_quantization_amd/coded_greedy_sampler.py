@@ -269,6 +269,10 @@ def group_size_threshold(max_group_size_bits):
 
 def group_starts(kl_divs, n_bits_per_group, max_group_size_bits=12):
     """coded_greedy_sampler.py:207-252 -> group_start_indices (a list, with D appended)."""
+    return _group_starts_array(kl_divs, n_bits_per_group, max_group_size_bits).tolist()
+
+
+def _group_starts_array(kl_divs, n_bits_per_group, max_group_size_bits=12):
     kl = np.ascontiguousarray(np.asarray(kl_divs, dtype=np.float32).reshape(-1))
     D = kl.size
     n_nats = n_bits_per_group * np.log(2) - 1
@@ -279,7 +283,7 @@ def group_starts(kl_divs, n_bits_per_group, max_group_size_bits=12):
                              group_size_threshold(max_group_size_bits), float(n_nats),
                              starts.ctypes.data, cap)
     _lib.check(n, "cwq_group_starts")
-    return [int(v) for v in starts[:n]]
+    return starts[:n]
 
 
 def _dist_parts(dist, dev, what):
@@ -325,7 +329,7 @@ def code_grouped_greedy_sample(sess, target, proposal, n_steps, n_bits_per_step,
               "coding {} dimensions".format(total_kl_bits, n_bits_per_group,
                                             total_kl_bits // n_bits_per_group + 1, D))
     # :207-252 grouping (sequential; host)
-    starts = group_starts(kl_divs, n_bits_per_group, max_group_size_bits)
+    starts = _group_starts_array(kl_divs, n_bits_per_group, max_group_size_bits)
     zeros = torch.zeros(D, dtype=torch.float32, device=dev)
     ones = torch.ones(D, dtype=torch.float32, device=dev)
     idx, sample = encode_blocks(t_loc, t_scale, zeros, ones, n_bits_per_step, n_steps, seed,
@@ -335,7 +339,7 @@ def code_grouped_greedy_sample(sess, target, proposal, n_steps, n_bits_per_step,
     out = torch.empty(D, dtype=torch.float32, device=dev)
     _lib.check(lib.cwq_destandardise(_ptr(sample), _ptr(p_loc), _ptr(p_scale), D, _ptr(out),
                                      stream), "cwq_destandardise")
-    return out.cpu().numpy(), bitcode, starts
+    return out.cpu().numpy(), bitcode, starts.tolist()
 
 
 def decode_grouped_greedy_sample(sess, bitcode, group_start_indices, proposal, n_bits_per_step,
@@ -348,7 +352,7 @@ def decode_grouped_greedy_sample(sess, bitcode, group_start_indices, proposal, n
     p_loc, p_scale = _dist_parts(proposal, dev, "Proposal")
     D = p_loc.numel()
     n_bits_per_group = n_bits_per_step * n_steps
-    starts = [int(s) for s in group_start_indices] + [D]  # :323 (without mutating)
+    starts = np.append(np.asarray(group_start_indices, dtype=np.int64).reshape(-1), D)  # :323
     n_listed = len(starts) - 1
     # :345-347 decode group i while its bit slice is non-empty
     n_avail = -(-len(bitcode) // n_bits_per_group) if n_bits_per_group else n_listed
