@@ -9,8 +9,6 @@ FLAGS="--offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -fno-fast-math -fP
 declare -A V=(
   [base]=""
   [w7]="-DCWQ_PRUNE_MIN_WAVES=7"
-  [g4]="-DCWQ_PRUNE_GRID=6144"
-  [gfull]="-DCWQ_PRUNE_GRID=1073741824"
   [stats]="-DCWQ_PRUNE_STATS"
 )
 if [ "$1" = build ]; then
