@@ -20,6 +20,7 @@ namespace cwq {
 
 constexpr int64_t kImpCandPerTile = 16384;
 constexpr int kImpScreenMaxD = 256;   // screening pass: per-dim constants live in LDS
+constexpr int64_t kImpPruneMinD = 5;  // rows of >= 5 dims take the pruned screening loop
 #ifndef CWQ_IMP_SURVIVOR_CAP
 #define CWQ_IMP_SURVIVOR_CAP 1024
 #endif
@@ -95,7 +96,7 @@ __device__ __forceinline__ float screen_row_imp(const PhiloxStream& st, uint64_t
 // A = (1 - a^2)/2, B = -a b, C = cp - ct - b^2/2.  Returns false if the dim
 // must not be screened.
 struct ImpScreenDim {
-  float A, B, C, err, mag;
+  float A, B, C, err, mag, umax;
 };
 __device__ __forceinline__ bool imp_screen_dim(float tl, float ts, float pl, float ps, float ct,
                                                float cp, ImpScreenDim& o) {
@@ -139,8 +140,18 @@ __device__ __forceinline__ bool imp_screen_dim(float tl, float ts, float pl, flo
                    0x1p-140;
   o.err = round_up_f32(e);
   o.mag = round_up_f32(lt_mag + lq_mag + e);  // bounds |t| and |t~|
+  // largest exact term over |z| <= Zm (pruning): the real quadratic's maximum
+  // on the interval (vertex or an end) plus the chain error
+  double qmax = A * Zm * Zm + __builtin_fabs(B) * Zm + C;
+  if (A < 0.0) {
+    double zv = -B / (2.0 * A);
+    zv = zv < -Zm ? -Zm : (zv > Zm ? Zm : zv);
+    qmax = A * zv * zv + B * zv + C;
+  }
+  qmax += 0x1p-40 * (__builtin_fabs(A) * Zm * Zm + __builtin_fabs(B) * Zm + __builtin_fabs(C));
+  o.umax = round_up_f32(qmax + e);
   return o.err - o.err == 0.0f && o.mag - o.mag == 0.0f && o.A - o.A == 0.0f &&
-         o.B - o.B == 0.0f && o.C - o.C == 0.0f;
+         o.B - o.B == 0.0f && o.C - o.C == 0.0f && o.umax - o.umax == 0.0f;
 }
 
 __global__ void __launch_bounds__(256) k_imp_eval(
@@ -154,6 +165,8 @@ __global__ void __launch_bounds__(256) k_imp_eval(
   __shared__ float4 coef[kImpScreenMaxD];   // A, B, C per dim (screening)
   __shared__ float derr[kImpScreenMaxD];    // per-dim error bound
   __shared__ float dmag[kImpScreenMaxD];    // per-dim magnitude bound
+  __shared__ float dumax[kImpScreenMaxD];   // per-dim largest exact term
+  __shared__ float dsuf[kImpScreenMaxD + 1];  // pruning: sum of dumax[j..d)
   __shared__ float etot_sh;
   __shared__ uint32_t tau_ord;
   __shared__ uint32_t sq_cnt;
@@ -188,7 +201,7 @@ __global__ void __launch_bounds__(256) k_imp_eval(
     const float* ps = p_scale + off;
     const float* ct = lnt + off;
     const float* cp = lnp + off;
-    auto exact_row = [&](int64_t n) -> float {
+    auto exact_row = [&](int64_t n) __attribute__((always_inline)) -> float {
       return eval_row_f<0>(st, (uint64_t)n * (uint64_t)d, d, (int)(((uint64_t)n * d) & 3u), logtab,
                            [&](int64_t e, float zz) -> float {
                              float x = ps[e] * zz;  // misc.py:14
@@ -207,6 +220,7 @@ __global__ void __launch_bounds__(256) k_imp_eval(
       coef[tid] = float4{o.A, o.B, o.C, 0.0f};
       derr[tid] = o.err;
       dmag[tid] = o.mag;
+      dumax[tid] = o.umax;
     }
     const bool screen = __syncthreads_and(ok) != 0;
     if (screen && tid == 0) {
@@ -219,6 +233,12 @@ __global__ void __launch_bounds__(256) k_imp_eval(
       const double gam = 1.01 * (double)d * 0x1p-24;
       const double et = (es + 2.0 * gam * ms) * (1.0 + 0x1p-20) + 0x1p-126;
       etot_sh = et < 1.0e3 ? round_up_f32(et) : __builtin_inff();
+      double suf = 0.0;
+      dsuf[d] = 0.0f;
+      for (int64_t j = d - 1; j >= 0; --j) {
+        suf += (double)dumax[j];
+        dsuf[j] = round_up_f32(suf * (1.0 + 0x1p-20) + 0x1p-126);  // covers the test's adds
+      }
       tau_ord = ord_f32(-__builtin_inff());
       sq_cnt = 0u;
     }
@@ -228,20 +248,79 @@ __global__ void __launch_bounds__(256) k_imp_eval(
     uint64_t bestk = 0;
     if (screen && E - E == 0.0f) {
       float tau = -__builtin_inff();
-      for (int64_t n = n0 + 4 * (int64_t)lane + wv; n < n1; n += 256) {
-        const float sh = screen_row_imp(st, (uint64_t)n * (uint64_t)d, d, align, coef);
-        const float slack = E + __builtin_fabsf(sh) * 0x1p-22f;
+      // may be the best: list it
+      auto keep = [&](int64_t n, float sh, float slack) __attribute__((always_inline)) {
         const float up = sh + slack;
-        if (up >= tau) {  // may be the best: keep it
-          tau = fmaxf(tau, sh - slack);
-          const uint32_t slot = atomicAdd(&sq_cnt, 1u);
-          if (slot < CWQ_IMP_SURVIVOR_CAP) {
-            sq_n[slot] = (uint32_t)(n - n0);
-            sq_up[slot] = up;
-          } else {  // list full: evaluate exactly now
-            const uint64_t k = argmax_key(exact_row(n), (uint32_t)n);
-            bestk = k > bestk ? k : bestk;
+        tau = fmaxf(tau, sh - slack);
+        const uint32_t slot = atomicAdd(&sq_cnt, 1u);
+        if (slot < CWQ_IMP_SURVIVOR_CAP) {
+          sq_n[slot] = (uint32_t)(n - n0);
+          sq_up[slot] = up;
+        } else {  // list full: evaluate exactly now
+          const uint64_t k = argmax_key(exact_row(n), (uint32_t)n);
+          bestk = k > bestk ? k : bestk;
+        }
+      };
+      if (d >= kImpPruneMinD) {
+        // pruned screening: one Philox block of the lane's row per iteration;
+        // a row stops once s + E + sum of the unvisited dims' maxima < tau.
+        // Lanes refill from the wave's contiguous candidate range.
+        const int64_t per_wave = (n1 - n0 + 3) / 4;
+        const int64_t w0 = n0 + (int64_t)wv * per_wave;
+        const int64_t w1 = (w0 + per_wave < n1) ? w0 + per_wave : n1;
+        int64_t wnext = w0 + 64;
+        int64_t n = w0 + lane;
+        bool active = n < w1;
+        int j = 0;
+        float s = 0.0f;
+        uint32_t iter = 0;
+        while (__ballot(active) != 0ull) {
+          const uint64_t k = (uint64_t)n * (uint64_t)d + (uint64_t)j;
+          const F4 z = normal4_screen(st, k >> 2);
+          const int wa = (int)(k & 3u);
+          const int cnt = (4 - wa) < (int)(d - j) ? (4 - wa) : (int)(d - j);
+#pragma unroll
+          for (int t = 0; t < 4; ++t) {
+            if (t < cnt) {
+              const int w = wa + t;
+              const float zz = w == 0 ? z.a : (w == 1 ? z.b : (w == 2 ? z.c : z.d));
+              const float4 c = coef[j + t];
+              s = s + __builtin_fmaf(__builtin_fmaf(c.x, zz, c.y), zz, c.z);
+            }
           }
+          j += cnt;
+          const bool complete = (j == (int)d);
+          const float slack = E + __builtin_fabsf(s) * 0x1p-22f;
+          const float upper = (s + slack) + dsuf[j];
+          const bool prune = !complete && (upper < tau);
+          if (complete && active && upper >= tau) keep(n, s, slack);
+          const bool done = complete || prune || !active;
+          const uint64_t m = __ballot(done);
+          const uint32_t rank = __builtin_amdgcn_mbcnt_hi(
+              (uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+          if (done) {
+            n = wnext + rank;
+            j = 0;
+            s = 0.0f;
+          }
+          wnext += (int64_t)__builtin_popcountll(m);
+          active = n < w1;
+          if (((++iter) & 15u) == 0u) {  // share tau with the workgroup and the group
+            const float tm = wave_max_f32(tau);
+            if (lane == 0) {
+              atomicMax(&tau_ord, ord_f32(tm));
+              atomicMax(&gtau[g], ord_f32(tm));
+            }
+            const uint32_t o1 = __atomic_load_n(&tau_ord, __ATOMIC_RELAXED);
+            const uint32_t o2 = __atomic_load_n(&gtau[g], __ATOMIC_RELAXED);
+            tau = fmaxf(tau, unord_f32(o1 > o2 ? o1 : o2));
+          }
+        }
+      } else {
+        for (int64_t n = n0 + 4 * (int64_t)lane + wv; n < n1; n += 256) {
+          const float sh = screen_row_imp(st, (uint64_t)n * (uint64_t)d, d, align, coef);
+          const float slack = E + __builtin_fabsf(sh) * 0x1p-22f;
+          if (sh + slack >= tau) keep(n, sh, slack);
         }
       }
       {
