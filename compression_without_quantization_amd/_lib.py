@@ -39,6 +39,10 @@ SIGNATURES = {
     "cwq_kl_normal_normal": (c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp]),
     "cwq_destandardise": (c_int, [c_vp, c_vp, c_vp, c_i64, c_vp, c_vp]),
     "cwq_group_starts": (c_i64, [c_vp, c_i64, c_i64, c_f64, c_vp, c_i64]),
+    "cwq_code_grouped_greedy_workspace_size": (c_size, [c_i64, c_int]),
+    "cwq_code_grouped_greedy": (c_i64, [c_vp, c_vp, c_vp, c_vp, c_i64, c_int, c_int, c_i32, c_f32,
+                                        c_i64, c_f64, c_vp, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp,
+                                        c_size, c_vp]),
     "cwq_importance_workspace_size": (c_size, [c_i64, c_i64]),
     "cwq_importance_encode": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i32,
                                       c_i64, c_vp, c_vp, c_vp, c_size, c_vp]),

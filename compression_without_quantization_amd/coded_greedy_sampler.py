@@ -24,6 +24,8 @@ Differences from the TF1 reference (deliberate, documented in DESIGN.md):
 
 All arithmetic runs in libcwq.so; nothing here computes samples on the CPU.
 """
+import ctypes
+
 import numpy as np
 import torch
 
@@ -309,37 +311,36 @@ def code_grouped_greedy_sample(sess, target, proposal, n_steps, n_bits_per_step,
     q_loc, q_scale = _dist_parts(target, dev, "Target")
     p_loc, p_scale = _dist_parts(proposal, dev, "Proposal")
     D = p_loc.numel()
+    n_steps, n_bits_per_step = int(n_steps), int(n_bits_per_step)
     n_bits_per_group = n_bits_per_step * n_steps
     stream = torch.cuda.current_stream(dev).cuda_stream
-    # :193-199 standardise the target by the proposal; proposal -> N(0, 1)
-    t_loc = torch.empty(D, dtype=torch.float32, device=dev)
-    t_scale = torch.empty(D, dtype=torch.float32, device=dev)
-    _lib.check(lib.cwq_standardise(_ptr(q_loc), _ptr(q_scale), _ptr(p_loc), _ptr(p_scale), D,
-                                   _ptr(t_loc), _ptr(t_scale), stream), "cwq_standardise")
-    # :201, :210 per-dim KL(target || proposal)
-    kl = torch.empty(D, dtype=torch.float32, device=dev)
-    _lib.check(lib.cwq_kl_normal_normal(_ptr(q_loc), _ptr(q_scale), _ptr(p_loc), _ptr(p_scale),
-                                        D, _ptr(kl), stream), "cwq_kl_normal_normal")
-    kl_divs = kl.cpu().numpy()
+    # one native call: standardise + KL (:193-210), host grouping (:207-252),
+    # one coder per group with seed + g (:273-284), destandardise (:292) and
+    # the LSB-first bitcode (:81-87, :288)
+    need = int(lib.cwq_code_grouped_greedy_workspace_size(D, n_steps))
+    ws = torch.empty(max(need, 1), dtype=torch.uint8, device=dev)
+    sample_h = np.empty(D, dtype=np.float32)
+    bits_h = np.empty(max(D * n_bits_per_group, 1), dtype=np.uint8)
+    starts_h = np.empty(D + 2, dtype=np.int64)
+    kl_sum = ctypes.c_double(0.0)
+    n_nats = n_bits_per_group * np.log(2) - 1
+    seed32 = int(np.int32(np.uint32(int(seed) & 0xFFFFFFFF)))
+    G = _lib.check(lib.cwq_code_grouped_greedy(
+        _ptr(q_loc), _ptr(q_scale), _ptr(p_loc), _ptr(p_scale), D, n_steps, n_bits_per_step,
+        seed32, float(rho), group_size_threshold(max_group_size_bits), float(n_nats),
+        sample_h.ctypes.data, bits_h.ctypes.data, bits_h.size, starts_h.ctypes.data,
+        starts_h.size, ctypes.byref(kl_sum) if VERBOSE else None, ws.data_ptr(), ws.numel(),
+        stream),
+        "cwq_code_grouped_greedy")
     if VERBOSE:
-        total_kl_bits = np.sum(kl_divs) / np.log(2)
+        total_kl_bits = kl_sum.value / np.log(2)
         print("Total KL to split up: {:.2f} bits, "
               "maximum bits per group: {}, "
               "estimated number of groups: {},"
               "coding {} dimensions".format(total_kl_bits, n_bits_per_group,
                                             total_kl_bits // n_bits_per_group + 1, D))
-    # :207-252 grouping (sequential; host)
-    starts = _group_starts_array(kl_divs, n_bits_per_group, max_group_size_bits)
-    zeros = torch.zeros(D, dtype=torch.float32, device=dev)
-    ones = torch.ones(D, dtype=torch.float32, device=dev)
-    idx, sample = encode_blocks(t_loc, t_scale, zeros, ones, n_bits_per_step, n_steps, seed,
-                                rho=rho, block_off=starts)
-    bitcode = indices_to_bitcode(idx.cpu().numpy(), int(n_bits_per_step))
-    # :292 rescale the sample
-    out = torch.empty(D, dtype=torch.float32, device=dev)
-    _lib.check(lib.cwq_destandardise(_ptr(sample), _ptr(p_loc), _ptr(p_scale), D, _ptr(out),
-                                     stream), "cwq_destandardise")
-    return out.cpu().numpy(), bitcode, starts.tolist()
+    bitcode = bits_h[:G * n_bits_per_group].tobytes().decode('ascii')
+    return sample_h, bitcode, starts_h[:G + 1].tolist()
 
 
 def decode_grouped_greedy_sample(sess, bitcode, group_start_indices, proposal, n_bits_per_step,

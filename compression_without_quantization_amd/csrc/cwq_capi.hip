@@ -9,6 +9,10 @@
 #include <stdio.h>
 #include <math.h>
 #include <string.h>
+#include <time.h>
+#include <immintrin.h>
+
+#include <vector>
 
 #include "../../include/cwq.h"
 #include "cwq_kernels.h"
@@ -92,24 +96,61 @@ int64_t group_starts_impl(const float* kl, int64_t D, int64_t size_threshold, do
                           int64_t* starts, int64_t cap, bool strict) {
   if (D < 0 || (D > 0 && !kl) || !starts || cap < 2)
     return fail(CWQ_ERR_INVALID, "group starts: bad arguments");
-  int64_t ns = 0;
-  starts[ns++] = 0;
-  int64_t cur_size = 0;
-  float cur_kl = 0.0f;  // numpy float32 scalar accumulator
-  for (int64_t i = 0; i < D; ++i) {
-    const float s = cur_kl + kl[i];  // float32 + float32
-    const bool over = strict ? ((double)s > n_nats) : ((double)s >= n_nats);
-    if (cur_size >= size_threshold || over || i == D - 1) {
-      if (ns >= cap) return fail(CWQ_ERR_INVALID, "group starts: cap too small");
-      starts[ns++] = i;
-      cur_size = 1;
-      cur_kl = kl[i];
-    } else {
-      cur_kl = s;
-      cur_size += 1;
+  if (cap < D + 2 || size_threshold > (1 << 24)) {
+    // exact but slower: the branch-free scan below writes one slot per dim and
+    // carries the group size in float32
+    int64_t ns = 0;
+    starts[ns++] = 0;
+    int64_t cur_size = 0;
+    float cur_kl = 0.0f;
+    for (int64_t i = 0; i < D; ++i) {
+      const float s = cur_kl + kl[i];
+      const bool over = strict ? ((double)s > n_nats) : ((double)s >= n_nats);
+      if (cur_size >= size_threshold || over || i == D - 1) {
+        if (ns >= cap) return fail(CWQ_ERR_INVALID, "group starts: cap too small");
+        starts[ns++] = i;
+        cur_size = 1;
+        cur_kl = kl[i];
+      } else {
+        cur_kl = s;
+        cur_size += 1;
+      }
     }
+    if (ns >= cap) return fail(CWQ_ERR_INVALID, "group starts: cap too small");
+    starts[ns++] = D;
+    ok();
+    return ns;
   }
-  if (ns >= cap) return fail(CWQ_ERR_INVALID, "group starts: cap too small");
+  // The reference compares the float32 running sum in float64 (`>=`, or `>`
+  // when strict).  For a float s that equals s >= thr with thr the smallest
+  // float satisfying the comparison, so the scan stays in float32, and it is
+  // branch-free (group boundaries are data-dependent: a branch mispredicts).
+  auto cond = [&](float f) { return strict ? ((double)f > n_nats) : ((double)f >= n_nats); };
+  float thr = (float)n_nats;
+  while (!cond(thr) && thr < __builtin_inff()) thr = nextafterf(thr, __builtin_inff());
+  while (cond(nextafterf(thr, -__builtin_inff())) && thr > -__builtin_inff())
+    thr = nextafterf(thr, -__builtin_inff());
+  int64_t ns = 1;
+  starts[0] = 0;
+  // Loop-carried state in SSE registers: running float32 sum, group size (as
+  // float: exact below 2^24, size_threshold <= 2^24 here), and the reset
+  // mask; the selects are and/andnot/or, so nothing branches on data.
+  const __m128 vthr = _mm_set_ss(thr);
+  const __m128 vthr_size = _mm_set_ss((float)size_threshold);
+  const __m128 one = _mm_set_ss(1.0f);
+  __m128 cur = _mm_setzero_ps();
+  __m128 size = _mm_setzero_ps();
+  const int64_t last = D - 1;
+  for (int64_t i = 0; i < last; ++i) {
+    const __m128 k = _mm_load_ss(kl + i);
+    const __m128 sum = _mm_add_ss(cur, k);  // float32 + float32
+    const __m128 m = _mm_or_ps(_mm_cmpge_ss(size, vthr_size), _mm_cmpge_ss(sum, vthr));
+    starts[ns] = i;
+    ns += _mm_movemask_ps(m) & 1;
+    cur = _mm_or_ps(_mm_and_ps(m, k), _mm_andnot_ps(m, sum));
+    size = _mm_or_ps(_mm_and_ps(m, one), _mm_andnot_ps(m, _mm_add_ss(size, one)));
+  }
+  if (D > 0) starts[ns++] = last;  // idx == D - 1 always starts a group (:232)
   starts[ns++] = D;
   ok();
   return ns;
@@ -285,6 +326,178 @@ int cwq_destandardise(const float* sample, const float* p_loc, const float* p_sc
       cwq::launch_destandardise(sample, p_loc, p_scale, n, out, (hipStream_t)stream);
   if (e != hipSuccess) return hip_fail(e, "cwq_destandardise");
   return ok();
+}
+
+// ---------------------------------------------------------------------------
+// The whole grouped greedy coder of one latent tensor in one call
+// (coded_greedy_sampler.py:170-296): device standardise + KL, host grouping,
+// device encode + destandardise, host bitcode.  Two host<->device round trips
+// per call instead of one per Python step.
+// ---------------------------------------------------------------------------
+namespace {
+struct GroupedWs {
+  size_t t_loc, t_scale, kl, zeros, ones, sample, out, offs, idx, enc, total;
+};
+GroupedWs grouped_ws(int64_t D, int n_steps) {
+  GroupedWs l;
+  size_t o = 0;
+  auto take = [&](size_t bytes) {
+    const size_t at = o;
+    o = align_up(o + bytes, 256);
+    return at;
+  };
+  const size_t fd = (size_t)(D > 0 ? D : 0) * 4;
+  l.t_loc = take(fd);
+  l.t_scale = take(fd);
+  l.kl = take(fd);
+  l.zeros = take(fd);
+  l.ones = take(fd);
+  l.sample = take(fd);
+  l.out = take(fd);
+  l.offs = take((size_t)(D + 2) * 8);
+  l.idx = take((size_t)(D > 0 ? D : 1) * (size_t)(n_steps > 0 ? n_steps : 1) * 4);
+  l.enc = take(ws_layout(D, D).total);
+  l.total = o;
+  return l;
+}
+thread_local std::vector<float> g_kl_host;
+thread_local std::vector<int32_t> g_idx_host;
+}  // namespace
+
+size_t cwq_code_grouped_greedy_workspace_size(int64_t D, int n_steps) {
+  if (D < 0 || n_steps < 0) return 0;
+  return grouped_ws(D, n_steps).total;
+}
+
+int64_t cwq_code_grouped_greedy(const float* q_loc, const float* q_scale, const float* p_loc,
+                                const float* p_scale, int64_t D, int n_steps,
+                                int n_bits_per_step, int32_t seed, float rho,
+                                int64_t size_threshold, double n_nats, float* sample_host,
+                                char* bits_host, int64_t bits_cap, int64_t* starts_host,
+                                int64_t starts_cap, double* kl_sum_out, void* workspace,
+                                size_t workspace_bytes, void* stream) {
+  if (D < 0 || n_steps < 1 || n_bits_per_step < 0 || n_bits_per_step > CWQ_MAX_BITS_PER_STEP)
+    return fail(CWQ_ERR_INVALID, "cwq_code_grouped_greedy: bad sizes");
+  if (D > 0 && (!q_loc || !q_scale || !p_loc || !p_scale || !sample_host))
+    return fail(CWQ_ERR_INVALID, "cwq_code_grouped_greedy: null pointer");
+  if (!starts_host || starts_cap < D + 2)
+    return fail(CWQ_ERR_CAPACITY, "cwq_code_grouped_greedy: starts_cap must be >= D + 2");
+  const GroupedWs l = grouped_ws(D, n_steps);
+  if (workspace_bytes < l.total || !workspace)
+    return fail(CWQ_ERR_WORKSPACE, "workspace %zu bytes < required %zu", workspace_bytes,
+                l.total);
+  hipStream_t s = (hipStream_t)stream;
+#ifdef CWQ_PHASE_TIMES  // tuning builds: per-phase host wall times to stderr
+  struct timespec ts0, ts1;
+  clock_gettime(CLOCK_MONOTONIC, &ts0);
+  auto lap = [&](const char* what) {
+    clock_gettime(CLOCK_MONOTONIC, &ts1);
+    fprintf(stderr, "[cwq] %-10s %8.1f us\n", what,
+            (ts1.tv_sec - ts0.tv_sec) * 1e6 + (ts1.tv_nsec - ts0.tv_nsec) * 1e-3);
+    ts0 = ts1;
+  };
+#else
+  auto lap = [](const char*) {};
+#endif
+  char* w = (char*)workspace;
+  float* t_loc = (float*)(w + l.t_loc);
+  float* t_scale = (float*)(w + l.t_scale);
+  float* kl = (float*)(w + l.kl);
+  float* zeros = (float*)(w + l.zeros);
+  float* ones = (float*)(w + l.ones);
+  float* sample = (float*)(w + l.sample);
+  float* out = (float*)(w + l.out);
+  int64_t* offs = (int64_t*)(w + l.offs);
+  int32_t* idx = (int32_t*)(w + l.idx);
+  hipError_t e = hipSuccess;
+  int rc;
+  if (D > 0) {
+    // :193-199 standardise; :201, :210 per-dim KL(target || proposal)
+    if ((rc = cwq_standardise(q_loc, q_scale, p_loc, p_scale, D, t_loc, t_scale, stream)) < 0)
+      return rc;
+    if ((rc = cwq_kl_normal_normal(q_loc, q_scale, p_loc, p_scale, D, kl, stream)) < 0) return rc;
+    if ((e = hipMemsetAsync(zeros, 0, (size_t)D * 4, s)) != hipSuccess) return hip_fail(e, "memset");
+    if ((e = hipMemsetD32Async((hipDeviceptr_t)ones, 0x3f800000u, (size_t)D, s)) != hipSuccess)
+      return hip_fail(e, "memset");
+    g_kl_host.resize((size_t)D);
+    if ((e = hipMemcpyAsync(g_kl_host.data(), kl, (size_t)D * 4, hipMemcpyDeviceToHost, s)) !=
+        hipSuccess)
+      return hip_fail(e, "KL to host");
+    if ((e = hipStreamSynchronize(s)) != hipSuccess) return hip_fail(e, "sync");
+  }
+  lap("kl");
+  if (kl_sum_out) {  // log line only: four independent accumulators
+    double t[4] = {0.0, 0.0, 0.0, 0.0};
+    int64_t i = 0;
+    for (; i + 4 <= D; i += 4)
+      for (int q = 0; q < 4; ++q) t[q] += (double)g_kl_host[(size_t)(i + q)];
+    for (; i < D; ++i) t[0] += (double)g_kl_host[(size_t)i];
+    *kl_sum_out = (t[0] + t[2]) + (t[1] + t[3]);
+  }
+  // :207-252 the sequential partition (host, exact reference semantics)
+  const int64_t n = group_starts_impl(D > 0 ? g_kl_host.data() : nullptr, D, size_threshold, n_nats,
+                                      starts_host, starts_cap, false);
+  if (n < 0) return n;
+  const int64_t G = n - 1;
+  lap("group");
+  const int64_t nbits = G * (int64_t)n_steps * n_bits_per_step;
+  if (bits_cap < nbits || (nbits > 0 && !bits_host))
+    return fail(CWQ_ERR_CAPACITY, "cwq_code_grouped_greedy: bits_cap %lld < %lld",
+                (long long)bits_cap, (long long)nbits);
+  if (G <= 0) {
+    cwq::set_error(CWQ_OK, "");
+    return G < 0 ? 0 : G;
+  }
+  int64_t maxd = 0;
+  for (int64_t g = 0; g < G; ++g) {
+    const int64_t dg = starts_host[g + 1] - starts_host[g];
+    maxd = dg > maxd ? dg : maxd;
+  }
+  if ((e = hipMemcpyAsync(offs, starts_host, (size_t)(G + 1) * 8, hipMemcpyHostToDevice, s)) !=
+      hipSuccess)
+    return hip_fail(e, "offsets to device");
+  // :273-284 one greedy coder per group, seed + g
+  if ((rc = cwq_greedy_encode(t_loc, t_scale, zeros, ones, offs, G, D, maxd, n_bits_per_step,
+                              n_steps, seed, rho, 0, idx, sample, w + l.enc,
+                              workspace_bytes - l.enc, stream)) < 0)
+    return rc;
+  // :292 destandardise
+  if ((rc = cwq_destandardise(sample, p_loc, p_scale, D, out, stream)) < 0) return rc;
+  g_idx_host.resize((size_t)(G * n_steps));
+  if ((e = hipMemcpyAsync(g_idx_host.data(), idx, (size_t)(G * n_steps) * 4,
+                          hipMemcpyDeviceToHost, s)) != hipSuccess)
+    return hip_fail(e, "indices to host");
+  if ((e = hipMemcpyAsync(sample_host, out, (size_t)D * 4, hipMemcpyDeviceToHost, s)) !=
+      hipSuccess)
+    return hip_fail(e, "sample to host");
+  if ((e = hipStreamSynchronize(s)) != hipSuccess) return hip_fail(e, "sync");
+  lap("encode");
+  // :81-87, :288 each index as n_bits_per_step LSB-first chars, steps then groups
+  static const struct ByteChars {  // byte value -> its 8 LSB-first '0'/'1' chars
+    uint64_t c[256];
+    ByteChars() {
+      for (int v = 0; v < 256; ++v) {
+        uint64_t w = 0;
+        for (int b = 0; b < 8; ++b) w |= (uint64_t)('0' + ((v >> b) & 1)) << (8 * b);
+        c[v] = w;
+      }
+    }
+  } kByteChars;
+  char* o = bits_host;
+  for (int64_t i = 0; i < G * n_steps; ++i) {
+    const uint32_t v = (uint32_t)g_idx_host[(size_t)i];
+    if (n_bits_per_step < 31 && (v >> n_bits_per_step) != 0)
+      return fail(CWQ_ERR_INVALID, "index %u does not fit %d bits", v, n_bits_per_step);
+    int b = 0;
+    for (; b + 8 <= n_bits_per_step; b += 8) {
+      memcpy(o, &kByteChars.c[(v >> b) & 0xffu], 8);
+      o += 8;
+    }
+    for (; b < n_bits_per_step; ++b) *o++ = (char)('0' + ((v >> b) & 1u));
+  }
+  lap("bits");
+  cwq::set_error(CWQ_OK, "");
+  return G;
 }
 
 int64_t cwq_group_starts(const float* kl, int64_t D, int64_t size_threshold, double n_nats,

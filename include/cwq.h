@@ -22,6 +22,8 @@
  *   cwq_destandardise            <- code/coded_greedy_sampler.py:292 / :362
  *   cwq_group_starts             <- code/coded_greedy_sampler.py:207-252
  *                                   (host-side sequential partition)
+ *   cwq_code_grouped_greedy      <- code/coded_greedy_sampler.py:170-296
+ *                                   (the whole grouped coder in one call)
  *
  * Conventions
  *   - All float/index pointers are DEVICE pointers (hipMalloc / torch cuda
@@ -132,6 +134,26 @@ int cwq_destandardise(const float* sample, const float* p_loc, const float* p_sc
  * cap is too small. */
 int64_t cwq_group_starts(const float* kl, int64_t D, int64_t size_threshold, double n_nats,
                          int64_t* starts, int64_t cap);
+
+/* code_grouped_greedy_sample (coded_greedy_sampler.py:170-296) in one call:
+ * device standardisation and KL (:193-210), the host partition (:207-252, as
+ * cwq_group_starts with size_threshold / n_nats), one greedy coder per group
+ * with seed + g (:273-284), destandardisation (:292) and the LSB-first
+ * bitcode (:81-87, :288).  q_* / p_*: DEVICE float32 [D] (target, proposal).
+ * Outputs are HOST memory: sample_host [D] float32, bits_host ('0'/'1' chars,
+ * groups x n_steps x n_bits_per_step of them), starts_host (the reference's
+ * group_start_indices incl. the trailing D; starts_cap >= D + 2) and, if
+ * non-NULL, kl_sum_out (sum of the per-dim KL in nats, for the reference's
+ * log line).  Returns the number of groups, or a negative error code.
+ * Synchronises the stream twice (after the KL, at the end). */
+size_t cwq_code_grouped_greedy_workspace_size(int64_t D, int n_steps);
+int64_t cwq_code_grouped_greedy(const float* q_loc, const float* q_scale, const float* p_loc,
+                                const float* p_scale, int64_t D, int n_steps,
+                                int n_bits_per_step, int32_t seed, float rho,
+                                int64_t size_threshold, double n_nats, float* sample_host,
+                                char* bits_host, int64_t bits_cap, int64_t* starts_host,
+                                int64_t starts_cap, double* kl_sum_out, void* workspace,
+                                size_t workspace_bytes, void* stream);
 
 /* ---- Importance sampler (code/coded_importance_sampler.py) ------------- */
 /* Workspace bytes for cwq_importance_encode. */

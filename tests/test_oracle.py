@@ -236,3 +236,43 @@ def test_kl_and_standardise_float32(oracle):
     tl, ts = oracle.standardise(ql, qs, pl, ps)
     assert np.array_equal(tl, ((ql - pl) / ps).astype(np.float32))
     assert np.array_equal(ts, (qs / ps).astype(np.float32))
+
+
+@pytest.mark.parametrize("strict", [False, True])
+def test_grouping_exact_threshold_ties(cwqlib, strict):
+    """Running sums landing exactly on the float32 neighbours of n_nats: the
+    native scan's float32 threshold must agree with the reference's float64
+    comparison (>= for the greedy coder, > for the importance coder)."""
+    from compression_without_quantization_amd.coded_greedy_sampler import (
+        group_size_threshold, group_starts)
+    from compression_without_quantization_amd.coded_importance_sampler import (
+        importance_group_size_threshold, importance_group_starts)
+    bits = 8 if not strict else 20
+    n_nats = bits * np.log(2) - 1
+    up = np.float32(n_nats)
+    while float(up) < n_nats:
+        up = np.nextafter(up, np.float32(np.inf))
+    cands = [up, np.nextafter(up, np.float32(0)), np.nextafter(up, np.float32(np.inf))]
+    if float(up) == n_nats:
+        cands.append(up)
+    kl = []
+    for c in cands * 5:
+        kl += [np.float32(c - np.float32(2.0)), np.float32(2.0), np.float32(0.25)]
+    kl = np.asarray(kl, np.float32)
+    if not strict:
+        want = _group_starts_py(kl, bits, 12)
+        assert group_starts(kl, bits, 12) == want
+    else:
+        # transcription of coded_importance_sampler.py:178-203 (strict >)
+        thr = importance_group_size_threshold(4)
+        starts, cur_size, cur_kl = [0], 0, np.float32(0)
+        for i in range(kl.size):
+            s = np.float32(cur_kl + kl[i])
+            if cur_size >= thr or float(s) > n_nats or i == kl.size - 1:
+                starts.append(i)
+                cur_size, cur_kl = 1, kl[i]
+            else:
+                cur_kl, cur_size = s, cur_size + 1
+        starts.append(kl.size)
+        got = importance_group_starts(kl, bits, 4)
+        assert list(got) == starts

@@ -1,6 +1,7 @@
 """Units-per-candidate histogram of the pruned encoder (run on the GPU box
 with a -DCWQ_PRUNE_STATS build selected through CWQ_LIB_PATH).
-Usage: CWQ_LIB_PATH=tools/variants/libcwq_stats.so python tools/prune_stats.py [nb] [mode]"""
+Usage: CWQ_LIB_PATH=tools/variants/libcwq_stats.so python tools/prune_stats.py [nb] [mode]
+(PS_D / PS_BITS select the block shape; default the C4 shape d=32, 16 bits)"""
 import ctypes, os, sys
 import numpy as np
 import torch
@@ -11,7 +12,8 @@ from compression_without_quantization_amd.synthetic import make_blocks
 
 nb = int(sys.argv[1]) if len(sys.argv) > 1 else 20000
 mode = int(sys.argv[2]) if len(sys.argv) > 2 else 2
-d, bits = 32, 16
+d = int(os.environ.get("PS_D", "32"))
+bits = int(os.environ.get("PS_BITS", "16"))
 lib = _lib.load()
 lib.cwq_set_pruning(mode)
 h = make_blocks(nb, d, bits, seed=20261015)

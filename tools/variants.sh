@@ -10,6 +10,7 @@ declare -A V=(
   [base]=""
   [w7]="-DCWQ_PRUNE_MIN_WAVES=7"
   [stats]="-DCWQ_PRUNE_STATS"
+  [phases]="-DCWQ_PHASE_TIMES"
 )
 if [ "$1" = build ]; then
   mkdir -p $OUT
@@ -21,6 +22,7 @@ if [ "$1" = build ]; then
 else
   for k in $(echo "${!V[@]}" | tr ' ' '\n' | sort); do
     [ "$k" = stats ] && continue  # counters only: tools/prune_stats.py
+    [ "$k" = phases ] && continue  # host phase timings only
     echo "== $k ${V[$k]}"
     CWQ_LIB_PATH=$PWD/$OUT/libcwq_$k.so timeout -k 10 300 python -u bench.py --no-cpu --no-e2e --steps 2 --warmup 1 $BENCH_ARGS | python -c "import json,sys; d=json.loads(sys.stdin.read()); print(d['value'], d['roofline']['kernel_ms'])"
   done
