@@ -90,6 +90,29 @@ float eigen_sum(const float* x, int64_t d) {
   return t + ((q0 + q2) + (q1 + q3));
 }
 
+// Branch-free float32 grouping scan over kl[i0, i1) (see group_starts_impl),
+// appending group starts to starts[ns...].
+void scan_sse(const float* kl, int64_t i0, int64_t i1, float thr, int64_t size_threshold,
+              int64_t* starts, int64_t& ns) {
+  // Loop-carried state in SSE registers: running float32 sum, group size (as
+  // float: exact below 2^24, size_threshold <= 2^24 here), and the reset
+  // mask; the selects are and/andnot/or, so nothing branches on data.
+  const __m128 vthr = _mm_set_ss(thr);
+  const __m128 vthr_size = _mm_set_ss((float)size_threshold);
+  const __m128 one = _mm_set_ss(1.0f);
+  __m128 cur = _mm_setzero_ps();
+  __m128 size = _mm_setzero_ps();
+  for (int64_t i = i0; i < i1; ++i) {
+    const __m128 k = _mm_load_ss(kl + i);
+    const __m128 sum = _mm_add_ss(cur, k);  // float32 + float32
+    const __m128 m = _mm_or_ps(_mm_cmpge_ss(size, vthr_size), _mm_cmpge_ss(sum, vthr));
+    starts[ns] = i;
+    ns += _mm_movemask_ps(m) & 1;
+    cur = _mm_or_ps(_mm_and_ps(m, k), _mm_andnot_ps(m, sum));
+    size = _mm_or_ps(_mm_and_ps(m, one), _mm_andnot_ps(m, _mm_add_ss(size, one)));
+  }
+}
+
 // coded_greedy_sampler.py:207-252 (strict=false) and
 // coded_importance_sampler.py:178-203 (strict=true).
 int64_t group_starts_impl(const float* kl, int64_t D, int64_t size_threshold, double n_nats,
@@ -130,27 +153,109 @@ int64_t group_starts_impl(const float* kl, int64_t D, int64_t size_threshold, do
   while (!cond(thr) && thr < __builtin_inff()) thr = nextafterf(thr, __builtin_inff());
   while (cond(nextafterf(thr, -__builtin_inff())) && thr > -__builtin_inff())
     thr = nextafterf(thr, -__builtin_inff());
+  if (D < 8 * 1024) {
+    int64_t ns = 1;
+    starts[0] = 0;
+    scan_sse(kl, 0, D - 1, thr, size_threshold, starts, ns);
+    if (D > 0) starts[ns++] = D - 1;  // idx == D - 1 always starts a group (:232)
+    starts[ns++] = D;
+    ok();
+    return ns;
+  }
+  // Long inputs: 8 chunks scanned at once (two 4-lane SSE chains), chunk l > 0
+  // starting speculatively from a fresh group; then a sequential fix-up runs
+  // the exact scan into each chunk from its true state until both scans start
+  // a group at the same index -- from there on they are identical (a group
+  // start resets the state), so the speculative rest of the chunk is taken.
+  constexpr int L = 8;
+  const int64_t n = D - 1;  // indices scanned before the forced last group
+  const int64_t len = n / L;
+  int64_t b[L + 1];
+  for (int l = 0; l < L; ++l) b[l] = (int64_t)l * len;
+  b[L] = n;
+  thread_local std::vector<int64_t> spec;
+  spec.resize((size_t)(n + L));
+  int64_t* sp[L];
+  int64_t cnt[L];
+  for (int l = 0; l < L; ++l) {
+    sp[l] = spec.data() + b[l] + l;
+    cnt[l] = 0;
+  }
+  const __m128 vthr = _mm_set1_ps(thr);
+  const __m128 vthr_size = _mm_set1_ps((float)size_threshold);
+  const __m128 one = _mm_set1_ps(1.0f);
+  __m128 cur0 = _mm_setzero_ps(), size0 = _mm_setzero_ps();
+  __m128 cur1 = _mm_setzero_ps(), size1 = _mm_setzero_ps();
+  for (int64_t t = 0; t < len; ++t) {
+    const __m128 k0 = _mm_setr_ps(kl[b[0] + t], kl[b[1] + t], kl[b[2] + t], kl[b[3] + t]);
+    const __m128 k1 = _mm_setr_ps(kl[b[4] + t], kl[b[5] + t], kl[b[6] + t], kl[b[7] + t]);
+    const __m128 s0 = _mm_add_ps(cur0, k0), s1 = _mm_add_ps(cur1, k1);
+    const __m128 m0 = _mm_or_ps(_mm_cmpge_ps(size0, vthr_size), _mm_cmpge_ps(s0, vthr));
+    const __m128 m1 = _mm_or_ps(_mm_cmpge_ps(size1, vthr_size), _mm_cmpge_ps(s1, vthr));
+    const int bits = _mm_movemask_ps(m0) | (_mm_movemask_ps(m1) << 4);
+    for (int l = 0; l < L; ++l) {
+      sp[l][cnt[l]] = b[l] + t;
+      cnt[l] += (bits >> l) & 1;
+    }
+    cur0 = _mm_or_ps(_mm_and_ps(m0, k0), _mm_andnot_ps(m0, s0));
+    cur1 = _mm_or_ps(_mm_and_ps(m1, k1), _mm_andnot_ps(m1, s1));
+    size0 = _mm_or_ps(_mm_and_ps(m0, one), _mm_andnot_ps(m0, _mm_add_ps(size0, one)));
+    size1 = _mm_or_ps(_mm_and_ps(m1, one), _mm_andnot_ps(m1, _mm_add_ps(size1, one)));
+  }
+  float ecur[L], esize[L];
+  _mm_storeu_ps(ecur, cur0);
+  _mm_storeu_ps(ecur + 4, cur1);
+  _mm_storeu_ps(esize, size0);
+  _mm_storeu_ps(esize + 4, size1);
+  // fix-up, chunk by chunk
   int64_t ns = 1;
   starts[0] = 0;
-  // Loop-carried state in SSE registers: running float32 sum, group size (as
-  // float: exact below 2^24, size_threshold <= 2^24 here), and the reset
-  // mask; the selects are and/andnot/or, so nothing branches on data.
-  const __m128 vthr = _mm_set_ss(thr);
-  const __m128 vthr_size = _mm_set_ss((float)size_threshold);
-  const __m128 one = _mm_set_ss(1.0f);
-  __m128 cur = _mm_setzero_ps();
-  __m128 size = _mm_setzero_ps();
-  const int64_t last = D - 1;
-  for (int64_t i = 0; i < last; ++i) {
-    const __m128 k = _mm_load_ss(kl + i);
-    const __m128 sum = _mm_add_ss(cur, k);  // float32 + float32
-    const __m128 m = _mm_or_ps(_mm_cmpge_ss(size, vthr_size), _mm_cmpge_ss(sum, vthr));
-    starts[ns] = i;
-    ns += _mm_movemask_ps(m) & 1;
-    cur = _mm_or_ps(_mm_and_ps(m, k), _mm_andnot_ps(m, sum));
-    size = _mm_or_ps(_mm_and_ps(m, one), _mm_andnot_ps(m, _mm_add_ss(size, one)));
+  for (int64_t q = 0; q < cnt[0]; ++q) starts[ns++] = sp[0][q];  // chunk 0 is exact
+  float cur = ecur[0];
+  int64_t csz = (int64_t)esize[0];
+  for (int l = 1; l < L; ++l) {
+    const int64_t e = (l == L - 1) ? n : b[l + 1];
+    const int64_t spec_end = b[l] + len;  // the speculative scan covered [b[l], b[l] + len)
+    int64_t p = 0;
+    int64_t i = b[l];
+    bool synced = false;
+    for (; i < spec_end; ++i) {
+      const float k = kl[i];
+      const float sm = cur + k;
+      const bool reset = (csz >= size_threshold) | (sm >= thr);
+      if (reset) {
+        starts[ns++] = i;
+        cur = k;
+        csz = 1;
+        while (p < cnt[l] && sp[l][p] < i) ++p;
+        if (p < cnt[l] && sp[l][p] == i) {  // same group start: identical from here on
+          for (++p; p < cnt[l]; ++p) starts[ns++] = sp[l][p];
+          cur = ecur[l];
+          csz = (int64_t)esize[l];
+          i = spec_end;
+          synced = true;
+          break;
+        }
+      } else {
+        cur = sm;
+        csz += 1;
+      }
+    }
+    (void)synced;
+    for (; i < e; ++i) {  // the last chunk's remainder past the common length
+      const float k = kl[i];
+      const float sm = cur + k;
+      if ((csz >= size_threshold) | (sm >= thr)) {
+        starts[ns++] = i;
+        cur = k;
+        csz = 1;
+      } else {
+        cur = sm;
+        csz += 1;
+      }
+    }
   }
-  if (D > 0) starts[ns++] = last;  // idx == D - 1 always starts a group (:232)
+  starts[ns++] = D - 1;  // idx == D - 1 always starts a group (:232)
   starts[ns++] = D;
   ok();
   return ns;

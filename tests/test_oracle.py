@@ -276,3 +276,29 @@ def test_grouping_exact_threshold_ties(cwqlib, strict):
         starts.append(kl.size)
         got = importance_group_starts(kl, bits, 4)
         assert list(got) == starts
+
+
+@pytest.mark.parametrize("kind", range(5))
+def test_grouping_chunked_scan_matches_reference_loop(cwqlib, kind):
+    """Inputs past 8K dims take the 8-chunk speculative scan with sequential
+    fix-up; it must reproduce the reference loop exactly, also when the size
+    cap binds everywhere or every dim is its own group."""
+    from compression_without_quantization_amd.coded_greedy_sampler import group_starts
+    from compression_without_quantization_amd.synthetic import make_latents
+    rng = np.random.default_rng(40 + kind)
+    D = [30011, 50000, 9000, 65537, 20000][kind]
+    if kind == 0:
+        kl = rng.gamma(0.7, 1.0, D)
+    elif kind == 1:
+        kl = np.full(D, 1e-5)                  # only the 4095-dim cap closes groups
+    elif kind == 2:
+        kl = rng.uniform(3, 10, D)             # every dim over the budget
+    elif kind == 3:
+        kl = np.where(rng.uniform(size=D) < 0.5, 1e-4, rng.gamma(2, 2, D))
+    else:
+        q, qs, p, ps = make_latents(D, seed=kind)
+        t, s = (q - p) / ps, qs / ps
+        kl = 0.5 * (s ** 2 + t ** 2 - 1 - 2 * np.log(s))
+    kl = kl.astype(np.float32)
+    bits, maxbits = [(8, 12), (8, 12), (4, 3), (16, 12), (8, 5)][kind]
+    assert group_starts(kl, bits, maxbits) == _group_starts_py(kl, bits, maxbits)
