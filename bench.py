@@ -4,8 +4,12 @@ One "step" = one greedy-coding pass (code_greedy_sample semantics, 2^16
 candidates per block, n_steps=1) over this rank's batch of synthetic blocks
 (config C4: 10^6 blocks x d=32 per GPU; weak scaling), inputs resident in HBM.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c4|c5|c1]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c4|c5|c1|c2|c3|i1|i2]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+
+c4 (default) is BASELINE.json's metric; c5/c1 are the other block configs;
+c2/c3 time the whole grouped greedy pipeline per image (code_grouped_greedy_sample)
+and i1/i2 the grouped importance pipeline.
 
 Rank 0 prints one JSON line.  `roofline` prices the dominant kernel (the
 candidate-scoring eval kernel, timed with HIP events on its launch stream);
