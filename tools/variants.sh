@@ -8,7 +8,6 @@ OUT=tools/variants
 FLAGS="--offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -fno-fast-math -fPIC -shared"
 declare -A V=(
   [base]=""
-  [w7]="-DCWQ_PRUNE_MIN_WAVES=7"
   [stats]="-DCWQ_PRUNE_STATS"
   [phases]="-DCWQ_PHASE_TIMES"
 )
