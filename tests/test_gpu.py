@@ -571,3 +571,27 @@ def test_importance_screening_matches_exact(cwq, cwqlib, oracle, kind):
         wi, ws = oracle.importance_encode(tl, ts, pl, ps, off, ns, 77)
         assert np.array_equal(i2, wi)
         _assert_bits_equal(s2, ws, f"importance vs oracle ({kind})")
+
+
+@pytest.mark.parametrize("trial", range(12))
+def test_pruned_random_stress(cwq, cwqlib, trial):
+    """Random shapes, budgets, step counts, rho, seeds and heavy-tailed
+    inputs: the three encoder modes must agree bit for bit."""
+    rng = np.random.default_rng(1000 + trial)
+    d = int(rng.choice([8, 16, 24, 32, 40, 48, 56, 64]))
+    bits = int(rng.integers(1, 19))
+    n_steps = int(rng.integers(1, 4))
+    nb = int(rng.integers(1, 9))
+    rho = float(rng.choice([1.0, 0.7, 1.3]))
+    seed = int(rng.integers(-2 ** 31, 2 ** 31 - 1))
+    n = nb * d
+    scale = np.exp(rng.uniform(-3, 3, n))
+    pl = (rng.standard_cauchy(n) * scale).astype(np.float32)
+    ps = (scale * rng.uniform(0.5, 2.0, n)).astype(np.float32)
+    tl = (pl + ps * rng.standard_normal(n) * rng.uniform(0, 2)).astype(np.float32)
+    ts = (ps * np.exp(rng.uniform(-2, 0.5, n))).astype(np.float32)
+    i0, s0 = _uniform_encode(cwq, cwqlib, tl, ts, pl, ps, d, bits, n_steps, seed, rho, 0)
+    for mode in (1, 2):
+        i1, s1 = _uniform_encode(cwq, cwqlib, tl, ts, pl, ps, d, bits, n_steps, seed, rho, mode)
+        assert np.array_equal(i1, i0), (trial, mode, d, bits, n_steps)
+        _assert_bits_equal(s1, s0, f"stress trial {trial} mode {mode}")
