@@ -34,11 +34,14 @@ from compression_without_quantization_amd import _lib  # noqa: E402
 from compression_without_quantization_amd.synthetic import DEFAULT_SEED, make_blocks  # noqa
 
 GROUPED = {
-    # name: (images, [latent dims per image], bits/group, description)
+    # name: (images, [latent dims per image], bits/step, description[, n_steps])
     "c2": (1, [32 * 48 * 128], 8,
            "C2: one 512x768 image, PLN level-1 latents (196,608 dims), 8 bits/group"),
     "c3": (24, [32 * 48 * 128, 8 * 12 * 24], 8,
            "C3: 24 images x (196,608 + 2,304) dims, both ladder levels, 8 bits/group"),
+    "c2cli": (1, [32 * 48 * 128], 14,
+              "C2 at the CLI's greedy defaults: 196,608 dims, n_steps=30 x 14 bits/step "
+              "(miracle_arguments.py:159-165)", 30),
 }
 IMPORTANCE = {
     # name: (images, latent dims, n_bits_per_group, max_group_size_bits, dim_kl_bit_limit, desc)
@@ -82,7 +85,8 @@ def grouped_main(args):
     import compression_without_quantization_amd.coded_greedy_sampler as S
     from compression_without_quantization_amd.synthetic import make_latents
     S.VERBOSE = False
-    n_img, dims, bits, desc = GROUPED[args.config]
+    n_img, dims, bits, desc = GROUPED[args.config][:4]
+    n_steps = GROUPED[args.config][4] if len(GROUPED[args.config]) > 4 else 1
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
     lat = []
@@ -95,7 +99,7 @@ def grouped_main(args):
     def step():
         out = []
         for target, proposal in lat:
-            out.append(C.code_grouped_greedy_sample(None, target, proposal, 1, bits, 42))
+            out.append(C.code_grouped_greedy_sample(None, target, proposal, n_steps, bits, 42))
         return out
     for _ in range(args.warmup):
         res = step()

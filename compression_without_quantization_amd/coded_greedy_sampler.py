@@ -136,6 +136,8 @@ def encode_blocks(t_loc, t_scale, p_loc, p_scale, n_bits_per_step, n_steps, seed
     if out_sample is None:
         out_sample = torch.empty(D, dtype=torch.float32, device=dev)
     need = encode_workspace_bytes(nb, D)
+    if offs is not None:  # room for the general pruned kernel's arrays (cwq.h)
+        need += 12 * D + 24 * nb + 1024
     if workspace is None or workspace.numel() < need:
         workspace = torch.empty(max(need, 1), dtype=torch.uint8, device=dev)
     stream = torch.cuda.current_stream(dev).cuda_stream

@@ -45,10 +45,21 @@ int hip_fail(hipError_t e, const char* where) {
 size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
 
 struct WsLayout {
-  size_t keys, loc_s, scale_s, lognorm, total;
+  size_t keys, loc_s, scale_s, lognorm, sab, bpre, grp, gtau, total;
+  bool csr;  // has the general pruned kernel's arrays
 };
 
-WsLayout ws_layout(int64_t nb, int64_t total_dims) {
+// Blocks the uniform fast pruned kernel takes (d % 8 == 0, 8 <= d <= 64) need
+// only keys + the per-dim shard constants; everything else (CSR, other d) also
+// gets the general pruned kernel's screening constants (12 B/dim + 24 B/block).
+bool ws_needs_csr(int64_t nb, int64_t total_dims) {
+  if (nb <= 0) return false;
+  if (total_dims % nb) return true;
+  const int64_t d = total_dims / nb;
+  return !(d % 8 == 0 && d >= 8 && d <= 64);
+}
+
+WsLayout ws_layout(int64_t nb, int64_t total_dims, bool csr) {
   WsLayout l;
   size_t o = 0;
   l.keys = o;
@@ -59,12 +70,25 @@ WsLayout ws_layout(int64_t nb, int64_t total_dims) {
   o = align_up(o + (size_t)total_dims * 4, 256);
   l.lognorm = o;
   o = align_up(o + (size_t)total_dims * 4, 256);
+  l.csr = csr;
+  l.sab = l.bpre = l.grp = l.gtau = o;
+  if (csr) {
+    l.sab = o;
+    o = align_up(o + (size_t)total_dims * 8, 256);
+    l.bpre = o;
+    o = align_up(o + (size_t)(total_dims + nb) * 4, 256);
+    l.grp = o;
+    o = align_up(o + (size_t)nb * 16, 256);
+    l.gtau = o;
+    o = align_up(o + (size_t)nb * 4, 256);
+  }
   l.total = o;
   return l;
 }
+WsLayout ws_layout(int64_t nb, int64_t total_dims) {
+  return ws_layout(nb, total_dims, ws_needs_csr(nb, total_dims));
+}
 
-// Tiling: split a block's 2^b candidates over several workgroups only when
-// there are too few blocks to fill the chip (256 CUs x several workgroups).
 void choose_tiling(int64_t nb, int64_t n_cand, int64_t* tiles_per_block, int64_t* cand_per_tile) {
   const int64_t kTargetTiles = 16384;
   int64_t want = nb > 0 ? (kTargetTiles + nb - 1) / nb : 1;
@@ -281,7 +305,12 @@ int encode_impl(const float* t_loc, const float* t_scale, const float* p_loc,
   if (nb > 0 && (!out_idx)) return fail(CWQ_ERR_INVALID, "out_idx is null");
   if (total_dims > 0 && (!t_loc || !t_scale || !p_loc || !p_scale || !out_sample))
     return fail(CWQ_ERR_INVALID, "null input/output pointer");
-  const WsLayout l = ws_layout(nb, total_dims);
+  // required: cwq_greedy_encode_workspace_size(nb, total_dims).  A CSR call
+  // whose sizes look uniform-fast also uses the general pruned kernel's arrays
+  // when the workspace has room for them.
+  const WsLayout lr = ws_layout(nb, total_dims);
+  const WsLayout lc = ws_layout(nb, total_dims, true);
+  const WsLayout l = (!lr.csr && block_off && workspace_bytes >= lc.total) ? lc : lr;
   if (workspace_bytes < l.total || (l.total && !workspace))
     return fail(CWQ_ERR_WORKSPACE, "workspace %zu bytes < required %zu", workspace_bytes,
                 l.total);
@@ -308,6 +337,10 @@ int encode_impl(const float* t_loc, const float* t_scale, const float* p_loc,
   a.loc_s = (float*)(w + l.loc_s);
   a.scale_s = (float*)(w + l.scale_s);
   a.lognorm = (float*)(w + l.lognorm);
+  a.sab = l.csr ? (float2*)(w + l.sab) : nullptr;
+  a.bpre = l.csr ? (float*)(w + l.bpre) : nullptr;
+  a.grp = l.csr ? (float4*)(w + l.grp) : nullptr;
+  a.gtau = l.csr ? (uint32_t*)(w + l.gtau) : nullptr;
   a.ev_start = g_ev_start;
   a.ev_stop = g_ev_stop;
   hipError_t e = cwq::launch_encode(a, (hipStream_t)stream);

@@ -239,7 +239,10 @@ __global__ void __launch_bounds__(256) k_imp_eval(
         suf += (double)dumax[j];
         dsuf[j] = round_up_f32(suf * (1.0 + 0x1p-20) + 0x1p-126);  // covers the test's adds
       }
-      tau_ord = ord_f32(-__builtin_inff());
+      // start from what earlier tiles of the group found (agent-scope load;
+      // the loop shares tau inside the workgroup only: per-iteration global
+      // atomics on gtau cost more than they prune)
+      tau_ord = __hip_atomic_load(&gtau[g], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       sq_cnt = 0u;
     }
     __syncthreads();
@@ -247,7 +250,7 @@ __global__ void __launch_bounds__(256) k_imp_eval(
 
     uint64_t bestk = 0;
     if (screen && E - E == 0.0f) {
-      float tau = -__builtin_inff();
+      float tau = unord_f32(tau_ord);
       // may be the best: list it
       auto keep = [&](int64_t n, float sh, float slack) __attribute__((always_inline)) {
         const float up = sh + slack;
@@ -305,15 +308,10 @@ __global__ void __launch_bounds__(256) k_imp_eval(
           }
           wnext += (int64_t)__builtin_popcountll(m);
           active = n < w1;
-          if (((++iter) & 15u) == 0u) {  // share tau with the workgroup and the group
+          if (((++iter) & 15u) == 0u) {  // share tau with the workgroup
             const float tm = wave_max_f32(tau);
-            if (lane == 0) {
-              atomicMax(&tau_ord, ord_f32(tm));
-              atomicMax(&gtau[g], ord_f32(tm));
-            }
-            const uint32_t o1 = __atomic_load_n(&tau_ord, __ATOMIC_RELAXED);
-            const uint32_t o2 = __atomic_load_n(&gtau[g], __ATOMIC_RELAXED);
-            tau = fmaxf(tau, unord_f32(o1 > o2 ? o1 : o2));
+            if (lane == 0) atomicMax(&tau_ord, ord_f32(tm));
+            tau = fmaxf(tau, unord_f32(__atomic_load_n(&tau_ord, __ATOMIC_RELAXED)));
           }
         }
       } else {

@@ -32,6 +32,12 @@ struct EncodeArgs {
   float* loc_s;              // [total_dims]
   float* scale_s;            // [total_dims]
   float* lognorm;            // [total_dims]
+  // screening constants of the general pruned kernel (k_encode_prune_csr);
+  // nullptr when the workspace was sized without them
+  float2* sab;               // [total_dims] (sA, sB)
+  float* bpre;               // [total_dims + nb] drop-test constants B_j, j = 0..d per block
+  float4* grp;               // [nb] (c1, c2, As, Pq); c1 == 0: block not screened
+  uint32_t* gtau;            // [nb] per-block shared threshold (ord)
   // optional profiling events around the eval launches (hipEvent_t)
   void* ev_start;
   void* ev_stop;

@@ -197,7 +197,10 @@ constexpr double kScreenKappa = 0.7070958018530696;  // sqrt(phi (1 - 2^-24) / 2
 
 #ifdef CWQ_PRUNE_STATS
 // tuning builds only (tools/prune_stats.py): [0..64] candidates finished after
-// k units, [65] completed rows, [66] survivors pushed, [67] screened tiles
+// k units, [65] completed rows, [66] survivors pushed, [67] screened tiles;
+// general kernel (tools/csr_stats.py): [40]/[41] screened/exact tiles, [42] rows
+// finished, [43] dims screened, [44] rows completed, [45] survivors pushed,
+// [46] list-full exact rows, [47] survivors re-evaluated, [48] lane-iterations
 __device__ unsigned long long g_prune_stats[72];
 // "oracle tau" experiment: each tile's best key is saved; with g_seed_tau set
 // the next launch starts every tile at the exact best value of the last one
@@ -545,6 +548,390 @@ __global__ void __launch_bounds__(256, CWQ_PRUNE_MIN_WAVES) k_encode_prune(
 }
 
 // ---------------------------------------------------------------------------
+// General pruned encoder: any block dimension, CSR or uniform (the greedy
+// coder's ragged groups, coded_greedy_sampler.py:207-284).  Same screening
+// bound as k_encode_prune (DESIGN.md "screening bound"), with three changes:
+//   * dims are visited in natural order (a candidate row starts at any word of
+//     a Philox block: each lane walks its row one Philox block at a time);
+//   * the per-dim constants live in global memory, computed once per step by
+//     k_csr_prep (one workgroup per block), with the float-summation factors
+//     of the bound scaled for the block's d (gamma_d = 1.01 (d+1) 2^-24);
+//   * tiles of one block share their threshold through gtau[g].
+// Blocks whose constants fail the gate are scored exactly.
+// ---------------------------------------------------------------------------
+struct CsrDim {
+  float sa, sb;     // a = RN(sa z' + sb), z' = screening z / sqrt(2 ln 2)
+  float A, C;       // additive error (a units) and C_j of the bound
+  double M;         // M_j = -c_j
+  bool ok;
+};
+
+template <bool STEP0>
+__device__ __forceinline__ CsrDim csr_dim(float ls, float ss, float mu, float sg, float c,
+                                          float bb) {
+  CsrDim o;
+  const double ssa = __builtin_fabs((double)ss), lsa = __builtin_fabs((double)ls);
+  const double mua = __builtin_fabs((double)mu);
+  const double bba = STEP0 ? 0.0 : __builtin_fabs((double)bb);
+  const double zs = kScreenZm * ssa;
+  const double mag = bba + lsa + zs + mua;
+  const double rho = 0x1p-24 * 1.0001 * (zs + (lsa + zs) + (STEP0 ? 0.0 : bba + lsa + zs) + mag);
+  const double offd = (STEP0 ? 0.0 : (double)bb) + (double)ls - (double)mu;
+  const double sig = (double)sg;
+  const double kq = kScreenKappa / sig;
+  o.sa = (float)((double)ss * kq * kSqrt2Ln2);
+  o.sb = (float)(offd * kq);
+  const double a0 = (kq * (rho + ssa * kScreenEz) +
+                     kq * 0x1p-24 * 1.0001 * (zs + __builtin_fabs(offd))) * (1.0 + 0x1p-20) +
+                    0x1p-140;
+  o.A = round_up_f32(a0 * 1.0001);
+  o.C = round_up_f32((1.0 / kScreenEps - 1.0) * a0 * a0 / kScreenPhi * (1.0 + 0x1p-20));
+  o.M = -(double)c;
+  o.ok = markstein_ok_den(sg) && mag <= 0x1p100 && mag / sig <= 0x1p50 && o.C <= 0x1p60f &&
+         o.sa - o.sa == 0.0f && o.sb - o.sb == 0.0f && c - c == 0.0f;
+  return o;
+}
+
+__device__ __forceinline__ double block_sum_d(double v, double* red) {
+  red[threadIdx.x] = v;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if ((int)threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+    __syncthreads();
+  }
+  const double r = red[0];
+  __syncthreads();
+  return r;
+}
+
+template <bool STEP0>
+__global__ void __launch_bounds__(256) k_csr_prep(
+    const float* __restrict__ t_loc, const float* __restrict__ t_scale,
+    const float* __restrict__ loc_s, const float* __restrict__ scale_s,
+    const float* __restrict__ lognorm, const float* __restrict__ best,
+    const int64_t* __restrict__ block_off, int64_t ud, int64_t nb, float2* __restrict__ sab,
+    float* __restrict__ bpre, float4* __restrict__ grp, uint32_t* __restrict__ gtau) {
+  __shared__ double red[256];
+  __shared__ double scan[256];
+  const int tid = threadIdx.x;
+  for (int64_t g = blockIdx.x; g < nb; g += gridDim.x) {
+    const BlockSpan sp = block_span(block_off, ud, g);
+    const int64_t off = sp.off, d = sp.d;
+    auto dim = [&](int64_t j) {
+      return csr_dim<STEP0>(loc_s[off + j], scale_s[off + j], t_loc[off + j], t_scale[off + j],
+                            lognorm[off + j], STEP0 ? 0.0f : best[off + j]);
+    };
+    double sm = 0.0, sa = 0.0, sk = 0.0, s2 = 0.0, mx = 0.0;
+    int ok = 1;
+    for (int64_t j = tid; j < d; j += 256) {
+      const CsrDim o = dim(j);
+      sab[off + j] = float2{o.sa, o.sb};
+      sm += o.M;
+      sa += __builtin_fabs(o.M);
+      sk += __builtin_fabs(o.M) + o.M;
+      s2 += (double)o.A * (double)o.A;
+      mx = (double)o.A > mx ? (double)o.A : mx;
+      ok &= o.ok ? 1 : 0;
+    }
+    const bool all_ok = __syncthreads_and(ok) != 0;
+    const double SM = block_sum_d(sm, red), SA = block_sum_d(sa, red);
+    const double SK = block_sum_d(sk, red), S2 = block_sum_d(s2, red);
+    red[tid] = mx;
+    __syncthreads();
+    for (int w = 128; w > 0; w >>= 1) {
+      if (tid < w) red[tid] = red[tid + w] > red[tid] ? red[tid + w] : red[tid];
+      __syncthreads();
+    }
+    const double MX = red[0];
+    __syncthreads();
+    const double gam = 1.01 * (double)(d + 1) * 0x1p-24;
+    const double sl = (3.0 * gam + 0x1p-14) * (__builtin_fabs(SM) + SA + SK) + 0x1p-126;
+    // B_j = sum M + (sum of C over the first j dims) + slack, j = 0..d
+    double carry = 0.0;
+    for (int64_t base = 0; base <= d; base += 256) {
+      const int64_t j = base + tid;
+      const double cj = (all_ok && j < d) ? (double)dim(j).C : 0.0;
+      scan[tid] = cj;
+      __syncthreads();
+      for (int w = 1; w < 256; w <<= 1) {  // inclusive scan
+        const double v = tid >= w ? scan[tid - w] : 0.0;
+        __syncthreads();
+        scan[tid] += v;
+        __syncthreads();
+      }
+      const double excl = carry + scan[tid] - cj;
+      if (j <= d) bpre[off + g + j] = round_up_f32(SM + excl * (1.0 + 0x1p-20) + sl);
+      carry += scan[255];
+      __syncthreads();
+    }
+    if (tid == 0) {
+      const float c1 = round_dn_f32(1.0 - 3.0 * gam - 0x1p-22);
+      const float c2 = round_up_f32(1.0 + 3.0 * gam + 0x1p-14);
+      const float as = round_dn_f32(SM - sl - 1.01 * S2 * (1.0 + 0x1p-11));
+      const float pq = round_up_f32(2.01 * MX * __builtin_sqrt((double)(d > 0 ? d : 1)) *
+                                    (1.0 + 0x1p-11));
+      const bool fin = as - as == 0.0f && pq - pq == 0.0f;
+      grp[g] = (all_ok && fin && d > 0) ? float4{c1, c2, as, pq} : float4{0.f, 0.f, 0.f, 0.f};
+      gtau[g] = ord_f32(-__builtin_inff());
+    }
+    __syncthreads();
+  }
+}
+
+// One candidate row evaluated exactly by a whole wave (the survivors of the
+// general pruned kernel; d is large there, so one lane per row would leave the
+// other 63 idle for a full row).  Lanes compute the terms of up to 63 Philox
+// blocks per 248-dim chunk into LDS; lanes 0-7 then fold them into the eight
+// Eigen accumulators and lane 8 into the tail, in exactly eval_row_f's order.
+// Every lane returns the row value.
+constexpr int kRowChunk = 248;  // multiple of 8; spans <= 63 Philox blocks
+
+template <bool STEP0>
+__device__ __forceinline__ float exact_row_wave(
+    const PhiloxStream& st, uint64_t kbase, int64_t d, const float* __restrict__ loc_s,
+    const float* __restrict__ scale_s, const float* __restrict__ mu,
+    const float* __restrict__ sg, const float* __restrict__ lognorm,
+    const float* __restrict__ best, const double* logtab, float* buf, uint32_t lane) {
+  const int64_t vec = d & ~(int64_t)7;
+  float acc = 0.0f;  // lane l < 8: p[l]; lane 8: the tail sum
+  for (int64_t j0 = 0; j0 < d; j0 += kRowChunk) {
+    const int64_t cnt = (d - j0) < kRowChunk ? d - j0 : kRowChunk;
+    const uint64_t k0 = kbase + (uint64_t)j0;
+    const uint64_t blk = (k0 >> 2) + lane;
+    const int64_t ef = (int64_t)(blk << 2) - (int64_t)k0;  // chunk index of the block's word 0
+    if (ef < cnt) {
+      const F4 z = normal4_dev(st, blk, logtab);
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const int64_t e = ef + t;
+        if (e >= 0 && e < cnt) {
+          const int64_t j = j0 + e;
+          const float zz = t == 0 ? z.a : (t == 1 ? z.b : (t == 2 ? z.c : z.d));
+          float v = scale_s[j] * zz;  // misc.py:14
+          v = loc_s[j] + v;           // misc.py:15
+          const float tv = STEP0 ? v : best[j] + v;
+          buf[e] = log_prob(tv, mu[j], sg[j], lognorm[j]);
+        }
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    if (lane < 8) {
+      for (int64_t e = lane; e < cnt && j0 + e < vec; e += 8) acc = acc + buf[e];
+    } else if (lane == 8) {
+      for (int64_t e = (vec > j0 ? vec - j0 : 0); e < cnt; ++e) acc = acc + buf[e];
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+  }
+  float p[8];
+#pragma unroll
+  for (int l = 0; l < 8; ++l) p[l] = __shfl(acc, l, 64);
+  const float t = __shfl(acc, 8, 64);
+  const float q0 = p[0] + p[4], q1 = p[1] + p[5], q2 = p[2] + p[6], q3 = p[3] + p[7];
+  return t + ((q0 + q2) + (q1 + q3));
+}
+
+#ifndef CWQ_CSR_LDS_DIMS
+#define CWQ_CSR_LDS_DIMS 1024  // blocks up to this d keep their screening constants in LDS
+#endif
+#ifndef CWQ_CSR_GTAU_SHARE
+#define CWQ_CSR_GTAU_SHARE 0  // 1: also share tau with the block's other tiles in the loop
+#endif
+#ifndef CWQ_CSR_SURVIVOR_CAP
+#define CWQ_CSR_SURVIVOR_CAP 512
+#endif
+
+template <bool STEP0>
+__global__ void __launch_bounds__(256, 6) k_encode_prune_csr(
+    const float* __restrict__ t_loc, const float* __restrict__ t_scale,
+    const float* __restrict__ loc_s, const float* __restrict__ scale_s,
+    const float* __restrict__ lognorm, const float* __restrict__ best,
+    const int64_t* __restrict__ block_off, int64_t ud, int64_t ntiles, int64_t tiles_per_block,
+    int64_t cand_per_tile, int64_t n_cand, int32_t seed, int64_t block_id_base, int32_t step,
+    const float2* __restrict__ sab, const float* __restrict__ bpre,
+    const float4* __restrict__ grp, uint32_t* __restrict__ gtau,
+    unsigned long long* __restrict__ keys) {
+  __shared__ double logtab[32];
+  __shared__ uint32_t tau_ord;
+  __shared__ uint32_t sq_cnt;
+  __shared__ uint32_t sq_n[CWQ_CSR_SURVIVOR_CAP];
+  __shared__ float sq_ub[CWQ_CSR_SURVIVOR_CAP];
+  __shared__ unsigned long long wkey[4];
+  __shared__ float2 l_ab[CWQ_CSR_LDS_DIMS];
+  __shared__ float l_bp[CWQ_CSR_LDS_DIMS + 1];
+  __shared__ float rowbuf[4][kRowChunk];
+  fill_logtab(logtab);
+  const uint32_t wv = wave_id();
+  const uint32_t lane = threadIdx.x & 63u;
+
+  for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    uint32_t tid = threadIdx.x;
+    asm volatile("" : "+v"(tid));
+    const int64_t g = tile / tiles_per_block;
+    const int64_t tt = tile - g * tiles_per_block;
+    const BlockSpan sp = block_span(block_off, ud, g);
+    const int64_t off = sp.off, d = sp.d;
+    const int64_t n0 = tt * cand_per_tile;
+    const int64_t n1 = (n0 + cand_per_tile < n_cand) ? n0 + cand_per_tile : n_cand;
+    const PhiloxStream st =
+        generate_key(step_seed(block_seed(seed, block_id_base + g), step), 42);
+    const float4 gc = grp[g];
+    const bool in_lds = d <= CWQ_CSR_LDS_DIMS;
+    if (gc.x != 0.0f && in_lds) {
+      for (int64_t j = tid; j <= d; j += blockDim.x) {
+        if (j < d) l_ab[j] = sab[off + j];
+        l_bp[j] = bpre[off + g + j];
+      }
+    }
+    if (tid == 0) {
+      tau_ord = __hip_atomic_load(&gtau[g], __ATOMIC_RELAXED,
+                                  __HIP_MEMORY_SCOPE_AGENT);  // earlier tiles of the block
+      sq_cnt = 0u;
+    }
+    __syncthreads();
+    uint64_t bestk = 0;
+#ifdef CWQ_PRUNE_STATS
+    if (tid == 0) atomicAdd(&g_prune_stats[gc.x != 0.0f ? 40 : 41], 1ull);
+#endif
+    if (gc.x != 0.0f) {
+      const int64_t per_wave = (n1 - n0 + 3) / 4;
+      const int64_t w0 = n0 + (int64_t)wv * per_wave;
+      const int64_t w1 = (w0 + per_wave < n1) ? w0 + per_wave : n1;
+      auto run = [&](const float2* ab, const float* bj) __attribute__((always_inline)) {
+        int64_t wnext = w0 + 64;
+        int64_t n = w0 + lane;
+        bool active = n < w1;
+        int64_t j = 0;
+        float s = 0.0f;
+        float tau = unord_f32(tau_ord);
+        uint32_t iter = 0;
+        while (__ballot(active) != 0ull) {
+          const uint64_t k = (uint64_t)n * (uint64_t)d + (uint64_t)j;
+          const F4 z = normal4_screen(st, k >> 2);
+          const int wa = (int)(k & 3u);
+          const int64_t left = d - j;
+          const int cnt = (int64_t)(4 - wa) < left ? 4 - wa : (int)left;
+#pragma unroll
+          for (int t = 0; t < 4; ++t) {
+            if (t < cnt) {
+              const int w = wa + t;
+              const float zz = w == 0 ? z.a : (w == 1 ? z.b : (w == 2 ? z.c : z.d));
+              const float2 c = ab[j + t];
+              const float a = __builtin_fmaf(c.x, zz, c.y);
+              s = __builtin_fmaf(-a, a, s);
+            }
+          }
+          j += cnt;
+#ifdef CWQ_PRUNE_STATS
+          if (active) atomicAdd(&g_prune_stats[43], (unsigned long long)cnt);
+#endif
+          const bool complete = (j == d);
+          const float upper = __builtin_fmaf(s, gc.x, bj[j]);
+          const bool prune = !complete && (upper < tau);
+          if (complete && active && upper >= tau) {  // may be the best: keep it
+            const float lower =
+                __builtin_fmaf(s, gc.y, gc.z) - gc.w * __builtin_amdgcn_sqrtf(-s);
+            tau = fmaxf(tau, lower);
+            const uint32_t slot = atomicAdd(&sq_cnt, 1u);
+            if (slot < CWQ_CSR_SURVIVOR_CAP) {
+              sq_n[slot] = (uint32_t)(n - n0);
+              sq_ub[slot] = upper;
+            } else {  // list full: evaluate exactly now
+#ifdef CWQ_PRUNE_STATS
+              atomicAdd(&g_prune_stats[46], 1ull);
+#endif
+              const float v = eval_row<0, STEP0>(
+                  st, (uint64_t)n * (uint64_t)d, d, (int)(((uint64_t)n * d) & 3u), loc_s + off,
+                  scale_s + off, t_loc + off, t_scale + off, lognorm + off,
+                  STEP0 ? nullptr : best + off, logtab);
+              const uint64_t kv = argmax_key(v, (uint32_t)n);
+              bestk = kv > bestk ? kv : bestk;
+            }
+          }
+          const bool done = complete || prune || !active;
+#ifdef CWQ_PRUNE_STATS
+          if (active && (complete || prune)) atomicAdd(&g_prune_stats[42], 1ull);
+          if (active && complete) atomicAdd(&g_prune_stats[44], 1ull);
+          if (active && complete && upper >= tau) atomicAdd(&g_prune_stats[45], 1ull);
+          atomicAdd(&g_prune_stats[48], 1ull);
+#endif
+          const uint64_t m = __ballot(done);
+          const uint32_t rank = __builtin_amdgcn_mbcnt_hi(
+              (uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+          if (done) {
+            n = wnext + rank;
+            j = 0;
+            s = 0.0f;
+          }
+          wnext += (int64_t)__builtin_popcountll(m);
+          active = n < w1;
+          if (((++iter) & CWQ_TAU_SHARE_MASK) == 0u) {  // share with the workgroup
+            const float tm = wave_max_f32(tau);
+            if (lane == 0) atomicMax(&tau_ord, ord_f32(tm));
+            uint32_t o = __atomic_load_n(&tau_ord, __ATOMIC_RELAXED);
+#if CWQ_CSR_GTAU_SHARE
+            if (lane == 0) atomicMax(&gtau[g], ord_f32(tm));
+            const uint32_t o2 = __hip_atomic_load(&gtau[g], __ATOMIC_RELAXED,
+                                                  __HIP_MEMORY_SCOPE_AGENT);
+            o = o > o2 ? o : o2;
+#endif
+            tau = fmaxf(tau, unord_f32(o));
+          }
+        }
+        const float tm = wave_max_f32(tau);
+        if (lane == 0) atomicMax(&tau_ord, ord_f32(tm));
+      };
+      if (in_lds)
+        run(l_ab, l_bp);
+      else
+        run(sab + off, bpre + off + g);
+      __syncthreads();
+      if (tid == 0) {
+        const uint32_t mine = tau_ord;
+        const uint32_t prev = atomicMax(&gtau[g], mine);
+        tau_ord = prev > mine ? prev : mine;
+      }
+      __syncthreads();
+      const float tau_final = unord_f32(tau_ord);
+      const uint32_t nsurv = sq_cnt < CWQ_CSR_SURVIVOR_CAP ? sq_cnt : CWQ_CSR_SURVIVOR_CAP;
+      for (uint32_t i = wv; i < nsurv; i += 4) {  // one survivor per wave
+        if (sq_ub[i] >= tau_final) {
+          const int64_t nn = n0 + (int64_t)sq_n[i];
+#ifdef CWQ_PRUNE_STATS
+          if (lane == 0) atomicAdd(&g_prune_stats[47], 1ull);
+#endif
+          const float v = exact_row_wave<STEP0>(
+              st, (uint64_t)nn * (uint64_t)d, d, loc_s + off, scale_s + off, t_loc + off,
+              t_scale + off, lognorm + off, STEP0 ? nullptr : best + off, logtab, rowbuf[wv],
+              lane);
+          const uint64_t kv = argmax_key(v, (uint32_t)nn);
+          bestk = kv > bestk ? kv : bestk;
+        }
+      }
+    } else {
+      const int align = (int)(((uint64_t)(n0 + wv) * (uint64_t)d) & 3u);
+      for (int64_t n = n0 + 4 * (int64_t)lane + wv; n < n1; n += 256) {
+        const float v = eval_row<0, STEP0>(st, (uint64_t)n * (uint64_t)d, d, align, loc_s + off,
+                                           scale_s + off, t_loc + off, t_scale + off,
+                                           lognorm + off, STEP0 ? nullptr : best + off, logtab);
+        const uint64_t kv = argmax_key(v, (uint32_t)n);
+        bestk = kv > bestk ? kv : bestk;
+      }
+    }
+    bestk = wave_max_u64(bestk);
+    if (lane == 0) wkey[wv] = bestk;
+    __syncthreads();
+    if (tid == 0) {
+      uint64_t mk = wkey[0];
+      for (int i = 1; i < 4; ++i) mk = wkey[i] > mk ? wkey[i] : mk;
+      if (mk) atomicMax(&keys[g], (unsigned long long)mk);
+    }
+    __syncthreads();
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Encoder, end of a step: index -> out_idx; best += winning candidate (:63).
 // One wave per block.
 // ---------------------------------------------------------------------------
@@ -793,6 +1180,27 @@ static void launch_prune_t(const EncodeArgs& a, int step, hipStream_t stream) {
 }
 
 template <bool STEP0>
+static void launch_prune_csr(const EncodeArgs& a, int step, hipStream_t stream) {
+  hipLaunchKernelGGL((k_csr_prep<STEP0>), dim3(grid_for(a.nb, 1, 65536)), dim3(256), 0, stream,
+                     a.t_loc, a.t_scale, a.loc_s, a.scale_s, a.lognorm, a.out_sample,
+                     a.block_off, a.ud, a.nb, a.sab, a.bpre, a.grp, a.gtau);
+  // own tiling: ~8192 tiles of >= 1024 candidates; tiles of a block share tau
+  // through gtau, and later tiles start from it
+  int64_t tpb = (8192 + a.nb - 1) / a.nb;
+  const int64_t max_tpb = a.n_cand / 1024 > 1 ? a.n_cand / 1024 : 1;
+  tpb = tpb < max_tpb ? tpb : max_tpb;
+  const int64_t cpt = (a.n_cand + tpb - 1) / tpb;
+  const int64_t ntiles = a.nb * tpb;
+  constexpr int64_t kGrid = 1 << 20;
+  const unsigned grid = (unsigned)(ntiles < kGrid ? ntiles : kGrid);
+  hipLaunchKernelGGL((k_encode_prune_csr<STEP0>), dim3(grid), dim3(256), 0, stream, a.t_loc,
+                     a.t_scale, a.loc_s, a.scale_s, a.lognorm, a.out_sample, a.block_off, a.ud,
+                     ntiles, tpb, cpt, a.n_cand, a.seed, a.block_id_base, step,
+                     (const float2*)a.sab, (const float*)a.bpre, (const float4*)a.grp, a.gtau,
+                     a.keys);
+}
+
+template <bool STEP0>
 static void launch_eval_dc(const EncodeArgs& a, int step, hipStream_t stream) {
   // pruned path: uniform D % 8 == 0, D <= 64, Philox block index n*D/4 < 2^32
   if (a.block_off == nullptr && a.prune && a.ud % 8 == 0 && a.ud >= 8 && a.ud <= 64 &&
@@ -809,6 +1217,9 @@ static void launch_eval_dc(const EncodeArgs& a, int step, hipStream_t stream) {
       default: break;
     }
   }
+  // general pruned path (screening): CSR or other uniform d, >= 4096 candidates
+  if (a.prune >= 2 && a.sab != nullptr && a.n_cand >= 4096)
+    return launch_prune_csr<STEP0>(a, step, stream);
   if (a.block_off == nullptr) {
     switch (a.ud) {
       case 8: return launch_eval_t<8, STEP0>(a, step, stream);

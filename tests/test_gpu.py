@@ -595,3 +595,111 @@ def test_pruned_random_stress(cwq, cwqlib, trial):
         i1, s1 = _uniform_encode(cwq, cwqlib, tl, ts, pl, ps, d, bits, n_steps, seed, rho, mode)
         assert np.array_equal(i1, i0), (trial, mode, d, bits, n_steps)
         _assert_bits_equal(s1, s0, f"stress trial {trial} mode {mode}")
+
+
+# ---------------------------------------------------------------------------
+# general pruned kernel (k_encode_prune_csr): ragged groups and uniform d the
+# fast kernel does not take, >= 4096 candidates
+# ---------------------------------------------------------------------------
+def _csr_encode(cwq, cwqlib, tl, ts, pl, ps, off, bits, n_steps, seed, rho, mode):
+    cwqlib.cwq_set_pruning(int(mode))
+    try:
+        i, s = cwq.encode_blocks(tl, ts, pl, ps, bits, n_steps, seed, rho=rho, block_off=off)
+        torch.cuda.synchronize()
+        return i.cpu().numpy(), s.cpu().numpy()
+    finally:
+        cwqlib.cwq_set_pruning(2)
+
+
+def _heavy_inputs(rng, n):
+    scale = np.exp(rng.uniform(-3, 3, n))
+    pl = (rng.standard_cauchy(n) * scale).astype(np.float32)
+    ps = (scale * rng.uniform(0.5, 2.0, n)).astype(np.float32)
+    tl = (pl + ps * rng.standard_normal(n) * rng.uniform(0, 2)).astype(np.float32)
+    ts = (ps * np.exp(rng.uniform(-2, 0.5, n))).astype(np.float32)
+    return tl, ts, pl, ps
+
+
+@pytest.mark.parametrize("sizes,bits,n_steps,rho", [
+    ([0, 3, 1, 0, 17, 8, 5, 0, 40, 2, 9, 130], 12, 1, 1.0),
+    ([5] * 9, 13, 2, 1.0),
+    ([7, 33, 301, 1, 12], 14, 1, 0.9),
+    ([100, 100, 100], 12, 3, 1.0),
+    ([1100, 40, 600], 12, 2, 1.0),
+])
+def test_csr_pruned_vs_oracle(cwq, cwqlib, oracle, sizes, bits, n_steps, rho):
+    rng = np.random.default_rng(sum(sizes) + bits)
+    off = np.concatenate([[0], np.cumsum(sizes)]).astype(np.int64)
+    D = int(off[-1])
+    tl = rng.standard_normal(D).astype(np.float32)
+    ts = rng.uniform(0.2, 1.0, D).astype(np.float32)
+    pl = (0.1 * rng.standard_normal(D)).astype(np.float32)
+    ps = rng.uniform(0.8, 1.2, D).astype(np.float32)
+    wi, ws = oracle.greedy_encode(tl, ts, pl, ps, off, bits, n_steps, 42, rho)
+    for mode in (0, 1, 2):
+        gi, gs = _csr_encode(cwq, cwqlib, tl, ts, pl, ps, off, bits, n_steps, 42, rho, mode)
+        assert np.array_equal(gi, wi), (mode, gi.reshape(-1)[:8], wi.reshape(-1)[:8])
+        _assert_bits_equal(gs, ws, f"csr mode {mode}")
+
+
+@pytest.mark.parametrize("kind", ["far_locs", "huge_locs", "tiny_locs"])
+def test_csr_pruned_adversarial(cwq, cwqlib, oracle, kind):
+    rng = np.random.default_rng(7)
+    sizes = [3, 20, 1, 45]
+    off = np.concatenate([[0], np.cumsum(sizes)]).astype(np.int64)
+    D = int(off[-1])
+    pl = np.zeros(D, np.float32)
+    ps = np.ones(D, np.float32)
+    ts = rng.uniform(0.3, 1.0, D).astype(np.float32)
+    if kind == "far_locs":
+        tl = (rng.standard_normal(D) * 40).astype(np.float32)
+    elif kind == "huge_locs":
+        tl = (rng.standard_normal(D) * 1e30).astype(np.float32)
+        pl = (rng.standard_normal(D) * 1e30).astype(np.float32)
+    else:
+        ts = (rng.uniform(0.3, 1.0, D) * 1e-20).astype(np.float32)
+        tl = (rng.standard_normal(D) * 1e-20).astype(np.float32)
+    wi, ws = oracle.greedy_encode(tl, ts, pl, ps, off, 12, 1, 5)
+    for mode in (0, 2):
+        gi, gs = _csr_encode(cwq, cwqlib, tl, ts, pl, ps, off, 12, 1, 5, 1.0, mode)
+        assert np.array_equal(gi, wi), (kind, mode)
+        _assert_bits_equal(gs, ws, f"csr {kind} mode {mode}")
+
+
+@pytest.mark.parametrize("trial", range(12))
+def test_csr_random_stress(cwq, cwqlib, trial):
+    """Random ragged layouts (empty groups included) and odd uniform d, heavy-
+    tailed inputs: modes 0 and 2 agree bit for bit."""
+    rng = np.random.default_rng(5000 + trial)
+    nb = int(rng.integers(1, 7))
+    if trial % 3 == 2:
+        sizes = [int(rng.choice([1, 3, 5, 7, 9, 12, 20, 72, 100]))] * nb
+    else:
+        sizes = [int(x) for x in rng.integers(0, 160, nb)]
+    off = np.concatenate([[0], np.cumsum(sizes)]).astype(np.int64)
+    D = int(off[-1])
+    if D == 0:
+        sizes[0] = 1
+        off = np.concatenate([[0], np.cumsum(sizes)]).astype(np.int64)
+        D = 1
+    bits = int(rng.integers(12, 17))
+    n_steps = int(rng.integers(1, 4))
+    rho = float(rng.choice([1.0, 0.7, 1.3]))
+    seed = int(rng.integers(-2 ** 31, 2 ** 31 - 1))
+    tl, ts, pl, ps = _heavy_inputs(rng, D)
+    i0, s0 = _csr_encode(cwq, cwqlib, tl, ts, pl, ps, off, bits, n_steps, seed, rho, 0)
+    i2, s2 = _csr_encode(cwq, cwqlib, tl, ts, pl, ps, off, bits, n_steps, seed, rho, 2)
+    assert np.array_equal(i2, i0), (trial, sizes, bits, n_steps)
+    _assert_bits_equal(s2, s0, f"csr stress trial {trial}")
+
+
+@pytest.mark.parametrize("d,bits,nb", [(5, 13, 7), (12, 12, 4), (100, 14, 2), (72, 12, 3)])
+def test_uniform_odd_d_general_pruned(cwq, cwqlib, oracle, d, bits, nb):
+    rng = np.random.default_rng(d * bits)
+    tl, ts, pl, ps = _heavy_inputs(rng, nb * d)
+    off = np.arange(nb + 1, dtype=np.int64) * d
+    wi, ws = oracle.greedy_encode(tl, ts, pl, ps, off, bits, 2, 11)
+    for mode in (0, 2):
+        gi, gs = _uniform_encode(cwq, cwqlib, tl, ts, pl, ps, d, bits, 2, 11, 1.0, mode)
+        assert np.array_equal(gi, wi), (d, mode)
+        _assert_bits_equal(gs, ws, f"uniform d={d} mode {mode}")

@@ -10,6 +10,8 @@ declare -A V=(
   [base]=""
   [stats]="-DCWQ_PRUNE_STATS"
   [phases]="-DCWQ_PHASE_TIMES"
+  [gshare]="-DCWQ_CSR_GTAU_SHARE=1"
+  [mask63]="-DCWQ_TAU_SHARE_MASK=63u"
 )
 if [ "$1" = build ]; then
   mkdir -p $OUT
@@ -23,6 +25,6 @@ else
     [ "$k" = stats ] && continue  # counters only: tools/prune_stats.py
     [ "$k" = phases ] && continue  # host phase timings only
     echo "== $k ${V[$k]}"
-    CWQ_LIB_PATH=$PWD/$OUT/libcwq_$k.so timeout -k 10 300 python -u bench.py --no-cpu --no-e2e --steps 2 --warmup 1 $BENCH_ARGS | python -c "import json,sys; d=json.loads(sys.stdin.read()); print(d['value'], d['roofline']['kernel_ms'])"
+    CWQ_LIB_PATH=$PWD/$OUT/libcwq_$k.so timeout -k 10 300 python -u bench.py --no-cpu --no-e2e --steps 2 --warmup 1 $BENCH_ARGS | python -c "import json,sys; d=json.loads(sys.stdin.read()); print(d['value'], d['ms_per_step'], d.get('roofline', {}).get('kernel_ms'))"
   done
 fi
