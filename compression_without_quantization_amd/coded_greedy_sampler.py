@@ -137,7 +137,7 @@ def encode_blocks(t_loc, t_scale, p_loc, p_scale, n_bits_per_step, n_steps, seed
         out_sample = torch.empty(D, dtype=torch.float32, device=dev)
     need = encode_workspace_bytes(nb, D)
     if offs is not None:  # room for the general pruned kernel's arrays (cwq.h)
-        need += 12 * D + 24 * nb + 1024
+        need += 16 * D + 192 * nb + 2048
     if workspace is None or workspace.numel() < need:
         workspace = torch.empty(max(need, 1), dtype=torch.uint8, device=dev)
     stream = torch.cuda.current_stream(dev).cuda_stream

@@ -45,13 +45,13 @@ int hip_fail(hipError_t e, const char* where) {
 size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
 
 struct WsLayout {
-  size_t keys, loc_s, scale_s, lognorm, sab, bpre, grp, gtau, total;
+  size_t keys, loc_s, scale_s, lognorm, sab, bpre, ordu, grp, gtau, total;
   bool csr;  // has the general pruned kernel's arrays
 };
 
 // Blocks the uniform fast pruned kernel takes (d % 8 == 0, 8 <= d <= 64) need
 // only keys + the per-dim shard constants; everything else (CSR, other d) also
-// gets the general pruned kernel's screening constants (12 B/dim + 24 B/block).
+// gets the general pruned kernel's screening constants (16 B/dim + 180 B/block).
 bool ws_needs_csr(int64_t nb, int64_t total_dims) {
   if (nb <= 0) return false;
   if (total_dims % nb) return true;
@@ -71,12 +71,14 @@ WsLayout ws_layout(int64_t nb, int64_t total_dims, bool csr) {
   l.lognorm = o;
   o = align_up(o + (size_t)total_dims * 4, 256);
   l.csr = csr;
-  l.sab = l.bpre = l.grp = l.gtau = o;
+  l.sab = l.bpre = l.ordu = l.grp = l.gtau = o;
   if (csr) {
     l.sab = o;
-    o = align_up(o + (size_t)total_dims * 8, 256);
+    o = align_up(o + (size_t)(total_dims + 8 * nb) * 8, 256);
     l.bpre = o;
-    o = align_up(o + (size_t)(total_dims + nb) * 4, 256);
+    o = align_up(o + (size_t)(total_dims + 12 * nb) * 4, 256);
+    l.ordu = o;
+    o = align_up(o + (size_t)(total_dims + 12 * nb) * 4, 256);
     l.grp = o;
     o = align_up(o + (size_t)nb * 16, 256);
     l.gtau = o;
@@ -339,6 +341,7 @@ int encode_impl(const float* t_loc, const float* t_scale, const float* p_loc,
   a.lognorm = (float*)(w + l.lognorm);
   a.sab = l.csr ? (float2*)(w + l.sab) : nullptr;
   a.bpre = l.csr ? (float*)(w + l.bpre) : nullptr;
+  a.ordu = l.csr ? (uint32_t*)(w + l.ordu) : nullptr;
   a.grp = l.csr ? (float4*)(w + l.grp) : nullptr;
   a.gtau = l.csr ? (uint32_t*)(w + l.gtau) : nullptr;
   a.ev_start = g_ev_start;

@@ -34,8 +34,9 @@ struct EncodeArgs {
   float* lognorm;            // [total_dims]
   // screening constants of the general pruned kernel (k_encode_prune_csr);
   // nullptr when the workspace was sized without them
-  float2* sab;               // [total_dims] (sA, sB)
-  float* bpre;               // [total_dims + nb] drop-test constants B_j, j = 0..d per block
+  float2* sab;               // [total_dims + 8 nb] (sA, sB), 4 zero pads either side per block
+  float* bpre;               // [total_dims + 12 nb] drop bounds per visit position (k_csr_prep)
+  uint32_t* ordu;            // [total_dims + 12 nb] unit visited at each position
   float4* grp;               // [nb] (c1, c2, As, Pq); c1 == 0: block not screened
   uint32_t* gtau;            // [nb] per-block shared threshold (ord)
   // optional profiling events around the eval launches (hipEvent_t)

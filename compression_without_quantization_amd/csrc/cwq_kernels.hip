@@ -604,15 +604,28 @@ __device__ __forceinline__ double block_sum_d(double v, double* red) {
   return r;
 }
 
+// Visit order.  A row starting at flat normal k0 = n*d has alignment class
+// c = k0 & 3; its Philox blocks ("units") u = 0..U_c-1, U_c = (d + c + 3) / 4,
+// hold dims 4u - c + t (t = word 0..3, kept if 0 <= dim < d).  Per block and
+// class, k_csr_prep sorts the units by expected a^2 (most informative first,
+// so rows cross tau early) and stores for visit position k the unit ord[k] and
+// the drop bound bpre[k] (units visited before position k).  Region of block g:
+// off + 12 g, class c at c * csr_cls_stride(d), csr_cls_stride(d) =
+// (d + 6) / 4 + 1 >= U_c + 1; 4 strides <= d + 10 entries.
+__host__ __device__ __forceinline__ int64_t csr_cls_stride(int64_t d) { return (d + 6) / 4 + 1; }
+constexpr int64_t kCsrSortUnits = 512;  // sorted if U_3 <= this (d <= 2045); else natural order
+
 template <bool STEP0>
 __global__ void __launch_bounds__(256) k_csr_prep(
     const float* __restrict__ t_loc, const float* __restrict__ t_scale,
     const float* __restrict__ loc_s, const float* __restrict__ scale_s,
     const float* __restrict__ lognorm, const float* __restrict__ best,
     const int64_t* __restrict__ block_off, int64_t ud, int64_t nb, float2* __restrict__ sab,
-    float* __restrict__ bpre, float4* __restrict__ grp, uint32_t* __restrict__ gtau) {
+    float* __restrict__ bpre, uint32_t* __restrict__ ordu, float4* __restrict__ grp,
+    uint32_t* __restrict__ gtau) {
   __shared__ double red[256];
   __shared__ double scan[256];
+  __shared__ unsigned long long skey[kCsrSortUnits];
   const int tid = threadIdx.x;
   for (int64_t g = blockIdx.x; g < nb; g += gridDim.x) {
     const BlockSpan sp = block_span(block_off, ud, g);
@@ -623,9 +636,14 @@ __global__ void __launch_bounds__(256) k_csr_prep(
     };
     double sm = 0.0, sa = 0.0, sk = 0.0, s2 = 0.0, mx = 0.0;
     int ok = 1;
+    float2* sabg = sab + off + 8 * g + 4;  // 4 zero pads either side (partial units)
+    if (tid < 4) {
+      sabg[tid - 4] = float2{0.f, 0.f};
+      sabg[d + tid] = float2{0.f, 0.f};
+    }
     for (int64_t j = tid; j < d; j += 256) {
       const CsrDim o = dim(j);
-      sab[off + j] = float2{o.sa, o.sb};
+      sabg[j] = float2{o.sa, o.sb};
       sm += o.M;
       sa += __builtin_fabs(o.M);
       sk += __builtin_fabs(o.M) + o.M;
@@ -646,23 +664,79 @@ __global__ void __launch_bounds__(256) k_csr_prep(
     __syncthreads();
     const double gam = 1.01 * (double)(d + 1) * 0x1p-24;
     const double sl = (3.0 * gam + 0x1p-14) * (__builtin_fabs(SM) + SA + SK) + 0x1p-126;
-    // B_j = sum M + (sum of C over the first j dims) + slack, j = 0..d
-    double carry = 0.0;
-    for (int64_t base = 0; base <= d; base += 256) {
-      const int64_t j = base + tid;
-      const double cj = (all_ok && j < d) ? (double)dim(j).C : 0.0;
-      scan[tid] = cj;
-      __syncthreads();
-      for (int w = 1; w < 256; w <<= 1) {  // inclusive scan
-        const double v = tid >= w ? scan[tid - w] : 0.0;
+    const int64_t reg = off + 12 * g, cs = csr_cls_stride(d);
+    // unit u of class c: its sum of C_j and its expected sum of a_j^2 - C_j
+    auto unit = [&](int c, int64_t u, double& csum, double& gain) {
+      csum = 0.0;
+      gain = 0.0;
+      for (int t = 0; t < 4; ++t) {
+        const int64_t j = 4 * u - c + t;
+        if (j >= 0 && j < d) {
+          const CsrDim o = dim(j);
+          csum += (double)o.C;
+          gain += (double)o.sa * (double)o.sa * (0.5 / 0.6931471805599453) +
+                  (double)o.sb * (double)o.sb - (double)o.C;
+        }
+      }
+    };
+    for (int c = 0; c < 4; ++c) {
+      const int64_t U = (d + c + 3) / 4;
+      const bool sorted = all_ok && U <= kCsrSortUnits;
+      if (sorted) {  // bitonic sort of (gain desc, u asc) keys
+        int64_t P = 1;
+        while (P < U) P <<= 1;
+        for (int64_t u = tid; u < P; u += 256) {
+          unsigned long long key = 0ull;
+          if (u < U) {
+            double cu, gu;
+            unit(c, u, cu, gu);
+            const float gf = (float)(gu > 0.0 ? gu : 0.0);
+            key = ((unsigned long long)ord_f32(gf) << 32) | (0xffffffffull - (uint64_t)u);
+          }
+          skey[u] = key;
+        }
         __syncthreads();
-        scan[tid] += v;
+        for (int64_t k = 2; k <= P; k <<= 1) {
+          for (int64_t jj = k >> 1; jj > 0; jj >>= 1) {
+            for (int64_t i = tid; i < P; i += 256) {
+              const int64_t l = i ^ jj;
+              if (l > i) {
+                const unsigned long long a = skey[i], b = skey[l];
+                const bool desc = (i & k) == 0;  // overall descending
+                if (desc ? (a < b) : (a > b)) {
+                  skey[i] = b;
+                  skey[l] = a;
+                }
+              }
+            }
+            __syncthreads();
+          }
+        }
+      }
+      // drop bounds along the visit order, positions k = 0..U
+      double carry = 0.0;
+      for (int64_t base = 0; base <= U; base += 256) {
+        const int64_t k = base + tid;
+        int64_t u = k;
+        if (sorted && k < U) u = (int64_t)(0xffffffffull - (skey[k] & 0xffffffffull));
+        double cu = 0.0, gu;
+        if (all_ok && k < U) unit(c, u, cu, gu);
+        scan[tid] = cu;
+        __syncthreads();
+        for (int w = 1; w < 256; w <<= 1) {  // inclusive scan
+          const double v = tid >= w ? scan[tid - w] : 0.0;
+          __syncthreads();
+          scan[tid] += v;
+          __syncthreads();
+        }
+        const double excl = carry + scan[tid] - cu;
+        if (k <= U) {
+          bpre[reg + c * cs + k] = round_up_f32(SM + excl * (1.0 + 0x1p-20) + sl);
+          ordu[reg + c * cs + k] = (uint32_t)(k < U ? u : 0);
+        }
+        carry += scan[255];
         __syncthreads();
       }
-      const double excl = carry + scan[tid] - cj;
-      if (j <= d) bpre[off + g + j] = round_up_f32(SM + excl * (1.0 + 0x1p-20) + sl);
-      carry += scan[255];
-      __syncthreads();
     }
     if (tid == 0) {
       const float c1 = round_dn_f32(1.0 - 3.0 * gam - 0x1p-22);
@@ -750,16 +824,17 @@ __global__ void __launch_bounds__(256, 6) k_encode_prune_csr(
     const int64_t* __restrict__ block_off, int64_t ud, int64_t ntiles, int64_t tiles_per_block,
     int64_t cand_per_tile, int64_t n_cand, int32_t seed, int64_t block_id_base, int32_t step,
     const float2* __restrict__ sab, const float* __restrict__ bpre,
-    const float4* __restrict__ grp, uint32_t* __restrict__ gtau,
-    unsigned long long* __restrict__ keys) {
+    const uint32_t* __restrict__ ordu, const float4* __restrict__ grp,
+    uint32_t* __restrict__ gtau, unsigned long long* __restrict__ keys) {
   __shared__ double logtab[32];
   __shared__ uint32_t tau_ord;
   __shared__ uint32_t sq_cnt;
   __shared__ uint32_t sq_n[CWQ_CSR_SURVIVOR_CAP];
   __shared__ float sq_ub[CWQ_CSR_SURVIVOR_CAP];
   __shared__ unsigned long long wkey[4];
-  __shared__ float2 l_ab[CWQ_CSR_LDS_DIMS];
-  __shared__ float l_bp[CWQ_CSR_LDS_DIMS + 1];
+  __shared__ float2 l_ab[CWQ_CSR_LDS_DIMS + 8];
+  __shared__ float l_bp[CWQ_CSR_LDS_DIMS + 12];
+  __shared__ uint32_t l_ord[CWQ_CSR_LDS_DIMS + 12];
   __shared__ float rowbuf[4][kRowChunk];
   fill_logtab(logtab);
   const uint32_t wv = wave_id();
@@ -768,8 +843,12 @@ __global__ void __launch_bounds__(256, 6) k_encode_prune_csr(
   for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
     uint32_t tid = threadIdx.x;
     asm volatile("" : "+v"(tid));
-    const int64_t g = tile / tiles_per_block;
-    const int64_t tt = tile - g * tiles_per_block;
+    // tile-major order: a block's later tiles start after its first ones have
+    // published their threshold in gtau (the loop shares tau inside the
+    // workgroup only: per-iteration global atomics cost more than they prune)
+    const int64_t nbk = ntiles / tiles_per_block;
+    const int64_t tt = tile / nbk;
+    const int64_t g = tile - tt * nbk;
     const BlockSpan sp = block_span(block_off, ud, g);
     const int64_t off = sp.off, d = sp.d;
     const int64_t n0 = tt * cand_per_tile;
@@ -778,10 +857,12 @@ __global__ void __launch_bounds__(256, 6) k_encode_prune_csr(
         generate_key(step_seed(block_seed(seed, block_id_base + g), step), 42);
     const float4 gc = grp[g];
     const bool in_lds = d <= CWQ_CSR_LDS_DIMS;
+    const int64_t reg = off + 12 * g, cs = csr_cls_stride(d);
     if (gc.x != 0.0f && in_lds) {
-      for (int64_t j = tid; j <= d; j += blockDim.x) {
-        if (j < d) l_ab[j] = sab[off + j];
-        l_bp[j] = bpre[off + g + j];
+      for (int64_t j = tid; j < d + 8; j += blockDim.x) l_ab[j] = sab[off + 8 * g + j];
+      for (int64_t j = tid; j < 4 * cs; j += blockDim.x) {
+        l_bp[j] = bpre[reg + j];
+        l_ord[j] = ordu[reg + j];
       }
     }
     if (tid == 0) {
@@ -798,36 +879,57 @@ __global__ void __launch_bounds__(256, 6) k_encode_prune_csr(
       const int64_t per_wave = (n1 - n0 + 3) / 4;
       const int64_t w0 = n0 + (int64_t)wv * per_wave;
       const int64_t w1 = (w0 + per_wave < n1) ? w0 + per_wave : n1;
-      auto run = [&](const float2* ab, const float* bj) __attribute__((always_inline)) {
-        int64_t wnext = w0 + 64;
-        int64_t n = w0 + lane;
-        bool active = n < w1;
-        int64_t j = 0;
+      // lane state: row n0 + r (class c, first Philox block rb, U units), visit
+      // position k.  ab is the padded constant array: entry 4 + j for dim j,
+      // zeros for the out-of-row words of a row's first and last unit.
+      const uint32_t r0 = (uint32_t)(w0 - n0), r1 = (uint32_t)(w1 - n0);
+      const int d32 = (int)d;
+      auto run = [&](const float2* ab, const float* bp, const uint32_t* od)
+                     __attribute__((always_inline)) {
+        uint32_t wnext = r0 + 64u;
+        uint32_t r = r0 + lane;
+        bool active = r < r1;
         float s = 0.0f;
         float tau = unord_f32(tau_ord);
         uint32_t iter = 0;
+        uint64_t rb;
+        int c, U, cb;
+        auto start_row = [&]() __attribute__((always_inline)) {
+          const uint64_t k0 = (uint64_t)(n0 + (int64_t)r) * (uint64_t)d;
+          rb = k0 >> 2;
+          c = (int)(k0 & 3u);
+          U = (d32 + c + 3) >> 2;
+          cb = c * (int)cs;
+        };
+        start_row();
+        int k = 0;
         while (__ballot(active) != 0ull) {
-          const uint64_t k = (uint64_t)n * (uint64_t)d + (uint64_t)j;
-          const F4 z = normal4_screen(st, k >> 2);
-          const int wa = (int)(k & 3u);
-          const int64_t left = d - j;
-          const int cnt = (int64_t)(4 - wa) < left ? 4 - wa : (int)left;
-#pragma unroll
-          for (int t = 0; t < 4; ++t) {
-            if (t < cnt) {
-              const int w = wa + t;
-              const float zz = w == 0 ? z.a : (w == 1 ? z.b : (w == 2 ? z.c : z.d));
-              const float2 c = ab[j + t];
-              const float a = __builtin_fmaf(c.x, zz, c.y);
-              s = __builtin_fmaf(-a, a, s);
-            }
-          }
-          j += cnt;
+          const uint32_t u = od[cb + k];
+          // round keys recomputed in SALU each iteration (opaque key): keeping
+          // all 20 live costs SGPRs the loop then spills into VGPR lanes
+          uint32_t kk0 = st.k0, kk1 = st.k1;
+          asm volatile("" : "+s"(kk0), "+s"(kk1));
+          const uint64_t blk = rb + u;
+          const U4 x = philox10_dev((uint32_t)blk, (uint32_t)(blk >> 32), st.c2, st.c3, kk0, kk1);
+          F4 z;
+          box_muller_screen(x.x, x.y, z.a, z.b);
+          box_muller_screen(x.z, x.w, z.c, z.d);
+          const int jp = 4 * (int)u - c + 4;  // padded index of word 0
+          const float2 e0 = ab[jp], e1 = ab[jp + 1], e2 = ab[jp + 2], e3 = ab[jp + 3];
+          const float a0 = __builtin_fmaf(e0.x, z.a, e0.y);
+          const float a1 = __builtin_fmaf(e1.x, z.b, e1.y);
+          const float a2 = __builtin_fmaf(e2.x, z.c, e2.y);
+          const float a3 = __builtin_fmaf(e3.x, z.d, e3.y);
+          s = __builtin_fmaf(-a0, a0, s);
+          s = __builtin_fmaf(-a1, a1, s);
+          s = __builtin_fmaf(-a2, a2, s);
+          s = __builtin_fmaf(-a3, a3, s);
+          k += 1;
 #ifdef CWQ_PRUNE_STATS
-          if (active) atomicAdd(&g_prune_stats[43], (unsigned long long)cnt);
+          if (active) atomicAdd(&g_prune_stats[43], 1ull);
 #endif
-          const bool complete = (j == d);
-          const float upper = __builtin_fmaf(s, gc.x, bj[j]);
+          const bool complete = k == U;
+          const float upper = __builtin_fmaf(s, gc.x, bp[cb + k]);
           const bool prune = !complete && (upper < tau);
           if (complete && active && upper >= tau) {  // may be the best: keep it
             const float lower =
@@ -835,12 +937,13 @@ __global__ void __launch_bounds__(256, 6) k_encode_prune_csr(
             tau = fmaxf(tau, lower);
             const uint32_t slot = atomicAdd(&sq_cnt, 1u);
             if (slot < CWQ_CSR_SURVIVOR_CAP) {
-              sq_n[slot] = (uint32_t)(n - n0);
+              sq_n[slot] = r;
               sq_ub[slot] = upper;
             } else {  // list full: evaluate exactly now
 #ifdef CWQ_PRUNE_STATS
               atomicAdd(&g_prune_stats[46], 1ull);
 #endif
+              const int64_t n = n0 + (int64_t)r;
               const float v = eval_row<0, STEP0>(
                   st, (uint64_t)n * (uint64_t)d, d, (int)(((uint64_t)n * d) & 3u), loc_s + off,
                   scale_s + off, t_loc + off, t_scale + off, lognorm + off,
@@ -860,12 +963,13 @@ __global__ void __launch_bounds__(256, 6) k_encode_prune_csr(
           const uint32_t rank = __builtin_amdgcn_mbcnt_hi(
               (uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
           if (done) {
-            n = wnext + rank;
-            j = 0;
+            r = wnext + rank;
+            start_row();
+            k = 0;
             s = 0.0f;
           }
-          wnext += (int64_t)__builtin_popcountll(m);
-          active = n < w1;
+          wnext += (uint32_t)__builtin_popcountll(m);
+          active = r < r1;
           if (((++iter) & CWQ_TAU_SHARE_MASK) == 0u) {  // share with the workgroup
             const float tm = wave_max_f32(tau);
             if (lane == 0) atomicMax(&tau_ord, ord_f32(tm));
@@ -883,9 +987,9 @@ __global__ void __launch_bounds__(256, 6) k_encode_prune_csr(
         if (lane == 0) atomicMax(&tau_ord, ord_f32(tm));
       };
       if (in_lds)
-        run(l_ab, l_bp);
+        run(l_ab, l_bp, l_ord);
       else
-        run(sab + off, bpre + off + g);
+        run(sab + off + 8 * g, bpre + reg, ordu + reg);
       __syncthreads();
       if (tid == 0) {
         const uint32_t mine = tau_ord;
@@ -1183,7 +1287,7 @@ template <bool STEP0>
 static void launch_prune_csr(const EncodeArgs& a, int step, hipStream_t stream) {
   hipLaunchKernelGGL((k_csr_prep<STEP0>), dim3(grid_for(a.nb, 1, 65536)), dim3(256), 0, stream,
                      a.t_loc, a.t_scale, a.loc_s, a.scale_s, a.lognorm, a.out_sample,
-                     a.block_off, a.ud, a.nb, a.sab, a.bpre, a.grp, a.gtau);
+                     a.block_off, a.ud, a.nb, a.sab, a.bpre, a.ordu, a.grp, a.gtau);
   // own tiling: ~8192 tiles of >= 1024 candidates; tiles of a block share tau
   // through gtau, and later tiles start from it
   int64_t tpb = (8192 + a.nb - 1) / a.nb;
@@ -1196,8 +1300,8 @@ static void launch_prune_csr(const EncodeArgs& a, int step, hipStream_t stream) 
   hipLaunchKernelGGL((k_encode_prune_csr<STEP0>), dim3(grid), dim3(256), 0, stream, a.t_loc,
                      a.t_scale, a.loc_s, a.scale_s, a.lognorm, a.out_sample, a.block_off, a.ud,
                      ntiles, tpb, cpt, a.n_cand, a.seed, a.block_id_base, step,
-                     (const float2*)a.sab, (const float*)a.bpre, (const float4*)a.grp, a.gtau,
-                     a.keys);
+                     (const float2*)a.sab, (const float*)a.bpre, (const uint32_t*)a.ordu,
+                     (const float4*)a.grp, a.gtau, a.keys);
 }
 
 template <bool STEP0>

@@ -74,9 +74,9 @@ int cwq_stateless_normal_sample(const float* loc, const float* scale, int64_t d,
 /* Workspace bytes needed by cwq_greedy_encode / cwq_greedy_encode_uniform for
  * nb blocks holding total_dims dims in all.  Unless every block has the same d
  * with d % 8 == 0 and 8 <= d <= 64 (the fast pruned kernel), this includes the
- * general pruned kernel's per-step constants (12 B/dim + 24 B/block).  A CSR
+ * general pruned kernel's per-step constants (16 B/dim + 180 B/block).  A CSR
  * call whose sizes happen to look like that uniform case may pass
- * 12 * total_dims + 24 * nb + 1024 more bytes to run the general pruned kernel;
+ * 16 * total_dims + 192 * nb + 2048 more bytes to run the general pruned kernel;
  * with exactly the returned size it runs unpruned. */
 size_t cwq_greedy_encode_workspace_size(int64_t nb, int64_t total_dims);
 
