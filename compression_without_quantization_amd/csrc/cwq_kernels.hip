@@ -875,7 +875,8 @@ __global__ void __launch_bounds__(256, 6) k_encode_prune_csr(
 #ifdef CWQ_PRUNE_STATS
     if (tid == 0) atomicAdd(&g_prune_stats[gc.x != 0.0f ? 40 : 41], 1ull);
 #endif
-    if (gc.x != 0.0f) {
+    bool exact_tile = gc.x == 0.0f;
+    if (!exact_tile) {
       const int64_t per_wave = (n1 - n0 + 3) / 4;
       const int64_t w0 = n0 + (int64_t)wv * per_wave;
       const int64_t w1 = (w0 + per_wave < n1) ? w0 + per_wave : n1;
@@ -936,20 +937,9 @@ __global__ void __launch_bounds__(256, 6) k_encode_prune_csr(
                 __builtin_fmaf(s, gc.y, gc.z) - gc.w * __builtin_amdgcn_sqrtf(-s);
             tau = fmaxf(tau, lower);
             const uint32_t slot = atomicAdd(&sq_cnt, 1u);
-            if (slot < CWQ_CSR_SURVIVOR_CAP) {
+            if (slot < CWQ_CSR_SURVIVOR_CAP) {  // else: overflow, the tile is redone
               sq_n[slot] = r;
               sq_ub[slot] = upper;
-            } else {  // list full: evaluate exactly now
-#ifdef CWQ_PRUNE_STATS
-              atomicAdd(&g_prune_stats[46], 1ull);
-#endif
-              const int64_t n = n0 + (int64_t)r;
-              const float v = eval_row<0, STEP0>(
-                  st, (uint64_t)n * (uint64_t)d, d, (int)(((uint64_t)n * d) & 3u), loc_s + off,
-                  scale_s + off, t_loc + off, t_scale + off, lognorm + off,
-                  STEP0 ? nullptr : best + off, logtab);
-              const uint64_t kv = argmax_key(v, (uint32_t)n);
-              bestk = kv > bestk ? kv : bestk;
             }
           }
           const bool done = complete || prune || !active;
@@ -986,17 +976,34 @@ __global__ void __launch_bounds__(256, 6) k_encode_prune_csr(
         const float tm = wave_max_f32(tau);
         if (lane == 0) atomicMax(&tau_ord, ord_f32(tm));
       };
-      if (in_lds)
-        run(l_ab, l_bp, l_ord);
-      else
-        run(sab + off + 8 * g, bpre + reg, ordu + reg);
-      __syncthreads();
-      if (tid == 0) {
-        const uint32_t mine = tau_ord;
-        const uint32_t prev = atomicMax(&gtau[g], mine);
-        tau_ord = prev > mine ? prev : mine;
+      // survivor list overflow (near-ties everywhere, or a weak early tau):
+      // redo the pass starting from the final tau, then score exactly
+      for (int pass = 0;; ++pass) {
+        if (in_lds)
+          run(l_ab, l_bp, l_ord);
+        else
+          run(sab + off + 8 * g, bpre + reg, ordu + reg);
+        __syncthreads();
+        if (tid == 0) {
+          const uint32_t mine = tau_ord;
+          const uint32_t prev = atomicMax(&gtau[g], mine);
+          tau_ord = prev > mine ? prev : mine;
+        }
+        __syncthreads();
+        if (sq_cnt <= CWQ_CSR_SURVIVOR_CAP) break;
+#ifdef CWQ_PRUNE_STATS
+        if (tid == 0) atomicAdd(&g_prune_stats[46], 1ull);
+#endif
+        if (pass == 1) {
+          exact_tile = true;
+          break;
+        }
+        __syncthreads();
+        if (tid == 0) sq_cnt = 0u;
+        __syncthreads();
       }
-      __syncthreads();
+    }
+    if (!exact_tile) {
       const float tau_final = unord_f32(tau_ord);
       const uint32_t nsurv = sq_cnt < CWQ_CSR_SURVIVOR_CAP ? sq_cnt : CWQ_CSR_SURVIVOR_CAP;
       for (uint32_t i = wv; i < nsurv; i += 4) {  // one survivor per wave

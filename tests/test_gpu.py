@@ -642,7 +642,7 @@ def test_csr_pruned_vs_oracle(cwq, cwqlib, oracle, sizes, bits, n_steps, rho):
         _assert_bits_equal(gs, ws, f"csr mode {mode}")
 
 
-@pytest.mark.parametrize("kind", ["far_locs", "huge_locs", "tiny_locs"])
+@pytest.mark.parametrize("kind", ["far_locs", "huge_locs", "tiny_locs", "flat"])
 def test_csr_pruned_adversarial(cwq, cwqlib, oracle, kind):
     rng = np.random.default_rng(7)
     sizes = [3, 20, 1, 45]
@@ -656,9 +656,12 @@ def test_csr_pruned_adversarial(cwq, cwqlib, oracle, kind):
     elif kind == "huge_locs":
         tl = (rng.standard_normal(D) * 1e30).astype(np.float32)
         pl = (rng.standard_normal(D) * 1e30).astype(np.float32)
-    else:
+    elif kind == "tiny_locs":
         ts = (rng.uniform(0.3, 1.0, D) * 1e-20).astype(np.float32)
         tl = (rng.standard_normal(D) * 1e-20).astype(np.float32)
+    else:  # near-ties everywhere: the survivor list overflows, tiles are redone
+        ts = np.full(D, 1e3, np.float32)
+        tl = np.zeros(D, np.float32)
     wi, ws = oracle.greedy_encode(tl, ts, pl, ps, off, 12, 1, 5)
     for mode in (0, 2):
         gi, gs = _csr_encode(cwq, cwqlib, tl, ts, pl, ps, off, 12, 1, 5, 1.0, mode)
