@@ -812,6 +812,9 @@ __device__ __forceinline__ float exact_row_wave(
 #ifndef CWQ_CSR_GTAU_SHARE
 #define CWQ_CSR_GTAU_SHARE 0  // 1: also share tau with the block's other tiles in the loop
 #endif
+#ifndef CWQ_CSR_GTAU_MASK
+#define CWQ_CSR_GTAU_MASK 15u  // ... every CWQ_CSR_GTAU_MASK + 1 iterations
+#endif
 #ifndef CWQ_CSR_SURVIVOR_CAP
 #define CWQ_CSR_SURVIVOR_CAP 512
 #endif
@@ -965,10 +968,12 @@ __global__ void __launch_bounds__(256, 6) k_encode_prune_csr(
             if (lane == 0) atomicMax(&tau_ord, ord_f32(tm));
             uint32_t o = __atomic_load_n(&tau_ord, __ATOMIC_RELAXED);
 #if CWQ_CSR_GTAU_SHARE
-            if (lane == 0) atomicMax(&gtau[g], ord_f32(tm));
-            const uint32_t o2 = __hip_atomic_load(&gtau[g], __ATOMIC_RELAXED,
-                                                  __HIP_MEMORY_SCOPE_AGENT);
-            o = o > o2 ? o : o2;
+            if ((iter & CWQ_CSR_GTAU_MASK) == 0u) {
+              if (lane == 0) atomicMax(&gtau[g], ord_f32(tm));
+              const uint32_t o2 = __hip_atomic_load(&gtau[g], __ATOMIC_RELAXED,
+                                                    __HIP_MEMORY_SCOPE_AGENT);
+              o = o > o2 ? o : o2;
+            }
 #endif
             tau = fmaxf(tau, unord_f32(o));
           }

@@ -10,8 +10,9 @@ declare -A V=(
   [base]=""
   [stats]="-DCWQ_PRUNE_STATS"
   [phases]="-DCWQ_PHASE_TIMES"
-  [gshare]="-DCWQ_CSR_GTAU_SHARE=1"
-  [mask63]="-DCWQ_TAU_SHARE_MASK=63u"
+  [g255]="-DCWQ_CSR_GTAU_SHARE=1 -DCWQ_CSR_GTAU_MASK=255u"
+  [g1023]="-DCWQ_CSR_GTAU_SHARE=1 -DCWQ_CSR_GTAU_MASK=1023u"
+  [mask7]="-DCWQ_TAU_SHARE_MASK=7u"
 )
 if [ "$1" = build ]; then
   mkdir -p $OUT
