@@ -52,6 +52,13 @@ IMPORTANCE = {
            "I2: 24 images' PLN level-2 latents (2,304 dims each), grouped importance coder, "
            "20 bits/group, groups <= 3 dims (miracle_arguments.py:168-174)"),
 }
+PLN = {
+    # name: (images, H, W, level-1 coder, description)
+    "pln": (1, 512, 768, "greedy",
+            "PLN image codec: one 512x768 image, both levels (level 2 importance 20 bits/group, "
+            "level 1 greedy 30 x 14 bits), group sizes arithmetic-coded, .miracle file "
+            "(miracle.py compress/decompress defaults, miracle_arguments.py:146-189)"),
+}
 CONFIGS = {
     # name: (blocks per GPU, block dim, kl bits, n_steps, description)
     "c4": (1_000_000, 32, 16, 1, "C4: 1e6 blocks x d=32, KL=16 bits (2^16 candidates/block)"),
@@ -68,7 +75,7 @@ def parse():
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", default="c4",
-                    choices=sorted(CONFIGS) + sorted(GROUPED) + sorted(IMPORTANCE))
+                    choices=sorted(CONFIGS) + sorted(GROUPED) + sorted(IMPORTANCE) + sorted(PLN))
     ap.add_argument("--blocks", type=int, default=0, help="override blocks per GPU")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu", action="store_true")
@@ -167,6 +174,74 @@ def importance_main(args):
     print(json.dumps(line), flush=True)
 
 
+def pln_main(args):
+    """The PLN image codec end to end (pln.py:213-817): transforms (MIOpen),
+    latent plumbing (HIP), both coders, the group-size arithmetic coder and
+    the .miracle file, then the decoder.  Seeded random weights (no trained
+    checkpoint offline) on a synthetic image."""
+    import tempfile
+    import compression_without_quantization_amd.coded_greedy_sampler as S
+    import compression_without_quantization_amd.coded_importance_sampler as I
+    from compression_without_quantization_amd import pln as P
+    S.VERBOSE = I.VERBOSE = False
+    n_img, H, W, level1, desc = PLN[args.config]
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    torch.backends.cudnn.benchmark = False
+    torch.backends.cudnn.deterministic = True
+    model = P.ProbabilisticLadderNetwork().to(dev).eval()
+    rng = np.random.default_rng(0)
+    yy, xx = np.mgrid[0:H, 0:W] / max(H, W)
+    imgs = []
+    for i in range(n_img):
+        base = np.stack([np.sin((6 + i) * xx + c) * np.cos(4 * yy - c) for c in range(3)], -1)
+        imgs.append(np.clip(0.5 + 0.35 * base + 0.05 * rng.standard_normal((H, W, 3)), 0, 1)
+                    .astype(np.float32)[None])
+    kw = dict(n_steps=30, n_bits_per_step=14, greedy_max_group_size_bits=12,
+              use_importance_sampling=(level1 == "importance"),
+              second_level_n_bits_per_group=20, second_level_max_group_size_bits=2,
+              second_level_dim_kl_bit_limit=16, first_level_n_bits_per_group=20,
+              first_level_max_group_size_bits=4, first_level_dim_kl_bit_limit=16)
+    tmp = tempfile.mkdtemp()
+    paths = [os.path.join(tmp, f"img{i}.miracle") for i in range(n_img)]
+
+    def compress():
+        return [model.code_image_greedy(None, im, 42, comp_file_path=p, **kw)[1]
+                for im, p in zip(imgs, paths)]
+
+    def decompress():
+        return [model.decode_image_greedy(None, p, use_importance_sampling=kw[
+            "use_importance_sampling"], second_level_max_group_size_bits=2,
+            first_level_max_group_size_bits=4) for p in paths]
+    for _ in range(args.warmup):
+        compress()
+        decompress()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        summ = compress()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        rec = decompress()
+    torch.cuda.synchronize()
+    eld = time.perf_counter() - t0
+    line = {"metric": "images compressed/s (PLN codec, miracle.py compress)",
+            "value": n_img * args.steps / el, "unit": "images/s", "n_gpus": 1,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": el / args.steps * 1e3,
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+            "data": "synthetic image, seeded random PLN weights (no checkpoint offline)",
+            "config": {"workload": desc, "decompress_images_per_s": n_img * args.steps / eld,
+                       "bytes": summ[0]["actual_byte_size"], "bpp": summ[0]["bpp"],
+                       "kl_bits_level1": summ[0]["first_level_theoretical"] * 8,
+                       "kl_bits_level2": summ[0]["second_level_theoretical"] * 8,
+                       "groups_level1": summ[0]["first_level_groups"],
+                       "groups_level2": summ[0]["second_level_groups"],
+                       "reconstruction_shape": list(rec[0].shape)}}
+    print(json.dumps(line), flush=True)
+
+
 def _importance_work(target, proposal, starts, kl_lim, dev):
     """sum_g N_g d_g for the plan code_grouped_importance_sample used."""
     import compression_without_quantization_amd.coded_importance_sampler as I
@@ -196,6 +271,8 @@ def main():
         return grouped_main(args)
     if args.config in IMPORTANCE:
         return importance_main(args)
+    if args.config in PLN:
+        return pln_main(args)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))

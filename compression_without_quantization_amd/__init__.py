@@ -19,6 +19,7 @@ from .coded_importance_sampler import (code_grouped_importance_sample,
                                        decode_importance_sample, importance_decode_blocks,
                                        importance_encode_blocks)
 from .misc import stateless_normal_sample
+from .pln import ProbabilisticLadderNetwork, build_empirical_dists
 from .parallel import gather_indices, shard_range
 
 __all__ = [
@@ -31,5 +32,5 @@ __all__ = [
     "code_importance_sample", "decode_importance_sample",
     "code_grouped_importance_sample", "decode_grouped_importance_sample",
     "importance_encode_blocks", "importance_decode_blocks", "ArithmeticCoder",
-    "write_bin_code", "read_bin_code",
+    "write_bin_code", "read_bin_code", "ProbabilisticLadderNetwork", "build_empirical_dists",
 ]

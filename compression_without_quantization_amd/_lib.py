@@ -62,6 +62,9 @@ SIGNATURES = {
     "cwq_debug_prune_stats": (c_int, [c_vp, c_int]),
     "cwq_profile_set_eval_events": (c_int, [c_vp, c_vp]),
     "cwq_set_pruning": (c_int, [c_int]),
+    "cwq_pln_posterior": (c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, c_f32, c_vp, c_vp, c_vp]),
+    "cwq_permute_gather": (c_int, [c_vp, c_i64, c_i64, c_vp, c_vp, c_vp]),
+    "cwq_permute_scatter": (c_int, [c_vp, c_i64, c_i64, c_vp, c_vp, c_vp]),
 }
 
 _lib = None

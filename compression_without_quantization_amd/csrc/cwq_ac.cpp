@@ -79,6 +79,10 @@ int64_t cwq_ac_encode(const int64_t* counts, int64_t K, int precision, const int
     const int64_t sym = message[k];
     if (sym < 0 || sym >= K)
       return cwq::set_error(CWQ_ERR_INVALID, "cwq_ac_encode: symbol outside [0, K)");
+    // a zero-count symbol has an empty interval: the reference's loop would
+    // spin forever at low == high == half (coding.pyx:92-115); reject it
+    if (m.C[(size_t)sym] == m.D[(size_t)sym])
+      return cwq::set_error(CWQ_ERR_INVALID, "cwq_ac_encode: symbol has a zero count");
     const int64_t width = high - low;
     high = low + scale(width, m.D[(size_t)sym], m.R);
     low = low + scale(width, m.C[(size_t)sym], m.R);

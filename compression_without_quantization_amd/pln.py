@@ -1,0 +1,676 @@
+"""PLN image codec around the coders.
+
+Restates, on PyTorch-ROCm + libcwq.so:
+
+* the probabilistic ladder network's four transforms (code/transforms.py:17-342)
+  and its latent distributions (code/pln.py:150-203);
+* the image codec driver ``code_image_greedy`` / ``decode_image_greedy``
+  (pln.py:213-627, 638-817): level 2 through the grouped importance coder,
+  level 1 through the grouped greedy coder (or the importance coder), the
+  group sizes through the arithmetic coder, and the ``.miracle`` container;
+* ``build_empirical_dists`` (miracle.py:521-667), which makes the group-size and
+  index count models the arithmetic coder needs.
+
+What runs where:
+* the convolutions are library convolutions (MIOpen through torch.nn.functional);
+* the latent plumbing between them and the coders (the posterior combination,
+  NHWC flattening + permutation and its inverse) is HIP (csrc/cwq_pln.hip);
+* the coders are the gfx950 kernels of the rest of the package.
+
+No trained checkpoint exists offline, so the model starts from a
+deterministic seeded initialisation and can load a state dict (``load_weights``).
+TFC's ``SignalConv2D``/``GDN`` are restated from their documented semantics
+(**[ext]**, parity unpinned): correlation + stride-2 down-sampling for the
+analysis layers and transposed convolution for the synthesis layers, both with
+'same' zero padding; GDN y_i = x_i / sqrt(beta_i + sum_j gamma_ji x_j^2), IGDN the
+product.
+
+Deliberate differences from pln.py, each a reference defect (SURVEY.md
+Appendix B) or a non-determinism:
+* the level-2 draw that conditions the level-1 posterior (pln.py:157, an
+  unseeded ``posterior.sample()``) is the stateless draw loc2 + scale2 * z with
+  z from seed ``[seed - 2, 42]``;
+* the level-1 prior is computed from the level-2 sample *as the decoder sees
+  it* (outliers dequantised, binary_io quint16).  The reference conditions the
+  encoder on the unquantised outlier draw (:394-404), so its decoder derives a
+  different prior whenever level 2 has outliers;
+* group sizes are numpy arrays (pln.py:477 subtracts Python lists, TypeError);
+* an empty group would be coded as the EOF symbol 0 (pln.py:517-529); this
+  raises instead of writing a file that decodes short;
+* the permutation comes from a local ``np.random.RandomState(seed)`` (the same
+  sequence as the reference's ``np.random.seed(seed)``, without touching numpy's
+  global state); nothing is written to hard-coded paths (:424, :754, :805).
+"""
+import math
+import os
+
+import numpy as np
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from . import _lib
+from .binary_io import read_bin_code, write_bin_code
+from .coded_greedy_sampler import (Normal, code_grouped_greedy_sample,
+                                   decode_grouped_greedy_sample)
+from .coded_importance_sampler import (_kl, code_grouped_importance_sample,
+                                       decode_grouped_importance_sample)
+from .coding import ArithmeticCoder
+from .misc import stateless_normal_sample
+
+LEAKY_RELU_ALPHA = 0.2   # tf.nn.leaky_relu default
+POSTERIOR_EPS = 1e-12    # pln.py:150 call(inputs, eps=1e-12)
+NUM_EXTRAS = 11          # pln.py:541-549 / :669-672
+
+
+# ---------------------------------------------------------------------------
+# Transforms (code/transforms.py)
+# ---------------------------------------------------------------------------
+
+class GDN(nn.Module):
+    """tfc.GDN (inverse=False) / IGDN (inverse=True), channels first.
+
+    ``gamma`` is stored in TFC's orientation [C_in, C_out]."""
+
+    def __init__(self, channels, inverse=False):
+        super().__init__()
+        self.inverse = inverse
+        self.beta = nn.Parameter(torch.ones(channels))
+        self.gamma = nn.Parameter(0.1 * torch.eye(channels))
+
+    def forward(self, x):
+        c = x.shape[1]
+        norm = torch.sqrt(F.conv2d(x * x, self.gamma.t().reshape(c, c, 1, 1), self.beta))
+        return x * norm if self.inverse else x / norm
+
+
+class SignalConv2D(nn.Module):
+    """tfc.SignalConv2D with 'same_zeros' padding (the configurations used in
+    transforms.py): corr=True with ``strides_down`` is a strided correlation,
+    corr=False with ``strides_up`` a transposed convolution; the output is
+    ceil(n / s) resp. n * s positions."""
+
+    def __init__(self, c_in, c_out, kernel, corr, strides_down=1, strides_up=1, use_bias=True,
+                 activation=None):
+        super().__init__()
+        self.corr = corr
+        self.k = kernel
+        self.stride = strides_down if corr else strides_up
+        shape = (c_out, c_in, kernel, kernel) if corr else (c_in, c_out, kernel, kernel)
+        self.kernel = nn.Parameter(torch.empty(shape))
+        self.bias = nn.Parameter(torch.zeros(c_out)) if use_bias else None
+        self.activation = activation
+
+    def forward(self, x):
+        pad = self.k // 2
+        if self.corr:
+            y = F.conv2d(x, self.kernel, self.bias, stride=self.stride, padding=pad)
+        else:
+            y = F.conv_transpose2d(x, self.kernel, self.bias, stride=self.stride, padding=pad,
+                                   output_padding=self.stride - 1)
+        return y if self.activation is None else self.activation(y)
+
+
+def _leaky_relu(x):
+    return F.leaky_relu(x, LEAKY_RELU_ALPHA)
+
+
+class AnalysisTransform1(nn.Module):
+    """transforms.py:17-105: three 5x5 stride-2 GDN layers, then 5x5 stride-2
+    loc (linear) and scale (exp) heads without bias."""
+
+    def __init__(self, num_filters, num_latent_channels):
+        super().__init__()
+        f = num_filters
+        self.layers = nn.ModuleList([
+            SignalConv2D(3, f, 5, True, strides_down=2, activation=GDN(f)),
+            SignalConv2D(f, f, 5, True, strides_down=2, activation=GDN(f)),
+            SignalConv2D(f, f, 5, True, strides_down=2, activation=GDN(f))])
+        self.loc_head = SignalConv2D(f, num_latent_channels, 5, True, strides_down=2,
+                                     use_bias=False)
+        self.scale_head = SignalConv2D(f, num_latent_channels, 5, True, strides_down=2,
+                                       use_bias=False, activation=torch.exp)
+
+    def forward(self, x):
+        for layer in self.layers:
+            x = layer(x)
+        return self.loc_head(x), self.scale_head(x)
+
+
+class SynthesisTransform1(nn.Module):
+    """transforms.py:109-177: three 5x5 up-2 IGDN layers and a 3-channel 5x5 up-2
+    output layer."""
+
+    def __init__(self, num_latent_channels, num_filters):
+        super().__init__()
+        f = num_filters
+        self.layers = nn.ModuleList([
+            SignalConv2D(num_latent_channels, f, 5, False, strides_up=2,
+                         activation=GDN(f, inverse=True)),
+            SignalConv2D(f, f, 5, False, strides_up=2, activation=GDN(f, inverse=True)),
+            SignalConv2D(f, f, 5, False, strides_up=2, activation=GDN(f, inverse=True)),
+            SignalConv2D(f, 3, 5, False, strides_up=2)])
+
+    def forward(self, x):
+        for layer in self.layers:
+            x = layer(x)
+        return x
+
+
+class AnalysisTransform2(nn.Module):
+    """transforms.py:187-267: 3x3 stride-1 and 5x5 stride-2 leaky-ReLU layers,
+    5x5 stride-2 loc (linear) and scale (sigmoid) heads without bias."""
+
+    def __init__(self, num_latent_channels_1, num_filters, num_latent_channels):
+        super().__init__()
+        f = num_filters
+        self.layers = nn.ModuleList([
+            SignalConv2D(num_latent_channels_1, f, 3, True, strides_down=1,
+                         activation=_leaky_relu),
+            SignalConv2D(f, f, 5, True, strides_down=2, activation=_leaky_relu)])
+        self.loc_head = SignalConv2D(f, num_latent_channels, 5, True, strides_down=2,
+                                     use_bias=False)
+        self.scale_head = SignalConv2D(f, num_latent_channels, 5, True, strides_down=2,
+                                       use_bias=False, activation=torch.sigmoid)
+
+    def forward(self, x):
+        for layer in self.layers:
+            x = layer(x)
+        return self.loc_head(x), self.scale_head(x)
+
+
+class SynthesisTransform2(nn.Module):
+    """transforms.py:270-342: two 5x5 up-2 leaky-ReLU layers, 3x3 stride-1 loc
+    (linear) and scale (softplus) heads with bias: the level-1 prior."""
+
+    def __init__(self, num_latent_channels, num_filters, num_output_channels):
+        super().__init__()
+        f = num_filters
+        self.layers = nn.ModuleList([
+            SignalConv2D(num_latent_channels, f, 5, False, strides_up=2, activation=_leaky_relu),
+            SignalConv2D(f, f, 5, False, strides_up=2, activation=_leaky_relu)])
+        self.loc_head = SignalConv2D(f, num_output_channels, 3, False, strides_up=1)
+        self.scale_head = SignalConv2D(f, num_output_channels, 3, False, strides_up=1,
+                                       activation=F.softplus)
+
+    def forward(self, x):
+        for layer in self.layers:
+            x = layer(x)
+        return self.loc_head(x), self.scale_head(x)
+
+
+# ---------------------------------------------------------------------------
+# Device helpers over csrc/cwq_pln.hip
+# ---------------------------------------------------------------------------
+
+def _stream(dev):
+    return torch.cuda.current_stream(dev).cuda_stream
+
+
+def _flat_f32(x):
+    return x.detach().to(torch.float32).contiguous()
+
+
+def posterior_combine(lik_loc, lik_scale, prior_loc, prior_scale, eps=POSTERIOR_EPS):
+    """pln.py:165-185 on the device (any shape, float32)."""
+    lib = _lib.load()
+    ll, ls, pl, ps = (_flat_f32(t) for t in (lik_loc, lik_scale, prior_loc, prior_scale))
+    if not (ll.shape == ls.shape == pl.shape == ps.shape):
+        raise ValueError("likelihood and prior tensors must have the same shape")
+    loc, scale = torch.empty_like(ll), torch.empty_like(ll)
+    _lib.check(lib.cwq_pln_posterior(ll.data_ptr(), ls.data_ptr(), pl.data_ptr(), ps.data_ptr(),
+                                     ll.numel(), float(eps), loc.data_ptr(), scale.data_ptr(),
+                                     _stream(ll.device)), "cwq_pln_posterior")
+    return loc, scale
+
+
+def permute_flatten(x, perm):
+    """pln.py:264-273 + :316-324: x [1, C, H, W] (NCHW) -> the reference's
+    Permute(perm).forward of its NHWC flattening, [C*H*W]."""
+    lib = _lib.load()
+    x = _flat_f32(x)
+    if x.dim() != 4 or x.shape[0] != 1:
+        raise ValueError("expected a [1, C, H, W] latent tensor")
+    C, HW = x.shape[1], x.shape[2] * x.shape[3]
+    if perm is not None and perm.numel() != C * HW:
+        raise ValueError("permutation size does not match the latent tensor")
+    out = torch.empty(C * HW, dtype=torch.float32, device=x.device)
+    _lib.check(lib.cwq_permute_gather(x.data_ptr(), C, HW, perm.data_ptr() if perm is not None
+                                      else None, out.data_ptr(), _stream(x.device)),
+               "cwq_permute_gather")
+    return out
+
+
+def unpermute_unflatten(v, perm, shape_nchw):
+    """pln.py:394-397 / :770-772: Permute.inverse then reshape to the latent
+    shape; returns [1, C, H, W] (NCHW)."""
+    lib = _lib.load()
+    _, C, H, W = shape_nchw
+    if v.numel() != C * H * W:
+        raise ValueError("sample size does not match the latent shape")
+    if perm is not None and perm.numel() != C * H * W:
+        raise ValueError("permutation size does not match the latent shape")
+    v = _flat_f32(v).reshape(-1)
+    out = torch.empty((1, C, H, W), dtype=torch.float32, device=v.device)
+    _lib.check(lib.cwq_permute_scatter(v.data_ptr(), C, H * W, perm.data_ptr() if perm is not None
+                                       else None, out.data_ptr(), _stream(v.device)),
+               "cwq_permute_scatter")
+    return out
+
+
+def permutations(seed, n1, n2, use_permutation=True):
+    """pln.py:304-313 / :693-701: np.random.seed(seed) then permutation(n1),
+    permutation(n2) (legacy MT19937 stream), as int32."""
+    if not use_permutation:
+        return np.arange(n1, dtype=np.int32), np.arange(n2, dtype=np.int32)
+    rs = np.random.RandomState(seed)
+    p1 = rs.permutation(n1).astype("int32")
+    p2 = rs.permutation(n2).astype("int32")
+    return p1, p2
+
+
+def quantize_image(image):
+    """miracle.py:47-53: round(x * 255) saturated to uint8."""
+    x = torch.round(torch.as_tensor(image, dtype=torch.float32) * 255)
+    return torch.clamp(x, 0, 255).to(torch.uint8)
+
+
+def _load_counts(counts, default_size):
+    """A count model: a path to a .npy file (the reference's --dist_prefix
+    files), an array, or None / "" for a uniform model over default_size
+    symbols (the reference has no default)."""
+    if counts is None or (isinstance(counts, str) and counts == ""):
+        return np.ones(default_size, dtype=np.int64)
+    if isinstance(counts, (str, os.PathLike)):
+        return np.load(counts, allow_pickle=False).astype(np.int64)
+    return np.asarray(counts, dtype=np.int64)
+
+
+def _as_coder(ac):
+    if isinstance(ac, ArithmeticCoder):
+        return ac
+    return ArithmeticCoder(_load_counts(ac, 0), precision=32)
+
+
+def _group_differences(starts):
+    d = np.diff(np.asarray(starts, dtype=np.int64))
+    if d.size and (d <= 0).any():
+        raise ValueError("an empty group would be coded as the EOF symbol 0 (pln.py:517-529)")
+    return d
+
+
+def _kl_sum(q, p):
+    kl = _kl(q.loc.device, _flat_f32(q.loc).reshape(-1), _flat_f32(q.scale).reshape(-1),
+             _flat_f32(p.loc).reshape(-1), _flat_f32(p.scale).reshape(-1))
+    return float(kl.double().sum().item())
+
+
+def _normal_log_prob_mean(dist, x):
+    """mean of TFP Normal.log_prob(x) (<= 0.7 form), for the summaries only."""
+    loc, scale = _flat_f32(dist.loc).reshape(-1), _flat_f32(dist.scale).reshape(-1)
+    z = (torch.as_tensor(x, device=loc.device).reshape(-1) - loc) / scale
+    return float((-0.5 * z * z - (0.9189385 + torch.log(scale))).mean().item())
+
+
+# ---------------------------------------------------------------------------
+# The ladder network and its codec (code/pln.py)
+# ---------------------------------------------------------------------------
+
+class ProbabilisticLadderNetwork(nn.Module):
+    """pln.py:46-203 (the codec-relevant part: transforms and latent
+    distributions) plus code_image_greedy / decode_image_greedy."""
+
+    def __init__(self, first_level_filters=196, second_level_filters=128,
+                 first_level_latent_channels=128, second_level_latent_channels=24,
+                 padding="same_zeros", likelihood="gaussian", learn_gamma=False, init_seed=0):
+        super().__init__()
+        if padding != "same_zeros":
+            raise ValueError("only padding='same_zeros' (the reference default) is restated")
+        self.first_level_filters = first_level_filters
+        self.second_level_filters = second_level_filters
+        self.first_level_latent_channels = first_level_latent_channels
+        self.second_level_latent_channels = second_level_latent_channels
+        self.likelihood = likelihood  # training only
+        self.analysis_transform_1 = AnalysisTransform1(first_level_filters,
+                                                       first_level_latent_channels)
+        self.synthesis_transform_1 = SynthesisTransform1(first_level_latent_channels,
+                                                         first_level_filters)
+        self.analysis_transform_2 = AnalysisTransform2(first_level_latent_channels,
+                                                       second_level_filters,
+                                                       second_level_latent_channels)
+        self.synthesis_transform_2 = SynthesisTransform2(second_level_latent_channels,
+                                                         second_level_filters,
+                                                         first_level_latent_channels)
+        self.log_gamma = nn.Parameter(torch.zeros(()), requires_grad=learn_gamma)
+        self.reset_parameters(init_seed)
+
+    @torch.no_grad()
+    def reset_parameters(self, seed=0):
+        """Deterministic initialisation: Glorot-uniform kernels, zero biases,
+        GDN beta = 1 and gamma = 0.1 I (TFC's defaults)."""
+        g = torch.Generator().manual_seed(int(seed))
+        for m in self.modules():
+            if isinstance(m, SignalConv2D):
+                k = m.kernel
+                rf = k.shape[2] * k.shape[3]
+                fan_in, fan_out = (k.shape[1] * rf, k.shape[0] * rf) if m.corr else \
+                    (k.shape[0] * rf, k.shape[1] * rf)
+                lim = math.sqrt(6.0 / (fan_in + fan_out))
+                k.copy_((torch.rand(k.shape, generator=g) * 2 - 1) * lim)
+                if m.bias is not None:
+                    m.bias.zero_()
+            elif isinstance(m, GDN):
+                m.beta.fill_(1.0)
+                m.gamma.copy_(0.1 * torch.eye(m.gamma.shape[0]))
+
+    def load_weights(self, path):
+        """Load a state dict (safetensors, or a torch file read with
+        weights_only=True) with this module's parameter names."""
+        if str(path).endswith(".safetensors"):
+            from safetensors.torch import load_file
+            sd = load_file(str(path))
+        else:
+            sd = torch.load(path, map_location="cpu", weights_only=True)
+        self.load_state_dict(sd, strict=True)
+
+    # -- latent distributions (pln.py:150-203) --------------------------------
+
+    @staticmethod
+    def _to_nchw(image, device):
+        x = torch.as_tensor(image, dtype=torch.float32)
+        if x.dim() == 3:
+            x = x.unsqueeze(0)
+        if x.dim() != 4 or x.shape[-1] != 3:
+            raise ValueError("image must be [1, H, W, 3] or [H, W, 3] (NHWC, values in [0, 1])")
+        return x.permute(0, 3, 1, 2).contiguous().to(device)
+
+    @torch.no_grad()
+    def latent_distributions(self, image, seed):
+        """pln.py:150-190 for one NHWC image: returns dict with NCHW tensors
+        q1 (posterior_1), q2 (posterior_2) and the level-1 prior used to form q1."""
+        dev = next(self.parameters()).device
+        x = self._to_nchw(image, dev)
+        loc1, scale1 = self.analysis_transform_1(x)                    # :153
+        loc2, scale2 = self.analysis_transform_2(loc1)                 # :157
+        z2 = stateless_normal_sample(loc2, scale2, 1, int(seed) - 2)[0]  # :157 (seeded)
+        ploc1, pscale1 = self.synthesis_transform_2(z2)                # :161
+        qloc1, qscale1 = posterior_combine(loc1, scale1, ploc1, pscale1)  # :165-185
+        return {"q1": Normal(qloc1, qscale1), "q2": Normal(loc2, scale2),
+                "p1_call": Normal(ploc1, pscale1), "image_shape": tuple(image_shape(image))}
+
+    @torch.no_grad()
+    def forward(self, image, seed=0):
+        """pln.py:150-203: the reconstruction from a level-1 posterior draw
+        (stateless, seed [seed - 3, 42])."""
+        lat = self.latent_distributions(image, seed)
+        q1 = lat["q1"]
+        z1 = stateless_normal_sample(q1.loc, q1.scale, 1, int(seed) - 3)[0]
+        return self.synthesis_transform_1(z1)
+
+    # -- codec (pln.py:213-627) ----------------------------------------------
+
+    @torch.no_grad()
+    def code_image_greedy(self, session, image, seed, n_steps=30, n_bits_per_step=14,
+                          greedy_max_group_size_bits=12, comp_file_path=None,
+                          backfitting_steps_level_1=0, backfitting_steps_level_2=0,
+                          use_log_prob=False, rho=1., use_importance_sampling=False,
+                          use_permutation=True,
+                          second_level_n_bits_per_group=20, second_level_max_group_size_bits=4,
+                          second_level_dim_kl_bit_limit=12, first_level_n_bits_per_group=20,
+                          first_level_max_group_size_bits=3, first_level_dim_kl_bit_limit=12,
+                          outlier_index_bytes=3, outlier_sample_bytes=2,
+                          second_level_group_dist_counts="", first_level_group_dist_counts="",
+                          second_level_sample_index_counts="", first_level_sample_index_counts="",
+                          second_level_sample_ac=None, first_level_sample_ac=None,
+                          use_index_ac=False,
+                          return_first_level_group_sizes=False, return_first_level_indices=False,
+                          return_second_level_group_sizes=False,
+                          return_second_level_indices=False, verbose=False):
+        """pln.py:213-627.  ``session`` is ignored.  Writes the .miracle file to
+        comp_file_path and returns ((sample2, sample1), summaries), or what the
+        return_* flags ask for.  Group-size count models are .npy paths or
+        arrays (uniform over 1 + 2^max_group_size_bits symbols when empty);
+        with use_index_ac the index coders are ArithmeticCoder objects or
+        count arrays (the reference unpickles them, :262-265)."""
+        del session, backfitting_steps_level_1, backfitting_steps_level_2, use_log_prob
+        if use_index_ac and not use_importance_sampling:
+            raise ValueError("use_index_ac needs use_importance_sampling=True: the greedy "
+                             "level-1 code is a bit string, not indices")
+        seed = int(seed)
+        dev = next(self.parameters()).device
+        # Step 1: latent distributions, flattened (NHWC order) and permuted
+        lat = self.latent_distributions(image, seed)
+        q1, q2 = lat["q1"], lat["q2"]
+        shape1, shape2 = tuple(q1.loc.shape), tuple(q2.loc.shape)
+        n1, n2 = q1.loc.numel(), q2.loc.numel()
+        perm_1, perm_2 = permutations(seed, n1, n2, use_permutation)
+        perm1_d = torch.from_numpy(perm_1).to(dev)
+        perm2_d = torch.from_numpy(perm_2).to(dev)
+        q1p = Normal(permute_flatten(q1.loc, perm1_d), permute_flatten(q1.scale, perm1_d))
+        q2p = Normal(permute_flatten(q2.loc, perm2_d), permute_flatten(q2.scale, perm2_d))
+        p2p = Normal(torch.zeros(n2, device=dev), torch.ones(n2, device=dev))  # prior_2 = N(0, 1)
+
+        # Step 2a: level 2, grouped importance coder (:346-358)
+        res = code_grouped_importance_sample(
+            None, q2p, p2p, seed, second_level_n_bits_per_group,
+            max_group_size_bits=second_level_max_group_size_bits,
+            dim_kl_bit_limit=second_level_dim_kl_bit_limit,
+            return_group_indices_only=return_second_level_group_sizes,
+            return_indices_only=return_second_level_indices, return_indices=use_index_ac)
+        if return_second_level_group_sizes:
+            return res[0]
+        if return_second_level_indices:
+            return res
+        sample2, code2, group_indices2, outlier_extras2 = res
+        outlier_extras2 = [np.asarray(x).reshape(-1) for x in outlier_extras2]
+        group_differences2 = _group_differences(group_indices2)
+        # the level-2 sample as the decoder will reconstruct it (outliers
+        # dequantised), then the level-1 prior from it (:393-408)
+        dec2 = decode_grouped_importance_sample(
+            None, code2, np.asarray(group_indices2)[:-1], p2p, second_level_n_bits_per_group,
+            seed, outlier_extras2[0], outlier_extras2[1], use_indices=use_index_ac)
+        if use_index_ac:   # symbols index + 1, then EOF (the reference omits the EOF)
+            code2 = ''.join(_as_coder(second_level_sample_ac).encode(list(code2) + [0]))
+        p1p = self._level1_prior(torch.from_numpy(dec2).to(dev), perm2_d, perm1_d, shape2)
+
+        # Step 2b: level 1 (:412-474)
+        if use_importance_sampling:
+            res = code_grouped_importance_sample(
+                None, q1p, p1p, seed, first_level_n_bits_per_group,
+                max_group_size_bits=first_level_max_group_size_bits,
+                dim_kl_bit_limit=first_level_dim_kl_bit_limit,
+                return_group_indices_only=return_first_level_group_sizes,
+                return_indices_only=return_first_level_indices, return_indices=use_index_ac)
+            if return_first_level_group_sizes:
+                return res[0]
+            if return_first_level_indices:
+                return res
+            sample1, code1, group_indices1, outlier_extras1 = res
+            if use_index_ac:
+                code1 = ''.join(_as_coder(first_level_sample_ac).encode(list(code1) + [0]))
+            outlier_extras1 = [np.asarray(x).reshape(-1) for x in outlier_extras1]
+        else:
+            sample1, code1, group_indices1 = code_grouped_greedy_sample(
+                None, q1p, p1p, n_steps, n_bits_per_step, seed,
+                max_group_size_bits=greedy_max_group_size_bits, rho=rho)
+            if return_first_level_group_sizes:
+                return np.asarray(group_indices1)
+            outlier_extras1 = None
+        group_differences1 = _group_differences(group_indices1)
+        bitcode = code1 + code2
+
+        # Step 3: the container (:498-537)
+        extras = [seed, n_steps, n_bits_per_step, first_level_n_bits_per_group,
+                  second_level_n_bits_per_group, len(code1), len(code2),
+                  shape1[2], shape1[3], shape2[2], shape2[3]]
+        var_length_extras = list(outlier_extras2)
+        var_length_bits = [outlier_index_bytes * 8, outlier_sample_bytes * 8]
+        if use_importance_sampling:
+            var_length_extras += list(outlier_extras1)
+            var_length_bits += [outlier_index_bytes * 8, outlier_sample_bytes * 8]
+        g1_bits = first_level_max_group_size_bits if use_importance_sampling else \
+            greedy_max_group_size_bits
+        coder2 = ArithmeticCoder(_load_counts(second_level_group_dist_counts,
+                                              1 + 2 ** second_level_max_group_size_bits), 32)
+        coder1 = ArithmeticCoder(_load_counts(first_level_group_dist_counts, 1 + 2 ** g1_bits), 32)
+        gi1_code = coder1.encode(np.concatenate((group_differences1, [0])))
+        gi2_code = coder2.encode(np.concatenate((group_differences2, [0])))
+        if comp_file_path is not None:
+            write_bin_code(bitcode, comp_file_path, extras=extras,
+                           extra_var_bits=[gi1_code, gi2_code],
+                           var_length_extras=var_length_extras, var_length_bits=var_length_bits)
+
+        # Step 4: summaries (:543-625)
+        kl1 = _kl_sum(q1p, p1p)
+        kl2 = _kl_sum(q2p, p2p)
+        total_kl = kl1 + kl2
+        shp = lat["image_shape"]
+        npix = shp[1] * shp[2]
+        actual = os.path.getsize(comp_file_path) if comp_file_path is not None else None
+        extra_bytes = len(gi1_code) + len(gi2_code) + 9 * 2 // 8
+        theo = lambda k: (k + 2 * np.log(k + 1)) / np.log(2) / 8
+        summaries = {
+            "image_shape": list(shp),
+            "theoretical_byte_size": float(theo(total_kl)),
+            "actual_byte_size": actual,
+            "extra_byte_size": extra_bytes,
+            "actual_no_extra": None if actual is None else actual - extra_bytes,
+            "second_bpp": (len(code2) / 8 + len(gi2_code) // 8 + 1) * 8 / npix,
+            "bpp": None if actual is None else 8 * actual / npix,
+            "first_level_theoretical": float(theo(kl1)),
+            "second_level_theoretical": float(theo(kl2)),
+            "first_level_groups": int(len(group_indices1)),
+            "second_level_groups": int(len(group_indices2)),
+            "first_level_avg_log_lik": _normal_log_prob_mean(q1p, torch.as_tensor(sample1)),
+            "second_level_avg_log_lik": _normal_log_prob_mean(q2p, torch.as_tensor(sample2)),
+        }
+        if verbose:
+            for k, v in summaries.items():
+                print("{}: {}".format(k, v))
+        return (sample2, sample1), summaries
+
+    def _level1_prior(self, sample2_perm, perm2_d, perm1_d, shape2):
+        """pln.py:393-408 / :770-779: un-permute the level-2 sample, run
+        SynthesisTransform_2, and permute its (loc, scale) like level 1."""
+        z2 = unpermute_unflatten(sample2_perm, perm2_d, shape2)
+        ploc1, pscale1 = self.synthesis_transform_2(z2)
+        return Normal(permute_flatten(ploc1, perm1_d), permute_flatten(pscale1, perm1_d))
+
+    # -- decoder (pln.py:638-817) ----------------------------------------------
+
+    @torch.no_grad()
+    def decode_image_greedy(self, session, comp_file_path, use_importance_sampling=True, rho=1.,
+                            use_permutation=True, second_level_group_dist_counts="",
+                            first_level_group_dist_counts="", second_level_sample_ac=None,
+                            first_level_sample_ac=None, use_index_ac=False, verbose=False,
+                            greedy_max_group_size_bits=12, first_level_max_group_size_bits=3,
+                            second_level_max_group_size_bits=4):
+        """pln.py:638-817.  Returns the reconstruction [H, W, 3] (float32 numpy,
+        tf.squeeze of the NHWC output).  As in the reference,
+        ``use_importance_sampling`` defaults to True and must match the encoder.
+        The *_max_group_size_bits only size the uniform default count models."""
+        del session
+        dev = next(self.parameters()).device
+        nvle = 4 if use_importance_sampling else 2
+        code, extras, extra_var_bits, vle = read_bin_code(comp_file_path, num_extras=NUM_EXTRAS,
+                                                          num_extra_var_bits=2,
+                                                          num_var_length_extras=nvle)
+        g1_bits = first_level_max_group_size_bits if use_importance_sampling else \
+            greedy_max_group_size_bits
+        coder2 = ArithmeticCoder(_load_counts(second_level_group_dist_counts,
+                                              1 + 2 ** second_level_max_group_size_bits), 32)
+        coder1 = ArithmeticCoder(_load_counts(first_level_group_dist_counts, 1 + 2 ** g1_bits), 32)
+        if verbose:
+            print("Extras: {}".format(extras))
+        seed, n_steps, n_bits_per_step = extras[0], extras[1], extras[2]
+        n_bits_group_1, n_bits_group_2 = extras[3], extras[4]
+        len1, len2 = extras[5], extras[6]
+        # extras are unsigned 32-bit on disk; the seed is an int (negative seeds wrap)
+        seed = int(np.int32(np.uint32(seed))) if seed >= 2 ** 31 else seed
+        shape1 = (1, self.first_level_latent_channels, extras[7], extras[8])
+        shape2 = (1, self.second_level_latent_channels, extras[9], extras[10])
+        n1 = int(np.prod(shape1))
+        n2 = int(np.prod(shape2))
+        perm_1, perm_2 = permutations(seed, n1, n2, use_permutation)
+        perm1_d = torch.from_numpy(perm_1).to(dev)
+        perm2_d = torch.from_numpy(perm_2).to(dev)
+        gd2 = coder2.decode_fast(extra_var_bits[1])[:-1]              # :705-709
+        gd1 = coder1.decode_fast(extra_var_bits[0])[:-1]
+        code1 = code[:len1]
+        code2 = code[len1:len1 + len2]
+        gi2 = np.concatenate(([0], np.cumsum(gd2, dtype=np.int64)))    # :730-734
+        gi1 = np.concatenate(([0], np.cumsum(gd1, dtype=np.int64)))    # :757-760
+        p2p = Normal(torch.zeros(n2, device=dev), torch.ones(n2, device=dev))
+        if use_index_ac:
+            idx2 = _as_coder(second_level_sample_ac).decode_fast(code2)[:-1]
+            dec2 = decode_grouped_importance_sample(None, idx2, gi2[:-1], p2p, n_bits_group_2,
+                                                    seed, vle[0], vle[1], use_indices=True)
+        else:
+            dec2 = decode_grouped_importance_sample(None, code2, gi2[:-1], p2p, n_bits_group_2,
+                                                    seed, vle[0], vle[1])
+        p1p = self._level1_prior(torch.from_numpy(dec2).to(dev), perm2_d, perm1_d, shape2)
+        if use_importance_sampling:
+            if use_index_ac:
+                idx1 = _as_coder(first_level_sample_ac).decode_fast(code1)[:-1]
+                dec1 = decode_grouped_importance_sample(None, idx1, gi1[:-1], p1p, n_bits_group_1,
+                                                        seed, vle[2], vle[3], use_indices=True)
+            else:
+                dec1 = decode_grouped_importance_sample(None, code1, gi1[:-1], p1p,
+                                                        n_bits_group_1, seed, vle[2], vle[3])
+        else:
+            dec1 = decode_grouped_greedy_sample(None, code1, gi1[:-1], p1p, n_bits_per_step,
+                                                n_steps, seed, rho=rho)
+        z1 = unpermute_unflatten(torch.from_numpy(dec1).to(dev), perm1_d, shape1)
+        rec = self.synthesis_transform_1(z1)                           # :809-815
+        return rec[0].permute(1, 2, 0).contiguous().cpu().numpy()
+
+
+def image_shape(image):
+    """[1, H, W, 3] of an NHWC image (or [H, W, 3])."""
+    s = tuple(np.shape(image))
+    return (1,) + s if len(s) == 3 else s
+
+
+def build_empirical_dists(model, images, seed=42, n_steps=30, n_bits_per_step=14,
+                          greedy_max_group_size_bits=12,
+                          second_level_n_bits_per_group=20, second_level_max_group_size_bits=2,
+                          second_level_dim_kl_bit_limit=16, first_level_n_bits_per_group=20,
+                          first_level_max_group_size_bits=4, first_level_dim_kl_bit_limit=16):
+    """miracle.py:521-667 over an iterable of NHWC images: the group-size and
+    sample-index count models, returned as (group_sizes1, group_sizes2,
+    sample_indices1, sample_indices2) int64 arrays (the reference np.saves them
+    as <prefix>_1.npy, _2.npy, _samp_ind_1.npy, _samp_ind_2.npy).  As in the
+    reference, level 1 uses the importance coder (miracle.py:591) and every
+    image adds one EOF count.  The index models count the symbols the coder
+    actually emits, index + 1 (the reference adds another +1, miracle.py:655,
+    :663, which shifts its model off the coded symbols)."""
+    group_sizes2 = np.zeros(1 + 2 ** second_level_max_group_size_bits, dtype=np.int64)
+    group_sizes1 = np.zeros(1 + 2 ** first_level_max_group_size_bits, dtype=np.int64)
+    sample_indices2 = np.zeros(1 + 2 ** second_level_n_bits_per_group, dtype=np.int64)
+    sample_indices1 = np.zeros(1 + 2 ** first_level_n_bits_per_group, dtype=np.int64)
+    kw = dict(seed=seed, n_steps=n_steps, n_bits_per_step=n_bits_per_step,
+              greedy_max_group_size_bits=greedy_max_group_size_bits, use_importance_sampling=True,
+              second_level_n_bits_per_group=second_level_n_bits_per_group,
+              second_level_max_group_size_bits=second_level_max_group_size_bits,
+              second_level_dim_kl_bit_limit=second_level_dim_kl_bit_limit,
+              first_level_n_bits_per_group=first_level_n_bits_per_group,
+              first_level_max_group_size_bits=first_level_max_group_size_bits,
+              first_level_dim_kl_bit_limit=first_level_dim_kl_bit_limit)
+    for image in images:
+        gi2 = model.code_image_greedy(None, image, return_second_level_group_sizes=True, **kw)
+        u, c = np.unique(np.diff(np.asarray(gi2)), return_counts=True)
+        group_sizes2[u] += c
+        group_sizes2[0] += 1
+        gi1 = model.code_image_greedy(None, image, return_first_level_group_sizes=True, **kw)
+        u, c = np.unique(np.diff(np.asarray(gi1)), return_counts=True)
+        group_sizes1[u] += c
+        group_sizes1[0] += 1
+        ind2 = model.code_image_greedy(None, image, return_second_level_indices=True, **kw)
+        u, c = np.unique(np.asarray(ind2), return_counts=True)
+        sample_indices2[u] += c
+        sample_indices2[0] += 1
+        ind1 = model.code_image_greedy(None, image, return_first_level_indices=True, **kw)
+        u, c = np.unique(np.asarray(ind1), return_counts=True)
+        sample_indices1[u] += c
+        sample_indices1[0] += 1
+    return group_sizes1, group_sizes2, sample_indices1, sample_indices2

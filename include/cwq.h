@@ -197,8 +197,10 @@ int cwq_importance_plan(const float* kl, const int64_t* starts, int64_t ng, int6
 /* ArithmeticCoder(P, precision).encode(message): writes the code as '0'/'1'
  * chars to out_bits (if non-null, at most cap) and returns the number of bits
  * (or a negative error).  counts: P[K] (non-negative, sum > 0); message
- * symbols in [0, K) and, as the reference's callers do, ending with the EOF
- * symbol 0.  precision in [3, 62] (the reference uses 32). */
+ * symbols in [0, K) with non-zero counts (CWQ_ERR_INVALID otherwise: the
+ * reference loops forever on a zero-count symbol) and, as the reference's
+ * callers do, ending with the EOF symbol 0.  precision in [3, 62] (the
+ * reference uses 32). */
 int64_t cwq_ac_encode(const int64_t* counts, int64_t K, int precision, const int64_t* message,
                       int64_t n, char* out_bits, int64_t cap);
 
@@ -265,6 +267,35 @@ int cwq_profile_set_eval_events(void* start_event, void* stop_event);
  * it, exact pruning elsewhere.  Mode 2 also turns on the importance sampler's
  * screening pass; modes 0 and 1 score its candidates exactly. */
 int cwq_set_pruning(int mode);
+
+/* ---- PLN image codec plumbing (csrc/cwq_pln.hip) ----
+ * The ladder network's transforms are library convolutions; these three
+ * stream kernels connect them to the coders.  Latent tensors are NCHW with
+ * batch 1 (C channels, HW = H*W positions); the reference flattens them in
+ * TF's NHWC order, index f = hw*C + c. */
+
+/* pln.py:165-185: level-1 posterior = precision-weighted combination of the
+ * likelihood N(lik_loc, lik_scale) (AnalysisTransform_1) and the prior
+ * N(prior_loc, prior_scale) (SynthesisTransform_2), float32 in the
+ * reference's order: lp = 1/(lik_scale^2 + eps), pp = 1/(prior_scale^2 + eps),
+ * var = 1/(lp + pp), scale = sqrt(var), loc = (lik_loc*pp + prior_loc*lp)*var.
+ * Elementwise over n values; any layout. */
+int cwq_pln_posterior(const float* lik_loc, const float* lik_scale, const float* prior_loc,
+                      const float* prior_scale, int64_t n, float eps, float* loc, float* scale,
+                      void* stream);
+
+/* pln.py:264-273 + :316-324: out[i] = src_nhwc[perm[i]] for i < C*HW, i.e.
+ * tfp.bijectors.Permute(perm).forward(tf.reshape(x_nhwc, [-1])), reading the
+ * NCHW tensor src.  perm: device int32 [C*HW] permutation, or NULL for the
+ * identity (use_permutation=False). */
+int cwq_permute_gather(const float* src, int64_t C, int64_t HW, const int32_t* perm, float* out,
+                       void* stream);
+
+/* pln.py:394-397, :770-772, :801-803: the inverse, Permute.inverse and the
+ * reshape back to the latent shape, written NCHW: out_nchw[c*HW + hw] = src[i]
+ * where perm[i] = hw*C + c. */
+int cwq_permute_scatter(const float* src, int64_t C, int64_t HW, const int32_t* perm, float* out,
+                        void* stream);
 
 #ifdef __cplusplus
 }

@@ -323,3 +323,50 @@ def code_grouped_importance_sample(q_loc, q_scale, p_loc, p_scale, seed, n_bits_
     idx, samp = importance_encode(tl, ts, zeros, ones, starts, ns, seed, 0, nthreads)
     sample = np.where(keep, destandardise(samp, pl, ps), target_samples).astype(np.float32)
     return sample, [int(i) + 1 for i in idx], starts, (out_idx, out_q)
+
+
+# --------------------------------------------------------------------------
+# PLN latent plumbing (code/pln.py), numpy float32 -- each op is one IEEE
+# operation, so numpy's results are the reference's float32 values
+# --------------------------------------------------------------------------
+def pln_posterior(lik_loc, lik_scale, prior_loc, prior_scale, eps=1e-12):
+    """pln.py:165-185 in the reference's operation order."""
+    ll, ls, pl, ps = map(lambda a: np.asarray(a, np.float32), (lik_loc, lik_scale, prior_loc,
+                                                               prior_scale))
+    e = np.float32(eps)
+    lv = ls * ls
+    pv = ps * ps
+    lp = np.float32(1) / (lv + e)
+    pp = np.float32(1) / (pv + e)
+    cv = np.float32(1) / (lp + pp)
+    cs = np.sqrt(cv)
+    cl = ll * pp
+    cl = cl + pl * lp
+    cl = cl * cv
+    return cl.astype(np.float32), cs.astype(np.float32)
+
+
+def pln_permutations(seed, n1, n2):
+    """pln.py:304-313: np.random.seed(seed); permutation(n1); permutation(n2)."""
+    state = np.random.get_state()
+    try:
+        np.random.seed(seed)
+        p1 = np.random.permutation(n1).astype("int32")
+        p2 = np.random.permutation(n2).astype("int32")
+    finally:
+        np.random.set_state(state)
+    return p1, p2
+
+
+def nhwc_permute_flatten(x_nchw, perm):
+    """tf.reshape(x_nhwc, [-1]) then tfp Permute.forward: y[i] = x[perm[i]]."""
+    flat = np.ascontiguousarray(np.transpose(np.asarray(x_nchw, np.float32), (0, 2, 3, 1)))
+    return flat.reshape(-1)[np.asarray(perm, np.int64)]
+
+
+def unpermute_to_nchw(v, perm, shape_nchw):
+    """Permute.inverse, reshape to NHWC, returned NCHW."""
+    n, c, h, w = shape_nchw
+    flat = np.empty(n * c * h * w, np.float32)
+    flat[np.asarray(perm, np.int64)] = np.asarray(v, np.float32).reshape(-1)
+    return np.ascontiguousarray(np.transpose(flat.reshape(n, h, w, c), (0, 3, 1, 2)))

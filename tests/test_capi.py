@@ -26,6 +26,9 @@ def test_exports_every_header_symbol(cwqlib):
 
 def test_version_and_error(cwqlib):
     assert cwqlib.cwq_version() >= 1
+    # the message is thread-local and kept until the next call: an empty
+    # (n = 0) call succeeds without touching the device and clears it
+    assert cwqlib.cwq_pln_posterior(None, None, None, None, 0, 1e-12, None, None, None) == 0
     assert cwqlib.cwq_last_error() == b""
 
 
