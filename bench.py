@@ -42,6 +42,10 @@ GROUPED = {
     "c2cli": (1, [32 * 48 * 128], 14,
               "C2 at the CLI's greedy defaults: 196,608 dims, n_steps=30 x 14 bits/step "
               "(miracle_arguments.py:159-165)", 30),
+    "c2low": (1, [32 * 48 * 128], 14,
+              "C2 at the CLI's greedy defaults, low-rate latents (0.06 bits/dim, the PLN "
+              "bench's level 1): ~50 groups of up to 4095 dims, n_steps=30 x 14 bits/step",
+              30, 0.06),
 }
 IMPORTANCE = {
     # name: (images, latent dims, n_bits_per_group, max_group_size_bits, dim_kl_bit_limit, desc)
@@ -94,12 +98,13 @@ def grouped_main(args):
     S.VERBOSE = False
     n_img, dims, bits, desc = GROUPED[args.config][:4]
     n_steps = GROUPED[args.config][4] if len(GROUPED[args.config]) > 4 else 1
+    bpd = GROUPED[args.config][5] if len(GROUPED[args.config]) > 5 else 1.1
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
     lat = []
     for i in range(n_img):
         for li, D in enumerate(dims):
-            q_loc, q_scale, p_loc, p_scale = make_latents(D, seed=1000 * i + li)
+            q_loc, q_scale, p_loc, p_scale = make_latents(D, bits_per_dim=bpd, seed=1000 * i + li)
             lat.append((C.Normal(torch.from_numpy(q_loc).to(dev), torch.from_numpy(q_scale).to(dev)),
                         C.Normal(torch.from_numpy(p_loc).to(dev), torch.from_numpy(p_scale).to(dev))))
 

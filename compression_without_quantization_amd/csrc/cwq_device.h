@@ -223,6 +223,22 @@ __device__ __forceinline__ float wave_max_f32(float v) {
   v = dpp_max_step<0x143, 0xc>(v);  // row_bcast:31 into rows 2, 3: lane 63 holds the max
   return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 63));
 }
+// Sum over each 16-lane DPP row, the same value in all 16 lanes: butterflies
+// (quad xor 1, quad xor 2, half-row mirror, row mirror) pair lanes
+// symmetrically and float addition commutes, so every lane forms the
+// identical ((x0+x1)+(x2+x3)) + ... tree.  Requires a full exec mask.
+template <int CTRL>
+__device__ __forceinline__ float dpp_add_step(float v) {
+  const int o = __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xf, 0xf, false);
+  return v + __builtin_bit_cast(float, o);
+}
+__device__ __forceinline__ float row16_sum_f32(float v) {
+  v = dpp_add_step<0xb1>(v);   // quad_perm [1,0,3,2]
+  v = dpp_add_step<0x4e>(v);   // quad_perm [2,3,0,1]
+  v = dpp_add_step<0x141>(v);  // row_half_mirror: quad 0 <-> quad 1 of each half row
+  v = dpp_add_step<0x140>(v);  // row_mirror: half 0 <-> half 1
+  return v;
+}
 // smallest float >= b (+inf for non-finite b: such a bound never drops anything)
 __device__ __forceinline__ float round_up_f32(double b) {
   if (!(b == b) || b > 3.0e38 || b < -3.0e38) return __builtin_inff();

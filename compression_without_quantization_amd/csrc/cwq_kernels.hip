@@ -613,7 +613,7 @@ __device__ __forceinline__ double block_sum_d(double v, double* red) {
 // off + 12 g, class c at c * csr_cls_stride(d), csr_cls_stride(d) =
 // (d + 6) / 4 + 1 >= U_c + 1; 4 strides <= d + 10 entries.
 __host__ __device__ __forceinline__ int64_t csr_cls_stride(int64_t d) { return (d + 6) / 4 + 1; }
-constexpr int64_t kCsrSortUnits = 512;  // sorted if U_3 <= this (d <= 2045); else natural order
+constexpr int64_t kCsrSortUnits = 2048;  // sorted if U_3 <= this (d <= 8189); else natural order
 
 template <bool STEP0>
 __global__ void __launch_bounds__(256) k_csr_prep(
@@ -622,7 +622,7 @@ __global__ void __launch_bounds__(256) k_csr_prep(
     const float* __restrict__ lognorm, const float* __restrict__ best,
     const int64_t* __restrict__ block_off, int64_t ud, int64_t nb, float2* __restrict__ sab,
     float* __restrict__ bpre, uint32_t* __restrict__ ordu, float4* __restrict__ grp,
-    uint32_t* __restrict__ gtau) {
+    uint32_t* __restrict__ gtau, int64_t coop_min_d) {
   __shared__ double red[256];
   __shared__ double scan[256];
   __shared__ unsigned long long skey[kCsrSortUnits];
@@ -662,8 +662,20 @@ __global__ void __launch_bounds__(256) k_csr_prep(
     }
     const double MX = red[0];
     __syncthreads();
-    const double gam = 1.01 * (double)(d + 1) * 0x1p-24;
-    const double sl = (3.0 * gam + 0x1p-14) * (__builtin_fabs(SM) + SA + SK) + 0x1p-126;
+    // Float summation error of depth h: gamma_h = 1.01 (h + 1) 2^-24 bounds
+    // |fl(sum) - sum| / sum|x| for any summation tree in which every term
+    // passes through at most h roundings.  Two sums of d terms enter the
+    // bound: the screening sum s (sequential over the row: h = d; cooperative
+    // rows: 4 in-lane + 4 butterfly + one per 16-unit chunk, <= 16 + d/64) and
+    // the exact Eigen-order row value (8 strided accumulators, predux, tail:
+    // <= d/8 + 8).  gamma is taken at the larger depth.  The additive margin
+    // 2^-20 covers the float rounding of B_k and of the tests' fma (u |B_k|);
+    // u |s| is covered by the 2^-22 / 2^-14 terms of c1 / c2.
+    const bool coop_blk = d >= coop_min_d;
+    const double h_s = coop_blk ? 16.0 + (double)d / 64.0 : (double)d;
+    const double h_e = (double)d / 8.0 + 8.0;
+    const double gam = 1.01 * ((h_s > h_e ? h_s : h_e) + 1.0) * 0x1p-24;
+    const double sl = (3.0 * gam + 0x1p-20) * (__builtin_fabs(SM) + SA + SK) + 0x1p-126;
     const int64_t reg = off + 12 * g, cs = csr_cls_stride(d);
     // unit u of class c: its sum of C_j and its expected sum of a_j^2 - C_j
     auto unit = [&](int c, int64_t u, double& csum, double& gain) {
@@ -818,6 +830,18 @@ __device__ __forceinline__ float exact_row_wave(
 #ifndef CWQ_CSR_SURVIVOR_CAP
 #define CWQ_CSR_SURVIVOR_CAP 512
 #endif
+#ifndef CWQ_CSR_COOP_ROWS_PER_LANE
+#define CWQ_CSR_COOP_ROWS_PER_LANE 8  // cooperative rows below this many rows per lane ...
+#endif
+#ifndef CWQ_CSR_COOP_TILE
+#define CWQ_CSR_COOP_TILE 128         // smallest tile (candidates) in cooperative launches
+#endif
+#ifndef CWQ_CSR_COOP_TILES
+#define CWQ_CSR_COOP_TILES 6144       // tiles a cooperative launch aims for (4 x 1536 slots)
+#endif
+#ifndef CWQ_CSR_COOP_MIN_D
+#define CWQ_CSR_COOP_MIN_D 256        // ... for blocks of at least this many dims
+#endif
 
 template <bool STEP0>
 __global__ void __launch_bounds__(256, 6) k_encode_prune_csr(
@@ -828,7 +852,7 @@ __global__ void __launch_bounds__(256, 6) k_encode_prune_csr(
     int64_t cand_per_tile, int64_t n_cand, int32_t seed, int64_t block_id_base, int32_t step,
     const float2* __restrict__ sab, const float* __restrict__ bpre,
     const uint32_t* __restrict__ ordu, const float4* __restrict__ grp,
-    uint32_t* __restrict__ gtau, unsigned long long* __restrict__ keys) {
+    uint32_t* __restrict__ gtau, unsigned long long* __restrict__ keys, int64_t coop_min_d) {
   __shared__ double logtab[32];
   __shared__ uint32_t tau_ord;
   __shared__ uint32_t sq_cnt;
@@ -981,10 +1005,112 @@ __global__ void __launch_bounds__(256, 6) k_encode_prune_csr(
         const float tm = wave_max_f32(tau);
         if (lane == 0) atomicMax(&tau_ord, ord_f32(tm));
       };
+      // Cooperative rows (long rows, few rows per lane): each 16-lane DPP row
+      // ("slot") walks one candidate row, lane t taking visit position k + t,
+      // 16 units per iteration.  The partial sums are added over the slot with
+      // a symmetric butterfly (row16_sum_f32), so s, the drop test and the
+      // refill are uniform within the slot; the drop test runs every 16 units.
+      // The bound's float-summation factor is taken at this tree's depth
+      // (k_csr_prep: 4 in-lane + 4 butterfly + one per chunk).
+      auto run_coop = [&](const float2* ab, const float* bp, const uint32_t* od)
+                          __attribute__((always_inline)) {
+        const uint32_t t = lane & 15u, slot = lane >> 4;
+        const uint64_t below = (1ull << (slot * 16u)) - 1ull;  // lanes of lower slots
+        uint32_t wnext = r0 + 4u;
+        uint32_t r = r0 + slot;
+        bool active = r < r1;
+        float s = 0.0f;
+        float tau = unord_f32(tau_ord);
+        uint32_t iter = 0;
+        uint64_t rb;
+        int c, U, cb;
+        auto start_row = [&]() __attribute__((always_inline)) {
+          const uint64_t k0 = (uint64_t)(n0 + (int64_t)r) * (uint64_t)d;
+          rb = k0 >> 2;
+          c = (int)(k0 & 3u);
+          U = (d32 + c + 3) >> 2;
+          cb = c * (int)cs;
+        };
+        start_row();
+        int k = 0;
+        while (__ballot(active) != 0ull) {
+          const int p = k + (int)t;
+          float part = 0.0f;
+          if (active && p < U) {
+            const uint32_t u = od[cb + p];
+            uint32_t kk0 = st.k0, kk1 = st.k1;
+            asm volatile("" : "+s"(kk0), "+s"(kk1));
+            const uint64_t blk = rb + u;
+            const U4 x = philox10_dev((uint32_t)blk, (uint32_t)(blk >> 32), st.c2, st.c3, kk0, kk1);
+            F4 z;
+            box_muller_screen(x.x, x.y, z.a, z.b);
+            box_muller_screen(x.z, x.w, z.c, z.d);
+            const int jp = 4 * (int)u - c + 4;
+            const float2 e0 = ab[jp], e1 = ab[jp + 1], e2 = ab[jp + 2], e3 = ab[jp + 3];
+            const float a0 = __builtin_fmaf(e0.x, z.a, e0.y);
+            const float a1 = __builtin_fmaf(e1.x, z.b, e1.y);
+            const float a2 = __builtin_fmaf(e2.x, z.c, e2.y);
+            const float a3 = __builtin_fmaf(e3.x, z.d, e3.y);
+            part = -(a0 * a0);
+            part = __builtin_fmaf(-a1, a1, part);
+            part = __builtin_fmaf(-a2, a2, part);
+            part = __builtin_fmaf(-a3, a3, part);
+          }
+#ifdef CWQ_PRUNE_STATS
+          if (active && p < U) atomicAdd(&g_prune_stats[43], 1ull);
+#endif
+          s = s + row16_sum_f32(part);
+          k = (k + 16 < U) ? k + 16 : U;
+          const bool complete = k == U;
+          const float upper = __builtin_fmaf(s, gc.x, bp[cb + k]);
+          const bool prune = !complete && (upper < tau);
+          if (complete && active && upper >= tau) {  // may be the best: keep it
+            const float lower =
+                __builtin_fmaf(s, gc.y, gc.z) - gc.w * __builtin_amdgcn_sqrtf(-s);
+            tau = fmaxf(tau, lower);
+            if (t == 0u) {
+              const uint32_t sl = atomicAdd(&sq_cnt, 1u);
+              if (sl < CWQ_CSR_SURVIVOR_CAP) {  // else: overflow, the tile is redone
+                sq_n[sl] = r;
+                sq_ub[sl] = upper;
+              }
+            }
+          }
+          const bool done = complete || prune || !active;
+#ifdef CWQ_PRUNE_STATS
+          if (t == 0u && active && (complete || prune)) atomicAdd(&g_prune_stats[42], 1ull);
+          if (t == 0u && active && complete) atomicAdd(&g_prune_stats[44], 1ull);
+          if (t == 0u && active && complete && upper >= tau) atomicAdd(&g_prune_stats[45], 1ull);
+          atomicAdd(&g_prune_stats[48], 1ull);
+#endif
+          const uint64_t m = __ballot(done);  // 16 bits per finished slot
+          if (done) {
+            r = wnext + (uint32_t)(__builtin_popcountll(m & below) >> 4);
+            start_row();
+            k = 0;
+            s = 0.0f;
+          }
+          wnext += (uint32_t)(__builtin_popcountll(m) >> 4);
+          active = r < r1;
+          if (((++iter) & CWQ_TAU_SHARE_MASK) == 0u) {  // share with the workgroup
+            const float tm = wave_max_f32(tau);
+            if (lane == 0) atomicMax(&tau_ord, ord_f32(tm));
+            tau = fmaxf(tau, unord_f32(__atomic_load_n(&tau_ord, __ATOMIC_RELAXED)));
+          }
+        }
+        const float tm = wave_max_f32(tau);
+        if (lane == 0) atomicMax(&tau_ord, ord_f32(tm));
+      };
+      const bool coop = d >= coop_min_d;
       // survivor list overflow (near-ties everywhere, or a weak early tau):
       // redo the pass starting from the final tau, then score exactly
       for (int pass = 0;; ++pass) {
-        if (in_lds)
+        if (coop) {
+          if (in_lds)
+            run_coop(l_ab, l_bp, l_ord);
+          else
+            run_coop(sab + off + 8 * g, bpre + reg, ordu + reg);
+        } else if (in_lds)
           run(l_ab, l_bp, l_ord);
         else
           run(sab + off + 8 * g, bpre + reg, ordu + reg);
@@ -1297,23 +1423,36 @@ static void launch_prune_t(const EncodeArgs& a, int step, hipStream_t stream) {
 
 template <bool STEP0>
 static void launch_prune_csr(const EncodeArgs& a, int step, hipStream_t stream) {
-  hipLaunchKernelGGL((k_csr_prep<STEP0>), dim3(grid_for(a.nb, 1, 65536)), dim3(256), 0, stream,
-                     a.t_loc, a.t_scale, a.loc_s, a.scale_s, a.lognorm, a.out_sample,
-                     a.block_off, a.ud, a.nb, a.sab, a.bpre, a.ordu, a.grp, a.gtau);
+
   // own tiling: ~8192 tiles of >= 1024 candidates; tiles of a block share tau
-  // through gtau, and later tiles start from it
-  int64_t tpb = (8192 + a.nb - 1) / a.nb;
-  const int64_t max_tpb = a.n_cand / 1024 > 1 ? a.n_cand / 1024 : 1;
+  // through gtau, and later tiles start from it.  With few rows per lane (a
+  // few large groups: the whole chip holds 1536 x 256 lanes) long rows are
+  // walked cooperatively by 16 lanes instead, in tiles of >= 128 candidates.
+  const int64_t kLanes = 1536 * 256;
+  const int64_t rows = a.nb * a.n_cand;
+  const bool coop = rows < CWQ_CSR_COOP_ROWS_PER_LANE * kLanes;
+  int64_t tpb, max_tpb;
+  if (coop) {
+    tpb = (CWQ_CSR_COOP_TILES + a.nb - 1) / a.nb;
+    max_tpb = a.n_cand / CWQ_CSR_COOP_TILE > 1 ? a.n_cand / CWQ_CSR_COOP_TILE : 1;
+  } else {
+    tpb = (8192 + a.nb - 1) / a.nb;
+    max_tpb = a.n_cand / 1024 > 1 ? a.n_cand / 1024 : 1;
+  }
   tpb = tpb < max_tpb ? tpb : max_tpb;
   const int64_t cpt = (a.n_cand + tpb - 1) / tpb;
   const int64_t ntiles = a.nb * tpb;
+  const int64_t coop_min_d = coop ? (int64_t)CWQ_CSR_COOP_MIN_D : INT64_MAX;
+  hipLaunchKernelGGL((k_csr_prep<STEP0>), dim3(grid_for(a.nb, 1, 65536)), dim3(256), 0, stream,
+                     a.t_loc, a.t_scale, a.loc_s, a.scale_s, a.lognorm, a.out_sample,
+                     a.block_off, a.ud, a.nb, a.sab, a.bpre, a.ordu, a.grp, a.gtau, coop_min_d);
   constexpr int64_t kGrid = 1 << 20;
   const unsigned grid = (unsigned)(ntiles < kGrid ? ntiles : kGrid);
   hipLaunchKernelGGL((k_encode_prune_csr<STEP0>), dim3(grid), dim3(256), 0, stream, a.t_loc,
                      a.t_scale, a.loc_s, a.scale_s, a.lognorm, a.out_sample, a.block_off, a.ud,
                      ntiles, tpb, cpt, a.n_cand, a.seed, a.block_id_base, step,
                      (const float2*)a.sab, (const float*)a.bpre, (const uint32_t*)a.ordu,
-                     (const float4*)a.grp, a.gtau, a.keys);
+                     (const float4*)a.grp, a.gtau, a.keys, coop_min_d);
 }
 
 template <bool STEP0>

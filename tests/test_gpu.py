@@ -706,3 +706,30 @@ def test_uniform_odd_d_general_pruned(cwq, cwqlib, oracle, d, bits, nb):
         gi, gs = _uniform_encode(cwq, cwqlib, tl, ts, pl, ps, d, bits, 2, 11, 1.0, mode)
         assert np.array_equal(gi, wi), (d, mode)
         _assert_bits_equal(gs, ws, f"uniform d={d} mode {mode}")
+
+
+@pytest.mark.parametrize("sizes,bits,n_steps,kind", [
+    ([4095, 2000, 300, 257], 14, 2, "normal"),   # few long rows: cooperative 16-lane rows
+    ([1500, 255, 256, 40], 13, 3, "normal"),     # coop and per-lane rows in one launch
+    ([600] * 3, 14, 1, "flat"),                  # near-ties: survivor overflow, redo, exact
+    ([700, 900], 12, 2, "heavy"),
+])
+def test_csr_cooperative_rows_vs_oracle(cwq, cwqlib, oracle, sizes, bits, n_steps, kind):
+    rng = np.random.default_rng(sum(sizes) * bits)
+    off = np.concatenate([[0], np.cumsum(sizes)]).astype(np.int64)
+    D = int(off[-1])
+    if kind == "heavy":
+        tl, ts, pl, ps = _heavy_inputs(rng, D)
+    else:
+        tl = rng.standard_normal(D).astype(np.float32)
+        ts = rng.uniform(0.2, 1.0, D).astype(np.float32)
+        pl = (0.1 * rng.standard_normal(D)).astype(np.float32)
+        ps = rng.uniform(0.8, 1.2, D).astype(np.float32)
+        if kind == "flat":
+            ts = np.full(D, 1e3, np.float32)
+            tl = np.zeros(D, np.float32)
+    wi, ws = oracle.greedy_encode(tl, ts, pl, ps, off, bits, n_steps, 42, 1.0)
+    for mode in (0, 2):
+        gi, gs = _csr_encode(cwq, cwqlib, tl, ts, pl, ps, off, bits, n_steps, 42, 1.0, mode)
+        assert np.array_equal(gi, wi), (kind, mode, gi.reshape(-1)[:8], wi.reshape(-1)[:8])
+        _assert_bits_equal(gs, ws, f"coop {kind} mode {mode}")

@@ -14,9 +14,10 @@ import bench
 cfg = sys.argv[1] if len(sys.argv) > 1 else "c2cli"
 n_img, dims, bits, desc = bench.GROUPED[cfg][:4]
 n_steps = bench.GROUPED[cfg][4] if len(bench.GROUPED[cfg]) > 4 else 1
+bpd = bench.GROUPED[cfg][5] if len(bench.GROUPED[cfg]) > 5 else 1.1
 S.VERBOSE = False
 lib = _lib.load()
-q = [torch.from_numpy(a).cuda() for a in make_latents(dims[0])]
+q = [torch.from_numpy(a).cuda() for a in make_latents(dims[0], bits_per_dim=bpd)]
 tgt, prop = C.Normal(q[0], q[1]), C.Normal(q[2], q[3])
 out = (ctypes.c_ulonglong * 72)()
 lib.cwq_debug_prune_stats(out, 1)

@@ -1,0 +1,6 @@
+set -o pipefail
+timeout -k 10 900 python -u -m pytest tests/test_gpu.py tests/test_pln_gpu.py -x -v --timeout 300 --timeout-method thread -k "csr or coop or odd_d or grouped or c2_image or codec" > gpurun_out/t_coop.log 2>&1 && \
+CWQ_LIB_PATH=$PWD/tools/variants/libcwq_stats.so timeout -k 10 300 python -u tools/csr_stats.py c2low > gpurun_out/csrstats2.log 2>&1 && \
+timeout -k 10 300 python -u bench.py --config c2low --steps 2 --warmup 1 >> gpurun_out/csrstats2.log 2>&1 && \
+timeout -k 10 300 python -u bench.py --config c2cli --steps 2 --warmup 1 >> gpurun_out/csrstats2.log 2>&1 && \
+timeout -k 10 300 python -u bench.py --config pln --steps 2 --warmup 1 >> gpurun_out/csrstats2.log 2>&1

@@ -10,15 +10,17 @@ declare -A V=(
   [base]=""
   [stats]="-DCWQ_PRUNE_STATS"
   [phases]="-DCWQ_PHASE_TIMES"
-  [g255]="-DCWQ_CSR_GTAU_SHARE=1 -DCWQ_CSR_GTAU_MASK=255u"
-  [g1023]="-DCWQ_CSR_GTAU_SHARE=1 -DCWQ_CSR_GTAU_MASK=1023u"
-  [mask7]="-DCWQ_TAU_SHARE_MASK=7u"
+  [nocoop]="-DCWQ_CSR_COOP_ROWS_PER_LANE=0"
+  [coop64]="-DCWQ_CSR_COOP_ROWS_PER_LANE=64"
+  [t64]="-DCWQ_CSR_COOP_TILE=64 -DCWQ_CSR_COOP_TILES=12288"
+  [t256]="-DCWQ_CSR_COOP_TILE=256 -DCWQ_CSR_COOP_TILES=3072"
+  [mind128]="-DCWQ_CSR_COOP_MIN_D=128 -DCWQ_CSR_COOP_ROWS_PER_LANE=64"
 )
 if [ "$1" = build ]; then
   mkdir -p $OUT
   for k in "${!V[@]}"; do
     [ "${V[$k]}" = prebuilt ] && continue  # built by hand from an older commit
-    hipcc $FLAGS ${V[$k]} -o $OUT/libcwq_$k.so $CSRC/cwq_kernels.hip $CSRC/cwq_importance.hip $CSRC/cwq_capi.hip $CSRC/cwq_ac.cpp &
+    hipcc $FLAGS ${V[$k]} -o $OUT/libcwq_$k.so $CSRC/cwq_kernels.hip $CSRC/cwq_importance.hip $CSRC/cwq_pln.hip $CSRC/cwq_capi.hip $CSRC/cwq_ac.cpp &
   done
   wait
 else
@@ -26,6 +28,6 @@ else
     [ "$k" = stats ] && continue  # counters only: tools/prune_stats.py
     [ "$k" = phases ] && continue  # host phase timings only
     echo "== $k ${V[$k]}"
-    CWQ_LIB_PATH=$PWD/$OUT/libcwq_$k.so timeout -k 10 300 python -u bench.py --no-cpu --no-e2e --steps 2 --warmup 1 $BENCH_ARGS | python -c "import json,sys; d=json.loads(sys.stdin.read()); print(d['value'], d['ms_per_step'], d.get('roofline', {}).get('kernel_ms'))"
+    CWQ_LIB_PATH=$PWD/$OUT/libcwq_$k.so timeout -k 10 300 python -u bench.py --no-cpu --no-e2e --steps 2 --warmup 1 $BENCH_ARGS | tail -1 | python -c "import json,sys; d=json.loads(sys.stdin.read()); print(d['value'], d['ms_per_step'], d.get('roofline', {}).get('kernel_ms'))"
   done
 fi
