@@ -111,6 +111,20 @@ class SignalConv2D(nn.Module):
         return y if self.activation is None else self.activation(y)
 
 
+def _deterministic_convs(fn):
+    """Run fn with deterministic convolution algorithms and no autotuning.
+    Encoder and decoder must derive the level-1 prior bit-identically
+    (SynthesisTransform_2 of the level-2 sample), so the convolution algorithm
+    must not change between calls."""
+    import functools
+
+    @functools.wraps(fn)
+    def wrapped(*a, **k):
+        with torch.backends.cudnn.flags(enabled=True, benchmark=False, deterministic=True):
+            return fn(*a, **k)
+    return wrapped
+
+
 def _leaky_relu(x):
     return F.leaky_relu(x, LEAKY_RELU_ALPHA)
 
@@ -385,6 +399,7 @@ class ProbabilisticLadderNetwork(nn.Module):
         return x.permute(0, 3, 1, 2).contiguous().to(device)
 
     @torch.no_grad()
+    @_deterministic_convs
     def latent_distributions(self, image, seed):
         """pln.py:150-190 for one NHWC image: returns dict with NCHW tensors
         q1 (posterior_1), q2 (posterior_2) and the level-1 prior used to form q1."""
@@ -410,6 +425,7 @@ class ProbabilisticLadderNetwork(nn.Module):
     # -- codec (pln.py:213-627) ----------------------------------------------
 
     @torch.no_grad()
+    @_deterministic_convs
     def code_image_greedy(self, session, image, seed, n_steps=30, n_bits_per_step=14,
                           greedy_max_group_size_bits=12, comp_file_path=None,
                           backfitting_steps_level_1=0, backfitting_steps_level_2=0,
@@ -559,6 +575,7 @@ class ProbabilisticLadderNetwork(nn.Module):
     # -- decoder (pln.py:638-817) ----------------------------------------------
 
     @torch.no_grad()
+    @_deterministic_convs
     def decode_image_greedy(self, session, comp_file_path, use_importance_sampling=True, rho=1.,
                             use_permutation=True, second_level_group_dist_counts="",
                             first_level_group_dist_counts="", second_level_sample_ac=None,
