@@ -409,6 +409,11 @@ class ProbabilisticLadderNetwork(nn.Module):
         loc2, scale2 = self.analysis_transform_2(loc1)                 # :157
         z2 = stateless_normal_sample(loc2, scale2, 1, int(seed) - 2)[0]  # :157 (seeded)
         ploc1, pscale1 = self.synthesis_transform_2(z2)                # :161
+        if ploc1.shape != loc1.shape:
+            raise ValueError(
+                "level-1 likelihood {} and prior {} do not have the same shape: the ladder "
+                "needs image sides that are multiples of 64 (the reference fails here too, "
+                "pln.py:165-185)".format(tuple(loc1.shape), tuple(ploc1.shape)))
         qloc1, qscale1 = posterior_combine(loc1, scale1, ploc1, pscale1)  # :165-185
         return {"q1": Normal(qloc1, qscale1), "q2": Normal(loc2, scale2),
                 "p1_call": Normal(ploc1, pscale1), "image_shape": tuple(image_shape(image))}

@@ -206,3 +206,39 @@ def test_return_flags(P):
     assert len(ind2) == len(gi2) - 1 and min(ind2) >= 1
     gi1 = model.code_image_greedy(None, img, 3, return_first_level_group_sizes=True, **KW)
     assert gi1[0] == 0 and gi1[-1] == 32 * 4 * 4
+
+
+def test_codec_rejects_grid_mismatch(P):
+    """Sizes that are not multiples of 64: TF 'same' padding rounds the level-1
+    grid up (100x150 -> 7x10) but SynthesisTransform_2 returns 4x the level-2
+    grid (8x12); the reference fails combining them (pln.py:165-185), so does
+    this codec, with a clear message."""
+    model = _model(P, seed=6)
+    with pytest.raises(ValueError, match="same shape"):
+        model.code_image_greedy(None, _image(100, 150, seed=6), 5, **KW)
+
+
+@pytest.mark.parametrize("hw,use_perm,level1", [((64, 320), False, "greedy"),
+                                                 ((192, 64), False, "importance")])
+def test_codec_no_permutation(P, oracle, tmp_path, hw, use_perm, level1):
+    """use_permutation=False (identity permutation) round trips bit-exactly,
+    on non-square grids."""
+    model = _model(P, seed=6)
+    img = _image(*hw, seed=6)
+    path = str(tmp_path / "np.miracle")
+    imp = level1 == "importance"
+    (s2, s1), summ = model.code_image_greedy(None, img, 5, comp_file_path=path,
+                                             use_permutation=use_perm,
+                                             use_importance_sampling=imp, **KW)
+    shape1 = tuple(model.latent_distributions(img, 5)["q1"].loc.shape)
+    rec = model.decode_image_greedy(None, path, use_importance_sampling=imp,
+                                    use_permutation=use_perm, first_level_max_group_size_bits=4,
+                                    second_level_max_group_size_bits=2)
+    assert rec.shape == (hw[0], hw[1], 3)
+    if not imp:
+        z1 = P.unpermute_unflatten(torch.from_numpy(s1).cuda(), None, shape1)
+        with torch.no_grad():
+            want = model.synthesis_transform_1(z1)[0].permute(1, 2, 0).cpu().numpy()
+        _eq(rec, want, "reconstruction")
+    else:
+        assert np.isfinite(rec).all()

@@ -15,6 +15,10 @@ declare -A V=(
   [t64]="-DCWQ_CSR_COOP_TILE=64 -DCWQ_CSR_COOP_TILES=12288"
   [t256]="-DCWQ_CSR_COOP_TILE=256 -DCWQ_CSR_COOP_TILES=3072"
   [mind128]="-DCWQ_CSR_COOP_MIN_D=128 -DCWQ_CSR_COOP_ROWS_PER_LANE=64"
+  [mask7]="-DCWQ_TAU_SHARE_MASK=7u"
+  [mask31]="-DCWQ_TAU_SHARE_MASK=31u"
+  [cap512]="-DCWQ_SURVIVOR_CAP=512"
+  [w7]="-DCWQ_PRUNE_MIN_WAVES=7"
 )
 if [ "$1" = build ]; then
   mkdir -p $OUT
