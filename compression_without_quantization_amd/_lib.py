@@ -50,6 +50,10 @@ SIGNATURES = {
                                       c_vp]),
     "cwq_importance_group_starts": (c_i64, [c_vp, c_i64, c_i64, c_f64, c_vp, c_i64]),
     "cwq_importance_plan": (c_int, [c_vp, c_vp, c_i64, c_vp]),
+    "cwq_code_grouped_importance_workspace_size": (c_size, [c_i64]),
+    "cwq_code_grouped_importance": (c_i64, [c_vp, c_vp, c_vp, c_vp, c_i64, c_i32, c_f32, c_i64,
+                                            c_f64, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp,
+                                            c_vp, c_vp, c_size, c_vp]),
     "cwq_ac_encode": (c_i64, [c_vp, c_i64, c_int, c_vp, c_i64, c_vp, c_i64]),
     "cwq_ac_decode": (c_i64, [c_vp, c_i64, c_int, c_vp, c_i64, c_vp, c_i64]),
     "cwq_elias_delta_encode": (c_i64, [c_vp, c_i64, c_vp, c_i64]),

@@ -21,6 +21,8 @@ Deliberate differences from the TF1 reference:
     (:294 mutates it);
   * results are concrete values; `sess` is accepted and ignored.
 """
+import ctypes
+
 import numpy as np
 import torch
 
@@ -30,6 +32,7 @@ from .binary_io import (elias_delta_code, elias_delta_code_many, elias_delta_dec
 from .coded_greedy_sampler import _device_of, _f32, _is_float32, _like_input, _ptr
 
 VERBOSE = True
+USE_FUSED = True   # code_grouped_importance_sample in one native call (tests compare both paths)
 QUANT_MIN, QUANT_MAX = -30.0, 30.0
 
 
@@ -202,6 +205,10 @@ def code_grouped_importance_sample(sess, target, proposal, seed, n_bits_per_grou
     p_loc, p_scale = _f32(proposal.loc, dev, "proposal.loc"), _f32(proposal.scale, dev,
                                                                    "proposal.scale")
     D = p_loc.numel()
+    if USE_FUSED and D > 0 and not (return_group_indices_only or return_indices_only):
+        return _code_grouped_fused(lib, dev, q_loc, q_scale, p_loc, p_scale, D, seed,
+                                   n_bits_per_group, max_group_size_bits, dim_kl_bit_limit,
+                                   return_indices)
     zeros = torch.zeros(D, dtype=torch.float32, device=dev)
     ones = torch.ones(D, dtype=torch.float32, device=dev)
     # :137-138 standardise
@@ -247,6 +254,45 @@ def code_grouped_importance_sample(sess, target, proposal, seed, n_bits_per_grou
         return sample_h, indices, group_start_indices, outlier_extras
     bitcode = elias_delta_code_many(indices)
     return sample_h, bitcode, group_start_indices, outlier_extras
+
+
+def _code_grouped_fused(lib, dev, q_loc, q_scale, p_loc, p_scale, D, seed, n_bits_per_group,
+                        max_group_size_bits, dim_kl_bit_limit, return_indices):
+    """The common path of code_grouped_importance_sample in one native call
+    (cwq_code_grouped_importance); same results as the step-by-step path."""
+    need = int(lib.cwq_code_grouped_importance_workspace_size(D))
+    ws = torch.empty(max(need, 1), dtype=torch.uint8, device=dev)
+    sample_h = np.empty(max(D, 1), dtype=np.float32)
+    index_h = np.empty(D + 2, dtype=np.int64)
+    starts_h = np.empty(D + 2, dtype=np.int64)
+    out_i = np.empty(max(D, 1), dtype=np.int64)
+    out_v = np.empty(max(D, 1), dtype=np.float32)
+    n_out = np.zeros(1, dtype=np.int64)
+    kl_sum = ctypes.c_double(0.0)
+    seed32 = int(np.int32(np.uint32(int(seed) & 0xFFFFFFFF)))
+    G = _lib.check(lib.cwq_code_grouped_importance(
+        _ptr(q_loc), _ptr(q_scale), _ptr(p_loc), _ptr(p_scale), D, seed32,
+        float(np.float32(dim_kl_bit_limit)), importance_group_size_threshold(max_group_size_bits),
+        float(n_bits_per_group * np.log(2) - 1), sample_h.ctypes.data, index_h.ctypes.data,
+        starts_h.ctypes.data, starts_h.size, out_i.ctypes.data, out_v.ctypes.data,
+        n_out.ctypes.data, ctypes.byref(kl_sum) if VERBOSE else None, ws.data_ptr(), ws.numel(),
+        _stream(dev)),
+        "cwq_code_grouped_importance")
+    if VERBOSE:
+        total_kl_bits = kl_sum.value / np.log(2)
+        print("Total KL to split up: {:.2f} bits, "
+              "maximum bits per group: {}, "
+              "estimated number of groups: {},"
+              "coding {} dimensions".format(total_kl_bits, n_bits_per_group,
+                                            total_kl_bits // n_bits_per_group + 1, D))
+    no = int(n_out[0])
+    outlier_extras = (out_i[:no].copy(), quantize_quint16(out_v[:no]))
+    group_start_indices = starts_h[:G + 1].copy()
+    indices = tuple(int(v) + 1 for v in index_h[:G])
+    sample_h = sample_h[:D].copy()
+    if return_indices:
+        return sample_h, indices, group_start_indices, outlier_extras
+    return sample_h, elias_delta_code_many(indices), group_start_indices, outlier_extras
 
 
 def _group_kls(kl_divs, starts):

@@ -641,6 +641,171 @@ int64_t cwq_code_grouped_greedy(const float* q_loc, const float* q_scale, const 
   return G;
 }
 
+// ---------------------------------------------------------------------------
+// code_grouped_importance_sample (coded_importance_sampler.py:112-274) in one
+// call: device standardisation, KL and outlier masking, the seeded outlier
+// target draw, host partition and sample-count plan, one CSR encode launch,
+// device destandardisation.  Elias-delta strings and quint16 packing stay with
+// the caller (host, cheap).
+// ---------------------------------------------------------------------------
+namespace {
+struct GroupedImpWs {
+  size_t t_loc, t_scale, kl, kl2, zeros, ones, tsamp, sample, out, keep, offs, nsamp, idx, enc,
+      total;
+};
+GroupedImpWs grouped_imp_ws(int64_t D) {
+  GroupedImpWs l;
+  size_t o = 0;
+  auto take = [&](size_t bytes) {
+    const size_t at = o;
+    o = align_up(o + bytes, 256);
+    return at;
+  };
+  const size_t n = (size_t)(D > 0 ? D : 0);
+  l.t_loc = take(n * 4);
+  l.t_scale = take(n * 4);
+  l.kl = take(n * 4);
+  l.kl2 = take(n * 4);
+  l.zeros = take(n * 4);
+  l.ones = take(n * 4);
+  l.tsamp = take(n * 4);
+  l.sample = take(n * 4);
+  l.out = take(n * 4);
+  l.keep = take(n);
+  l.offs = take((n + 2) * 8);
+  l.nsamp = take((n + 1) * 8);
+  l.idx = take((n + 1) * 8);
+  l.enc = take(cwq::importance_workspace_size(D + 1, D));
+  l.total = o;
+  return l;
+}
+thread_local std::vector<float> g_imp_kl, g_imp_ts, g_imp_out;
+thread_local std::vector<uint8_t> g_imp_keep;
+thread_local std::vector<int64_t> g_imp_ns;
+}  // namespace
+
+size_t cwq_code_grouped_importance_workspace_size(int64_t D) {
+  if (D < 0) return 0;
+  return grouped_imp_ws(D).total;
+}
+
+int64_t cwq_code_grouped_importance(const float* q_loc, const float* q_scale,
+                                    const float* p_loc, const float* p_scale, int64_t D,
+                                    int32_t seed, float dim_kl_bit_limit, int64_t size_threshold,
+                                    double n_nats, float* sample_host, int64_t* index_host,
+                                    int64_t* starts_host, int64_t starts_cap,
+                                    int64_t* outlier_idx_host, float* outlier_val_host,
+                                    int64_t* n_outliers, double* kl_sum_out, void* workspace,
+                                    size_t workspace_bytes, void* stream) {
+  if (D < 0) return fail(CWQ_ERR_INVALID, "cwq_code_grouped_importance: negative size");
+  if (D > 0 && (!q_loc || !q_scale || !p_loc || !p_scale || !sample_host || !index_host ||
+                !outlier_idx_host || !outlier_val_host))
+    return fail(CWQ_ERR_INVALID, "cwq_code_grouped_importance: null pointer");
+  if (!n_outliers) return fail(CWQ_ERR_INVALID, "cwq_code_grouped_importance: null pointer");
+  if (!starts_host || starts_cap < D + 2)
+    return fail(CWQ_ERR_CAPACITY, "cwq_code_grouped_importance: starts_cap must be >= D + 2");
+  const GroupedImpWs l = grouped_imp_ws(D);
+  if (workspace_bytes < l.total || !workspace)
+    return fail(CWQ_ERR_WORKSPACE, "workspace %zu bytes < required %zu", workspace_bytes,
+                l.total);
+  hipStream_t s = (hipStream_t)stream;
+  char* w = (char*)workspace;
+  float* t_loc = (float*)(w + l.t_loc);
+  float* t_scale = (float*)(w + l.t_scale);
+  float* kl = (float*)(w + l.kl);
+  float* kl2 = (float*)(w + l.kl2);
+  float* zeros = (float*)(w + l.zeros);
+  float* ones = (float*)(w + l.ones);
+  float* tsamp = (float*)(w + l.tsamp);
+  float* sample = (float*)(w + l.sample);
+  float* out = (float*)(w + l.out);
+  uint8_t* keep = (uint8_t*)(w + l.keep);
+  int64_t* offs = (int64_t*)(w + l.offs);
+  int64_t* nsamp = (int64_t*)(w + l.nsamp);
+  int64_t* idx = (int64_t*)(w + l.idx);
+  hipError_t e = hipSuccess;
+  int rc;
+  *n_outliers = 0;
+  if (D == 0) {
+    starts_host[0] = 0;
+    return ok();
+  }
+  // :137-138 standardise; :142 KL(target || proposal); :144-148 outliers
+  if ((rc = cwq_standardise(q_loc, q_scale, p_loc, p_scale, D, t_loc, t_scale, stream)) < 0)
+    return rc;
+  if ((rc = cwq_kl_normal_normal(q_loc, q_scale, p_loc, p_scale, D, kl, stream)) < 0) return rc;
+  if ((e = cwq::launch_imp_outliers(kl, D, dim_kl_bit_limit, t_loc, t_scale, keep, s)) !=
+      hipSuccess)
+    return hip_fail(e, "outliers");
+  // :150 the outlier dims' target draw, seeded [seed - 1, 42]
+  const int32_t s1 = (int32_t)((uint32_t)seed - 1u);
+  if ((rc = cwq_stateless_normal_sample(q_loc, q_scale, D, 1, s1, tsamp, stream)) < 0) return rc;
+  // :160-163 KL of the standardised target against N(0, 1)
+  if ((e = hipMemsetAsync(zeros, 0, (size_t)D * 4, s)) != hipSuccess) return hip_fail(e, "memset");
+  if ((e = hipMemsetD32Async((hipDeviceptr_t)ones, 0x3f800000u, (size_t)D, s)) != hipSuccess)
+    return hip_fail(e, "memset");
+  if ((rc = cwq_kl_normal_normal(t_loc, t_scale, zeros, ones, D, kl2, stream)) < 0) return rc;
+  g_imp_kl.resize((size_t)D);
+  g_imp_keep.resize((size_t)D);
+  g_imp_ts.resize((size_t)D);
+  if ((e = hipMemcpyAsync(g_imp_kl.data(), kl2, (size_t)D * 4, hipMemcpyDeviceToHost, s)) !=
+          hipSuccess ||
+      (e = hipMemcpyAsync(g_imp_keep.data(), keep, (size_t)D, hipMemcpyDeviceToHost, s)) !=
+          hipSuccess ||
+      (e = hipMemcpyAsync(g_imp_ts.data(), tsamp, (size_t)D * 4, hipMemcpyDeviceToHost, s)) !=
+          hipSuccess)
+    return hip_fail(e, "to host");
+  if ((e = hipStreamSynchronize(s)) != hipSuccess) return hip_fail(e, "sync");
+  int64_t no = 0;
+  for (int64_t j = 0; j < D; ++j)
+    if (!g_imp_keep[(size_t)j]) {
+      outlier_idx_host[no] = j;
+      outlier_val_host[no] = g_imp_ts[(size_t)j];
+      ++no;
+    }
+  *n_outliers = no;
+  if (kl_sum_out) {  // log line only
+    double t = 0.0;
+    for (int64_t j = 0; j < D; ++j) t += (double)g_imp_kl[(size_t)j];
+    *kl_sum_out = t;
+  }
+  // :164-203 the sequential partition (strict >), :48-51 ceil(exp(sum KL)) per group
+  const int64_t n = group_starts_impl(g_imp_kl.data(), D, size_threshold, n_nats, starts_host,
+                                      starts_cap, true);
+  if (n < 0) return n;
+  const int64_t G = n - 1;
+  g_imp_ns.resize((size_t)(G > 0 ? G : 1));
+  if ((rc = cwq_importance_plan(g_imp_kl.data(), starts_host, G, g_imp_ns.data())) < 0)
+    return rc;
+  if (G > 0) {
+    if ((e = hipMemcpyAsync(offs, starts_host, (size_t)(G + 1) * 8, hipMemcpyHostToDevice, s)) !=
+            hipSuccess ||
+        (e = hipMemcpyAsync(nsamp, g_imp_ns.data(), (size_t)G * 8, hipMemcpyHostToDevice, s)) !=
+            hipSuccess)
+      return hip_fail(e, "plan to device");
+    // :212-245 every group's importance coder, seed + g
+    if ((rc = cwq_importance_encode(t_loc, t_scale, zeros, ones, offs, nsamp, G, D, seed, 0, idx,
+                                    sample, w + l.enc, workspace_bytes - l.enc, stream)) < 0)
+      return rc;
+  } else {
+    if ((e = hipMemsetAsync(sample, 0, (size_t)D * 4, s)) != hipSuccess)
+      return hip_fail(e, "memset");
+  }
+  // :265 rescale, :267 outliers keep their target draw
+  if ((rc = cwq_destandardise(sample, p_loc, p_scale, D, out, stream)) < 0) return rc;
+  g_imp_out.resize((size_t)D);
+  if ((G > 0 && (e = hipMemcpyAsync(index_host, idx, (size_t)G * 8, hipMemcpyDeviceToHost, s)) !=
+                    hipSuccess) ||
+      (e = hipMemcpyAsync(g_imp_out.data(), out, (size_t)D * 4, hipMemcpyDeviceToHost, s)) !=
+          hipSuccess)
+    return hip_fail(e, "to host");
+  if ((e = hipStreamSynchronize(s)) != hipSuccess) return hip_fail(e, "sync");
+  for (int64_t j = 0; j < D; ++j)
+    sample_host[j] = g_imp_keep[(size_t)j] ? g_imp_out[(size_t)j] : g_imp_ts[(size_t)j];
+  cwq::set_error(CWQ_OK, "");
+  return G;
+}
+
 int64_t cwq_group_starts(const float* kl, int64_t D, int64_t size_threshold, double n_nats,
                          int64_t* starts, int64_t cap) {
   return group_starts_impl(kl, D, size_threshold, n_nats, starts, cap, false);

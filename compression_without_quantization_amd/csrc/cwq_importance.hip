@@ -407,6 +407,35 @@ __global__ void __launch_bounds__(256) k_imp_rows(
   }
 }
 
+// :142-145, :148: per-dim KL in bits against dim_kl_bit_limit (float32, as
+// numpy compares the float32 array); outlier dims get the standard target
+// N(0, 1) (t_loc = 0, t_scale = 1).  keep[j] = 1 for coded dims.
+__global__ void __launch_bounds__(256) k_imp_outliers(const float* __restrict__ kl, int64_t n,
+                                                      float limit, float* __restrict__ t_loc,
+                                                      float* __restrict__ t_scale,
+                                                      uint8_t* __restrict__ keep) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const float bits = kl[i] / 0.6931472f;  // kl / np.float32(np.log(2))
+    const bool k = bits <= limit;           // NaN: an outlier, as in numpy
+    if (!k) {
+      t_loc[i] = 0.0f;
+      t_scale[i] = 1.0f;
+    }
+    keep[i] = k ? 1 : 0;
+  }
+}
+
+hipError_t launch_imp_outliers(const float* kl, int64_t n, float limit, float* t_loc,
+                               float* t_scale, uint8_t* keep, hipStream_t stream) {
+  if (n <= 0) return hipSuccess;
+  int64_t g = (n + 255) / 256;
+  g = g < 8192 ? g : 8192;
+  hipLaunchKernelGGL(k_imp_outliers, dim3((unsigned)g), dim3(256), 0, stream, kl, n, limit,
+                     t_loc, t_scale, keep);
+  return hipGetLastError();
+}
+
 size_t importance_workspace_size(int64_t nb, int64_t total_dims) {
   auto up = [](size_t v) { return (v + 255) / 256 * 256; };
   return up((size_t)nb * 8) + up((size_t)(nb + 1) * 8) + 2 * up((size_t)total_dims * 4) +

@@ -61,6 +61,8 @@ hipError_t launch_destandardise(const float* sample, const float* p_loc, const f
                                 int64_t n, float* out, hipStream_t stream);
 
 size_t importance_workspace_size(int64_t nb, int64_t total_dims);
+hipError_t launch_imp_outliers(const float* kl, int64_t n, float limit, float* t_loc,
+                               float* t_scale, uint8_t* keep, hipStream_t stream);
 hipError_t launch_importance_encode(const float* t_loc, const float* t_scale, const float* p_loc,
                                     const float* p_scale, const int64_t* block_off,
                                     const int64_t* n_samples, int64_t nb, int64_t total_dims,

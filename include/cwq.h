@@ -193,6 +193,29 @@ int64_t cwq_importance_group_starts(const float* kl, int64_t D, int64_t size_thr
  * Eigen inner-dim order))), for groups [starts[g], starts[g+1]) of HOST kl. */
 int cwq_importance_plan(const float* kl, const int64_t* starts, int64_t ng, int64_t* n_samples);
 
+/* coded_importance_sampler.py:112-274 code_grouped_importance_sample in one
+ * call (the counterpart of cwq_code_grouped_greedy): device standardisation,
+ * KL and outlier masking (kl / ln 2 > dim_kl_bit_limit, float32), the seeded
+ * outlier target draw q_loc + q_scale z, z from [seed - 1, 42],
+ * the host partition (size_threshold and n_nats as cwq_importance_group_starts)
+ * and sample-count plan, one encode launch, device destandardisation.
+ * Device inputs; HOST outputs: sample_host [D] (outlier dims hold the target
+ * draw, :267), index_host [G] (argmax index, the reference codes index + 1),
+ * starts_host (group starts incl. the trailing D; starts_cap >= D + 2), the
+ * outlier dims and their unquantised draws (outlier_*_host, capacity D,
+ * *n_outliers of them), and optionally (kl_sum_out) the total standardised KL
+ * in nats for the reference's log line.  Returns G or a negative error code.
+ * Blocks the host until the results are on it. */
+size_t cwq_code_grouped_importance_workspace_size(int64_t D);
+int64_t cwq_code_grouped_importance(const float* q_loc, const float* q_scale,
+                                    const float* p_loc, const float* p_scale, int64_t D,
+                                    int32_t seed, float dim_kl_bit_limit, int64_t size_threshold,
+                                    double n_nats, float* sample_host, int64_t* index_host,
+                                    int64_t* starts_host, int64_t starts_cap,
+                                    int64_t* outlier_idx_host, float* outlier_val_host,
+                                    int64_t* n_outliers, double* kl_sum_out, void* workspace,
+                                    size_t workspace_bytes, void* stream);
+
 /* ---- Arithmetic coder (code/coding.pyx:27-310), HOST functions ---------- */
 /* ArithmeticCoder(P, precision).encode(message): writes the code as '0'/'1'
  * chars to out_bits (if non-null, at most cap) and returns the number of bits

@@ -733,3 +733,36 @@ def test_csr_cooperative_rows_vs_oracle(cwq, cwqlib, oracle, sizes, bits, n_step
         gi, gs = _csr_encode(cwq, cwqlib, tl, ts, pl, ps, off, bits, n_steps, 42, 1.0, mode)
         assert np.array_equal(gi, wi), (kind, mode, gi.reshape(-1)[:8], wi.reshape(-1)[:8])
         _assert_bits_equal(gs, ws, f"coop {kind} mode {mode}")
+
+
+@pytest.mark.parametrize("kind", ["pln_like", "outliers", "nan_dim", "single"])
+def test_importance_grouped_fused_matches_stepwise(cwq, kind):
+    """cwq_code_grouped_importance (one native call) returns exactly what the
+    step-by-step host pipeline returns: sample bits, bitcode, starts, outliers."""
+    import compression_without_quantization_amd.coded_importance_sampler as I
+    from compression_without_quantization_amd.synthetic import make_latents
+    D = {"pln_like": 4000, "outliers": 777, "nan_dim": 300, "single": 1}[kind]
+    q_loc, q_scale, p_loc, p_scale = make_latents(D, bits_per_dim=1.5, seed=D)
+    if kind == "outliers":
+        q_loc[::50] = p_loc[::50] + 40 * p_scale[::50]   # KL far above the limit
+    if kind == "nan_dim":
+        q_loc[17] = np.nan
+    t, p = cwq.Normal(q_loc, q_scale), cwq.Normal(p_loc, p_scale)
+    old = (I.USE_FUSED, I.VERBOSE)
+    try:
+        I.VERBOSE = False
+        res = {}
+        for fused in (True, False):
+            I.USE_FUSED = fused
+            res[fused] = I.code_grouped_importance_sample(None, t, p, 42, 16,
+                                                          max_group_size_bits=3,
+                                                          dim_kl_bit_limit=12)
+    finally:
+        I.USE_FUSED, I.VERBOSE = old
+    a, b = res[True], res[False]
+    _assert_bits_equal(a[0], b[0], f"fused sample ({kind})")
+    assert a[1] == b[1]
+    assert np.array_equal(np.asarray(a[2]), np.asarray(b[2]))
+    assert np.array_equal(a[3][0], b[3][0]) and np.array_equal(a[3][1], b[3][1])
+    if kind == "outliers":
+        assert a[3][0].size >= 15
