@@ -82,7 +82,7 @@ WsLayout ws_layout(int64_t nb, int64_t total_dims, bool csr) {
     l.grp = o;
     o = align_up(o + (size_t)nb * 16, 256);
     l.gtau = o;
-    o = align_up(o + (size_t)nb * 4, 256);
+    o = align_up(o + (size_t)nb * 4 * CWQ_CSR_GTAU_STRIDE, 256);
   }
   l.total = o;
   return l;

@@ -5,6 +5,10 @@
 
 namespace cwq {
 
+#ifndef CWQ_CSR_GTAU_STRIDE
+#define CWQ_CSR_GTAU_STRIDE 1  // words between blocks' shared thresholds (tuning builds)
+#endif
+
 // Records `msg` for cwq_last_error() (thread-local) and returns `code`.
 int set_error(int code, const char* msg);
 

@@ -758,7 +758,7 @@ __global__ void __launch_bounds__(256) k_csr_prep(
                                     (1.0 + 0x1p-11));
       const bool fin = as - as == 0.0f && pq - pq == 0.0f;
       grp[g] = (all_ok && fin && d > 0) ? float4{c1, c2, as, pq} : float4{0.f, 0.f, 0.f, 0.f};
-      gtau[g] = ord_f32(-__builtin_inff());
+      gtau[g * CWQ_CSR_GTAU_STRIDE] = ord_f32(-__builtin_inff());
     }
     __syncthreads();
   }
@@ -822,10 +822,10 @@ __device__ __forceinline__ float exact_row_wave(
 #define CWQ_CSR_LDS_DIMS 1024  // blocks up to this d keep their screening constants in LDS
 #endif
 #ifndef CWQ_CSR_GTAU_SHARE
-#define CWQ_CSR_GTAU_SHARE 0  // 1: also share tau with the block's other tiles in the loop
+#define CWQ_CSR_GTAU_SHARE 1  // 1: also share tau with the block's other tiles in the loop
 #endif
 #ifndef CWQ_CSR_GTAU_MASK
-#define CWQ_CSR_GTAU_MASK 15u  // ... every CWQ_CSR_GTAU_MASK + 1 iterations
+#define CWQ_CSR_GTAU_MASK 63u  // ... every CWQ_CSR_GTAU_MASK + 1 iterations
 #endif
 #ifndef CWQ_CSR_SURVIVOR_CAP
 #define CWQ_CSR_SURVIVOR_CAP 512
@@ -893,7 +893,7 @@ __global__ void __launch_bounds__(256, 6) k_encode_prune_csr(
       }
     }
     if (tid == 0) {
-      tau_ord = __hip_atomic_load(&gtau[g], __ATOMIC_RELAXED,
+      tau_ord = __hip_atomic_load(&gtau[g * CWQ_CSR_GTAU_STRIDE], __ATOMIC_RELAXED,
                                   __HIP_MEMORY_SCOPE_AGENT);  // earlier tiles of the block
       sq_cnt = 0u;
     }
@@ -993,9 +993,12 @@ __global__ void __launch_bounds__(256, 6) k_encode_prune_csr(
             uint32_t o = __atomic_load_n(&tau_ord, __ATOMIC_RELAXED);
 #if CWQ_CSR_GTAU_SHARE
             if ((iter & CWQ_CSR_GTAU_MASK) == 0u) {
-              if (lane == 0) atomicMax(&gtau[g], ord_f32(tm));
-              const uint32_t o2 = __hip_atomic_load(&gtau[g], __ATOMIC_RELAXED,
+              // publish only an improvement (atomics are rare once tau settles),
+              // read the block's threshold every time
+              uint32_t* gt = &gtau[g * CWQ_CSR_GTAU_STRIDE];
+              const uint32_t o2 = __hip_atomic_load(gt, __ATOMIC_RELAXED,
                                                     __HIP_MEMORY_SCOPE_AGENT);
+              if (lane == 0 && ord_f32(tm) > o2) atomicMax(gt, ord_f32(tm));
               o = o > o2 ? o : o2;
             }
 #endif
@@ -1117,7 +1120,7 @@ __global__ void __launch_bounds__(256, 6) k_encode_prune_csr(
         __syncthreads();
         if (tid == 0) {
           const uint32_t mine = tau_ord;
-          const uint32_t prev = atomicMax(&gtau[g], mine);
+          const uint32_t prev = atomicMax(&gtau[g * CWQ_CSR_GTAU_STRIDE], mine);
           tau_ord = prev > mine ? prev : mine;
         }
         __syncthreads();

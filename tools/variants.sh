@@ -15,6 +15,9 @@ declare -A V=(
   [t64]="-DCWQ_CSR_COOP_TILE=64 -DCWQ_CSR_COOP_TILES=12288"
   [t256]="-DCWQ_CSR_COOP_TILE=256 -DCWQ_CSR_COOP_TILES=3072"
   [mind128]="-DCWQ_CSR_COOP_MIN_D=128 -DCWQ_CSR_COOP_ROWS_PER_LANE=64"
+  [gs16]="-DCWQ_CSR_GTAU_SHARE=1 -DCWQ_CSR_GTAU_MASK=15u -DCWQ_CSR_GTAU_STRIDE=32"
+  [gs64]="-DCWQ_CSR_GTAU_SHARE=1 -DCWQ_CSR_GTAU_MASK=63u -DCWQ_CSR_GTAU_STRIDE=32"
+  [gs16n]="-DCWQ_CSR_GTAU_SHARE=1 -DCWQ_CSR_GTAU_MASK=15u"
   [mask7]="-DCWQ_TAU_SHARE_MASK=7u"
   [mask31]="-DCWQ_TAU_SHARE_MASK=31u"
   [cap512]="-DCWQ_SURVIVOR_CAP=512"
