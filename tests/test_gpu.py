@@ -795,3 +795,26 @@ def test_capi_from_plain_c(cwq):
         s = (s * 1000003 + int(np.uint32(v))) % (1 << 64)
     assert int(f["idx0"]) == int(idx[0]) and int(f["checksum"]) == s
     assert int(f["roundtrip_mismatch"]) == 0
+
+
+def test_philox_counter_crosses_2_32(cwq, oracle):
+    """Rows whose flat normal index n*d passes 4 * 2^32 (Philox block index
+    above 2^32: TF's 128-bit counter carries into its second word): decoding
+    rows on both sides of the carry matches the oracle, and the encoder's
+    winner row round trips (d=136, 2^27 candidates, one block)."""
+    d, bits, seed = 136, 27, 11
+    rng = np.random.default_rng(9)
+    tl = rng.standard_normal(d).astype(np.float32) * 0.3
+    ts = rng.uniform(0.5, 1.0, d).astype(np.float32)
+    pl = np.zeros(d, np.float32)
+    ps = np.ones(d, np.float32)
+    off = np.array([0, d], np.int64)
+    cross = (1 << 34) // d                      # first row whose block index is >= 2^32
+    for n in (0, cross - 1, cross, cross + 1, (1 << bits) - 1):
+        want = oracle.greedy_decode(np.array([[n]], np.int32), pl, ps, off, bits, 1, seed)
+        got = cwq.decode_blocks(np.array([[n]], np.int32), pl, ps, bits, 1, seed, block_off=off)
+        _assert_bits_equal(got.cpu().numpy(), want, f"decode row {n}")
+    idx, sample = cwq.encode_blocks(tl, ts, pl, ps, bits, 1, seed, block_off=off)
+    i = idx.cpu().numpy().reshape(-1)
+    want = oracle.greedy_decode(i.reshape(1, 1).astype(np.int32), pl, ps, off, bits, 1, seed)
+    _assert_bits_equal(sample.cpu().numpy(), want, "encoder winner row")
