@@ -62,6 +62,10 @@ PLN = {
             "PLN image codec: one 512x768 image, both levels (level 2 importance 20 bits/group, "
             "level 1 greedy 30 x 14 bits), group sizes arithmetic-coded, .miracle file "
             "(miracle.py compress/decompress defaults, miracle_arguments.py:146-189)"),
+    "pln_is": (1, 512, 768, "importance",
+               "PLN image codec, level 1 through the importance coder (--use_importance_sampling: "
+               "20 bits/group, groups <= 15 dims), level 2 as pln; the path the reference's "
+               "kodim05 timings most likely used (SURVEY.md 6)"),
 }
 CONFIGS = {
     # name: (blocks per GPU, block dim, kl bits, n_steps, description)

@@ -833,6 +833,12 @@ __device__ __forceinline__ float exact_row_wave(
 #ifndef CWQ_CSR_COOP_ROWS_PER_LANE
 #define CWQ_CSR_COOP_ROWS_PER_LANE 8  // cooperative rows below this many rows per lane ...
 #endif
+#ifndef CWQ_CSR_TILE
+#define CWQ_CSR_TILE 1024             // smallest tile (candidates), per-lane rows
+#endif
+#ifndef CWQ_CSR_TILES
+#define CWQ_CSR_TILES 8192            // tiles a launch aims for
+#endif
 #ifndef CWQ_CSR_COOP_TILE
 #define CWQ_CSR_COOP_TILE 128         // smallest tile (candidates) in cooperative launches
 #endif
@@ -1439,8 +1445,8 @@ static void launch_prune_csr(const EncodeArgs& a, int step, hipStream_t stream) 
     tpb = (CWQ_CSR_COOP_TILES + a.nb - 1) / a.nb;
     max_tpb = a.n_cand / CWQ_CSR_COOP_TILE > 1 ? a.n_cand / CWQ_CSR_COOP_TILE : 1;
   } else {
-    tpb = (8192 + a.nb - 1) / a.nb;
-    max_tpb = a.n_cand / 1024 > 1 ? a.n_cand / 1024 : 1;
+    tpb = (CWQ_CSR_TILES + a.nb - 1) / a.nb;
+    max_tpb = a.n_cand / CWQ_CSR_TILE > 1 ? a.n_cand / CWQ_CSR_TILE : 1;
   }
   tpb = tpb < max_tpb ? tpb : max_tpb;
   const int64_t cpt = (a.n_cand + tpb - 1) / tpb;

@@ -18,6 +18,9 @@ declare -A V=(
   [gs16]="-DCWQ_CSR_GTAU_SHARE=1 -DCWQ_CSR_GTAU_MASK=15u -DCWQ_CSR_GTAU_STRIDE=32"
   [gs64]="-DCWQ_CSR_GTAU_SHARE=1 -DCWQ_CSR_GTAU_MASK=63u -DCWQ_CSR_GTAU_STRIDE=32"
   [gs16n]="-DCWQ_CSR_GTAU_SHARE=1 -DCWQ_CSR_GTAU_MASK=15u"
+  [t512]="-DCWQ_CSR_TILE=512 -DCWQ_CSR_TILES=16384"
+  [t256b]="-DCWQ_CSR_TILE=256 -DCWQ_CSR_TILES=32768"
+  [t2048]="-DCWQ_CSR_TILE=2048 -DCWQ_CSR_TILES=4096"
   [mask7]="-DCWQ_TAU_SHARE_MASK=7u"
   [mask31]="-DCWQ_TAU_SHARE_MASK=31u"
   [cap512]="-DCWQ_SURVIVOR_CAP=512"
