@@ -1495,17 +1495,15 @@ static void launch_eval_dc(const EncodeArgs& a, int step, hipStream_t stream) {
   launch_eval_t<0, STEP0>(a, step, stream);
 }
 
-hipError_t launch_encode(const EncodeArgs& a, hipStream_t stream) {
+// The step loop of one block range on one stream: reset the argmax keys, score
+// the candidates, finalize (index + best) -- steps are sequential per block.
+static hipError_t encode_steps(const EncodeArgs& a, hipStream_t stream, bool events) {
   hipError_t e;
-  e = launch_prep_dims(a.t_scale, a.p_loc, a.p_scale, a.total_dims, a.n_steps, a.rho, a.loc_s,
-                       a.scale_s, a.lognorm, a.out_sample, stream);
-  if (e != hipSuccess) return e;
-  if (a.nb == 0) return hipSuccess;
   const unsigned fgrid = grid_for(a.nb, 4, 65536);
   for (int s = 0; s < a.n_steps; ++s) {
     e = hipMemsetAsync(a.keys, 0, (size_t)a.nb * sizeof(unsigned long long), stream);
     if (e != hipSuccess) return e;
-    if (s == 0 && a.ev_start) {
+    if (events && s == 0 && a.ev_start) {
       e = hipEventRecord((hipEvent_t)a.ev_start, stream);
       if (e != hipSuccess) return e;
     }
@@ -1513,7 +1511,7 @@ hipError_t launch_encode(const EncodeArgs& a, hipStream_t stream) {
       launch_eval_dc<true>(a, s, stream);
     else
       launch_eval_dc<false>(a, s, stream);
-    if (s == a.n_steps - 1 && a.ev_stop) {
+    if (events && s == a.n_steps - 1 && a.ev_stop) {
       e = hipEventRecord((hipEvent_t)a.ev_stop, stream);
       if (e != hipSuccess) return e;
     }
@@ -1525,6 +1523,78 @@ hipError_t launch_encode(const EncodeArgs& a, hipStream_t stream) {
     e = hipGetLastError();
     if (e != hipSuccess) return e;
   }
+  return hipSuccess;
+}
+
+// Two library streams per device (created once per host thread) onto which a
+// multi-step CSR encode forks: the two halves of the block range run their
+// step loops concurrently, so one half's end-of-step tail (the last tiles of
+// a step, and the finalize/prep launches between steps) overlaps the other
+// half's work.  Fork and join are events on the caller's stream, so the call
+// stays stream-ordered (and capturable) for the caller.
+#ifndef CWQ_ENCODE_SPLIT
+#define CWQ_ENCODE_SPLIT 2
+#endif
+namespace {
+struct ForkStreams {
+  bool ok = false;
+  hipStream_t s[2];
+  hipEvent_t fork, join[2];
+};
+thread_local ForkStreams tl_fork[16];
+ForkStreams* fork_streams() {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 16) return nullptr;
+  ForkStreams& f = tl_fork[dev];
+  if (!f.ok) {
+    for (int i = 0; i < 2; ++i) {
+      if (hipStreamCreateWithFlags(&f.s[i], hipStreamNonBlocking) != hipSuccess) return nullptr;
+      if (hipEventCreateWithFlags(&f.join[i], hipEventDisableTiming) != hipSuccess)
+        return nullptr;
+    }
+    if (hipEventCreateWithFlags(&f.fork, hipEventDisableTiming) != hipSuccess) return nullptr;
+    f.ok = true;
+  }
+  return &f;
+}
+}  // namespace
+
+hipError_t launch_encode(const EncodeArgs& a, hipStream_t stream) {
+  hipError_t e;
+  e = launch_prep_dims(a.t_scale, a.p_loc, a.p_scale, a.total_dims, a.n_steps, a.rho, a.loc_s,
+                       a.scale_s, a.lognorm, a.out_sample, stream);
+  if (e != hipSuccess) return e;
+  if (a.nb == 0) return hipSuccess;
+  ForkStreams* f = (CWQ_ENCODE_SPLIT > 1 && a.block_off != nullptr && a.n_steps > 1 &&
+                    a.nb >= 2)
+                       ? fork_streams()
+                       : nullptr;
+  if (f == nullptr) return encode_steps(a, stream, true);
+  // blocks [0, h) and [h, nb): block-indexed arrays move by g0, the padded
+  // per-block regions of the general kernel by 8 g0 / 12 g0 (their layout is
+  // off + 8 g / off + 12 g with absolute dim offsets off)
+  if (a.ev_start && (e = hipEventRecord((hipEvent_t)a.ev_start, stream)) != hipSuccess) return e;
+  if ((e = hipEventRecord(f->fork, stream)) != hipSuccess) return e;
+  const int64_t h = a.nb / 2;
+  for (int i = 0; i < 2; ++i) {
+    const int64_t g0 = i == 0 ? 0 : h, g1 = i == 0 ? h : a.nb;
+    EncodeArgs p = a;
+    p.block_off = a.block_off + g0;
+    p.nb = g1 - g0;
+    p.block_id_base = a.block_id_base + g0;
+    p.keys = a.keys + g0;
+    p.out_idx = a.out_idx + g0 * a.n_steps;
+    if (a.sab) p.sab = a.sab + 8 * g0;
+    if (a.bpre) p.bpre = a.bpre + 12 * g0;
+    if (a.ordu) p.ordu = a.ordu + 12 * g0;
+    if (a.grp) p.grp = a.grp + g0;
+    if (a.gtau) p.gtau = a.gtau + g0 * CWQ_CSR_GTAU_STRIDE;
+    if ((e = hipStreamWaitEvent(f->s[i], f->fork, 0)) != hipSuccess) return e;
+    if ((e = encode_steps(p, f->s[i], false)) != hipSuccess) return e;
+    if ((e = hipEventRecord(f->join[i], f->s[i])) != hipSuccess) return e;
+    if ((e = hipStreamWaitEvent(stream, f->join[i], 0)) != hipSuccess) return e;
+  }
+  if (a.ev_stop && (e = hipEventRecord((hipEvent_t)a.ev_stop, stream)) != hipSuccess) return e;
   return hipSuccess;
 }
 

@@ -28,9 +28,12 @@
  * Conventions
  *   - All float/index pointers are DEVICE pointers (hipMalloc / torch cuda
  *     tensors) unless documented as host.  `stream` is a hipStream_t (NULL =
- *     default stream).  Calls are stream-ordered and asynchronous; nothing is
- *     allocated and nothing synchronises (graph-capturable), except
- *     cwq_group_starts which is pure host code.
+ *     default stream).  Calls are stream-ordered and asynchronous; no device
+ *     memory is allocated and nothing synchronises (graph-capturable), except
+ *     the host functions and the fused grouped pipelines documented as such.
+ *     A multi-step CSR encode forks its two block halves onto two library
+ *     streams (created once per host thread and device) and joins them back
+ *     with events on the caller's stream.
  *   - Blocks ("groups" in the reference) are described in CSR form:
  *     block g covers dims [block_off[g], block_off[g+1]) of the flat arrays;
  *     block_off is a device int64 array of nb+1 entries.  The *_uniform
