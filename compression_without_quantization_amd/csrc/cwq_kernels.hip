@@ -1533,13 +1533,14 @@ static hipError_t encode_steps(const EncodeArgs& a, hipStream_t stream, bool eve
 // half's work.  Fork and join are events on the caller's stream, so the call
 // stays stream-ordered (and capturable) for the caller.
 #ifndef CWQ_ENCODE_SPLIT
-#define CWQ_ENCODE_SPLIT 2
+#define CWQ_ENCODE_SPLIT 3  // most parts a multi-step CSR encode forks into
 #endif
 namespace {
+constexpr int kMaxSplit = 3;
 struct ForkStreams {
   bool ok = false;
-  hipStream_t s[2];
-  hipEvent_t fork, join[2];
+  hipStream_t s[kMaxSplit];
+  hipEvent_t fork, join[kMaxSplit];
 };
 thread_local ForkStreams tl_fork[16];
 ForkStreams* fork_streams() {
@@ -1547,7 +1548,7 @@ ForkStreams* fork_streams() {
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 16) return nullptr;
   ForkStreams& f = tl_fork[dev];
   if (!f.ok) {
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < kMaxSplit; ++i) {
       if (hipStreamCreateWithFlags(&f.s[i], hipStreamNonBlocking) != hipSuccess) return nullptr;
       if (hipEventCreateWithFlags(&f.join[i], hipEventDisableTiming) != hipSuccess)
         return nullptr;
@@ -1570,14 +1571,19 @@ hipError_t launch_encode(const EncodeArgs& a, hipStream_t stream) {
                        ? fork_streams()
                        : nullptr;
   if (f == nullptr) return encode_steps(a, stream, true);
-  // blocks [0, h) and [h, nb): block-indexed arrays move by g0, the padded
+  // k parts of the block range: block-indexed arrays move by g0, the padded
   // per-block regions of the general kernel by 8 g0 / 12 g0 (their layout is
-  // off + 8 g / off + 12 g with absolute dim offsets off)
+  // off + 8 g / off + 12 g with absolute dim offsets off).  Launches of few
+  // long rows (the cooperative mode) overlap best in three parts, others in two
+  // (tools/stream_overlap.py).
+  const bool few_rows = a.nb * a.n_cand < (int64_t)CWQ_CSR_COOP_ROWS_PER_LANE * 1536 * 256;
+  int k = few_rows ? 3 : 2;
+  k = k < CWQ_ENCODE_SPLIT ? k : CWQ_ENCODE_SPLIT;
+  k = (int64_t)k < a.nb ? k : (int)a.nb;
   if (a.ev_start && (e = hipEventRecord((hipEvent_t)a.ev_start, stream)) != hipSuccess) return e;
   if ((e = hipEventRecord(f->fork, stream)) != hipSuccess) return e;
-  const int64_t h = a.nb / 2;
-  for (int i = 0; i < 2; ++i) {
-    const int64_t g0 = i == 0 ? 0 : h, g1 = i == 0 ? h : a.nb;
+  for (int i = 0; i < k; ++i) {
+    const int64_t g0 = a.nb * i / k, g1 = a.nb * (i + 1) / k;
     EncodeArgs p = a;
     p.block_off = a.block_off + g0;
     p.nb = g1 - g0;
