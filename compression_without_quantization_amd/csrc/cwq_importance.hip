@@ -41,7 +41,9 @@ __global__ void __launch_bounds__(256) k_imp_prep(const float* __restrict__ t_sc
 __global__ void __launch_bounds__(1024) k_imp_tiles(const int64_t* __restrict__ n_samples,
                                                     int64_t nb, int64_t cpt,
                                                     int64_t* __restrict__ tprefix,
-                                                    uint32_t* __restrict__ gtau) {
+                                                    uint32_t* __restrict__ gtau,
+                                                    unsigned long long* __restrict__ next_tile) {
+  if (threadIdx.x == 0) *next_tile = 0ull;
   __shared__ int64_t part[1024];
   const int64_t chunk = (nb + 1023) / 1024;
   const int64_t g0 = threadIdx.x * chunk;
@@ -154,13 +156,21 @@ __device__ __forceinline__ bool imp_screen_dim(float tl, float ts, float pl, flo
          o.B - o.B == 0.0f && o.C - o.C == 0.0f && o.umax - o.umax == 0.0f;
 }
 
-__global__ void __launch_bounds__(256) k_imp_eval(
+#ifndef CWQ_IMP_DYNAMIC_MIN_GROUPS
+#define CWQ_IMP_DYNAMIC_MIN_GROUPS 4096  // dynamic tile hand-out from this many groups
+#endif
+#ifndef CWQ_IMP_MIN_WAVES
+#define CWQ_IMP_MIN_WAVES 1  // waves/SIMD the register allocator must allow (tools/variants.sh)
+#endif
+__global__ void __launch_bounds__(256, CWQ_IMP_MIN_WAVES) k_imp_eval(
     const float* __restrict__ t_loc, const float* __restrict__ t_scale,
     const float* __restrict__ p_loc, const float* __restrict__ p_scale,
     const float* __restrict__ lnt, const float* __restrict__ lnp,
     const int64_t* __restrict__ block_off, const int64_t* __restrict__ n_samples, int64_t nb,
     const int64_t* __restrict__ tprefix, int64_t cpt, int32_t seed, int64_t block_id_base,
-    int allow_screen, uint32_t* __restrict__ gtau, unsigned long long* __restrict__ keys) {
+    int allow_screen, uint32_t* __restrict__ gtau, unsigned long long* __restrict__ keys,
+    unsigned long long* __restrict__ next_tile) {
+  __shared__ int64_t s_tile;
   __shared__ double logtab[32];
   __shared__ float4 coef[kImpScreenMaxD];   // A, B, C per dim (screening)
   __shared__ float derr[kImpScreenMaxD];    // per-dim error bound
@@ -178,7 +188,18 @@ __global__ void __launch_bounds__(256) k_imp_eval(
   const uint32_t lane = threadIdx.x & 63u;
   const int64_t total = tprefix[nb];
 
-  for (int64_t tile = blockIdx.x; tile < total; tile += gridDim.x) {
+  // Many groups: tiles differ in size by orders of magnitude (N_g from 1 to
+  // ~4e5), so they are handed out one at a time through a global counter
+  // (I1: -7%).  Few groups (fewer tiles than workgroups): the fixed
+  // assignment, which saves the counter's round trip per tile (I2: -5%).
+  int64_t tile = blockIdx.x;
+  if (next_tile) {
+    if (threadIdx.x == 0) s_tile = (int64_t)atomicAdd(next_tile, 1ull);
+    __syncthreads();
+    tile = s_tile;
+    __syncthreads();
+  }
+  for (; tile < total;) {
     uint32_t tid = threadIdx.x;
     asm volatile("" : "+v"(tid));
     // group of this tile: last g with tprefix[g] <= tile
@@ -365,6 +386,14 @@ __global__ void __launch_bounds__(256) k_imp_eval(
       if (m) atomicMax(&keys[g], (unsigned long long)m);
     }
     __syncthreads();
+    if (next_tile) {
+      if (threadIdx.x == 0) s_tile = (int64_t)atomicAdd(next_tile, 1ull);
+      __syncthreads();
+      tile = s_tile;
+      __syncthreads();
+    } else {
+      tile += gridDim.x;
+    }
   }
 }
 
@@ -439,7 +468,7 @@ hipError_t launch_imp_outliers(const float* kl, int64_t n, float limit, float* t
 size_t importance_workspace_size(int64_t nb, int64_t total_dims) {
   auto up = [](size_t v) { return (v + 255) / 256 * 256; };
   return up((size_t)nb * 8) + up((size_t)(nb + 1) * 8) + 2 * up((size_t)total_dims * 4) +
-         up((size_t)nb * 4);
+         up((size_t)nb * 4) + 256;
 }
 
 hipError_t launch_importance_encode(const float* t_loc, const float* t_scale, const float* p_loc,
@@ -456,16 +485,18 @@ hipError_t launch_importance_encode(const float* t_loc, const float* t_scale, co
   float* lnt = (float*)(w + up((size_t)nb * 8) + up((size_t)(nb + 1) * 8));
   float* lnp = lnt + up((size_t)total_dims * 4) / 4;
   uint32_t* gtau = (uint32_t*)((char*)lnp + up((size_t)total_dims * 4));
+  unsigned long long* next_tile = (unsigned long long*)((char*)gtau + up((size_t)nb * 4));
   hipError_t e = hipMemsetAsync(keys, 0, (size_t)nb * 8, stream);
   if (e != hipSuccess) return e;
   if (total_dims > 0)
     hipLaunchKernelGGL(k_imp_prep, dim3(grid_for(total_dims, 256, 65536)), dim3(256), 0, stream,
                        t_scale, p_scale, total_dims, lnt, lnp);
   hipLaunchKernelGGL(k_imp_tiles, dim3(1), dim3(1024), 0, stream, n_samples, nb,
-                     kImpCandPerTile, tprefix, gtau);
+                     kImpCandPerTile, tprefix, gtau, next_tile);
   hipLaunchKernelGGL(k_imp_eval, dim3(256 * 16), dim3(256), 0, stream, t_loc, t_scale, p_loc,
                      p_scale, lnt, lnp, block_off, n_samples, nb, tprefix, kImpCandPerTile, seed,
-                     block_id_base, allow_screen, gtau, keys);
+                     block_id_base, allow_screen, gtau, keys,
+                     nb >= CWQ_IMP_DYNAMIC_MIN_GROUPS ? next_tile : nullptr);
   hipLaunchKernelGGL(k_imp_rows, dim3(grid_for(nb, 4, 65536)), dim3(256), 0, stream,
                      (const unsigned long long*)keys, (const int64_t*)nullptr, p_loc, p_scale,
                      block_off, nb, seed, block_id_base, out_index, out_sample);

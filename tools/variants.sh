@@ -21,6 +21,9 @@ declare -A V=(
   [t512]="-DCWQ_CSR_TILE=512 -DCWQ_CSR_TILES=16384"
   [t256b]="-DCWQ_CSR_TILE=256 -DCWQ_CSR_TILES=32768"
   [t2048]="-DCWQ_CSR_TILE=2048 -DCWQ_CSR_TILES=4096"
+  [idyn]="-DCWQ_IMP_DYNAMIC_MIN_GROUPS=0"
+  [iw6]="-DCWQ_IMP_MIN_WAVES=6"
+  [iw8]="-DCWQ_IMP_MIN_WAVES=8"
   [mask7]="-DCWQ_TAU_SHARE_MASK=7u"
   [mask31]="-DCWQ_TAU_SHARE_MASK=31u"
   [cap512]="-DCWQ_SURVIVOR_CAP=512"
