@@ -1,6 +1,7 @@
 #!/bin/bash
 # Build compile-time tuning variants of libcwq.so into tools/variants/ and
-# time each on the C4 bench (run on the GPU box).  Usage: tools/variants.sh build|run
+# time each on a bench config (run on the GPU box).
+# Usage: tools/variants.sh build | [VARIANTS="base t512"] [BENCH_ARGS="--config c2cli"] tools/variants.sh run
 set -e
 cd "$(dirname "$0")/.."
 CSRC=compression_without_quantization_amd/csrc
@@ -37,7 +38,8 @@ if [ "$1" = build ]; then
   done
   wait
 else
-  for k in $(echo "${!V[@]}" | tr ' ' '\n' | sort); do
+  # VARIANTS="base t512" selects variants; BENCH_ARGS="--config c2cli" the workload
+  for k in ${VARIANTS:-$(echo "${!V[@]}" | tr ' ' '\n' | sort)}; do
     [ "$k" = stats ] && continue  # counters only: tools/prune_stats.py
     [ "$k" = phases ] && continue  # host phase timings only
     echo "== $k ${V[$k]}"
