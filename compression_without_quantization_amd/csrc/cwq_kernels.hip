@@ -845,6 +845,9 @@ __device__ __forceinline__ float exact_row_wave(
 #ifndef CWQ_CSR_COOP_TILES
 #define CWQ_CSR_COOP_TILES 6144       // tiles a cooperative launch aims for (4 x 1536 slots)
 #endif
+#ifndef CWQ_CSR_COOP_CLASS_WAVES
+#define CWQ_CSR_COOP_CLASS_WAVES 1    // 1: cooperative rows n = wave (mod 4) per wave
+#endif
 #ifndef CWQ_CSR_COOP_MIN_D
 #define CWQ_CSR_COOP_MIN_D 256        // ... for blocks of at least this many dims
 #endif
@@ -1025,9 +1028,20 @@ __global__ void __launch_bounds__(256, 6) k_encode_prune_csr(
                           __attribute__((always_inline)) {
         const uint32_t t = lane & 15u, slot = lane >> 4;
         const uint64_t below = (1ull << (slot * 16u)) - 1ull;  // lanes of lower slots
-        uint32_t wnext = r0 + 4u;
-        uint32_t r = r0 + slot;
-        bool active = r < r1;
+#if CWQ_CSR_COOP_CLASS_WAVES
+        // wave wv walks rows wv, wv + 4, wv + 8, ... of the tile: one alignment
+        // class per wave, so its slots share one class's visit order
+        const uint32_t nrows = (uint32_t)(n1 - n0);
+        const uint32_t q0 = 0u, q1 = nrows > wv ? (nrows - wv + 3u) / 4u : 0u;
+        auto row_of = [&](uint32_t q) { return wv + 4u * q; };
+#else
+        const uint32_t q0 = r0, q1 = r1;
+        auto row_of = [&](uint32_t q) { return q; };
+#endif
+        uint32_t wnext = q0 + 4u;
+        uint32_t q = q0 + slot;
+        bool active = q < q1;
+        uint32_t r = row_of(q);
         float s = 0.0f;
         float tau = unord_f32(tau_ord);
         uint32_t iter = 0;
@@ -1094,13 +1108,14 @@ __global__ void __launch_bounds__(256, 6) k_encode_prune_csr(
 #endif
           const uint64_t m = __ballot(done);  // 16 bits per finished slot
           if (done) {
-            r = wnext + (uint32_t)(__builtin_popcountll(m & below) >> 4);
+            q = wnext + (uint32_t)(__builtin_popcountll(m & below) >> 4);
+            r = row_of(q);
             start_row();
             k = 0;
             s = 0.0f;
           }
           wnext += (uint32_t)(__builtin_popcountll(m) >> 4);
-          active = r < r1;
+          active = q < q1;
           if (((++iter) & CWQ_TAU_SHARE_MASK) == 0u) {  // share with the workgroup
             const float tm = wave_max_f32(tau);
             if (lane == 0) atomicMax(&tau_ord, ord_f32(tm));
