@@ -24,6 +24,8 @@ declare -A V=(
   [t2048]="-DCWQ_CSR_TILE=2048 -DCWQ_CSR_TILES=4096"
   [idyn]="-DCWQ_IMP_DYNAMIC_MIN_GROUPS=0"
   [cw]="-DCWQ_CSR_COOP_CLASS_WAVES=1"
+  [lds4096]="-DCWQ_CSR_LDS_DIMS=4096"
+  [lds2048]="-DCWQ_CSR_LDS_DIMS=2048"
   [iw6]="-DCWQ_IMP_MIN_WAVES=6"
   [iw8]="-DCWQ_IMP_MIN_WAVES=8"
   [mask7]="-DCWQ_TAU_SHARE_MASK=7u"
