@@ -818,3 +818,60 @@ def test_philox_counter_crosses_2_32(cwq, oracle):
     i = idx.cpu().numpy().reshape(-1)
     want = oracle.greedy_decode(i.reshape(1, 1).astype(np.int32), pl, ps, off, bits, 1, seed)
     _assert_bits_equal(sample.cpu().numpy(), want, "encoder winner row")
+
+
+def test_encode_captured_in_hip_graph(cwq, cwqlib):
+    """The C ABI is stream-ordered and capturable (include/cwq.h): a multi-step
+    CSR encode, which forks onto the library's streams and joins back, and a
+    uniform encode are captured into one HIP graph; replays reproduce the eager
+    results bit for bit."""
+    rng = np.random.default_rng(21)
+    sizes = [300, 17, 450, 5, 260, 33, 1]
+    off = np.concatenate([[0], np.cumsum(sizes)]).astype(np.int64)
+    D = int(off[-1])
+    dev = torch.device("cuda")
+    f = lambda a: torch.from_numpy(np.ascontiguousarray(a, np.float32)).to(dev)
+    tl = f(rng.standard_normal(D))
+    ts = f(rng.uniform(0.3, 1.0, D))
+    z, o = torch.zeros(D, device=dev), torch.ones(D, device=dev)
+    offs = torch.from_numpy(off).to(dev)
+    nb, steps, bits = len(sizes), 3, 12
+    idx = torch.zeros((nb, steps), dtype=torch.int32, device=dev)
+    smp = torch.zeros(D, dtype=torch.float32, device=dev)
+    ws = torch.empty(cwqlib.cwq_greedy_encode_workspace_size(nb, D) + 16 * D + 192 * nb + 2048,
+                     dtype=torch.uint8, device=dev)
+    ub, ud = 64, 32                                    # uniform C4-shaped blocks
+    utl = f(rng.standard_normal(ub * ud) * 0.5)
+    uts = f(rng.uniform(0.3, 0.9, ub * ud))
+    uz, uo = torch.zeros(ub * ud, device=dev), torch.ones(ub * ud, device=dev)
+    uidx = torch.zeros((ub, 1), dtype=torch.int32, device=dev)
+    usmp = torch.zeros(ub * ud, dtype=torch.float32, device=dev)
+    uws = torch.empty(cwqlib.cwq_greedy_encode_workspace_size(ub, ub * ud), dtype=torch.uint8,
+                      device=dev)
+
+    def run():
+        st = torch.cuda.current_stream().cuda_stream
+        assert cwqlib.cwq_greedy_encode(
+            tl.data_ptr(), ts.data_ptr(), z.data_ptr(), o.data_ptr(), offs.data_ptr(), nb, D,
+            max(sizes), bits, steps, 42, 1.0, 0, idx.data_ptr(), smp.data_ptr(), ws.data_ptr(),
+            ws.numel(), st) == 0
+        assert cwqlib.cwq_greedy_encode_uniform(
+            utl.data_ptr(), uts.data_ptr(), uz.data_ptr(), uo.data_ptr(), ub, ud, 14, 1, 7, 1.0,
+            0, uidx.data_ptr(), usmp.data_ptr(), uws.data_ptr(), uws.numel(), st) == 0
+
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        run()                                          # eager (creates the library streams)
+    torch.cuda.synchronize()
+    want = [t.clone() for t in (idx, smp, uidx, usmp)]
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, capture_error_mode="relaxed"):
+        run()
+    for _ in range(2):
+        for t in (idx, smp, uidx, usmp):
+            t.zero_()
+        g.replay()
+        torch.cuda.synchronize()
+        for got, w in zip((idx, smp, uidx, usmp), want):
+            assert torch.equal(got.view(torch.int32), w.view(torch.int32))
