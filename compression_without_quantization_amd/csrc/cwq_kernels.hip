@@ -889,6 +889,7 @@ __global__ void __launch_bounds__(256, 6) k_encode_prune_csr(
     const int64_t off = sp.off, d = sp.d;
     const int64_t n0 = tt * cand_per_tile;
     const int64_t n1 = (n0 + cand_per_tile < n_cand) ? n0 + cand_per_tile : n_cand;
+    if (n1 <= n0) continue;  // empty tile (the launcher sizes tiles so there are none)
     const PhiloxStream st =
         generate_key(step_seed(block_seed(seed, block_id_base + g), step), 42);
     const float4 gc = grp[g];
@@ -1465,6 +1466,7 @@ static void launch_prune_csr(const EncodeArgs& a, int step, hipStream_t stream) 
   }
   tpb = tpb < max_tpb ? tpb : max_tpb;
   const int64_t cpt = (a.n_cand + tpb - 1) / tpb;
+  tpb = (a.n_cand + cpt - 1) / cpt;  // no tile may start at or past n_cand
   const int64_t ntiles = a.nb * tpb;
   const int64_t coop_min_d = coop ? (int64_t)CWQ_CSR_COOP_MIN_D : INT64_MAX;
   hipLaunchKernelGGL((k_csr_prep<STEP0>), dim3(grid_for(a.nb, 1, 65536)), dim3(256), 0, stream,

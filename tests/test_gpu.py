@@ -735,6 +735,23 @@ def test_csr_cooperative_rows_vs_oracle(cwq, cwqlib, oracle, sizes, bits, n_step
         _assert_bits_equal(gs, ws, f"coop {kind} mode {mode}")
 
 
+@pytest.mark.parametrize("sizes,bits,n_steps", [
+    ([300, 40] * 7, 16, 1),    # 14 groups: 439 tiles/group asked, 437 hold candidates
+    ([260] * 3 + [20] * 36, 16, 2),  # three stream parts of 13 groups: 473 asked, 472 used
+])
+def test_csr_tiling_leaves_no_empty_tile(cwq, cwqlib, oracle, sizes, bits, n_steps):
+    """Tile counts that do not divide the candidates evenly (found by
+    tools/stress_csr.py): the launcher must not create tiles past the last
+    candidate, whose negative row ranges would never drain."""
+    rng = np.random.default_rng(len(sizes) * bits)
+    off = np.concatenate([[0], np.cumsum(sizes)]).astype(np.int64)
+    tl, ts, pl, ps = _heavy_inputs(rng, int(off[-1]))
+    wi, ws = oracle.greedy_encode(tl, ts, pl, ps, off, bits, n_steps, 7, 1.0)
+    gi, gs = _csr_encode(cwq, cwqlib, tl, ts, pl, ps, off, bits, n_steps, 7, 1.0, 2)
+    assert np.array_equal(gi, wi)
+    _assert_bits_equal(gs, ws, "uneven csr tiling")
+
+
 @pytest.mark.parametrize("kind", ["pln_like", "outliers", "nan_dim", "single"])
 def test_importance_grouped_fused_matches_stepwise(cwq, kind):
     """cwq_code_grouped_importance (one native call) returns exactly what the
