@@ -4,7 +4,8 @@ kernel (k_encode_prune_csr), pruned (mode 2) against unpruned exact (mode 0).
 Wider than tests/test_gpu.py::test_csr_random_stress: group sizes up to a few
 thousand dims, so it reaches the cooperative 16-lane rows (d >= 256), the
 constants read from global memory (d > 1024), the 2- and 3-stream step splits,
-and near-tie (low-rate) inputs.  Prints one line per trial; exits 1 on a mismatch.
+near-tie (low-rate) inputs, per-lane rows of long groups (constants in global
+memory) and groups past the sorted-order limit (8189 dims).  Prints one line per trial; exits 1 on a mismatch.
 
 Usage: python tools/stress_csr.py [trials] [first_seed] [max_seconds]
 """
@@ -67,8 +68,13 @@ def main():
             break
         rng = np.random.default_rng(t)
         nb = int(rng.integers(1, 9))
-        shape = t % 4
-        if shape == 0:    # a few long groups: cooperative rows, some beyond LDS
+        shape = t % 6
+        if shape == 4:    # many long groups: per-lane rows reading constants from global
+            nb = int(rng.integers(50, 120))
+            sizes = rng.integers(900, 3000, nb)
+        elif shape == 5:  # one huge group: unsorted (natural) visit order
+            sizes = np.array([int(rng.integers(8200, 20000))] + list(rng.integers(0, 50, nb - 1)))
+        elif shape == 0:    # a few long groups: cooperative rows, some beyond LDS
             sizes = rng.integers(200, 4000, nb)
         elif shape == 1:  # mixed short and long in one launch
             sizes = np.where(rng.random(nb) < 0.5, rng.integers(0, 200, nb),
