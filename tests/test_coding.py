@@ -37,6 +37,31 @@ def test_ac_matches_reference_restatement(cwqlib, case):
         assert ref.decode(want) == msg
 
 
+def test_ac_fuzz_against_restatement(cwqlib):
+    """Random alphabets, counts (zeros included for unused symbols), messages and
+    precisions: the C++ coder's bits equal the restatement's and decode back."""
+    from hypothesis import given, settings, strategies as st
+
+    @settings(max_examples=150, deadline=None, derandomize=True)
+    @given(st.data())
+    def run(data):
+        K = data.draw(st.integers(2, 40))
+        prec = data.draw(st.sampled_from([16, 24, 32]))
+        P = np.array(data.draw(st.lists(st.integers(0, 200), min_size=K, max_size=K)),
+                     np.int64)
+        P[0] = max(P[0], 1)                      # EOF must be codable
+        used = [s for s in range(1, K) if P[s] > 0]
+        body = data.draw(st.lists(st.sampled_from(used), max_size=60)) if used else []
+        msg = [int(s) for s in body] + [0]
+        want = ArithmeticCoderRef(P, precision=prec).encode(msg)
+        ac = ArithmeticCoder(P, precision=prec)
+        got = ac.encode(msg)
+        assert got == want
+        assert ac.decode_fast(got) == msg
+
+    run()
+
+
 def test_ac_precision_and_empty(cwqlib):
     P = np.array([3, 1, 1, 5])
     for prec in (16, 24, 32, 40):
