@@ -5,10 +5,11 @@ CXX ?= g++
 
 ORACLE_SO := oracle/libcwq_oracle.so
 MATHCHECK_SO := tests/native/libcwq_mathcheck.so
+ROCRAND_PIN_SO := tests/native/librocrand_pin.so
 CAPI_DEMO := examples/capi_demo
 LIBCWQ := compression_without_quantization_amd/libcwq.so
 
-all: $(ORACLE_SO) $(MATHCHECK_SO) $(CAPI_DEMO)
+all: $(ORACLE_SO) $(MATHCHECK_SO) $(ROCRAND_PIN_SO) $(CAPI_DEMO)
 
 # Oracle: plain C, glibc libm, no FMA contraction, OpenMP over blocks.
 $(ORACLE_SO): oracle/cwq_oracle.c
@@ -18,6 +19,10 @@ $(ORACLE_SO): oracle/cwq_oracle.c
 $(MATHCHECK_SO): tests/native/mathcheck.cpp compression_without_quantization_amd/csrc/cwq_math.h
 	$(CXX) -std=c++17 -O2 -ffp-contract=off -fno-fast-math -mfma -fPIC -shared -o $@ $<
 
+# rocRAND's Philox4x32-10 (SDK header) on the host: an independent pin (test shim).
+$(ROCRAND_PIN_SO): tests/native/rocrand_pin.cpp
+	$(CXX) -std=c++17 -O2 -fPIC -shared -D__HIP_PLATFORM_AMD__ -I/opt/rocm/include -o $@ $<
+
 # The C ABI from plain C (no Python, no torch), linked against the in-tree libcwq.so.
 $(CAPI_DEMO): examples/capi_demo.c include/cwq.h $(LIBCWQ)
 	$(CC) -O2 -std=c99 -D__HIP_PLATFORM_AMD__ -I/opt/rocm/include -Iinclude -o $@ $< \
@@ -25,6 +30,6 @@ $(CAPI_DEMO): examples/capi_demo.c include/cwq.h $(LIBCWQ)
 	  -Wl,-rpath,'$$ORIGIN/../compression_without_quantization_amd' -Wl,-rpath,/opt/rocm/lib
 
 clean:
-	rm -f $(ORACLE_SO) $(MATHCHECK_SO) $(CAPI_DEMO)
+	rm -f $(ORACLE_SO) $(MATHCHECK_SO) $(ROCRAND_PIN_SO) $(CAPI_DEMO)
 
 .PHONY: all clean

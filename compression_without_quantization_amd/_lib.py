@@ -21,16 +21,40 @@ c_size = ctypes.c_size_t
 c_vp = ctypes.c_void_p
 c_str = ctypes.c_char_p
 
+
+class Options(ctypes.Structure):
+    """cwq_options (include/cwq.h): per-call encoder options."""
+    _fields_ = [("prune_mode", ctypes.c_int32), ("reserved", ctypes.c_int32),
+                ("eval_start_event", c_vp), ("eval_stop_event", c_vp)]
+
+
+c_opts = ctypes.POINTER(Options)
+
+
+def options(prune_mode=None, eval_events=None):
+    """A cwq_options pointer for one call, or None (the library defaults:
+    prune_mode 2, no events).  eval_events: (start, stop) hipEvent_t handles."""
+    if prune_mode is None and eval_events is None:
+        return None
+    o = Options(2 if prune_mode is None else int(prune_mode), 0, None, None)
+    if eval_events is not None:
+        o.eval_start_event, o.eval_stop_event = eval_events
+    return ctypes.pointer(o)
+
+
 # name -> (restype, argtypes); mirrors include/cwq.h one-to-one.
 SIGNATURES = {
     "cwq_version": (c_int, []),
     "cwq_last_error": (c_str, []),
     "cwq_stateless_normal_sample": (c_int, [c_vp, c_vp, c_i64, c_i64, c_i32, c_vp, c_vp]),
     "cwq_greedy_encode_workspace_size": (c_size, [c_i64, c_i64]),
+    "cwq_greedy_encode_uniform_workspace_size": (c_size, [c_i64, c_i64]),
     "cwq_greedy_encode": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_int,
-                                  c_int, c_i32, c_f32, c_i64, c_vp, c_vp, c_vp, c_size, c_vp]),
+                                  c_int, c_i32, c_f32, c_i64, c_vp, c_vp, c_vp, c_size, c_opts,
+                                  c_vp]),
     "cwq_greedy_encode_uniform": (c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_int, c_int,
-                                          c_i32, c_f32, c_i64, c_vp, c_vp, c_vp, c_size, c_vp]),
+                                          c_i32, c_f32, c_i64, c_vp, c_vp, c_vp, c_size, c_opts,
+                                          c_vp]),
     "cwq_greedy_decode": (c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_int, c_int,
                                   c_i32, c_f32, c_i64, c_vp, c_vp]),
     "cwq_greedy_decode_uniform": (c_int, [c_vp, c_vp, c_vp, c_i64, c_i64, c_int, c_int, c_i32,
@@ -42,10 +66,10 @@ SIGNATURES = {
     "cwq_code_grouped_greedy_workspace_size": (c_size, [c_i64, c_int]),
     "cwq_code_grouped_greedy": (c_i64, [c_vp, c_vp, c_vp, c_vp, c_i64, c_int, c_int, c_i32, c_f32,
                                         c_i64, c_f64, c_vp, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp,
-                                        c_size, c_vp]),
+                                        c_size, c_opts, c_vp]),
     "cwq_importance_workspace_size": (c_size, [c_i64, c_i64]),
     "cwq_importance_encode": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i32,
-                                      c_i64, c_vp, c_vp, c_vp, c_size, c_vp]),
+                                      c_i64, c_vp, c_vp, c_vp, c_size, c_opts, c_vp]),
     "cwq_importance_decode": (c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i32, c_i64, c_vp,
                                       c_vp]),
     "cwq_importance_group_starts": (c_i64, [c_vp, c_i64, c_i64, c_f64, c_vp, c_i64]),
@@ -53,7 +77,7 @@ SIGNATURES = {
     "cwq_code_grouped_importance_workspace_size": (c_size, [c_i64]),
     "cwq_code_grouped_importance": (c_i64, [c_vp, c_vp, c_vp, c_vp, c_i64, c_i32, c_f32, c_i64,
                                             c_f64, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp,
-                                            c_vp, c_vp, c_size, c_vp]),
+                                            c_vp, c_vp, c_size, c_opts, c_vp]),
     "cwq_ac_encode": (c_i64, [c_vp, c_i64, c_int, c_vp, c_i64, c_vp, c_i64]),
     "cwq_ac_decode": (c_i64, [c_vp, c_i64, c_int, c_vp, c_i64, c_vp, c_i64]),
     "cwq_elias_delta_encode": (c_i64, [c_vp, c_i64, c_vp, c_i64]),
@@ -64,8 +88,6 @@ SIGNATURES = {
     "cwq_selftest_wave_max": (c_int, [c_vp, c_i64, c_vp, c_vp]),
     "cwq_selftest_div": (c_int, [c_vp, c_vp, c_i64, c_vp, c_vp]),
     "cwq_debug_prune_stats": (c_int, [c_vp, c_int]),
-    "cwq_profile_set_eval_events": (c_int, [c_vp, c_vp]),
-    "cwq_set_pruning": (c_int, [c_int]),
     "cwq_pln_posterior": (c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, c_f32, c_vp, c_vp, c_vp]),
     "cwq_permute_gather": (c_int, [c_vp, c_i64, c_i64, c_vp, c_vp, c_vp]),
     "cwq_permute_scatter": (c_int, [c_vp, c_i64, c_i64, c_vp, c_vp, c_vp]),

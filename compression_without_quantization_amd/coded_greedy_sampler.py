@@ -90,19 +90,27 @@ class Normal:
 # ---------------------------------------------------------------------------
 # batched block API (C ABI: cwq_greedy_encode[_uniform], cwq_greedy_decode[_uniform])
 # ---------------------------------------------------------------------------
-def encode_workspace_bytes(nb, total_dims):
-    return int(_lib.load().cwq_greedy_encode_workspace_size(int(nb), int(total_dims)))
+def encode_workspace_bytes(nb, total_dims, block_dim=None):
+    """Workspace bytes of encode_blocks: CSR blocks (nb, total_dims), or
+    uniform blocks of ``block_dim`` (cwq_greedy_encode[_uniform]_workspace_size)."""
+    lib = _lib.load()
+    if block_dim is not None:
+        return int(lib.cwq_greedy_encode_uniform_workspace_size(int(nb), int(block_dim)))
+    return int(lib.cwq_greedy_encode_workspace_size(int(nb), int(total_dims)))
 
 
 def encode_blocks(t_loc, t_scale, p_loc, p_scale, n_bits_per_step, n_steps, seed, rho=1.,
                   block_dim=None, block_off=None, max_block_dim=None, block_id_base=0,
-                  out_idx=None, out_sample=None, workspace=None):
+                  out_idx=None, out_sample=None, workspace=None, prune_mode=None,
+                  eval_events=None):
     """code_greedy_sample over many blocks at once.
 
     Blocks are either uniform (``block_dim``) or CSR (``block_off``, nb+1
     offsets).  Block g is coded with seed ``seed + block_id_base + g``
     (coded_greedy_sampler.py:282).  Returns (idx int32 [nb, n_steps],
-    sample f32 [D]) as cuda tensors.
+    sample f32 [D]) as cuda tensors.  ``prune_mode`` (0/1/2, default 2) and
+    ``eval_events`` ((start, stop) hipEvent_t handles) are this call's
+    cwq_options (include/cwq.h); results never depend on the mode.
     """
     lib = _lib.load()
     dev = _device_of(t_loc, t_scale, p_loc, p_scale)
@@ -135,23 +143,24 @@ def encode_blocks(t_loc, t_scale, p_loc, p_scale, n_bits_per_step, n_steps, seed
         out_idx = torch.empty((nb, n_steps), dtype=torch.int32, device=dev)
     if out_sample is None:
         out_sample = torch.empty(D, dtype=torch.float32, device=dev)
-    need = encode_workspace_bytes(nb, D)
-    if offs is not None:  # room for the general pruned kernel's arrays (cwq.h)
-        need += 16 * D + 192 * nb + 2048
+    need = encode_workspace_bytes(nb, D, block_dim if offs is None else None)
     if workspace is None or workspace.numel() < need:
         workspace = torch.empty(max(need, 1), dtype=torch.uint8, device=dev)
-    stream = torch.cuda.current_stream(dev).cuda_stream
+    opts = _lib.options(prune_mode, eval_events)
     seed32 = int(np.int32(np.uint32(int(seed) & 0xFFFFFFFF)))
-    if offs is None:
-        rc = lib.cwq_greedy_encode_uniform(
-            _ptr(tl), _ptr(ts), _ptr(pl), _ptr(ps), nb, block_dim, int(n_bits_per_step),
-            n_steps, seed32, float(rho), int(block_id_base), _ptr(out_idx), _ptr(out_sample),
-            workspace.data_ptr(), workspace.numel(), stream)
-    else:
-        rc = lib.cwq_greedy_encode(
-            _ptr(tl), _ptr(ts), _ptr(pl), _ptr(ps), offs.data_ptr(), nb, D, int(max_block_dim),
-            int(n_bits_per_step), n_steps, seed32, float(rho), int(block_id_base),
-            _ptr(out_idx), _ptr(out_sample), workspace.data_ptr(), workspace.numel(), stream)
+    with torch.cuda.device(dev):
+        stream = torch.cuda.current_stream(dev).cuda_stream
+        if offs is None:
+            rc = lib.cwq_greedy_encode_uniform(
+                _ptr(tl), _ptr(ts), _ptr(pl), _ptr(ps), nb, block_dim, int(n_bits_per_step),
+                n_steps, seed32, float(rho), int(block_id_base), _ptr(out_idx),
+                _ptr(out_sample), workspace.data_ptr(), workspace.numel(), opts, stream)
+        else:
+            rc = lib.cwq_greedy_encode(
+                _ptr(tl), _ptr(ts), _ptr(pl), _ptr(ps), offs.data_ptr(), nb, D,
+                int(max_block_dim), int(n_bits_per_step), n_steps, seed32, float(rho),
+                int(block_id_base), _ptr(out_idx), _ptr(out_sample), workspace.data_ptr(),
+                workspace.numel(), opts, stream)
     _lib.check(rc, "cwq_greedy_encode")
     return out_idx, out_sample
 
@@ -175,6 +184,13 @@ def decode_blocks(idx, p_loc, p_scale, n_bits_per_step, n_steps, seed, rho=1.,
     seed32 = int(np.int32(np.uint32(int(seed) & 0xFFFFFFFF)))
     if (block_dim is None) == (block_off is None):
         raise ValueError("give exactly one of block_dim / block_off")
+    with torch.cuda.device(dev):
+        return _decode_blocks_on(lib, it, pl, ps, D, n_steps, n_bits_per_step, seed32, rho,
+                                 block_dim, block_off, block_id_base, out_sample, dev, stream)
+
+
+def _decode_blocks_on(lib, it, pl, ps, D, n_steps, n_bits_per_step, seed32, rho, block_dim,
+                      block_off, block_id_base, out_sample, dev, stream):
     if block_dim is not None:
         block_dim = int(block_dim)
         nb = D // block_dim if block_dim else 0
@@ -298,10 +314,12 @@ def _dist_parts(dist, dev, what):
 
 def code_grouped_greedy_sample(sess, target, proposal, n_steps, n_bits_per_step, seed,
                                max_group_size_bits=12, adaptive=True, backfitting_steps=0,
-                               use_log_prob=False, rho=1.):
+                               use_log_prob=False, rho=1., *, prune_mode=None):
     """coded_greedy_sampler.py:170-296.
 
     Returns (sample np.float32 [D], bitcode str, group_start_indices list).
+    ``prune_mode`` (keyword only, not in the reference): the encoder's
+    cwq_options.prune_mode; results never depend on it.
     """
     lib = _lib.load()
     dev = _device_of(target.loc, target.scale, proposal.loc, proposal.scale)
@@ -327,13 +345,14 @@ def code_grouped_greedy_sample(sess, target, proposal, n_steps, n_bits_per_step,
     kl_sum = ctypes.c_double(0.0)
     n_nats = n_bits_per_group * np.log(2) - 1
     seed32 = int(np.int32(np.uint32(int(seed) & 0xFFFFFFFF)))
-    G = _lib.check(lib.cwq_code_grouped_greedy(
-        _ptr(q_loc), _ptr(q_scale), _ptr(p_loc), _ptr(p_scale), D, n_steps, n_bits_per_step,
-        seed32, float(rho), group_size_threshold(max_group_size_bits), float(n_nats),
-        sample_h.ctypes.data, bits_h.ctypes.data, bits_h.size, starts_h.ctypes.data,
-        starts_h.size, ctypes.byref(kl_sum) if VERBOSE else None, ws.data_ptr(), ws.numel(),
-        stream),
-        "cwq_code_grouped_greedy")
+    with torch.cuda.device(dev):
+        G = _lib.check(lib.cwq_code_grouped_greedy(
+            _ptr(q_loc), _ptr(q_scale), _ptr(p_loc), _ptr(p_scale), D, n_steps, n_bits_per_step,
+            seed32, float(rho), group_size_threshold(max_group_size_bits), float(n_nats),
+            sample_h.ctypes.data, bits_h.ctypes.data, bits_h.size, starts_h.ctypes.data,
+            starts_h.size, ctypes.byref(kl_sum) if VERBOSE else None, ws.data_ptr(), ws.numel(),
+            _lib.options(prune_mode), stream),
+            "cwq_code_grouped_greedy")
     if VERBOSE:
         total_kl_bits = kl_sum.value / np.log(2)
         print("Total KL to split up: {:.2f} bits, "
@@ -369,7 +388,8 @@ def decode_grouped_greedy_sample(sess, bitcode, group_start_indices, proposal, n
     sample = decode_blocks(idx.astype(np.int32), zeros, ones, n_bits_per_step, n_steps, seed,
                            rho=rho, block_off=offs)
     out = torch.empty(D, dtype=torch.float32, device=dev)
-    stream = torch.cuda.current_stream(dev).cuda_stream
-    _lib.check(lib.cwq_destandardise(_ptr(sample), _ptr(p_loc), _ptr(p_scale), D, _ptr(out),
-                                     stream), "cwq_destandardise")
+    with torch.cuda.device(dev):
+        stream = torch.cuda.current_stream(dev).cuda_stream
+        _lib.check(lib.cwq_destandardise(_ptr(sample), _ptr(p_loc), _ptr(p_scale), D, _ptr(out),
+                                         stream), "cwq_destandardise")
     return out.cpu().numpy()

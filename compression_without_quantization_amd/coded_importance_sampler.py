@@ -87,8 +87,10 @@ def _kl(dev, a_loc, a_scale, b_loc, b_scale):
 
 
 def importance_encode_blocks(t_loc, t_scale, p_loc, p_scale, block_off, n_samples, seed,
-                             block_id_base=0):
-    """cwq_importance_encode over CSR groups.  Returns (index int64 [nb], sample f32 [D])."""
+                             block_id_base=0, prune_mode=None):
+    """cwq_importance_encode over CSR groups.  Returns (index int64 [nb], sample f32 [D]).
+    ``prune_mode`` 2 (default) screens candidates, 0/1 score them all exactly
+    (cwq_options); results never depend on it."""
     lib = _lib.load()
     dev = _device_of(t_loc, t_scale, p_loc, p_scale)
     tl, ts, pl, ps = (_f32(x, dev, w) for x, w in ((t_loc, "t_loc"), (t_scale, "t_scale"),
@@ -102,10 +104,11 @@ def importance_encode_blocks(t_loc, t_scale, p_loc, p_scale, block_off, n_sample
     need = int(lib.cwq_importance_workspace_size(nb, D))
     ws = torch.empty(max(need, 1), dtype=torch.uint8, device=dev)
     seed32 = int(np.int32(np.uint32(int(seed) & 0xFFFFFFFF)))
-    _lib.check(lib.cwq_importance_encode(_ptr(tl), _ptr(ts), _ptr(pl), _ptr(ps), offs.data_ptr(),
-                                         _ptr(ns), nb, D, seed32, int(block_id_base), _ptr(idx),
-                                         _ptr(sample), ws.data_ptr(), ws.numel(), _stream(dev)),
-               "cwq_importance_encode")
+    with torch.cuda.device(dev):
+        _lib.check(lib.cwq_importance_encode(
+            _ptr(tl), _ptr(ts), _ptr(pl), _ptr(ps), offs.data_ptr(), _ptr(ns), nb, D, seed32,
+            int(block_id_base), _ptr(idx), _ptr(sample), ws.data_ptr(), ws.numel(),
+            _lib.options(prune_mode), _stream(dev)), "cwq_importance_encode")
     return idx, sample
 
 
@@ -121,9 +124,10 @@ def importance_decode_blocks(index, p_loc, p_scale, block_off, seed, block_id_ba
                                     dtype=np.int64)).to(dev)
     out = torch.empty(D, dtype=torch.float32, device=dev)
     seed32 = int(np.int32(np.uint32(int(seed) & 0xFFFFFFFF)))
-    _lib.check(lib.cwq_importance_decode(_ptr(ix), _ptr(pl), _ptr(ps), offs.data_ptr(), nb, D,
-                                         seed32, int(block_id_base), _ptr(out), _stream(dev)),
-               "cwq_importance_decode")
+    with torch.cuda.device(dev):
+        _lib.check(lib.cwq_importance_decode(_ptr(ix), _ptr(pl), _ptr(ps), offs.data_ptr(), nb,
+                                             D, seed32, int(block_id_base), _ptr(out),
+                                             _stream(dev)), "cwq_importance_decode")
     return out
 
 
@@ -192,15 +196,27 @@ def _outlier_target_draw(dev, q_loc, q_scale, seed):
 def code_grouped_importance_sample(sess, target, proposal, seed, n_bits_per_group,
                                    max_group_size_bits=4, dim_kl_bit_limit=12,
                                    return_group_indices_only=False, return_indices=False,
-                                   return_indices_only=False):
+                                   return_indices_only=False, *, prune_mode=None):
     """:112-274.  Returns (sample np.float32 [D], bitcode str | indices,
-    group_start_indices np.ndarray, outlier_extras (indices int64, quint16))."""
+    group_start_indices np.ndarray, outlier_extras (indices int64, quint16)).
+    ``prune_mode`` (keyword only, not in the reference): cwq_options.prune_mode
+    of the encoder; results never depend on it."""
     if not _is_float32(target.loc) or not _is_float32(target.scale):
         raise Exception("Target datatype must be float32!")
     if not _is_float32(proposal.loc) or not _is_float32(proposal.scale):
         raise Exception("Proposal datatype must be float32!")
-    lib = _lib.load()
     dev = _device_of(target.loc, target.scale, proposal.loc, proposal.scale)
+    with torch.cuda.device(dev):
+        return _code_grouped_importance_on(dev, target, proposal, seed, n_bits_per_group,
+                                           max_group_size_bits, dim_kl_bit_limit,
+                                           return_group_indices_only, return_indices,
+                                           return_indices_only, prune_mode)
+
+
+def _code_grouped_importance_on(dev, target, proposal, seed, n_bits_per_group,
+                                max_group_size_bits, dim_kl_bit_limit, return_group_indices_only,
+                                return_indices, return_indices_only, prune_mode):
+    lib = _lib.load()
     q_loc, q_scale = _f32(target.loc, dev, "target.loc"), _f32(target.scale, dev, "target.scale")
     p_loc, p_scale = _f32(proposal.loc, dev, "proposal.loc"), _f32(proposal.scale, dev,
                                                                    "proposal.scale")
@@ -208,7 +224,7 @@ def code_grouped_importance_sample(sess, target, proposal, seed, n_bits_per_grou
     if USE_FUSED and D > 0 and not (return_group_indices_only or return_indices_only):
         return _code_grouped_fused(lib, dev, q_loc, q_scale, p_loc, p_scale, D, seed,
                                    n_bits_per_group, max_group_size_bits, dim_kl_bit_limit,
-                                   return_indices)
+                                   return_indices, prune_mode)
     zeros = torch.zeros(D, dtype=torch.float32, device=dev)
     ones = torch.ones(D, dtype=torch.float32, device=dev)
     # :137-138 standardise
@@ -241,7 +257,8 @@ def code_grouped_importance_sample(sess, target, proposal, seed, n_bits_per_grou
     if return_group_indices_only:
         return group_start_indices, _group_kls(kl_divs, starts)
     n_samples = num_samples_plan(kl_divs, starts)
-    idx, sample = importance_encode_blocks(t_loc, t_scale, zeros, ones, starts, n_samples, seed)
+    idx, sample = importance_encode_blocks(t_loc, t_scale, zeros, ones, starts, n_samples, seed,
+                                           prune_mode=prune_mode)
     indices = tuple(int(v) + 1 for v in idx.cpu().numpy())
     if return_indices_only:
         return indices
@@ -257,7 +274,7 @@ def code_grouped_importance_sample(sess, target, proposal, seed, n_bits_per_grou
 
 
 def _code_grouped_fused(lib, dev, q_loc, q_scale, p_loc, p_scale, D, seed, n_bits_per_group,
-                        max_group_size_bits, dim_kl_bit_limit, return_indices):
+                        max_group_size_bits, dim_kl_bit_limit, return_indices, prune_mode=None):
     """The common path of code_grouped_importance_sample in one native call
     (cwq_code_grouped_importance); same results as the step-by-step path."""
     need = int(lib.cwq_code_grouped_importance_workspace_size(D))
@@ -276,7 +293,7 @@ def _code_grouped_fused(lib, dev, q_loc, q_scale, p_loc, p_scale, D, seed, n_bit
         float(n_bits_per_group * np.log(2) - 1), sample_h.ctypes.data, index_h.ctypes.data,
         starts_h.ctypes.data, starts_h.size, out_i.ctypes.data, out_v.ctypes.data,
         n_out.ctypes.data, ctypes.byref(kl_sum) if VERBOSE else None, ws.data_ptr(), ws.numel(),
-        _stream(dev)),
+        _lib.options(prune_mode), _stream(dev)),
         "cwq_code_grouped_importance")
     if VERBOSE:
         total_kl_bits = kl_sum.value / np.log(2)

@@ -20,9 +20,6 @@
 namespace {
 
 thread_local char g_err[512] = {0};
-thread_local void* g_ev_start = nullptr;
-thread_local void* g_ev_stop = nullptr;
-thread_local int g_prune = 2;  // 0 off, 1 exact pruning, 2 + screening
 
 int fail(int code, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
 int fail(int code, const char* fmt, ...) {
@@ -287,6 +284,18 @@ int64_t group_starts_impl(const float* kl, int64_t D, int64_t size_threshold, do
   return ns;
 }
 
+// cwq_options (NULL = CWQ_OPTIONS_INIT), validated.
+int read_options(const cwq_options* opts, cwq_options* out) {
+  const cwq_options def = CWQ_OPTIONS_INIT;
+  *out = opts ? *opts : def;
+  if (out->prune_mode < 0 || out->prune_mode > 2)
+    return fail(CWQ_ERR_INVALID, "cwq_options.prune_mode=%d outside [0, 2]", out->prune_mode);
+  if (out->reserved != 0) return fail(CWQ_ERR_INVALID, "cwq_options.reserved must be 0");
+  if ((out->eval_start_event == nullptr) != (out->eval_stop_event == nullptr))
+    return fail(CWQ_ERR_INVALID, "cwq_options: give both eval events or neither");
+  return CWQ_OK;
+}
+
 int check_common(int n_bits, int n_steps, int64_t nb) {
   if (n_bits < 0 || n_bits > CWQ_MAX_BITS_PER_STEP)
     return fail(CWQ_ERR_INVALID, "n_bits_per_step=%d outside [0, %d]", n_bits,
@@ -300,19 +309,18 @@ int encode_impl(const float* t_loc, const float* t_scale, const float* p_loc,
                 const float* p_scale, const int64_t* block_off, int64_t ud, int64_t nb,
                 int64_t total_dims, int n_bits, int n_steps, int32_t seed, float rho,
                 int64_t block_id_base, int32_t* out_idx, float* out_sample, void* workspace,
-                size_t workspace_bytes, void* stream) {
+                size_t workspace_bytes, const cwq_options* opts, void* stream) {
   int rc = check_common(n_bits, n_steps, nb);
   if (rc) return rc;
+  cwq_options o;
+  if ((rc = read_options(opts, &o))) return rc;
   if (total_dims < 0) return fail(CWQ_ERR_INVALID, "total_dims must be >= 0");
   if (nb > 0 && (!out_idx)) return fail(CWQ_ERR_INVALID, "out_idx is null");
   if (total_dims > 0 && (!t_loc || !t_scale || !p_loc || !p_scale || !out_sample))
     return fail(CWQ_ERR_INVALID, "null input/output pointer");
-  // required: cwq_greedy_encode_workspace_size(nb, total_dims).  A CSR call
-  // whose sizes look uniform-fast also uses the general pruned kernel's arrays
-  // when the workspace has room for them.
-  const WsLayout lr = ws_layout(nb, total_dims);
-  const WsLayout lc = ws_layout(nb, total_dims, true);
-  const WsLayout l = (!lr.csr && block_off && workspace_bytes >= lc.total) ? lc : lr;
+  // required: cwq_greedy_encode_workspace_size (CSR: always the general pruned
+  // kernel's arrays) or cwq_greedy_encode_uniform_workspace_size
+  const WsLayout l = block_off ? ws_layout(nb, total_dims, true) : ws_layout(nb, total_dims);
   if (workspace_bytes < l.total || (l.total && !workspace))
     return fail(CWQ_ERR_WORKSPACE, "workspace %zu bytes < required %zu", workspace_bytes,
                 l.total);
@@ -328,7 +336,7 @@ int encode_impl(const float* t_loc, const float* t_scale, const float* p_loc,
   a.n_cand = (int64_t)1 << n_bits;
   choose_tiling(nb, a.n_cand, &a.tiles_per_block, &a.cand_per_tile);
   a.n_steps = n_steps;
-  a.prune = g_prune;
+  a.prune = o.prune_mode;
   a.seed = seed;
   a.rho = rho;
   a.block_id_base = block_id_base;
@@ -344,8 +352,8 @@ int encode_impl(const float* t_loc, const float* t_scale, const float* p_loc,
   a.ordu = l.csr ? (uint32_t*)(w + l.ordu) : nullptr;
   a.grp = l.csr ? (float4*)(w + l.grp) : nullptr;
   a.gtau = l.csr ? (uint32_t*)(w + l.gtau) : nullptr;
-  a.ev_start = g_ev_start;
-  a.ev_stop = g_ev_stop;
+  a.ev_start = o.eval_start_event;
+  a.ev_stop = o.eval_stop_event;
   hipError_t e = cwq::launch_encode(a, (hipStream_t)stream);
   if (e != hipSuccess) return hip_fail(e, "cwq_greedy_encode");
   return ok();
@@ -376,7 +384,12 @@ int cwq_stateless_normal_sample(const float* loc, const float* scale, int64_t d,
 
 size_t cwq_greedy_encode_workspace_size(int64_t nb, int64_t total_dims) {
   if (nb < 0 || total_dims < 0) return 0;
-  return ws_layout(nb, total_dims).total;
+  return ws_layout(nb, total_dims, true).total;
+}
+
+size_t cwq_greedy_encode_uniform_workspace_size(int64_t nb, int64_t d) {
+  if (nb < 0 || d < 0 || (d > 0 && nb > INT64_MAX / d)) return 0;
+  return ws_layout(nb, nb * d).total;
 }
 
 int cwq_greedy_encode(const float* t_loc, const float* t_scale, const float* p_loc,
@@ -384,23 +397,25 @@ int cwq_greedy_encode(const float* t_loc, const float* t_scale, const float* p_l
                       int64_t total_dims, int64_t max_block_dim, int n_bits_per_step,
                       int n_steps, int32_t seed, float rho, int64_t block_id_base,
                       int32_t* out_idx, float* out_sample, void* workspace,
-                      size_t workspace_bytes, void* stream) {
+                      size_t workspace_bytes, const cwq_options* opts, void* stream) {
   if (nb > 0 && !block_off) return fail(CWQ_ERR_INVALID, "block_off is null");
   if (max_block_dim < 0) return fail(CWQ_ERR_INVALID, "max_block_dim must be >= 0");
   return encode_impl(t_loc, t_scale, p_loc, p_scale, block_off, 0, nb, total_dims,
                      n_bits_per_step, n_steps, seed, rho, block_id_base, out_idx, out_sample,
-                     workspace, workspace_bytes, stream);
+                     workspace, workspace_bytes, opts, stream);
 }
 
 int cwq_greedy_encode_uniform(const float* t_loc, const float* t_scale, const float* p_loc,
                               const float* p_scale, int64_t nb, int64_t d,
                               int n_bits_per_step, int n_steps, int32_t seed, float rho,
                               int64_t block_id_base, int32_t* out_idx, float* out_sample,
-                              void* workspace, size_t workspace_bytes, void* stream) {
+                              void* workspace, size_t workspace_bytes, const cwq_options* opts,
+                              void* stream) {
   if (d < 0) return fail(CWQ_ERR_INVALID, "d must be >= 0");
+  if (nb < 0 || (d > 0 && nb > INT64_MAX / d)) return fail(CWQ_ERR_INVALID, "bad nb");
   return encode_impl(t_loc, t_scale, p_loc, p_scale, nullptr, d, nb, nb * d, n_bits_per_step,
                      n_steps, seed, rho, block_id_base, out_idx, out_sample, workspace,
-                     workspace_bytes, stream);
+                     workspace_bytes, opts, stream);
 }
 
 int cwq_greedy_decode(const int32_t* idx, const float* p_loc, const float* p_scale,
@@ -516,7 +531,12 @@ int64_t cwq_code_grouped_greedy(const float* q_loc, const float* q_scale, const 
                                 int64_t size_threshold, double n_nats, float* sample_host,
                                 char* bits_host, int64_t bits_cap, int64_t* starts_host,
                                 int64_t starts_cap, double* kl_sum_out, void* workspace,
-                                size_t workspace_bytes, void* stream) {
+                                size_t workspace_bytes, const cwq_options* opts, void* stream) {
+  {
+    cwq_options o;
+    const int rc0 = read_options(opts, &o);
+    if (rc0) return rc0;
+  }
   if (D < 0 || n_steps < 1 || n_bits_per_step < 0 || n_bits_per_step > CWQ_MAX_BITS_PER_STEP)
     return fail(CWQ_ERR_INVALID, "cwq_code_grouped_greedy: bad sizes");
   if (D > 0 && (!q_loc || !q_scale || !p_loc || !p_scale || !sample_host))
@@ -600,7 +620,7 @@ int64_t cwq_code_grouped_greedy(const float* q_loc, const float* q_scale, const 
   // :273-284 one greedy coder per group, seed + g
   if ((rc = cwq_greedy_encode(t_loc, t_scale, zeros, ones, offs, G, D, maxd, n_bits_per_step,
                               n_steps, seed, rho, 0, idx, sample, w + l.enc,
-                              workspace_bytes - l.enc, stream)) < 0)
+                              workspace_bytes - l.enc, opts, stream)) < 0)
     return rc;
   // :292 destandardise
   if ((rc = cwq_destandardise(sample, p_loc, p_scale, D, out, stream)) < 0) return rc;
@@ -696,7 +716,13 @@ int64_t cwq_code_grouped_importance(const float* q_loc, const float* q_scale,
                                     int64_t* starts_host, int64_t starts_cap,
                                     int64_t* outlier_idx_host, float* outlier_val_host,
                                     int64_t* n_outliers, double* kl_sum_out, void* workspace,
-                                    size_t workspace_bytes, void* stream) {
+                                    size_t workspace_bytes, const cwq_options* opts,
+                                    void* stream) {
+  {
+    cwq_options o;
+    const int rc0 = read_options(opts, &o);
+    if (rc0) return rc0;
+  }
   if (D < 0) return fail(CWQ_ERR_INVALID, "cwq_code_grouped_importance: negative size");
   if (D > 0 && (!q_loc || !q_scale || !p_loc || !p_scale || !sample_host || !index_host ||
                 !outlier_idx_host || !outlier_val_host))
@@ -785,7 +811,7 @@ int64_t cwq_code_grouped_importance(const float* q_loc, const float* q_scale,
       return hip_fail(e, "plan to device");
     // :212-245 every group's importance coder, seed + g
     if ((rc = cwq_importance_encode(t_loc, t_scale, zeros, ones, offs, nsamp, G, D, seed, 0, idx,
-                                    sample, w + l.enc, workspace_bytes - l.enc, stream)) < 0)
+                                    sample, w + l.enc, workspace_bytes - l.enc, opts, stream)) < 0)
       return rc;
   } else {
     if ((e = hipMemsetAsync(sample, 0, (size_t)D * 4, s)) != hipSuccess)
@@ -838,8 +864,12 @@ int cwq_importance_encode(const float* t_loc, const float* t_scale, const float*
                           const float* p_scale, const int64_t* block_off,
                           const int64_t* n_samples, int64_t nb, int64_t total_dims, int32_t seed,
                           int64_t block_id_base, int64_t* out_index, float* out_sample,
-                          void* workspace, size_t workspace_bytes, void* stream) {
+                          void* workspace, size_t workspace_bytes, const cwq_options* opts,
+                          void* stream) {
   if (nb < 0 || total_dims < 0) return fail(CWQ_ERR_INVALID, "negative size");
+  cwq_options o;
+  int rc = read_options(opts, &o);
+  if (rc) return rc;
   if (nb > 0 && (!block_off || !n_samples || !out_index))
     return fail(CWQ_ERR_INVALID, "null pointer");
   if (total_dims > 0 && (!t_loc || !t_scale || !p_loc || !p_scale || !out_sample))
@@ -849,7 +879,7 @@ int cwq_importance_encode(const float* t_loc, const float* t_scale, const float*
     return fail(CWQ_ERR_WORKSPACE, "workspace %zu bytes < required %zu", workspace_bytes, need);
   hipError_t e = cwq::launch_importance_encode(t_loc, t_scale, p_loc, p_scale, block_off,
                                                n_samples, nb, total_dims, seed, block_id_base,
-                                               g_prune >= 2 ? 1 : 0, out_index, out_sample,
+                                               o.prune_mode >= 2 ? 1 : 0, out_index, out_sample,
                                                workspace, (hipStream_t)stream);
   if (e != hipSuccess) return hip_fail(e, "cwq_importance_encode");
   return ok();
@@ -865,19 +895,6 @@ int cwq_importance_decode(const int64_t* index, const float* p_loc, const float*
   hipError_t e = cwq::launch_importance_decode(index, p_loc, p_scale, block_off, nb, seed,
                                                block_id_base, out_sample, (hipStream_t)stream);
   if (e != hipSuccess) return hip_fail(e, "cwq_importance_decode");
-  return ok();
-}
-
-int cwq_profile_set_eval_events(void* start_event, void* stop_event) {
-  if ((start_event == nullptr) != (stop_event == nullptr))
-    return fail(CWQ_ERR_INVALID, "give both events or neither");
-  g_ev_start = start_event;
-  g_ev_stop = stop_event;
-  return ok();
-}
-
-int cwq_set_pruning(int enable) {  // mode, see include/cwq.h
-  g_prune = enable < 0 ? 0 : (enable > 2 ? 2 : enable);
   return ok();
 }
 

@@ -1233,6 +1233,52 @@ __global__ void __launch_bounds__(256) k_encode_finalize(
   }
 }
 
+// Uniform blocks with d % 4 == 0, d <= 256: every row n*d starts on a Philox
+// block, so one lane owns Philox block q of its block's winning row and with
+// it dims 4q..4q+3 -- one Philox + two Box-Muller pairs per 4 dims, float4
+// loads and stores.  A wave holds 64 / (d/4) whole blocks (lane -> (block,
+// q) is fixed per lane: no 64-bit division in the loop); its chunks of blocks
+// are strided over the grid's waves.
+struct Q4Lane {
+  bool active;
+  uint32_t lb, q;  // block within the wave's chunk, Philox block within the row
+};
+__device__ __forceinline__ Q4Lane q4_lane(uint32_t qpb, uint32_t bpw) {
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t lb = lane / qpb;
+  return Q4Lane{lb < bpw, lb, lane - lb * qpb};
+}
+
+__global__ void __launch_bounds__(256) k_encode_finalize_q4(
+    const float4* __restrict__ loc_s, const float4* __restrict__ scale_s, uint32_t qpb,
+    uint32_t bpw, int64_t nb, int32_t seed, int64_t block_id_base, int32_t step, int n_steps,
+    const unsigned long long* __restrict__ keys, int32_t* __restrict__ out_idx,
+    float4* __restrict__ out_sample) {
+  __shared__ double logtab[32];
+  fill_logtab(logtab);
+  const Q4Lane L = q4_lane(qpb, bpw);
+  const int64_t nwaves = (int64_t)gridDim.x * 4;
+  for (int64_t c = (int64_t)blockIdx.x * 4 + wave_id(); c * bpw < nb; c += nwaves) {
+    const int64_t g = c * bpw + L.lb;
+    if (!L.active || g >= nb) continue;
+    const int64_t t = g * qpb + L.q;
+    const uint64_t key = keys[g];
+    const uint32_t idx = (key >> 32) > kArgmaxClampOrd ? argmax_key_index(key) : 0u;
+    if (L.q == 0) out_idx[g * n_steps + step] = (int32_t)idx;
+    const PhiloxStream st =
+        generate_key(step_seed(block_seed(seed, block_id_base + g), step), 42);
+    const F4 z = normal4_dev(st, (uint64_t)idx * qpb + L.q, logtab);
+    const float4 l = loc_s[t], sc = scale_s[t];
+    float4 b = out_sample[t];
+    float s;
+    s = sc.x * z.a; s = l.x + s; b.x = b.x + s;
+    s = sc.y * z.b; s = l.y + s; b.y = b.y + s;
+    s = sc.z * z.c; s = l.z + s; b.z = b.z + s;
+    s = sc.w * z.d; s = l.w + s; b.w = b.w + s;
+    out_sample[t] = b;
+  }
+}
+
 // ---------------------------------------------------------------------------
 // Decoder (coded_greedy_sampler.py:93-167), O(n_steps * d) per block.
 // ---------------------------------------------------------------------------
@@ -1270,6 +1316,59 @@ __global__ void __launch_bounds__(256) k_decode(
       }
       out_sample[sp.off + j] = v;
     }
+  }
+}
+
+// Decoder for uniform blocks with d % 4 == 0, d <= 256 (the C4/C5 shapes):
+// one lane per Philox block of the selected row -- dims 4q..4q+3 of block g,
+// the same dims at every step because n*d is a multiple of 4 -- so each lane
+// runs one Philox + two Box-Muller pairs per step, and p_loc / p_scale / the
+// sample move as float4 (coalesced across the wave).  Lanes map to blocks as
+// in k_encode_finalize_q4.  With n_steps == 1 the shard divisions are by 1.0f
+// (exact identities; skipped on a uniform branch).
+__global__ void __launch_bounds__(256) k_decode_q4(
+    const int32_t* __restrict__ idx, const float4* __restrict__ p_loc,
+    const float4* __restrict__ p_scale, uint32_t qpb, uint32_t bpw, int64_t nb, int n_steps,
+    int64_t n_cand, float nst, float sdiv, float rho, int32_t seed, int64_t block_id_base,
+    float4* __restrict__ out_sample) {
+  __shared__ double logtab[32];
+  fill_logtab(logtab);
+  const Q4Lane L = q4_lane(qpb, bpw);
+  const int64_t nwaves = (int64_t)gridDim.x * 4;
+  const bool unit = n_steps == 1;  // nst == sdiv == 1.0f
+  for (int64_t c = (int64_t)blockIdx.x * 4 + wave_id(); c * bpw < nb; c += nwaves) {
+    const int64_t g = c * bpw + L.lb;
+    if (!L.active || g >= nb) continue;
+    const int64_t t = g * qpb + L.q;
+    const float4 pl = p_loc[t], ps = p_scale[t];
+    float ls[4] = {pl.x, pl.y, pl.z, pl.w};
+    float ss[4] = {rho * ps.x, rho * ps.y, rho * ps.z, rho * ps.w};
+    if (!unit) {
+#pragma unroll
+      for (int w = 0; w < 4; ++w) {
+        ls[w] = ls[w] / nst;
+        ss[w] = ss[w] / sdiv;
+      }
+    }
+    float v[4] = {0.0f, 0.0f, 0.0f, 0.0f};  // sample = tf.zeros (:143)
+    const int32_t sg = block_seed(seed, block_id_base + g);
+    for (int i = 0; i < n_steps; ++i) {
+      const int64_t n = idx[g * n_steps + i];
+      if (n < 0 || n >= n_cand) {
+        v[0] = v[1] = v[2] = v[3] = __builtin_nanf("");
+        continue;
+      }
+      const PhiloxStream st = generate_key(step_seed(sg, i), 42);
+      const F4 z = normal4_dev(st, (uint64_t)n * qpb + L.q, logtab);
+      const float zz[4] = {z.a, z.b, z.c, z.d};
+#pragma unroll
+      for (int w = 0; w < 4; ++w) {
+        float s = ss[w] * zz[w];
+        s = ls[w] + s;
+        v[w] = v[w] + s;  // :153 tile(sample) + samples, row indices[i]
+      }
+    }
+    out_sample[t] = make_float4(v[0], v[1], v[2], v[3]);
   }
 }
 
@@ -1408,6 +1507,15 @@ __global__ void __launch_bounds__(256) k_selftest_div(const float* __restrict__ 
 // Host-side launchers.
 // ---------------------------------------------------------------------------
 
+// The float4 lane-per-Philox-block kernels: uniform d % 4 == 0, d <= 256.
+static bool q4_shape(const int64_t* block_off, int64_t ud) {
+  return block_off == nullptr && ud > 0 && ud % 4 == 0 && ud <= 256;
+}
+// float4 access needs 16-byte aligned bases (callers may pass offset views)
+static bool aligned16(const void* a, const void* b, const void* c) {
+  return (((uintptr_t)a | (uintptr_t)b | (uintptr_t)c) & 15u) == 0;
+}
+
 hipError_t launch_prep_dims(const float* t_scale, const float* p_loc, const float* p_scale,
                             int64_t n, int n_steps, float rho, float* loc_s, float* scale_s,
                             float* lognorm, float* out_sample, hipStream_t stream) {
@@ -1534,9 +1642,17 @@ static hipError_t encode_steps(const EncodeArgs& a, hipStream_t stream, bool eve
     }
     e = hipGetLastError();
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_encode_finalize, dim3(fgrid), dim3(256), 0, stream, a.loc_s,
-                       a.scale_s, a.block_off, a.ud, a.nb, a.seed, a.block_id_base, s,
-                       a.n_steps, a.keys, a.out_idx, a.out_sample);
+    if (q4_shape(a.block_off, a.ud) && aligned16(a.loc_s, a.scale_s, a.out_sample)) {
+      const uint32_t qpb = (uint32_t)(a.ud / 4), bpw = 64u / qpb;
+      hipLaunchKernelGGL(k_encode_finalize_q4, dim3(grid_for(a.nb, 4 * (int64_t)bpw, 1u << 20)),
+                         dim3(256), 0, stream, (const float4*)a.loc_s, (const float4*)a.scale_s,
+                         qpb, bpw, a.nb, a.seed, a.block_id_base, s, a.n_steps, a.keys,
+                         a.out_idx, (float4*)a.out_sample);
+    } else {
+      hipLaunchKernelGGL(k_encode_finalize, dim3(fgrid), dim3(256), 0, stream, a.loc_s,
+                         a.scale_s, a.block_off, a.ud, a.nb, a.seed, a.block_id_base, s,
+                         a.n_steps, a.keys, a.out_idx, a.out_sample);
+    }
     e = hipGetLastError();
     if (e != hipSuccess) return e;
   }
@@ -1554,23 +1670,47 @@ static hipError_t encode_steps(const EncodeArgs& a, hipStream_t stream, bool eve
 #endif
 namespace {
 constexpr int kMaxSplit = 3;
+constexpr int kMaxDevices = 16;
 struct ForkStreams {
   bool ok = false;
-  hipStream_t s[kMaxSplit];
-  hipEvent_t fork, join[kMaxSplit];
+  hipStream_t s[kMaxSplit] = {};
+  hipEvent_t fork = nullptr, join[kMaxSplit] = {};
+  ~ForkStreams() {  // thread exit (the process's main thread: exit(), before HIP's teardown)
+    if (!ok) return;
+    for (int i = 0; i < kMaxSplit; ++i) {
+      (void)hipStreamDestroy(s[i]);
+      (void)hipEventDestroy(join[i]);
+    }
+    (void)hipEventDestroy(fork);
+  }
 };
-thread_local ForkStreams tl_fork[16];
-ForkStreams* fork_streams() {
+thread_local ForkStreams tl_fork[kMaxDevices];
+// The helper streams of the device the caller's stream belongs to (not the
+// thread's current device: a caller may enqueue onto another GPU's stream).
+ForkStreams* fork_streams(hipStream_t stream) {
   int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 16) return nullptr;
+  if (hipStreamGetDevice(stream, &dev) != hipSuccess || dev < 0 || dev >= kMaxDevices)
+    return nullptr;
   ForkStreams& f = tl_fork[dev];
   if (!f.ok) {
-    for (int i = 0; i < kMaxSplit; ++i) {
-      if (hipStreamCreateWithFlags(&f.s[i], hipStreamNonBlocking) != hipSuccess) return nullptr;
-      if (hipEventCreateWithFlags(&f.join[i], hipEventDisableTiming) != hipSuccess)
-        return nullptr;
+    int cur = 0;
+    if (hipGetDevice(&cur) != hipSuccess) return nullptr;
+    if (cur != dev && hipSetDevice(dev) != hipSuccess) return nullptr;
+    bool good = true;
+    int made_s = 0, made_e = 0;
+    for (int i = 0; i < kMaxSplit && good; ++i) {
+      good = hipStreamCreateWithFlags(&f.s[i], hipStreamNonBlocking) == hipSuccess;
+      made_s += good;
+      good = good && hipEventCreateWithFlags(&f.join[i], hipEventDisableTiming) == hipSuccess;
+      made_e += good;
     }
-    if (hipEventCreateWithFlags(&f.fork, hipEventDisableTiming) != hipSuccess) return nullptr;
+    good = good && hipEventCreateWithFlags(&f.fork, hipEventDisableTiming) == hipSuccess;
+    if (!good) {  // nothing half-made stays behind; the caller runs unsplit
+      for (int i = 0; i < made_s; ++i) (void)hipStreamDestroy(f.s[i]);
+      for (int i = 0; i < made_e; ++i) (void)hipEventDestroy(f.join[i]);
+    }
+    if (cur != dev) (void)hipSetDevice(cur);
+    if (!good) return nullptr;
     f.ok = true;
   }
   return &f;
@@ -1585,7 +1725,7 @@ hipError_t launch_encode(const EncodeArgs& a, hipStream_t stream) {
   if (a.nb == 0) return hipSuccess;
   ForkStreams* f = (CWQ_ENCODE_SPLIT > 1 && a.block_off != nullptr && a.n_steps > 1 &&
                     a.nb >= 2)
-                       ? fork_streams()
+                       ? fork_streams(stream)
                        : nullptr;
   if (f == nullptr) return encode_steps(a, stream, true);
   // k parts of the block range: block-indexed arrays move by g0, the padded
@@ -1599,7 +1739,8 @@ hipError_t launch_encode(const EncodeArgs& a, hipStream_t stream) {
   k = (int64_t)k < a.nb ? k : (int)a.nb;
   if (a.ev_start && (e = hipEventRecord((hipEvent_t)a.ev_start, stream)) != hipSuccess) return e;
   if ((e = hipEventRecord(f->fork, stream)) != hipSuccess) return e;
-  for (int i = 0; i < k; ++i) {
+  int forked = 0;
+  for (int i = 0; i < k && e == hipSuccess; ++i) {
     const int64_t g0 = a.nb * i / k, g1 = a.nb * (i + 1) / k;
     EncodeArgs p = a;
     p.block_off = a.block_off + g0;
@@ -1612,11 +1753,21 @@ hipError_t launch_encode(const EncodeArgs& a, hipStream_t stream) {
     if (a.ordu) p.ordu = a.ordu + 12 * g0;
     if (a.grp) p.grp = a.grp + g0;
     if (a.gtau) p.gtau = a.gtau + g0 * CWQ_CSR_GTAU_STRIDE;
-    if ((e = hipStreamWaitEvent(f->s[i], f->fork, 0)) != hipSuccess) return e;
-    if ((e = encode_steps(p, f->s[i], false)) != hipSuccess) return e;
-    if ((e = hipEventRecord(f->join[i], f->s[i])) != hipSuccess) return e;
-    if ((e = hipStreamWaitEvent(stream, f->join[i], 0)) != hipSuccess) return e;
+    if ((e = hipStreamWaitEvent(f->s[i], f->fork, 0)) != hipSuccess) break;
+    forked = i + 1;
+    e = encode_steps(p, f->s[i], false);
   }
+  // join every stream that was forked, also after an error: the caller's
+  // stream must not run ahead of (or free buffers under) work already queued
+  for (int i = 0; i < forked; ++i) {
+    hipError_t ej = hipEventRecord(f->join[i], f->s[i]);
+    if (ej == hipSuccess) ej = hipStreamWaitEvent(stream, f->join[i], 0);
+    if (ej != hipSuccess) {
+      (void)hipStreamSynchronize(f->s[i]);  // last resort: drain it on the host
+      if (e == hipSuccess) e = ej;
+    }
+  }
+  if (e != hipSuccess) return e;
   if (a.ev_stop && (e = hipEventRecord((hipEvent_t)a.ev_stop, stream)) != hipSuccess) return e;
   return hipSuccess;
 }
@@ -1628,6 +1779,14 @@ hipError_t launch_decode(const int32_t* idx, const float* p_loc, const float* p_
   if (nb <= 0) return hipSuccess;
   const float nst = (float)n_steps;
   const float sdiv = (float)__builtin_sqrt((double)n_steps);
+  if (q4_shape(block_off, ud) && aligned16(p_loc, p_scale, out_sample)) {
+    const uint32_t qpb = (uint32_t)(ud / 4), bpw = 64u / qpb;
+    hipLaunchKernelGGL(k_decode_q4, dim3(grid_for(nb, 4 * (int64_t)bpw, 1u << 20)), dim3(256), 0,
+                       stream, idx, (const float4*)p_loc, (const float4*)p_scale, qpb, bpw, nb,
+                       n_steps, (int64_t)1 << n_bits, nst, sdiv, rho, seed, block_id_base,
+                       (float4*)out_sample);
+    return hipGetLastError();
+  }
   hipLaunchKernelGGL(k_decode, dim3(grid_for(nb, 4, 65536)), dim3(256), 0, stream, idx, p_loc,
                      p_scale, block_off, ud, nb, n_steps, (int64_t)1 << n_bits, nst, sdiv, rho,
                      seed, block_id_base, out_sample);

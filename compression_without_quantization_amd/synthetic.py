@@ -61,6 +61,22 @@ def make_blocks(nb, d, kl_bits, seed=DEFAULT_SEED, exact_kl=False, chunk=1 << 16
     return out
 
 
+def make_blocks_range(b0, b1, d, kl_bits, seed=DEFAULT_SEED, chunk=1 << 16):
+    """Blocks [b0, b1) of a global synthetic set of the make_blocks kind whose
+    chunk c (blocks [c*chunk, (c+1)*chunk)) comes from its own generator
+    PCG64(SeedSequence([seed, c])): any rank can build its shard without
+    generating the blocks before it, and every sharding of the same global
+    set sees the same data (bench.py strong/weak scaling)."""
+    out = {k: np.empty((max(b1 - b0, 0), d), dtype=np.float32)
+           for k in ("prior_loc", "prior_scale", "post_loc", "post_scale")}
+    for c in range(b0 // chunk, (b1 + chunk - 1) // chunk if b1 > b0 else 0):
+        part = make_blocks(chunk, d, kl_bits, seed=np.random.SeedSequence([seed, c]))
+        lo, hi = max(b0, c * chunk), min(b1, (c + 1) * chunk)
+        for k in out:
+            out[k][lo - b0:hi - b0] = part[k][lo - c * chunk:hi - c * chunk]
+    return out
+
+
 def make_latents(D, bits_per_dim=1.1, off_fraction=0.5, seed=DEFAULT_SEED):
     """Flat PLN-like latents for the grouped path (configs C2/C3).
 

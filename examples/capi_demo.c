@@ -54,7 +54,7 @@ int main(int argc, char** argv) {
   float *d_in, *d_sample, *d_dec;
   int32_t* d_idx;
   void* d_ws;
-  const size_t ws = cwq_greedy_encode_workspace_size(nb, n);
+  const size_t ws = cwq_greedy_encode_uniform_workspace_size(nb, d);
   CHECK_HIP(hipMalloc((void**)&d_in, (size_t)n * 4 * sizeof(float)));
   CHECK_HIP(hipMalloc((void**)&d_sample, (size_t)n * sizeof(float)));
   CHECK_HIP(hipMalloc((void**)&d_dec, (size_t)n * sizeof(float)));
@@ -64,7 +64,7 @@ int main(int argc, char** argv) {
   hipStream_t st;
   CHECK_HIP(hipStreamCreate(&st));
   CHECK_CWQ(cwq_greedy_encode_uniform(d_in, d_in + n, d_in + 2 * n, d_in + 3 * n, nb, d, bits, 1,
-                                      seed, 1.0f, 0, d_idx, d_sample, d_ws, ws, st));
+                                      seed, 1.0f, 0, d_idx, d_sample, d_ws, ws, NULL, st));
   CHECK_CWQ(cwq_greedy_decode_uniform(d_idx, d_in + 2 * n, d_in + 3 * n, nb, d, bits, 1, seed,
                                       1.0f, 0, d_dec, st));
   CHECK_HIP(hipStreamSynchronize(st));

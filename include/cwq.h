@@ -74,14 +74,37 @@ const char* cwq_last_error(void);
 int cwq_stateless_normal_sample(const float* loc, const float* scale, int64_t d,
                                 int64_t num_samples, int32_t seed, float* out, void* stream);
 
-/* Workspace bytes needed by cwq_greedy_encode / cwq_greedy_encode_uniform for
- * nb blocks holding total_dims dims in all.  Unless every block has the same d
- * with d % 8 == 0 and 8 <= d <= 64 (the fast pruned kernel), this includes the
- * general pruned kernel's per-step constants (16 B/dim + 180 B/block).  A CSR
- * call whose sizes happen to look like that uniform case may pass
- * 16 * total_dims + 192 * nb + 2048 more bytes to run the general pruned kernel;
- * with exactly the returned size it runs unpruned. */
+/* Per-call options of the encoders (no process or thread state: every call
+ * says what it wants; opts == NULL means the defaults below).
+ *   prune_mode: 2 (default) = candidate pruning with the screening pass
+ *               (DESIGN.md "screening bound") where a tile's constants allow
+ *               it, exact pruning elsewhere; 1 = pruning on exact values only;
+ *               0 = every candidate scored exactly.  Results never depend on
+ *               it.  For the importance encoders, 2 turns on their screening
+ *               pass, 0 and 1 score every candidate exactly.
+ *   eval_start_event / eval_stop_event: hipEvent_t handles (both or neither)
+ *               recorded on the call's stream right before the first
+ *               candidate-scoring launch and right after the last one, so a
+ *               caller can time the dominant kernel alone (bench.py). */
+typedef struct cwq_options {
+  int32_t prune_mode;
+  int32_t reserved; /* must be 0 */
+  void* eval_start_event;
+  void* eval_stop_event;
+} cwq_options;
+#define CWQ_OPTIONS_INIT {2, 0, NULL, NULL}
+
+/* Workspace bytes needed by cwq_greedy_encode (CSR blocks) for nb blocks
+ * holding total_dims dims in all: the argmax keys and per-dim shard constants
+ * plus the general pruned kernel's per-step screening constants (16 B/dim +
+ * 180 B/block).  A CSR call given less returns CWQ_ERR_WORKSPACE (it never
+ * silently falls back to a slower kernel). */
 size_t cwq_greedy_encode_workspace_size(int64_t nb, int64_t total_dims);
+
+/* Workspace bytes needed by cwq_greedy_encode_uniform for nb blocks of
+ * dimension d: keys + shard constants only when d % 8 == 0, 8 <= d <= 64 (the
+ * fast pruned kernel), the cwq_greedy_encode_workspace_size layout otherwise. */
+size_t cwq_greedy_encode_uniform_workspace_size(int64_t nb, int64_t d);
 
 /* Greedy coded sampling, encoder (coded_greedy_sampler.py:29-89) for nb
  * independent blocks.
@@ -96,14 +119,15 @@ int cwq_greedy_encode(const float* t_loc, const float* t_scale, const float* p_l
                       int64_t total_dims, int64_t max_block_dim, int n_bits_per_step,
                       int n_steps, int32_t seed, float rho, int64_t block_id_base,
                       int32_t* out_idx, float* out_sample, void* workspace,
-                      size_t workspace_bytes, void* stream);
+                      size_t workspace_bytes, const cwq_options* opts, void* stream);
 
 /* Same with every block of dimension d (block g = dims [g*d, (g+1)*d)). */
 int cwq_greedy_encode_uniform(const float* t_loc, const float* t_scale, const float* p_loc,
                               const float* p_scale, int64_t nb, int64_t d,
                               int n_bits_per_step, int n_steps, int32_t seed, float rho,
                               int64_t block_id_base, int32_t* out_idx, float* out_sample,
-                              void* workspace, size_t workspace_bytes, void* stream);
+                              void* workspace, size_t workspace_bytes, const cwq_options* opts,
+                              void* stream);
 
 /* Decoder (coded_greedy_sampler.py:93-167): sample = sum over steps of the
  * proposal-shard candidate idx[g*n_steps + i] of step i.  O(n_steps * d) per
@@ -161,7 +185,7 @@ int64_t cwq_code_grouped_greedy(const float* q_loc, const float* q_scale, const 
                                 int64_t size_threshold, double n_nats, float* sample_host,
                                 char* bits_host, int64_t bits_cap, int64_t* starts_host,
                                 int64_t starts_cap, double* kl_sum_out, void* workspace,
-                                size_t workspace_bytes, void* stream);
+                                size_t workspace_bytes, const cwq_options* opts, void* stream);
 
 /* ---- Importance sampler (code/coded_importance_sampler.py) ------------- */
 /* Workspace bytes for cwq_importance_encode. */
@@ -177,7 +201,8 @@ int cwq_importance_encode(const float* t_loc, const float* t_scale, const float*
                           const float* p_scale, const int64_t* block_off,
                           const int64_t* n_samples, int64_t nb, int64_t total_dims, int32_t seed,
                           int64_t block_id_base, int64_t* out_index, float* out_sample,
-                          void* workspace, size_t workspace_bytes, void* stream);
+                          void* workspace, size_t workspace_bytes, const cwq_options* opts,
+                          void* stream);
 
 /* decode_importance_sample (:82-109): the last of index+1 samples, i.e. row
  * `index` of group g's stream. */
@@ -217,7 +242,8 @@ int64_t cwq_code_grouped_importance(const float* q_loc, const float* q_scale,
                                     int64_t* starts_host, int64_t starts_cap,
                                     int64_t* outlier_idx_host, float* outlier_val_host,
                                     int64_t* n_outliers, double* kl_sum_out, void* workspace,
-                                    size_t workspace_bytes, void* stream);
+                                    size_t workspace_bytes, const cwq_options* opts,
+                                    void* stream);
 
 /* ---- Arithmetic coder (code/coding.pyx:27-310), HOST functions ---------- */
 /* ArithmeticCoder(P, precision).encode(message): writes the code as '0'/'1'
@@ -279,20 +305,6 @@ int cwq_selftest_wave_max(const float* x, int64_t n_waves, float* out, void* str
  * last launch found for it). */
 int cwq_debug_prune_stats(unsigned long long* out72, int flags);
 
-/* Profiling hook (bench.py): when set, every later encode call made by this
- * host thread records hipEvent_t `start_event` on its stream right before its
- * first candidate-scoring (eval) launch and `stop_event` right after its last
- * one, so the caller can time the dominant kernel alone.  NULL, NULL clears. */
-int cwq_profile_set_eval_events(void* start_event, void* stop_event);
-
-/* Candidate pruning (DESIGN.md "pruning bound") is on by default for uniform
- * blocks with d % 8 == 0, d <= 64; it never changes results.  Modes for this
- * host thread (A/B timing and tests): 0 = off (every candidate scored
- * exactly), 1 = pruning on exact values, 2 (default) = pruning with the
- * screening pass (DESIGN.md "screening bound") where a tile's constants allow
- * it, exact pruning elsewhere.  Mode 2 also turns on the importance sampler's
- * screening pass; modes 0 and 1 score its candidates exactly. */
-int cwq_set_pruning(int mode);
 
 /* ---- PLN image codec plumbing (csrc/cwq_pln.hip) ----
  * The ladder network's transforms are library convolutions; these three

@@ -70,6 +70,12 @@ CWQO_API void cwqo_philox4x32_10(const uint32_t ctr_in[4], const uint32_t key_in
   out[0] = c0; out[1] = c1; out[2] = c2; out[3] = c3;
 }
 
+/* n independent blocks: out[4i..] = Philox4x32-10(ctr[4i..], key[2i..]) (pin tests) */
+CWQO_API void cwqo_philox4x32_10_many(const uint32_t* ctr, const uint32_t* key, int64_t n,
+                                      uint32_t* out) {
+  for (int64_t i = 0; i < n; ++i) cwqo_philox4x32_10(ctr + 4 * i, key + 2 * i, out + 4 * i);
+}
+
 /* A.2 TF stateless seed scrambling (stateless_random_ops.cc GenerateKey).
  * seed = [s0, s1] int32 (misc.py:11 passes [1000*seed+i, 42]); each is
  * sign-extended to 64 bits. */

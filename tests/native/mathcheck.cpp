@@ -23,4 +23,7 @@ void mc_philox(const uint32_t* ctr, const uint32_t* key, uint32_t* out) {
   cwq::U4 r = cwq::philox10(ctr[0], ctr[1], ctr[2], ctr[3], key[0], key[1]);
   out[0] = r.x; out[1] = r.y; out[2] = r.z; out[3] = r.w;
 }
+void mc_philox_many(const uint32_t* ctr, const uint32_t* key, int64_t n, uint32_t* out) {
+  for (int64_t i = 0; i < n; ++i) mc_philox(ctr + 4 * i, key + 2 * i, out + 4 * i);
+}
 }

@@ -35,16 +35,43 @@ def test_version_and_error(cwqlib):
 def test_invalid_args_rejected_before_launch(cwqlib):
     # argument validation happens on the host before any HIP call
     rc = cwqlib.cwq_greedy_encode_uniform(None, None, None, None, 1, 4, 31, 1, 42, 1.0, 0,
-                                          None, None, None, 0, None)
+                                          None, None, None, 0, None, None)
     assert rc == -1 and b"n_bits_per_step" in cwqlib.cwq_last_error()
     rc = cwqlib.cwq_greedy_encode_uniform(None, None, None, None, 1, 4, 8, 0, 42, 1.0, 0,
-                                          None, None, None, 0, None)
+                                          None, None, None, 0, None, None)
     assert rc == -1 and b"n_steps" in cwqlib.cwq_last_error()
-    need = cwqlib.cwq_greedy_encode_workspace_size(10, 40)
+    need = cwqlib.cwq_greedy_encode_uniform_workspace_size(10, 4)
     assert need >= 10 * 8 + 3 * 40 * 4
     rc = cwqlib.cwq_greedy_encode_uniform(1, 1, 1, 1, 10, 4, 8, 1, 42, 1.0, 0, 1, 1, 1,
-                                          need - 1, None)
+                                          need - 1, None, None)
     assert rc == -3
+
+
+def test_workspace_sizes_and_options_rejected(cwqlib):
+    """CSR encodes need the general pruned kernel's arrays: the CSR size always
+    holds them, so a CSR call given only the uniform-kernel size is refused
+    with CWQ_ERR_WORKSPACE (no silent unpruned run); bad options are refused
+    before any launch."""
+    from compression_without_quantization_amd import _lib
+    nb, d = 10, 32
+    uni = cwqlib.cwq_greedy_encode_uniform_workspace_size(nb, d)
+    csr = cwqlib.cwq_greedy_encode_workspace_size(nb, nb * d)
+    assert csr >= uni + 16 * nb * d + 180 * nb
+    # uniform d outside the fast kernel: the general layout either way
+    assert cwqlib.cwq_greedy_encode_uniform_workspace_size(nb, 9) == \
+        cwqlib.cwq_greedy_encode_workspace_size(nb, nb * 9)
+    rc = cwqlib.cwq_greedy_encode(1, 1, 1, 1, 1, nb, nb * d, d, 8, 1, 42, 1.0, 0, 1, 1, 1,
+                                  uni, None, None)
+    assert rc == -3 and b"workspace" in cwqlib.cwq_last_error()
+    for bad in (_lib.options(prune_mode=3), _lib.options(prune_mode=-1),
+                _lib.options(eval_events=(1, None))):
+        rc = cwqlib.cwq_greedy_encode_uniform(1, 1, 1, 1, nb, d, 8, 1, 42, 1.0, 0, 1, 1, 1,
+                                              uni, bad, None)
+        assert rc == -1 and b"cwq_options" in cwqlib.cwq_last_error()
+    o = _lib.options(prune_mode=1)
+    o.contents.reserved = 5
+    assert cwqlib.cwq_greedy_encode_uniform(1, 1, 1, 1, nb, d, 8, 1, 42, 1.0, 0, 1, 1, 1, uni,
+                                            o, None) == -1
 
 
 def test_group_starts_host(cwqlib):

@@ -1,9 +1,13 @@
-"""CPU: multi-rank block sharding over gloo (world_size 2), as bench.py --gpus N
-uses it (no collective on the data path; optional all-gather of indices)."""
+"""CPU: multi-rank block sharding over gloo (world_size 2 and 3), as bench.py
+--gpus N uses it (no collective on the data path; optional all-gather of
+indices).  Each rank codes its shard with the CPU oracle (the checker, allowed
+in tests) using block_id_base = its first global block; the gathered indices
+must equal one single-process encode of all blocks."""
 import os
 import socket
 
 import numpy as np
+import pytest
 import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
@@ -37,31 +41,63 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, nb, out):
+def _worker(rank, world, port, nb, cost, out):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
+    from oracle import oracle as O
+    from compression_without_quantization_amd.synthetic import make_blocks_range
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    b0, b1 = shard_range(nb, world, rank)
-    # stand-in for per-rank coded indices: a deterministic function of the
-    # global block id (what block_id_base guarantees for the real coder)
-    local = torch.arange(b0, b1, dtype=torch.int32) * 7 + 3
-    full = gather_indices(local, b1 - b0)
+    d, bits = 8, 6
+    b0, b1 = shard_range(nb, world, rank, cost)
+    h = make_blocks_range(b0, b1, d, bits)
+    idx, _ = O.greedy_encode(h["post_loc"], h["post_scale"], h["prior_loc"], h["prior_scale"],
+                             np.arange(b1 - b0 + 1, dtype=np.int64) * d, bits, 1, 42, 1.0, b0, 1)
+    local = torch.from_numpy(idx.reshape(-1).astype(np.int32))
+    # ranks may own different block counts (cost-balanced cuts): pad to the max
+    n = torch.tensor([local.numel()])
+    sizes = [torch.zeros_like(n) for _ in range(world)]
+    dist.all_gather(sizes, n)
+    m = int(max(int(v) for v in sizes))
+    padded = torch.full((m,), -1, dtype=torch.int32)
+    padded[:local.numel()] = local
+    full = gather_indices(padded, m)
     if rank == 0:
-        out.put(full.numpy().tolist())
+        parts = [full[r * m:r * m + int(sizes[r])] for r in range(world)]
+        out.put(torch.cat(parts).numpy().tolist())
     dist.barrier()
     dist.destroy_process_group()
 
 
-def test_gloo_two_ranks_gather():
-    world, nb = 2, 10
+@pytest.mark.parametrize("world,balanced", [(2, False), (3, True)])
+def test_gloo_ranks_gather_oracle_coded_shards(world, balanced):
+    from oracle import oracle as O
+    from compression_without_quantization_amd.synthetic import make_blocks_range
+    O.build()
+    nb, d, bits = 40, 8, 6
+    cost = None
+    if balanced:
+        cost = np.random.default_rng(3).integers(1, 50, nb).astype(np.float64).tolist()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, nb, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, nb, cost, q))
+             for r in range(world)]
     for p in procs:
         p.start()
-    got = q.get(timeout=120)
+    got = q.get(timeout=180)
     for p in procs:
         p.join(timeout=120)
         assert p.exitcode == 0
-    assert got == [b * 7 + 3 for b in range(nb)]
+    h = make_blocks_range(0, nb, d, bits)
+    want, _ = O.greedy_encode(h["post_loc"], h["post_scale"], h["prior_loc"], h["prior_scale"],
+                              np.arange(nb + 1, dtype=np.int64) * d, bits, 1, 42)
+    assert got == want.reshape(-1).tolist()
+
+
+def test_make_blocks_range_is_shard_independent():
+    from compression_without_quantization_amd.synthetic import make_blocks_range
+    full = make_blocks_range(0, 70000, 4, 8, chunk=1 << 15)
+    for b0, b1 in ((0, 1), (32767, 32769), (40000, 70000), (65535, 65536)):
+        part = make_blocks_range(b0, b1, 4, 8, chunk=1 << 15)
+        for k in full:
+            assert np.array_equal(part[k], full[k][b0:b1])

@@ -276,14 +276,12 @@ def test_c4_full_size_roundtrip_and_sample(cwq, oracle):
 # the oracle, including adversarial inputs where the bound is tight or useless
 # ---------------------------------------------------------------------------
 def _uniform_encode(cwq, cwqlib, tl, ts, pl, ps, d, bits, n_steps, seed, rho, mode):
-    """mode: 0 unpruned, 1 pruning on exact values, 2 pruning with screening."""
-    cwqlib.cwq_set_pruning(int(mode))
-    try:
-        i, s = cwq.encode_blocks(tl, ts, pl, ps, bits, n_steps, seed, rho=rho, block_dim=d)
-        torch.cuda.synchronize()
-        return i.cpu().numpy(), s.cpu().numpy()
-    finally:
-        cwqlib.cwq_set_pruning(2)
+    """mode: 0 unpruned, 1 pruning on exact values, 2 pruning with screening
+    (cwq_options.prune_mode of this call only)."""
+    i, s = cwq.encode_blocks(tl, ts, pl, ps, bits, n_steps, seed, rho=rho, block_dim=d,
+                             prune_mode=int(mode))
+    torch.cuda.synchronize()
+    return i.cpu().numpy(), s.cpu().numpy()
 
 
 @pytest.mark.parametrize("d,bits,n_steps,nb,rho", [
@@ -520,13 +518,9 @@ def test_importance_grouped_golden(cwq, golden):
 def _importance_modes(cwq, cwqlib, tl, ts, pl, ps, off, ns, seed):
     out = []
     for mode in (0, 2):
-        cwqlib.cwq_set_pruning(mode)
-        try:
-            i, s = cwq.importance_encode_blocks(tl, ts, pl, ps, off, ns, seed)
-            torch.cuda.synchronize()
-            out.append((i.cpu().numpy(), s.cpu().numpy()))
-        finally:
-            cwqlib.cwq_set_pruning(2)
+        i, s = cwq.importance_encode_blocks(tl, ts, pl, ps, off, ns, seed, prune_mode=mode)
+        torch.cuda.synchronize()
+        out.append((i.cpu().numpy(), s.cpu().numpy()))
     return out
 
 
@@ -602,13 +596,10 @@ def test_pruned_random_stress(cwq, cwqlib, trial):
 # fast kernel does not take, >= 4096 candidates
 # ---------------------------------------------------------------------------
 def _csr_encode(cwq, cwqlib, tl, ts, pl, ps, off, bits, n_steps, seed, rho, mode):
-    cwqlib.cwq_set_pruning(int(mode))
-    try:
-        i, s = cwq.encode_blocks(tl, ts, pl, ps, bits, n_steps, seed, rho=rho, block_off=off)
-        torch.cuda.synchronize()
-        return i.cpu().numpy(), s.cpu().numpy()
-    finally:
-        cwqlib.cwq_set_pruning(2)
+    i, s = cwq.encode_blocks(tl, ts, pl, ps, bits, n_steps, seed, rho=rho, block_off=off,
+                             prune_mode=int(mode))
+    torch.cuda.synchronize()
+    return i.cpu().numpy(), s.cpu().numpy()
 
 
 def _heavy_inputs(rng, n):
@@ -855,15 +846,15 @@ def test_encode_captured_in_hip_graph(cwq, cwqlib):
     nb, steps, bits = len(sizes), 3, 12
     idx = torch.zeros((nb, steps), dtype=torch.int32, device=dev)
     smp = torch.zeros(D, dtype=torch.float32, device=dev)
-    ws = torch.empty(cwqlib.cwq_greedy_encode_workspace_size(nb, D) + 16 * D + 192 * nb + 2048,
-                     dtype=torch.uint8, device=dev)
+    ws = torch.empty(cwqlib.cwq_greedy_encode_workspace_size(nb, D), dtype=torch.uint8,
+                     device=dev)
     ub, ud = 64, 32                                    # uniform C4-shaped blocks
     utl = f(rng.standard_normal(ub * ud) * 0.5)
     uts = f(rng.uniform(0.3, 0.9, ub * ud))
     uz, uo = torch.zeros(ub * ud, device=dev), torch.ones(ub * ud, device=dev)
     uidx = torch.zeros((ub, 1), dtype=torch.int32, device=dev)
     usmp = torch.zeros(ub * ud, dtype=torch.float32, device=dev)
-    uws = torch.empty(cwqlib.cwq_greedy_encode_workspace_size(ub, ub * ud), dtype=torch.uint8,
+    uws = torch.empty(cwqlib.cwq_greedy_encode_uniform_workspace_size(ub, ud), dtype=torch.uint8,
                       device=dev)
 
     def run():
@@ -871,10 +862,10 @@ def test_encode_captured_in_hip_graph(cwq, cwqlib):
         assert cwqlib.cwq_greedy_encode(
             tl.data_ptr(), ts.data_ptr(), z.data_ptr(), o.data_ptr(), offs.data_ptr(), nb, D,
             max(sizes), bits, steps, 42, 1.0, 0, idx.data_ptr(), smp.data_ptr(), ws.data_ptr(),
-            ws.numel(), st) == 0
+            ws.numel(), None, st) == 0
         assert cwqlib.cwq_greedy_encode_uniform(
             utl.data_ptr(), uts.data_ptr(), uz.data_ptr(), uo.data_ptr(), ub, ud, 14, 1, 7, 1.0,
-            0, uidx.data_ptr(), usmp.data_ptr(), uws.data_ptr(), uws.numel(), st) == 0
+            0, uidx.data_ptr(), usmp.data_ptr(), uws.data_ptr(), uws.numel(), None, st) == 0
 
     side = torch.cuda.Stream()
     side.wait_stream(torch.cuda.current_stream())

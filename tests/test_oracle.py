@@ -8,7 +8,7 @@ import os
 import numpy as np
 import pytest
 
-from conftest import GOLDEN
+from conftest import GOLDEN, REPO
 from compression_without_quantization_amd import binary_io as B
 from compression_without_quantization_amd.coded_greedy_sampler import group_size_threshold
 
@@ -29,6 +29,41 @@ def test_philox_random123_kat(oracle, mathcheck):
                             key.ctypes.data_as(ctypes.c_void_p),
                             out.ctypes.data_as(ctypes.c_void_p))
         assert list(out) == want  # the product header's Philox
+
+
+def test_philox_three_implementations_agree(oracle, mathcheck):
+    """SURVEY.md 8(c) pin 1: the oracle's Philox4x32-10, the product header's
+    (csrc/cwq_math.h) and ROCm's own rocRAND engine
+    (/opt/rocm/include/rocrand/rocrand_philox4x32_10.h:270-302, compiled for the
+    host by tests/native/rocrand_pin.cpp) on 10^6 random (counter, key) pairs,
+    plus the edge words 0 and 0xffffffff."""
+    import subprocess
+    subprocess.check_call(["make", "-C", REPO, "tests/native/librocrand_pin.so"],
+                          stdout=subprocess.DEVNULL)
+    rr = ctypes.CDLL(os.path.join(REPO, "tests", "native", "librocrand_pin.so"))
+    vp = ctypes.c_void_p
+    for f in (rr.rr_philox_many, oracle.lib().cwqo_philox4x32_10_many, mathcheck.mc_philox_many):
+        f.argtypes = [vp, vp, ctypes.c_int64, vp]
+        f.restype = None
+    rng = np.random.default_rng(123)
+    n = 1_000_000
+    ctr = rng.integers(0, 1 << 32, (n, 4), dtype=np.uint64).astype(np.uint32)
+    key = rng.integers(0, 1 << 32, (n, 2), dtype=np.uint64).astype(np.uint32)
+    ctr[:16] = np.array([0, 0xffffffff], np.uint32)[(np.arange(64).reshape(16, 4) >> 1) & 1]
+    key[:16] = np.array([0, 0xffffffff], np.uint32)[np.arange(32).reshape(16, 2) & 1]
+    outs = []
+    for f in (rr.rr_philox_many, oracle.lib().cwqo_philox4x32_10_many, mathcheck.mc_philox_many):
+        o = np.zeros((n, 4), np.uint32)
+        f(ctr.ctypes.data, key.ctypes.data, n, o.ctypes.data)
+        outs.append(o)
+    assert np.array_equal(outs[0], outs[1]), "rocRAND vs oracle"
+    assert np.array_equal(outs[0], outs[2]), "rocRAND vs product header"
+    kat = _json("philox_kat.json")["vectors"][0]  # ctr 0, key 0
+    assert [int(x, 16) for x in kat["ctr"]] == [0, 0, 0, 0]
+    o = np.zeros(4, np.uint32)
+    z = np.zeros(4, np.uint32)
+    rr.rr_philox_many(z.ctypes.data, z.ctypes.data, 1, o.ctypes.data)
+    assert list(o) == [int(x, 16) for x in kat["out"]]
 
 
 def test_stateless_normal_fixture(oracle):

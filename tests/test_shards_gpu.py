@@ -1,0 +1,212 @@
+"""GPU: the multi-GPU partitioning on the HIP path, the C3 workload, and the
+bench's own N-rank launcher.
+
+Sharding rests on one property of the reference: group g is coded with seed
+``seed + g`` (coded_greedy_sampler.py:282), so a shard coded with
+block_id_base = its first global block reproduces the single-call result.
+These tests check that property bit for bit on the kernels (uniform and
+ragged CSR blocks, the multi-step CSR path that forks onto the library's
+streams, even and cost-balanced cuts), then run the C3 image set through the
+grouped pipeline, and finally run ``bench.py --gpus 2`` as a fresh process.
+"""
+import json
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import REPO
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def cwq(cwqlib):
+    assert torch.cuda.is_available(), "GPU tests need a ROCm device"
+    import compression_without_quantization_amd as C
+    return C
+
+
+def _u32(a):
+    return np.ascontiguousarray(np.asarray(a, np.float32)).view(np.uint32)
+
+
+def _encode_sharded(cwq, arrays, cuts, bits, n_steps, seed, off=None, d=None):
+    """Encode [cuts[r], cuts[r+1]) blocks per shard with block_id_base = cuts[r];
+    return the concatenated (idx, sample) as host arrays."""
+    tl, ts, pl, ps = arrays
+    idx_parts, smp_parts = [], []
+    for b0, b1 in zip(cuts[:-1], cuts[1:]):
+        if off is None:
+            sl = slice(b0 * d, b1 * d)
+            i, s = cwq.encode_blocks(tl[sl], ts[sl], pl[sl], ps[sl], bits, n_steps, seed,
+                                     block_dim=d, block_id_base=b0)
+        else:
+            sl = slice(int(off[b0]), int(off[b1]))
+            i, s = cwq.encode_blocks(tl[sl], ts[sl], pl[sl], ps[sl], bits, n_steps, seed,
+                                     block_off=off[b0:b1 + 1] - off[b0], block_id_base=b0)
+        idx_parts.append(i.cpu().numpy().reshape(-1, n_steps))
+        smp_parts.append(s.cpu().numpy())
+    return np.concatenate(idx_parts), np.concatenate(smp_parts)
+
+
+def _cuts(nb, world, cost=None):
+    from compression_without_quantization_amd.parallel import shard_range
+    spans = [shard_range(nb, world, r, cost) for r in range(world)]
+    return [spans[0][0]] + [b for _, b in spans]
+
+
+def test_uniform_shards_concatenate_to_single_call(cwq, oracle):
+    """C4-shaped slice (d=32, 16 bits): one call == 2 even shards == 3
+    cost-balanced shards, bit for bit; oracle on sampled blocks of each shard."""
+    from compression_without_quantization_amd.synthetic import make_blocks_range
+    nb, d, bits, seed = 6000, 32, 16, 42
+    h = make_blocks_range(0, nb, d, bits)
+    host = [h[k].reshape(-1) for k in ("post_loc", "post_scale", "prior_loc", "prior_scale")]
+    dev = torch.device("cuda")
+    arrays = [torch.from_numpy(a).to(dev) for a in host]
+    i1, s1 = _encode_sharded(cwq, arrays, [0, nb], bits, 1, seed, d=d)
+    for cuts in (_cuts(nb, 2), _cuts(nb, 3, cost=np.full(nb, d * 2.0 ** bits)), [0, 1, 4097, nb]):
+        ik, sk = _encode_sharded(cwq, arrays, cuts, bits, 1, seed, d=d)
+        assert np.array_equal(ik, i1), f"indices differ for cuts {cuts}"
+        assert np.array_equal(_u32(sk), _u32(s1)), f"samples differ for cuts {cuts}"
+    # oracle: first, last and a middle block of every 3-way shard
+    for b in sorted({0, 1999, 2000, 2001, 3999, 4000, nb - 1}):
+        sl = slice(b * d, (b + 1) * d)
+        wi, ws = oracle.greedy_encode(host[0][sl], host[1][sl], host[2][sl], host[3][sl],
+                                      np.array([0, d], np.int64), bits, 1, seed, 1.0, b)
+        assert int(wi.reshape(-1)[0]) == int(i1[b, 0]), f"block {b}"
+        assert np.array_equal(_u32(ws), _u32(s1[sl])), f"block {b}"
+
+
+def test_ragged_csr_shards_multistep(cwq, oracle):
+    """Ragged groups (sizes 1..4095, the C2/C3 group-size range), 14 bits x 3
+    steps -- the general pruned kernel and the multi-stream step split -- one
+    call vs 2 even and 3 cost-balanced shard_range cuts (cost d_g 2^b n_steps)."""
+    rng = np.random.default_rng(2026)
+    sizes = np.concatenate([rng.integers(1, 64, 40), rng.integers(64, 4096, 6), [1, 4095]])
+    rng.shuffle(sizes)
+    off = np.concatenate([[0], np.cumsum(sizes)]).astype(np.int64)
+    D, nb = int(off[-1]), sizes.size
+    bits, n_steps, seed = 14, 3, 7
+    tl = rng.standard_normal(D).astype(np.float32) * 0.3
+    ts = rng.uniform(0.5, 1.0, D).astype(np.float32)
+    pl = np.zeros(D, np.float32)
+    ps = np.ones(D, np.float32)
+    dev = torch.device("cuda")
+    arrays = [torch.from_numpy(a).to(dev) for a in (tl, ts, pl, ps)]
+    i1, s1 = _encode_sharded(cwq, arrays, [0, nb], bits, n_steps, seed, off=off)
+    cost = sizes.astype(np.float64) * 2.0 ** bits * n_steps
+    for cuts in (_cuts(nb, 2), _cuts(nb, 3, cost=cost)):
+        ik, sk = _encode_sharded(cwq, arrays, cuts, bits, n_steps, seed, off=off)
+        assert np.array_equal(ik, i1), f"indices differ for cuts {cuts}"
+        assert np.array_equal(_u32(sk), _u32(s1)), f"samples differ for cuts {cuts}"
+    # oracle on a few groups (incl. the longest and a single-dim group)
+    for g in sorted({0, int(np.argmax(sizes)), int(np.argmin(sizes)), nb - 1}):
+        sl = slice(int(off[g]), int(off[g + 1]))
+        wi, ws = oracle.greedy_encode(tl[sl], ts[sl], pl[sl], ps[sl],
+                                      np.array([0, sizes[g]], np.int64), bits, n_steps, seed,
+                                      1.0, g)
+        assert np.array_equal(wi.reshape(-1), i1[g]), f"group {g}"
+        assert np.array_equal(_u32(ws), _u32(s1[sl])), f"group {g}"
+
+
+def test_q4_kernels_match_unaligned_fallback(cwq, oracle):
+    """The float4 finalize/decode kernels (uniform d % 4 == 0) against the
+    per-dim kernels they replace, reached through 4-byte-offset views (the
+    launchers fall back when a base is not 16-byte aligned); d=12 (3 Philox
+    blocks per row) and d=32, 1 and 3 steps."""
+    rng = np.random.default_rng(5)
+    dev = torch.device("cuda")
+    for d, bits, n_steps in ((12, 10, 1), (32, 12, 3), (32, 16, 1)):
+        nb = 300
+        n = nb * d
+        buf = [torch.from_numpy(np.concatenate([[0.0], a]).astype(np.float32)).to(dev)
+               for a in (rng.standard_normal(n) * 0.5, rng.uniform(0.3, 0.9, n),
+                         rng.standard_normal(n), rng.uniform(0.5, 2.0, n))]
+        al = [b[1:].clone() for b in buf]          # aligned copies
+        un = [b[1:] for b in buf]                  # offset views: 4 bytes past a 256-B base
+        assert un[0].data_ptr() % 16 == 4
+        ia, sa = cwq.encode_blocks(*al, bits, n_steps, 42, block_dim=d)
+        out_u = torch.empty(n + 1, dtype=torch.float32, device=dev)[1:]
+        iu, su = cwq.encode_blocks(*un, bits, n_steps, 42, block_dim=d, out_sample=out_u)
+        assert torch.equal(ia, iu)
+        assert torch.equal(sa.view(torch.int32), su.view(torch.int32))
+        da = cwq.decode_blocks(ia, al[2], al[3], bits, n_steps, 42, block_dim=d)
+        dec_u = torch.empty(n + 1, dtype=torch.float32, device=dev)[1:]
+        du = cwq.decode_blocks(ia, un[2], un[3], bits, n_steps, 42, block_dim=d,
+                               out_sample=dec_u)
+        assert torch.equal(da.view(torch.int32), sa.view(torch.int32))
+        assert torch.equal(du.view(torch.int32), sa.view(torch.int32))
+        h = [a.cpu().numpy() for a in al]
+        for b in (0, nb - 1):
+            sl = slice(b * d, (b + 1) * d)
+            wi, ws = oracle.greedy_encode(h[0][sl], h[1][sl], h[2][sl], h[3][sl],
+                                          np.array([0, d], np.int64), bits, n_steps, 42, 1.0, b)
+            assert np.array_equal(wi.reshape(-1), ia[b].cpu().numpy())
+            assert np.array_equal(_u32(ws), _u32(sa[sl].cpu().numpy()))
+
+
+def test_c3_image_set(cwq, oracle):
+    """C3: 24 images x (196,608 level-1 + 2,304 level-2 latents) through
+    code_grouped_greedy_sample at 8 bits/group (pln.py:350, :463-472; the two
+    levels as independent latent sets -- no trained SynthesisTransform_2 links
+    them offline).  Images 0 and 23 against the oracle in full; every image:
+    bitcode length = groups x 8 and a bit-exact decode round trip."""
+    from compression_without_quantization_amd.synthetic import make_latents
+    cwq.coded_greedy_sampler.VERBOSE = False
+    thr = cwq.group_size_threshold(12)
+    for i in range(24):
+        for li, D in enumerate((32 * 48 * 128, 8 * 12 * 24)):
+            q_loc, q_scale, p_loc, p_scale = make_latents(D, seed=1000 * i + li)
+            target, proposal = cwq.Normal(q_loc, q_scale), cwq.Normal(p_loc, p_scale)
+            sample, bitcode, starts = cwq.code_grouped_greedy_sample(None, target, proposal, 1,
+                                                                     8, 42)
+            assert starts[0] == 0 and starts[-1] == D
+            assert len(bitcode) == (len(starts) - 1) * 8, f"image {i} level {li}"
+            dec = cwq.decode_grouped_greedy_sample(None, bitcode, starts, proposal, 8, 1, 42)
+            assert np.array_equal(_u32(dec), _u32(sample)), f"image {i} level {li} decode"
+            if i in (0, 23):
+                ws, wi, wst = oracle.code_grouped_greedy_sample(q_loc, q_scale, p_loc, p_scale,
+                                                                1, 8, 42, thr)
+                assert starts == wst, f"image {i} level {li} groups"
+                assert bitcode == cwq.indices_to_bitcode(wi, 8), f"image {i} level {li} code"
+                assert np.array_equal(_u32(sample), _u32(ws)), f"image {i} level {li} sample"
+
+
+def _bench(args, timeout=300):
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    r = subprocess.run([sys.executable, "-u", os.path.join(REPO, "bench.py")] + args,
+                       cwd=REPO, env=env, capture_output=True, text=True, timeout=timeout)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    return json.loads(lines[0])
+
+
+def test_bench_launches_two_ranks_itself(cwq):
+    """`bench.py --gpus 2` with no launcher environment starts two rank
+    processes (here sharing the one GPU over gloo), codes 8192 C4 blocks split
+    between them (strong scaling) and checks every rank's sample against the
+    oracle: one JSON line with n_gpus == 2 and no mismatch."""
+    line = _bench(["--gpus", "2", "--blocks", "8192", "--steps", "1", "--warmup", "0",
+                   "--no-e2e"])
+    assert line["n_gpus"] == 2 and line["config"]["world_size_checked"] == 2
+    assert line["scaling"] == "strong"
+    assert line["config"]["blocks_total"] == 8192 and line["config"]["blocks_per_gpu"] == 4096
+    assert line["parity"]["index_mismatches"] == 0
+    assert line["parity"]["sample_word_mismatches"] == 0
+    assert line["parity"]["blocks_checked"] >= 2 * 16
+    assert line["decode_roundtrip_bit_exact"] is True
+    assert line["value"] > 0
+
+
+def test_bench_weak_scaling_two_ranks(cwq):
+    line = _bench(["--gpus", "2", "--blocks", "2048", "--steps", "1", "--warmup", "0",
+                   "--no-e2e", "--scaling", "weak", "--config", "c4"])
+    assert line["n_gpus"] == 2 and line["scaling"] == "weak"
+    assert line["config"]["blocks_total"] == 4096 and line["config"]["blocks_per_gpu"] == 2048
+    assert line["parity"]["index_mismatches"] == 0

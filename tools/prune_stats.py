@@ -15,7 +15,6 @@ mode = int(sys.argv[2]) if len(sys.argv) > 2 else 2
 d = int(os.environ.get("PS_D", "32"))
 bits = int(os.environ.get("PS_BITS", "16"))
 lib = _lib.load()
-lib.cwq_set_pruning(mode)
 h = make_blocks(nb, d, bits, seed=20261015)
 t = {k: torch.from_numpy(v.reshape(-1)).cuda() for k, v in h.items()}
 out = (ctypes.c_ulonglong * 72)()
@@ -24,7 +23,7 @@ out = (ctypes.c_ulonglong * 72)()
 def run(flags):
     lib.cwq_debug_prune_stats(out, 1 | flags)
     i, _ = C.encode_blocks(t["post_loc"], t["post_scale"], t["prior_loc"], t["prior_scale"], bits,
-                           1, 42, block_dim=d)
+                           1, 42, block_dim=d, prune_mode=mode)
     torch.cuda.synchronize()
     assert lib.cwq_debug_prune_stats(out, 1) == 1, "not a CWQ_PRUNE_STATS build"
     return i.cpu().numpy(), np.array(out[:], dtype=np.float64)

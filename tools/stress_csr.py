@@ -47,13 +47,10 @@ VERBOSE = bool(os.environ.get("STRESS_VERBOSE"))
 def encode(lib, tl, ts, pl, ps, off, bits, n_steps, seed, rho, mode):
     if VERBOSE:
         print(f"  mode {mode} ...", flush=True)
-    lib.cwq_set_pruning(mode)
-    try:
-        i, s = C.encode_blocks(tl, ts, pl, ps, bits, n_steps, seed, rho=rho, block_off=off)
-        torch.cuda.synchronize()
-        return i.cpu().numpy(), s.cpu().numpy().view(np.uint32)
-    finally:
-        lib.cwq_set_pruning(2)
+    i, s = C.encode_blocks(tl, ts, pl, ps, bits, n_steps, seed, rho=rho, block_off=off,
+                           prune_mode=mode)
+    torch.cuda.synchronize()
+    return i.cpu().numpy(), s.cpu().numpy().view(np.uint32)
 
 
 def main():

@@ -67,13 +67,9 @@ def main():
         seed = int(rng.integers(-2 ** 31, 2 ** 31 - 1))
         out = []
         for mode in (0, 2):
-            lib.cwq_set_pruning(mode)
-            try:
-                i, s = C.importance_encode_blocks(tl, ts, pl, ps, off, ns, seed)
-                torch.cuda.synchronize()
-                out.append((i.cpu().numpy(), s.cpu().numpy().view(np.uint32)))
-            finally:
-                lib.cwq_set_pruning(2)
+            i, s = C.importance_encode_blocks(tl, ts, pl, ps, off, ns, seed, prune_mode=mode)
+            torch.cuda.synchronize()
+            out.append((i.cpu().numpy(), s.cpu().numpy().view(np.uint32)))
         dec = C.importance_decode_blocks(out[1][0], pl, ps, off, seed)
         dec = dec.cpu().numpy().view(np.uint32)
         ok = (np.array_equal(out[0][0], out[1][0]) and np.array_equal(out[0][1], out[1][1])

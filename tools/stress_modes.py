@@ -32,11 +32,10 @@ for t in range(first, first + trials):
         ts = (ps * np.exp(rng.uniform(-9, -6, n))).astype(np.float32)
     outs = []
     for mode in (0, 1, 2):
-        lib.cwq_set_pruning(mode)
-        i, s = C.encode_blocks(tl, ts, pl, ps, bits, n_steps, seed, rho=rho, block_dim=d)
+        i, s = C.encode_blocks(tl, ts, pl, ps, bits, n_steps, seed, rho=rho, block_dim=d,
+                               prune_mode=mode)
         torch.cuda.synchronize()
         outs.append((i.cpu().numpy(), s.cpu().numpy().view(np.uint32)))
-    lib.cwq_set_pruning(2)
     ok = all(np.array_equal(outs[0][0], o[0]) and np.array_equal(outs[0][1], o[1]) for o in outs[1:])
     if not ok:
         bad += 1
