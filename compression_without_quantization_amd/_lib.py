@@ -47,7 +47,7 @@ SIGNATURES = {
     "cwq_version": (c_int, []),
     "cwq_last_error": (c_str, []),
     "cwq_stateless_normal_sample": (c_int, [c_vp, c_vp, c_i64, c_i64, c_i32, c_vp, c_vp]),
-    "cwq_greedy_encode_workspace_size": (c_size, [c_i64, c_i64]),
+    "cwq_greedy_encode_workspace_size": (c_size, [c_i64, c_i64, c_i64]),
     "cwq_greedy_encode_uniform_workspace_size": (c_size, [c_i64, c_i64]),
     "cwq_greedy_encode": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_int,
                                   c_int, c_i32, c_f32, c_i64, c_vp, c_vp, c_vp, c_size, c_opts,

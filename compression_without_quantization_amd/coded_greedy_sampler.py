@@ -90,13 +90,15 @@ class Normal:
 # ---------------------------------------------------------------------------
 # batched block API (C ABI: cwq_greedy_encode[_uniform], cwq_greedy_decode[_uniform])
 # ---------------------------------------------------------------------------
-def encode_workspace_bytes(nb, total_dims, block_dim=None):
-    """Workspace bytes of encode_blocks: CSR blocks (nb, total_dims), or
-    uniform blocks of ``block_dim`` (cwq_greedy_encode[_uniform]_workspace_size)."""
+def encode_workspace_bytes(nb, total_dims, block_dim=None, max_block_dim=None):
+    """Workspace bytes of encode_blocks: CSR blocks (nb, total_dims, none
+    longer than ``max_block_dim``, default total_dims), or uniform blocks of
+    ``block_dim`` (cwq_greedy_encode[_uniform]_workspace_size)."""
     lib = _lib.load()
     if block_dim is not None:
         return int(lib.cwq_greedy_encode_uniform_workspace_size(int(nb), int(block_dim)))
-    return int(lib.cwq_greedy_encode_workspace_size(int(nb), int(total_dims)))
+    mbd = int(total_dims if max_block_dim is None else max_block_dim)
+    return int(lib.cwq_greedy_encode_workspace_size(int(nb), int(total_dims), mbd))
 
 
 def encode_blocks(t_loc, t_scale, p_loc, p_scale, n_bits_per_step, n_steps, seed, rho=1.,
@@ -143,7 +145,8 @@ def encode_blocks(t_loc, t_scale, p_loc, p_scale, n_bits_per_step, n_steps, seed
         out_idx = torch.empty((nb, n_steps), dtype=torch.int32, device=dev)
     if out_sample is None:
         out_sample = torch.empty(D, dtype=torch.float32, device=dev)
-    need = encode_workspace_bytes(nb, D, block_dim if offs is None else None)
+    need = encode_workspace_bytes(nb, D, block_dim if offs is None else None,
+                                  None if offs is None else max_block_dim)
     if workspace is None or workspace.numel() < need:
         workspace = torch.empty(max(need, 1), dtype=torch.uint8, device=dev)
     opts = _lib.options(prune_mode, eval_events)

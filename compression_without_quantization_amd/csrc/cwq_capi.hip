@@ -42,21 +42,19 @@ int hip_fail(hipError_t e, const char* where) {
 size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
 
 struct WsLayout {
-  size_t keys, loc_s, scale_s, lognorm, sab, bpre, ordu, grp, gtau, total;
-  bool csr;  // has the general pruned kernel's arrays
+  size_t keys, loc_s, scale_s, lognorm, sab, bpre, ordu, grp, gtau, abp, total;
+  bool csr;   // has the general pruned kernel's arrays
+  bool recs;  // ... and the visit-order records of blocks longer than CWQ_CSR_LDS_DIMS
 };
 
 // Blocks the uniform fast pruned kernel takes (d % 8 == 0, 8 <= d <= 64) need
 // only keys + the per-dim shard constants; everything else (CSR, other d) also
-// gets the general pruned kernel's screening constants (16 B/dim + 180 B/block).
-bool ws_needs_csr(int64_t nb, int64_t total_dims) {
-  if (nb <= 0) return false;
-  if (total_dims % nb) return true;
-  const int64_t d = total_dims / nb;
-  return !(d % 8 == 0 && d >= 8 && d <= 64);
-}
+// gets the general pruned kernel's screening constants (16 B/dim + 180 B/block),
+// and, when some block may exceed CWQ_CSR_LDS_DIMS dims, its visit-order
+// records (32 B/dim + 384 B/block).
+bool uniform_fast(int64_t d) { return d % 8 == 0 && d >= 8 && d <= 64; }
 
-WsLayout ws_layout(int64_t nb, int64_t total_dims, bool csr) {
+WsLayout ws_layout(int64_t nb, int64_t total_dims, bool csr, bool recs) {
   WsLayout l;
   size_t o = 0;
   l.keys = o;
@@ -68,7 +66,8 @@ WsLayout ws_layout(int64_t nb, int64_t total_dims, bool csr) {
   l.lognorm = o;
   o = align_up(o + (size_t)total_dims * 4, 256);
   l.csr = csr;
-  l.sab = l.bpre = l.ordu = l.grp = l.gtau = o;
+  l.recs = csr && recs;
+  l.sab = l.bpre = l.ordu = l.grp = l.gtau = l.abp = o;
   if (csr) {
     l.sab = o;
     o = align_up(o + (size_t)(total_dims + 8 * nb) * 8, 256);
@@ -80,12 +79,21 @@ WsLayout ws_layout(int64_t nb, int64_t total_dims, bool csr) {
     o = align_up(o + (size_t)nb * 16, 256);
     l.gtau = o;
     o = align_up(o + (size_t)nb * 4 * CWQ_CSR_GTAU_STRIDE, 256);
+    if (l.recs) {
+      l.abp = o;
+      o = align_up(o + (size_t)(total_dims + 12 * nb) * 32, 256);
+    }
   }
   l.total = o;
   return l;
 }
-WsLayout ws_layout(int64_t nb, int64_t total_dims) {
-  return ws_layout(nb, total_dims, ws_needs_csr(nb, total_dims));
+// CSR blocks of at most max_block_dim dims
+WsLayout ws_layout_csr(int64_t nb, int64_t total_dims, int64_t max_block_dim) {
+  return ws_layout(nb, total_dims, true, max_block_dim > CWQ_CSR_LDS_DIMS);
+}
+WsLayout ws_layout_uniform(int64_t nb, int64_t d) {
+  const bool csr = nb > 0 && !uniform_fast(d);
+  return ws_layout(nb, nb * d, csr, d > CWQ_CSR_LDS_DIMS);
 }
 
 void choose_tiling(int64_t nb, int64_t n_cand, int64_t* tiles_per_block, int64_t* cand_per_tile) {
@@ -307,7 +315,7 @@ int check_common(int n_bits, int n_steps, int64_t nb) {
 
 int encode_impl(const float* t_loc, const float* t_scale, const float* p_loc,
                 const float* p_scale, const int64_t* block_off, int64_t ud, int64_t nb,
-                int64_t total_dims, int n_bits, int n_steps, int32_t seed, float rho,
+                int64_t total_dims, int64_t max_block_dim, int n_bits, int n_steps, int32_t seed, float rho,
                 int64_t block_id_base, int32_t* out_idx, float* out_sample, void* workspace,
                 size_t workspace_bytes, const cwq_options* opts, void* stream) {
   int rc = check_common(n_bits, n_steps, nb);
@@ -320,7 +328,8 @@ int encode_impl(const float* t_loc, const float* t_scale, const float* p_loc,
     return fail(CWQ_ERR_INVALID, "null input/output pointer");
   // required: cwq_greedy_encode_workspace_size (CSR: always the general pruned
   // kernel's arrays) or cwq_greedy_encode_uniform_workspace_size
-  const WsLayout l = block_off ? ws_layout(nb, total_dims, true) : ws_layout(nb, total_dims);
+  const WsLayout l =
+      block_off ? ws_layout_csr(nb, total_dims, max_block_dim) : ws_layout_uniform(nb, ud);
   if (workspace_bytes < l.total || (l.total && !workspace))
     return fail(CWQ_ERR_WORKSPACE, "workspace %zu bytes < required %zu", workspace_bytes,
                 l.total);
@@ -352,6 +361,11 @@ int encode_impl(const float* t_loc, const float* t_scale, const float* p_loc,
   a.ordu = l.csr ? (uint32_t*)(w + l.ordu) : nullptr;
   a.grp = l.csr ? (float4*)(w + l.grp) : nullptr;
   a.gtau = l.csr ? (uint32_t*)(w + l.gtau) : nullptr;
+#ifdef CWQ_NO_RECS
+  a.abp = nullptr;
+#else
+  a.abp = l.recs ? (float4*)(w + l.abp) : nullptr;
+#endif
   a.ev_start = o.eval_start_event;
   a.ev_stop = o.eval_stop_event;
   hipError_t e = cwq::launch_encode(a, (hipStream_t)stream);
@@ -382,14 +396,14 @@ int cwq_stateless_normal_sample(const float* loc, const float* scale, int64_t d,
   return ok();
 }
 
-size_t cwq_greedy_encode_workspace_size(int64_t nb, int64_t total_dims) {
-  if (nb < 0 || total_dims < 0) return 0;
-  return ws_layout(nb, total_dims, true).total;
+size_t cwq_greedy_encode_workspace_size(int64_t nb, int64_t total_dims, int64_t max_block_dim) {
+  if (nb < 0 || total_dims < 0 || max_block_dim < 0) return 0;
+  return ws_layout_csr(nb, total_dims, max_block_dim).total;
 }
 
 size_t cwq_greedy_encode_uniform_workspace_size(int64_t nb, int64_t d) {
   if (nb < 0 || d < 0 || (d > 0 && nb > INT64_MAX / d)) return 0;
-  return ws_layout(nb, nb * d).total;
+  return ws_layout_uniform(nb, d).total;
 }
 
 int cwq_greedy_encode(const float* t_loc, const float* t_scale, const float* p_loc,
@@ -400,7 +414,7 @@ int cwq_greedy_encode(const float* t_loc, const float* t_scale, const float* p_l
                       size_t workspace_bytes, const cwq_options* opts, void* stream) {
   if (nb > 0 && !block_off) return fail(CWQ_ERR_INVALID, "block_off is null");
   if (max_block_dim < 0) return fail(CWQ_ERR_INVALID, "max_block_dim must be >= 0");
-  return encode_impl(t_loc, t_scale, p_loc, p_scale, block_off, 0, nb, total_dims,
+  return encode_impl(t_loc, t_scale, p_loc, p_scale, block_off, 0, nb, total_dims, max_block_dim,
                      n_bits_per_step, n_steps, seed, rho, block_id_base, out_idx, out_sample,
                      workspace, workspace_bytes, opts, stream);
 }
@@ -413,7 +427,7 @@ int cwq_greedy_encode_uniform(const float* t_loc, const float* t_scale, const fl
                               void* stream) {
   if (d < 0) return fail(CWQ_ERR_INVALID, "d must be >= 0");
   if (nb < 0 || (d > 0 && nb > INT64_MAX / d)) return fail(CWQ_ERR_INVALID, "bad nb");
-  return encode_impl(t_loc, t_scale, p_loc, p_scale, nullptr, d, nb, nb * d, n_bits_per_step,
+  return encode_impl(t_loc, t_scale, p_loc, p_scale, nullptr, d, nb, nb * d, d, n_bits_per_step,
                      n_steps, seed, rho, block_id_base, out_idx, out_sample, workspace,
                      workspace_bytes, opts, stream);
 }
@@ -428,7 +442,8 @@ int cwq_greedy_decode(const int32_t* idx, const float* p_loc, const float* p_sca
   if (total_dims > 0 && (!p_loc || !p_scale || !out_sample))
     return fail(CWQ_ERR_INVALID, "null pointer");
   (void)max_block_dim;
-  hipError_t e = cwq::launch_decode(idx, p_loc, p_scale, block_off, 0, nb, n_bits_per_step,
+  hipError_t e = cwq::launch_decode(idx, p_loc, p_scale, block_off, 0, nb, total_dims,
+                                    n_bits_per_step,
                                     n_steps, seed, rho, block_id_base, out_sample,
                                     (hipStream_t)stream);
   if (e != hipSuccess) return hip_fail(e, "cwq_greedy_decode");
@@ -445,7 +460,8 @@ int cwq_greedy_decode_uniform(const int32_t* idx, const float* p_loc, const floa
   if (nb > 0 && !idx) return fail(CWQ_ERR_INVALID, "null pointer");
   if (nb * d > 0 && (!p_loc || !p_scale || !out_sample))
     return fail(CWQ_ERR_INVALID, "null pointer");
-  hipError_t e = cwq::launch_decode(idx, p_loc, p_scale, nullptr, d, nb, n_bits_per_step,
+  hipError_t e = cwq::launch_decode(idx, p_loc, p_scale, nullptr, d, nb, nb * d,
+                                    n_bits_per_step,
                                     n_steps, seed, rho, block_id_base, out_sample,
                                     (hipStream_t)stream);
   if (e != hipSuccess) return hip_fail(e, "cwq_greedy_decode_uniform");
@@ -512,7 +528,7 @@ GroupedWs grouped_ws(int64_t D, int n_steps) {
   l.out = take(fd);
   l.offs = take((size_t)(D + 2) * 8);
   l.idx = take((size_t)(D > 0 ? D : 1) * (size_t)(n_steps > 0 ? n_steps : 1) * 4);
-  l.enc = take(ws_layout(D, D).total);
+  l.enc = take(ws_layout_csr(D, D, D).total);
   l.total = o;
   return l;
 }

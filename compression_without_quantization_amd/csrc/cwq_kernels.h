@@ -12,6 +12,11 @@ namespace cwq {
 // Records `msg` for cwq_last_error() (thread-local) and returns `code`.
 int set_error(int code, const char* msg);
 
+#ifndef CWQ_CSR_LDS_DIMS
+#define CWQ_CSR_LDS_DIMS 1024  // general pruned kernel: blocks up to this d keep their
+                               // screening constants in LDS (longer: abp records)
+#endif
+
 struct EncodeArgs {
   const float* t_loc;
   const float* t_scale;
@@ -43,6 +48,8 @@ struct EncodeArgs {
   uint32_t* ordu;            // [total_dims + 12 nb] unit visited at each position
   float4* grp;               // [nb] (c1, c2, As, Pq); c1 == 0: block not screened
   uint32_t* gtau;            // [nb] per-block shared threshold (ord)
+  float4* abp;               // [2 (total_dims + 12 nb)] visit-order (sa, sb) records of the
+                             // blocks longer than CWQ_CSR_LDS_DIMS; nullptr if none are
   // optional profiling events around the eval launches (hipEvent_t)
   void* ev_start;
   void* ev_stop;
@@ -50,7 +57,8 @@ struct EncodeArgs {
 
 hipError_t launch_encode(const EncodeArgs& a, hipStream_t stream);
 hipError_t launch_decode(const int32_t* idx, const float* p_loc, const float* p_scale,
-                         const int64_t* block_off, int64_t ud, int64_t nb, int n_bits,
+                         const int64_t* block_off, int64_t ud, int64_t nb, int64_t total_dims,
+                         int n_bits,
                          int n_steps, int32_t seed, float rho, int64_t block_id_base,
                          float* out_sample, hipStream_t stream);
 hipError_t launch_stateless_normal_sample(const float* loc, const float* scale, int64_t d,

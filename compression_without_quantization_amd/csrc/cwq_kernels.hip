@@ -615,6 +615,18 @@ __device__ __forceinline__ double block_sum_d(double v, double* red) {
 __host__ __device__ __forceinline__ int64_t csr_cls_stride(int64_t d) { return (d + 6) / 4 + 1; }
 constexpr int64_t kCsrSortUnits = 2048;  // sorted if U_3 <= this (d <= 8189); else natural order
 
+// Per block: the per-dim constants and sums, then for each alignment class
+// its sorted visit order and drop bounds.  The per-dim constants are
+// recomputed where a unit needs them rather than cached in LDS: a prep
+// workgroup with a large LDS footprint cannot start on a CU that the other
+// streams' scoring kernels occupy (measured: +10% on the multi-step coders).  With few blocks the four classes go to four workgroups
+// (blockIdx.y), each recomputing the block's sums, so the sorts run side by
+// side; the blockIdx.y == 0 workgroup also writes the natural-order (sa, sb)
+// array and the block's gate constants.
+// Blocks longer than lds_dims (whose constants the scoring kernel reads from
+// global memory, not LDS) also get abp: for visit position k of class c the
+// (sa, sb) of unit ord[k]'s four words in one 32-byte record, so the scoring
+// lanes of a slot read consecutive records instead of gathering.
 template <bool STEP0>
 __global__ void __launch_bounds__(256) k_csr_prep(
     const float* __restrict__ t_loc, const float* __restrict__ t_scale,
@@ -622,11 +634,16 @@ __global__ void __launch_bounds__(256) k_csr_prep(
     const float* __restrict__ lognorm, const float* __restrict__ best,
     const int64_t* __restrict__ block_off, int64_t ud, int64_t nb, float2* __restrict__ sab,
     float* __restrict__ bpre, uint32_t* __restrict__ ordu, float4* __restrict__ grp,
-    uint32_t* __restrict__ gtau, int64_t coop_min_d) {
+    uint32_t* __restrict__ gtau, float4* __restrict__ abp, int64_t lds_dims,
+    int64_t coop_min_d) {
   __shared__ double red[256];
   __shared__ double scan[256];
   __shared__ unsigned long long skey[kCsrSortUnits];
   const int tid = threadIdx.x;
+  // gridDim.y == 4: one class per workgroup (few blocks: the four sorts run
+  // side by side); gridDim.y == 1: one workgroup walks all four classes (many
+  // blocks: the per-dim constants are computed once per block, not per class)
+  const bool lead = blockIdx.y == 0;  // writes the block's class-independent outputs
   for (int64_t g = blockIdx.x; g < nb; g += gridDim.x) {
     const BlockSpan sp = block_span(block_off, ud, g);
     const int64_t off = sp.off, d = sp.d;
@@ -637,13 +654,13 @@ __global__ void __launch_bounds__(256) k_csr_prep(
     double sm = 0.0, sa = 0.0, sk = 0.0, s2 = 0.0, mx = 0.0;
     int ok = 1;
     float2* sabg = sab + off + 8 * g + 4;  // 4 zero pads either side (partial units)
-    if (tid < 4) {
+    if (lead && tid < 4) {
       sabg[tid - 4] = float2{0.f, 0.f};
       sabg[d + tid] = float2{0.f, 0.f};
     }
     for (int64_t j = tid; j < d; j += 256) {
       const CsrDim o = dim(j);
-      sabg[j] = float2{o.sa, o.sb};
+      if (lead) sabg[j] = float2{o.sa, o.sb};
       sm += o.M;
       sa += __builtin_fabs(o.M);
       sk += __builtin_fabs(o.M) + o.M;
@@ -677,21 +694,30 @@ __global__ void __launch_bounds__(256) k_csr_prep(
     const double gam = 1.01 * ((h_s > h_e ? h_s : h_e) + 1.0) * 0x1p-24;
     const double sl = (3.0 * gam + 0x1p-20) * (__builtin_fabs(SM) + SA + SK) + 0x1p-126;
     const int64_t reg = off + 12 * g, cs = csr_cls_stride(d);
-    // unit u of class c: its sum of C_j and its expected sum of a_j^2 - C_j
-    auto unit = [&](int c, int64_t u, double& csum, double& gain) {
-      csum = 0.0;
-      gain = 0.0;
-      for (int t = 0; t < 4; ++t) {
-        const int64_t j = 4 * u - c + t;
-        if (j >= 0 && j < d) {
-          const CsrDim o = dim(j);
-          csum += (double)o.C;
-          gain += (double)o.sa * (double)o.sa * (0.5 / 0.6931471805599453) +
-                  (double)o.sb * (double)o.sb - (double)o.C;
-        }
-      }
+    auto consts = [&](int64_t j, float& xa, float& xb, float& xc) {
+      const CsrDim o = dim(j);
+      xa = o.sa;
+      xb = o.sb;
+      xc = o.C;
     };
-    for (int c = 0; c < 4; ++c) {
+    const bool recs = abp != nullptr && d > lds_dims;
+    for (int c = (int)blockIdx.y; c < 4; c += (int)gridDim.y) {
+      // word t of unit u of class c is dim 4u - c + t (absent outside [0, d));
+      // unit u: its sum of C_j and its expected sum of a_j^2 - C_j
+      auto unit = [&](int64_t u, double& csum, double& gain) {
+        csum = 0.0;
+        gain = 0.0;
+        for (int t = 0; t < 4; ++t) {
+          const int64_t j = 4 * u - c + t;
+          if (j >= 0 && j < d) {
+            float xa, xb, xc;
+            consts(j, xa, xb, xc);
+            csum += (double)xc;
+            gain += (double)xa * (double)xa * (0.5 / 0.6931471805599453) +
+                    (double)xb * (double)xb - (double)xc;
+          }
+        }
+      };
       const int64_t U = (d + c + 3) / 4;
       const bool sorted = all_ok && U <= kCsrSortUnits;
       if (sorted) {  // bitonic sort of (gain desc, u asc) keys
@@ -701,7 +727,7 @@ __global__ void __launch_bounds__(256) k_csr_prep(
           unsigned long long key = 0ull;
           if (u < U) {
             double cu, gu;
-            unit(c, u, cu, gu);
+            unit(u, cu, gu);
             const float gf = (float)(gu > 0.0 ? gu : 0.0);
             key = ((unsigned long long)ord_f32(gf) << 32) | (0xffffffffull - (uint64_t)u);
           }
@@ -713,11 +739,11 @@ __global__ void __launch_bounds__(256) k_csr_prep(
             for (int64_t i = tid; i < P; i += 256) {
               const int64_t l = i ^ jj;
               if (l > i) {
-                const unsigned long long a = skey[i], b = skey[l];
+                const unsigned long long x = skey[i], y = skey[l];
                 const bool desc = (i & k) == 0;  // overall descending
-                if (desc ? (a < b) : (a > b)) {
-                  skey[i] = b;
-                  skey[l] = a;
+                if (desc ? (x < y) : (x > y)) {
+                  skey[i] = y;
+                  skey[l] = x;
                 }
               }
             }
@@ -732,7 +758,20 @@ __global__ void __launch_bounds__(256) k_csr_prep(
         int64_t u = k;
         if (sorted && k < U) u = (int64_t)(0xffffffffull - (skey[k] & 0xffffffffull));
         double cu = 0.0, gu;
-        if (all_ok && k < U) unit(c, u, cu, gu);
+        if (all_ok && k < U) unit(u, cu, gu);
+        if (recs && k < U) {  // the unit's four (sa, sb), zero for absent words
+          float e[8];
+          for (int t = 0; t < 4; ++t) {
+            const int64_t j = 4 * u - c + t;
+            float xa = 0.f, xb = 0.f, xc;
+            if (j >= 0 && j < d) consts(j, xa, xb, xc);
+            e[2 * t] = xa;
+            e[2 * t + 1] = xb;
+          }
+          float4* r = abp + 2 * (reg + c * cs + k);
+          r[0] = float4{e[0], e[1], e[2], e[3]};
+          r[1] = float4{e[4], e[5], e[6], e[7]};
+        }
         scan[tid] = cu;
         __syncthreads();
         for (int w = 1; w < 256; w <<= 1) {  // inclusive scan
@@ -750,7 +789,7 @@ __global__ void __launch_bounds__(256) k_csr_prep(
         __syncthreads();
       }
     }
-    if (tid == 0) {
+    if (lead && tid == 0) {
       const float c1 = round_dn_f32(1.0 - 3.0 * gam - 0x1p-22);
       const float c2 = round_up_f32(1.0 + 3.0 * gam + 0x1p-14);
       const float as = round_dn_f32(SM - sl - 1.01 * S2 * (1.0 + 0x1p-11));
@@ -818,9 +857,6 @@ __device__ __forceinline__ float exact_row_wave(
   return t + ((q0 + q2) + (q1 + q3));
 }
 
-#ifndef CWQ_CSR_LDS_DIMS
-#define CWQ_CSR_LDS_DIMS 1024  // blocks up to this d keep their screening constants in LDS
-#endif
 #ifndef CWQ_CSR_GTAU_SHARE
 #define CWQ_CSR_GTAU_SHARE 1  // 1: also share tau with the block's other tiles in the loop
 #endif
@@ -861,7 +897,8 @@ __global__ void __launch_bounds__(256, 6) k_encode_prune_csr(
     int64_t cand_per_tile, int64_t n_cand, int32_t seed, int64_t block_id_base, int32_t step,
     const float2* __restrict__ sab, const float* __restrict__ bpre,
     const uint32_t* __restrict__ ordu, const float4* __restrict__ grp,
-    uint32_t* __restrict__ gtau, unsigned long long* __restrict__ keys, int64_t coop_min_d) {
+    uint32_t* __restrict__ gtau, unsigned long long* __restrict__ keys, int64_t coop_min_d,
+    const float4* __restrict__ abp) {
   __shared__ double logtab[32];
   __shared__ uint32_t tau_ord;
   __shared__ uint32_t sq_cnt;
@@ -922,8 +959,10 @@ __global__ void __launch_bounds__(256, 6) k_encode_prune_csr(
       // zeros for the out-of-row words of a row's first and last unit.
       const uint32_t r0 = (uint32_t)(w0 - n0), r1 = (uint32_t)(w1 - n0);
       const int d32 = (int)d;
-      auto run = [&](const float2* ab, const float* bp, const uint32_t* od)
-                     __attribute__((always_inline)) {
+      // ab: natural-order (sa, sb) (LDS or global); rec (REC true): the
+      // visit-order records of k_csr_prep's abp, read at the lane's position
+      auto run = [&](const float2* ab, const float* bp, const uint32_t* od, const float4* rec,
+                     auto REC) __attribute__((always_inline)) {
         uint32_t wnext = r0 + 64u;
         uint32_t r = r0 + lane;
         bool active = r < r1;
@@ -941,8 +980,17 @@ __global__ void __launch_bounds__(256, 6) k_encode_prune_csr(
         };
         start_row();
         int k = 0;
+        // the unit of the next visit position is loaded one iteration ahead
+        // (the Philox counter needs it first thing: a load at the top of the
+        // iteration would expose its latency every time); a new row reloads
+        uint32_t u_nx = od[cb];
         while (__ballot(active) != 0ull) {
+#ifdef CWQ_NO_PREFETCH
           const uint32_t u = od[cb + k];
+#else
+          const uint32_t u = u_nx;
+          u_nx = od[cb + (k + 1 < U ? k + 1 : U)];
+#endif
           // round keys recomputed in SALU each iteration (opaque key): keeping
           // all 20 live costs SGPRs the loop then spills into VGPR lanes
           uint32_t kk0 = st.k0, kk1 = st.k1;
@@ -952,8 +1000,20 @@ __global__ void __launch_bounds__(256, 6) k_encode_prune_csr(
           F4 z;
           box_muller_screen(x.x, x.y, z.a, z.b);
           box_muller_screen(x.z, x.w, z.c, z.d);
-          const int jp = 4 * (int)u - c + 4;  // padded index of word 0
-          const float2 e0 = ab[jp], e1 = ab[jp + 1], e2 = ab[jp + 2], e3 = ab[jp + 3];
+          float2 e0, e1, e2, e3;
+          if constexpr (decltype(REC)::value) {
+            const float4 ra = rec[2 * (cb + k)], rb2 = rec[2 * (cb + k) + 1];
+            e0 = float2{ra.x, ra.y};
+            e1 = float2{ra.z, ra.w};
+            e2 = float2{rb2.x, rb2.y};
+            e3 = float2{rb2.z, rb2.w};
+          } else {
+            const int jp = 4 * (int)u - c + 4;  // padded index of word 0
+            e0 = ab[jp];
+            e1 = ab[jp + 1];
+            e2 = ab[jp + 2];
+            e3 = ab[jp + 3];
+          }
           const float a0 = __builtin_fmaf(e0.x, z.a, e0.y);
           const float a1 = __builtin_fmaf(e1.x, z.b, e1.y);
           const float a2 = __builtin_fmaf(e2.x, z.c, e2.y);
@@ -994,6 +1054,7 @@ __global__ void __launch_bounds__(256, 6) k_encode_prune_csr(
             start_row();
             k = 0;
             s = 0.0f;
+            u_nx = od[cb];
           }
           wnext += (uint32_t)__builtin_popcountll(m);
           active = r < r1;
@@ -1025,8 +1086,8 @@ __global__ void __launch_bounds__(256, 6) k_encode_prune_csr(
       // refill are uniform within the slot; the drop test runs every 16 units.
       // The bound's float-summation factor is taken at this tree's depth
       // (k_csr_prep: 4 in-lane + 4 butterfly + one per chunk).
-      auto run_coop = [&](const float2* ab, const float* bp, const uint32_t* od)
-                          __attribute__((always_inline)) {
+      auto run_coop = [&](const float2* ab, const float* bp, const uint32_t* od,
+                          const float4* rec, auto REC) __attribute__((always_inline)) {
         const uint32_t t = lane & 15u, slot = lane >> 4;
         const uint64_t below = (1ull << (slot * 16u)) - 1ull;  // lanes of lower slots
 #if CWQ_CSR_COOP_CLASS_WAVES
@@ -1057,11 +1118,13 @@ __global__ void __launch_bounds__(256, 6) k_encode_prune_csr(
         };
         start_row();
         int k = 0;
+        uint32_t u_nx = od[cb + ((int)t < U ? (int)t : U)];  // one iteration ahead, as in run
         while (__ballot(active) != 0ull) {
           const int p = k + (int)t;
           float part = 0.0f;
+          const uint32_t u = u_nx;
+          u_nx = od[cb + (p + 16 < U ? p + 16 : U)];
           if (active && p < U) {
-            const uint32_t u = od[cb + p];
             uint32_t kk0 = st.k0, kk1 = st.k1;
             asm volatile("" : "+s"(kk0), "+s"(kk1));
             const uint64_t blk = rb + u;
@@ -1069,8 +1132,20 @@ __global__ void __launch_bounds__(256, 6) k_encode_prune_csr(
             F4 z;
             box_muller_screen(x.x, x.y, z.a, z.b);
             box_muller_screen(x.z, x.w, z.c, z.d);
-            const int jp = 4 * (int)u - c + 4;
-            const float2 e0 = ab[jp], e1 = ab[jp + 1], e2 = ab[jp + 2], e3 = ab[jp + 3];
+            float2 e0, e1, e2, e3;
+            if constexpr (decltype(REC)::value) {
+              const float4 ra = rec[2 * (cb + p)], rb2 = rec[2 * (cb + p) + 1];
+              e0 = float2{ra.x, ra.y};
+              e1 = float2{ra.z, ra.w};
+              e2 = float2{rb2.x, rb2.y};
+              e3 = float2{rb2.z, rb2.w};
+            } else {
+              const int jp = 4 * (int)u - c + 4;
+              e0 = ab[jp];
+              e1 = ab[jp + 1];
+              e2 = ab[jp + 2];
+              e3 = ab[jp + 3];
+            }
             const float a0 = __builtin_fmaf(e0.x, z.a, e0.y);
             const float a1 = __builtin_fmaf(e1.x, z.b, e1.y);
             const float a2 = __builtin_fmaf(e2.x, z.c, e2.y);
@@ -1114,6 +1189,7 @@ __global__ void __launch_bounds__(256, 6) k_encode_prune_csr(
             start_row();
             k = 0;
             s = 0.0f;
+            u_nx = od[cb + ((int)t < U ? (int)t : U)];
           }
           wnext += (uint32_t)(__builtin_popcountll(m) >> 4);
           active = q < q1;
@@ -1130,15 +1206,21 @@ __global__ void __launch_bounds__(256, 6) k_encode_prune_csr(
       // survivor list overflow (near-ties everywhere, or a weak early tau):
       // redo the pass starting from the final tau, then score exactly
       for (int pass = 0;; ++pass) {
+        using NoRec = std::integral_constant<bool, false>;
+        using Rec = std::integral_constant<bool, true>;
         if (coop) {
           if (in_lds)
-            run_coop(l_ab, l_bp, l_ord);
+            run_coop(l_ab, l_bp, l_ord, nullptr, NoRec{});
+          else if (abp)
+            run_coop(nullptr, bpre + reg, ordu + reg, abp + 2 * reg, Rec{});
           else
-            run_coop(sab + off + 8 * g, bpre + reg, ordu + reg);
+            run_coop(sab + off + 8 * g, bpre + reg, ordu + reg, nullptr, NoRec{});
         } else if (in_lds)
-          run(l_ab, l_bp, l_ord);
+          run(l_ab, l_bp, l_ord, nullptr, NoRec{});
+        else if (abp)
+          run(nullptr, bpre + reg, ordu + reg, abp + 2 * reg, Rec{});
         else
-          run(sab + off + 8 * g, bpre + reg, ordu + reg);
+          run(sab + off + 8 * g, bpre + reg, ordu + reg, nullptr, NoRec{});
         __syncthreads();
         if (tid == 0) {
           const uint32_t mine = tau_ord;
@@ -1200,8 +1282,30 @@ __global__ void __launch_bounds__(256, 6) k_encode_prune_csr(
 
 // ---------------------------------------------------------------------------
 // Encoder, end of a step: index -> out_idx; best += winning candidate (:63).
-// One wave per block.
+// General shapes (CSR groups, uniform d the float4 kernel does not take): one
+// thread per flat dim i, which finds its block by binary search in block_off
+// and regenerates its own word of the winning row; threads t < nb also write
+// block t's index.  Work is spread evenly whatever the group sizes (a few
+// 4095-dim groups or 10^5 tiny ones).  The dims covered are
+// [block_off[0], block_off[nb]) (absolute: a forked part of a launch passes
+// block_off + g0).
 // ---------------------------------------------------------------------------
+__device__ __forceinline__ int64_t block_of_dim(const int64_t* __restrict__ off, int64_t nb,
+                                                int64_t i) {
+  int64_t lo = 0, hi = nb;  // off[lo] <= i < off[hi]; empty blocks are skipped
+  while (hi - lo > 1) {
+    const int64_t m = (lo + hi) >> 1;
+    if (off[m] <= i) lo = m; else hi = m;
+  }
+  return lo;
+}
+
+__device__ __forceinline__ uint32_t key_index(uint64_t key) {
+  // ArgMaxTupleReducer starts at (index 0, lowest()) and only a value strictly
+  // above lowest() replaces it: a winning key at the clamp level means index 0
+  return (key >> 32) > kArgmaxClampOrd ? argmax_key_index(key) : 0u;
+}
+
 __global__ void __launch_bounds__(256) k_encode_finalize(
     const float* __restrict__ loc_s, const float* __restrict__ scale_s,
     const int64_t* __restrict__ block_off, int64_t ud, int64_t nb, int32_t seed,
@@ -1210,26 +1314,27 @@ __global__ void __launch_bounds__(256) k_encode_finalize(
     float* __restrict__ out_sample) {
   __shared__ double logtab[32];
   fill_logtab(logtab);
-  const uint32_t wv = wave_id();
-  const uint32_t lane = threadIdx.x & 63u;
-  for (int64_t g = (int64_t)blockIdx.x * 4 + wv; g < nb; g += (int64_t)gridDim.x * 4) {
-    const BlockSpan sp = block_span(block_off, ud, g);
-    const uint64_t key = keys[g];
-    // ArgMaxTupleReducer starts at (index 0, lowest()) and only a value strictly
-    // above lowest() replaces it: a winning key at the clamp level means index 0
-    const uint32_t idx = (key >> 32) > kArgmaxClampOrd ? argmax_key_index(key) : 0u;
-    if (lane == 0) out_idx[g * n_steps + step] = (int32_t)idx;
+  const int64_t d0 = block_off ? block_off[0] : 0;
+  const int64_t d1 = block_off ? block_off[nb] : nb * ud;
+  const int64_t nt = (d1 - d0) > nb ? (d1 - d0) : nb;
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < nt;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    if (t < nb) out_idx[t * n_steps + step] = (int32_t)key_index(keys[t]);
+    const int64_t i = d0 + t;
+    if (i >= d1) continue;
+    const int64_t g = block_off ? block_of_dim(block_off, nb, i) : i / ud;
+    const int64_t off = block_off ? block_off[g] : g * ud;
+    const int64_t d = block_off ? block_off[g + 1] - off : ud;
+    const uint32_t idx = key_index(keys[g]);
     const PhiloxStream st =
         generate_key(step_seed(block_seed(seed, block_id_base + g), step), 42);
-    for (int64_t j = lane; j < sp.d; j += 64) {
-      const uint64_t k = (uint64_t)idx * (uint64_t)sp.d + (uint64_t)j;
-      const F4 z = normal4_dev(st, k >> 2, logtab);
-      const uint32_t w = (uint32_t)(k & 3u);
-      const float zz = w == 0 ? z.a : (w == 1 ? z.b : (w == 2 ? z.c : z.d));
-      float s = scale_s[sp.off + j] * zz;
-      s = loc_s[sp.off + j] + s;
-      out_sample[sp.off + j] = out_sample[sp.off + j] + s;
-    }
+    const uint64_t k = (uint64_t)idx * (uint64_t)d + (uint64_t)(i - off);
+    const F4 z = normal4_dev(st, k >> 2, logtab);
+    const uint32_t w = (uint32_t)(k & 3u);
+    const float zz = w == 0 ? z.a : (w == 1 ? z.b : (w == 2 ? z.c : z.d));
+    float sv = scale_s[i] * zz;
+    sv = loc_s[i] + sv;
+    out_sample[i] = out_sample[i] + sv;
   }
 }
 
@@ -1280,7 +1385,9 @@ __global__ void __launch_bounds__(256) k_encode_finalize_q4(
 }
 
 // ---------------------------------------------------------------------------
-// Decoder (coded_greedy_sampler.py:93-167), O(n_steps * d) per block.
+// Decoder (coded_greedy_sampler.py:93-167), O(n_steps * d) per block: only the
+// selected row of each step is regenerated.  General shapes: one thread per
+// flat dim, block found as in k_encode_finalize.
 // ---------------------------------------------------------------------------
 __global__ void __launch_bounds__(256) k_decode(
     const int32_t* __restrict__ idx, const float* __restrict__ p_loc,
@@ -1289,33 +1396,34 @@ __global__ void __launch_bounds__(256) k_decode(
     int64_t block_id_base, float* __restrict__ out_sample) {
   __shared__ double logtab[32];
   fill_logtab(logtab);
-  const uint32_t wv = wave_id();
-  const uint32_t lane = threadIdx.x & 63u;
-  for (int64_t g = (int64_t)blockIdx.x * 4 + wv; g < nb; g += (int64_t)gridDim.x * 4) {
-    const BlockSpan sp = block_span(block_off, ud, g);
+  const int64_t d0 = block_off ? block_off[0] : 0;
+  const int64_t d1 = block_off ? block_off[nb] : nb * ud;
+  for (int64_t i = d0 + blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < d1;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t g = block_off ? block_of_dim(block_off, nb, i) : i / ud;
+    const int64_t off = block_off ? block_off[g] : g * ud;
+    const int64_t d = block_off ? block_off[g + 1] - off : ud;
     const int32_t sg = block_seed(seed, block_id_base + g);
-    for (int64_t j = lane; j < sp.d; j += 64) {
-      const float ls = p_loc[sp.off + j] / nst;
-      const float rs = rho * p_scale[sp.off + j];
-      const float ss = rs / sdiv;
-      float v = 0.0f;  // sample = tf.zeros (:143)
-      for (int i = 0; i < n_steps; ++i) {
-        const int64_t n = idx[g * n_steps + i];
-        if (n < 0 || n >= n_cand) {
-          v = __builtin_nanf("");
-          continue;
-        }
-        const PhiloxStream st = generate_key(step_seed(sg, i), 42);
-        const uint64_t k = (uint64_t)n * (uint64_t)sp.d + (uint64_t)j;
-        const F4 z = normal4_dev(st, k >> 2, logtab);
-        const uint32_t w = (uint32_t)(k & 3u);
-        const float zz = w == 0 ? z.a : (w == 1 ? z.b : (w == 2 ? z.c : z.d));
-        float s = ss * zz;
-        s = ls + s;
-        v = v + s;  // :153 tile(sample) + samples, row indices[i]
+    const float ls = p_loc[i] / nst;
+    const float rs = rho * p_scale[i];
+    const float ss = rs / sdiv;
+    float v = 0.0f;  // sample = tf.zeros (:143)
+    for (int s = 0; s < n_steps; ++s) {
+      const int64_t n = idx[g * n_steps + s];
+      if (n < 0 || n >= n_cand) {
+        v = __builtin_nanf("");
+        continue;
       }
-      out_sample[sp.off + j] = v;
+      const PhiloxStream st = generate_key(step_seed(sg, s), 42);
+      const uint64_t k = (uint64_t)n * (uint64_t)d + (uint64_t)(i - off);
+      const F4 z = normal4_dev(st, k >> 2, logtab);
+      const uint32_t w = (uint32_t)(k & 3u);
+      const float zz = w == 0 ? z.a : (w == 1 ? z.b : (w == 2 ? z.c : z.d));
+      float sv = ss * zz;
+      sv = ls + sv;
+      v = v + sv;  // :153 tile(sample) + samples, row indices[i]
     }
+    out_sample[i] = v;
   }
 }
 
@@ -1577,16 +1685,22 @@ static void launch_prune_csr(const EncodeArgs& a, int step, hipStream_t stream) 
   tpb = (a.n_cand + cpt - 1) / cpt;  // no tile may start at or past n_cand
   const int64_t ntiles = a.nb * tpb;
   const int64_t coop_min_d = coop ? (int64_t)CWQ_CSR_COOP_MIN_D : INT64_MAX;
-  hipLaunchKernelGGL((k_csr_prep<STEP0>), dim3(grid_for(a.nb, 1, 65536)), dim3(256), 0, stream,
-                     a.t_loc, a.t_scale, a.loc_s, a.scale_s, a.lognorm, a.out_sample,
-                     a.block_off, a.ud, a.nb, a.sab, a.bpre, a.ordu, a.grp, a.gtau, coop_min_d);
+#ifndef CWQ_PREP_SPLIT_MAX_NB
+#define CWQ_PREP_SPLIT_MAX_NB 256
+#endif
+  // few blocks: one workgroup per class
+  const unsigned cls_wgs = a.nb <= CWQ_PREP_SPLIT_MAX_NB ? 4 : 1;
+  hipLaunchKernelGGL((k_csr_prep<STEP0>), dim3(grid_for(a.nb, 1, 65536), cls_wgs), dim3(256), 0,
+                     stream, a.t_loc, a.t_scale, a.loc_s, a.scale_s, a.lognorm, a.out_sample,
+                     a.block_off, a.ud, a.nb, a.sab, a.bpre, a.ordu, a.grp, a.gtau, a.abp,
+                     (int64_t)CWQ_CSR_LDS_DIMS, coop_min_d);
   constexpr int64_t kGrid = 1 << 20;
   const unsigned grid = (unsigned)(ntiles < kGrid ? ntiles : kGrid);
   hipLaunchKernelGGL((k_encode_prune_csr<STEP0>), dim3(grid), dim3(256), 0, stream, a.t_loc,
                      a.t_scale, a.loc_s, a.scale_s, a.lognorm, a.out_sample, a.block_off, a.ud,
                      ntiles, tpb, cpt, a.n_cand, a.seed, a.block_id_base, step,
                      (const float2*)a.sab, (const float*)a.bpre, (const uint32_t*)a.ordu,
-                     (const float4*)a.grp, a.gtau, a.keys, coop_min_d);
+                     (const float4*)a.grp, a.gtau, a.keys, coop_min_d, (const float4*)a.abp);
 }
 
 template <bool STEP0>
@@ -1624,7 +1738,12 @@ static void launch_eval_dc(const EncodeArgs& a, int step, hipStream_t stream) {
 // the candidates, finalize (index + best) -- steps are sequential per block.
 static hipError_t encode_steps(const EncodeArgs& a, hipStream_t stream, bool events) {
   hipError_t e;
-  const unsigned fgrid = grid_for(a.nb, 4, 65536);
+  // the general finalize covers max(nb, dims of this block range) threads
+#ifndef CWQ_FIN_MAX_WGS
+#define CWQ_FIN_MAX_WGS 16384
+#endif
+  const unsigned fgrid_dims =
+      grid_for(a.total_dims > a.nb ? a.total_dims : a.nb, 256, CWQ_FIN_MAX_WGS);
   for (int s = 0; s < a.n_steps; ++s) {
     e = hipMemsetAsync(a.keys, 0, (size_t)a.nb * sizeof(unsigned long long), stream);
     if (e != hipSuccess) return e;
@@ -1649,7 +1768,7 @@ static hipError_t encode_steps(const EncodeArgs& a, hipStream_t stream, bool eve
                          qpb, bpw, a.nb, a.seed, a.block_id_base, s, a.n_steps, a.keys,
                          a.out_idx, (float4*)a.out_sample);
     } else {
-      hipLaunchKernelGGL(k_encode_finalize, dim3(fgrid), dim3(256), 0, stream, a.loc_s,
+      hipLaunchKernelGGL(k_encode_finalize, dim3(fgrid_dims), dim3(256), 0, stream, a.loc_s,
                          a.scale_s, a.block_off, a.ud, a.nb, a.seed, a.block_id_base, s,
                          a.n_steps, a.keys, a.out_idx, a.out_sample);
     }
@@ -1753,6 +1872,7 @@ hipError_t launch_encode(const EncodeArgs& a, hipStream_t stream) {
     if (a.ordu) p.ordu = a.ordu + 12 * g0;
     if (a.grp) p.grp = a.grp + g0;
     if (a.gtau) p.gtau = a.gtau + g0 * CWQ_CSR_GTAU_STRIDE;
+    if (a.abp) p.abp = a.abp + 2 * 12 * g0;
     if ((e = hipStreamWaitEvent(f->s[i], f->fork, 0)) != hipSuccess) break;
     forked = i + 1;
     e = encode_steps(p, f->s[i], false);
@@ -1773,7 +1893,8 @@ hipError_t launch_encode(const EncodeArgs& a, hipStream_t stream) {
 }
 
 hipError_t launch_decode(const int32_t* idx, const float* p_loc, const float* p_scale,
-                         const int64_t* block_off, int64_t ud, int64_t nb, int n_bits,
+                         const int64_t* block_off, int64_t ud, int64_t nb, int64_t total_dims,
+                         int n_bits,
                          int n_steps, int32_t seed, float rho, int64_t block_id_base,
                          float* out_sample, hipStream_t stream) {
   if (nb <= 0) return hipSuccess;
@@ -1787,9 +1908,9 @@ hipError_t launch_decode(const int32_t* idx, const float* p_loc, const float* p_
                        (float4*)out_sample);
     return hipGetLastError();
   }
-  hipLaunchKernelGGL(k_decode, dim3(grid_for(nb, 4, 65536)), dim3(256), 0, stream, idx, p_loc,
-                     p_scale, block_off, ud, nb, n_steps, (int64_t)1 << n_bits, nst, sdiv, rho,
-                     seed, block_id_base, out_sample);
+  hipLaunchKernelGGL(k_decode, dim3(grid_for(total_dims, 256, 16384)), dim3(256), 0, stream, idx,
+                     p_loc, p_scale, block_off, ud, nb, n_steps, (int64_t)1 << n_bits, nst, sdiv,
+                     rho, seed, block_id_base, out_sample);
   return hipGetLastError();
 }
 

@@ -95,11 +95,13 @@ typedef struct cwq_options {
 #define CWQ_OPTIONS_INIT {2, 0, NULL, NULL}
 
 /* Workspace bytes needed by cwq_greedy_encode (CSR blocks) for nb blocks
- * holding total_dims dims in all: the argmax keys and per-dim shard constants
- * plus the general pruned kernel's per-step screening constants (16 B/dim +
- * 180 B/block).  A CSR call given less returns CWQ_ERR_WORKSPACE (it never
- * silently falls back to a slower kernel). */
-size_t cwq_greedy_encode_workspace_size(int64_t nb, int64_t total_dims);
+ * holding total_dims dims in all, none longer than max_block_dim: the argmax
+ * keys and per-dim shard constants plus the general pruned kernel's per-step
+ * screening constants (16 B/dim + 180 B/block) and, when max_block_dim > 1024,
+ * their visit-order copies for the long blocks (32 B/dim + 384 B/block).  A
+ * CSR call given less returns CWQ_ERR_WORKSPACE (it never silently falls back
+ * to a slower kernel). */
+size_t cwq_greedy_encode_workspace_size(int64_t nb, int64_t total_dims, int64_t max_block_dim);
 
 /* Workspace bytes needed by cwq_greedy_encode_uniform for nb blocks of
  * dimension d: keys + shard constants only when d % 8 == 0, 8 <= d <= 64 (the
@@ -111,7 +113,8 @@ size_t cwq_greedy_encode_uniform_workspace_size(int64_t nb, int64_t d);
  *   out_idx    [nb * n_steps] int32: the argmax index of every step (the
  *              reference emits these as LSB-first bit strings, :81-87)
  *   out_sample [total_dims] f32: best_sample of every block (:89)
- *   max_block_dim: an upper bound on the largest block's dimension.
+ *   max_block_dim: an upper bound on the largest block's dimension (the same
+ *              value the workspace was sized with).
  * Block g is coded with seed (seed + block_id_base + g) (int32 wrap), step i of
  * it with the stateless seed [1000*(that) + i, 42] (:55). */
 int cwq_greedy_encode(const float* t_loc, const float* t_scale, const float* p_loc,

@@ -55,11 +55,15 @@ def test_workspace_sizes_and_options_rejected(cwqlib):
     from compression_without_quantization_amd import _lib
     nb, d = 10, 32
     uni = cwqlib.cwq_greedy_encode_uniform_workspace_size(nb, d)
-    csr = cwqlib.cwq_greedy_encode_workspace_size(nb, nb * d)
+    csr = cwqlib.cwq_greedy_encode_workspace_size(nb, nb * d, d)
     assert csr >= uni + 16 * nb * d + 180 * nb
     # uniform d outside the fast kernel: the general layout either way
     assert cwqlib.cwq_greedy_encode_uniform_workspace_size(nb, 9) == \
-        cwqlib.cwq_greedy_encode_workspace_size(nb, nb * 9)
+        cwqlib.cwq_greedy_encode_workspace_size(nb, nb * 9, 9)
+    # blocks longer than 1024 dims add the visit-order records (32 B/dim)
+    long_ = cwqlib.cwq_greedy_encode_workspace_size(nb, nb * 2000, 2000)
+    assert long_ >= cwqlib.cwq_greedy_encode_workspace_size(nb, nb * 2000, 1024) + 32 * nb * 2000
+    assert cwqlib.cwq_greedy_encode_uniform_workspace_size(nb, 2000) == long_
     rc = cwqlib.cwq_greedy_encode(1, 1, 1, 1, 1, nb, nb * d, d, 8, 1, 42, 1.0, 0, 1, 1, 1,
                                   uni, None, None)
     assert rc == -3 and b"workspace" in cwqlib.cwq_last_error()

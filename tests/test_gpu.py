@@ -846,8 +846,8 @@ def test_encode_captured_in_hip_graph(cwq, cwqlib):
     nb, steps, bits = len(sizes), 3, 12
     idx = torch.zeros((nb, steps), dtype=torch.int32, device=dev)
     smp = torch.zeros(D, dtype=torch.float32, device=dev)
-    ws = torch.empty(cwqlib.cwq_greedy_encode_workspace_size(nb, D), dtype=torch.uint8,
-                     device=dev)
+    ws = torch.empty(cwqlib.cwq_greedy_encode_workspace_size(nb, D, max(sizes)),
+                     dtype=torch.uint8, device=dev)
     ub, ud = 64, 32                                    # uniform C4-shaped blocks
     utl = f(rng.standard_normal(ub * ud) * 0.5)
     uts = f(rng.uniform(0.3, 0.9, ub * ud))

@@ -10,8 +10,8 @@ from compression_without_quantization_amd import _lib
 import compression_without_quantization_amd as C
 from compression_without_quantization_amd.synthetic import make_blocks
 
-nb = int(sys.argv[1]) if len(sys.argv) > 1 else 20000
-mode = int(sys.argv[2]) if len(sys.argv) > 2 else 2
+nb = int(sys.argv[1]) if len(sys.argv) > 1 and not sys.argv[1].startswith("-") else 20000
+mode = int(sys.argv[2]) if len(sys.argv) > 2 and not sys.argv[2].startswith("-") else 2
 d = int(os.environ.get("PS_D", "32"))
 bits = int(os.environ.get("PS_BITS", "16"))
 lib = _lib.load()
@@ -46,3 +46,16 @@ print(f"completed rows {a[65]:.0f} ({a[65] / nb:.2f}/block), survivors pushed {a
       f"({a[66] / nb:.2f}/block), screened tiles {a[67]:.0f}")
 print(f"survivors re-evaluated exactly {a[68]:.0f} ({a[68] / nb:.2f}/block), "
       f"in-loop exact evaluations (list full) {a[69]:.0f}")
+if "--json" in sys.argv:   # record for bench.py's roofline.valu.evaluated
+    import json
+    path = sys.argv[sys.argv.index("--json") + 1]
+    with open(path, "w") as f:
+        json.dump({"config": os.environ.get("PS_CONFIG", "c4"), "blocks": nb, "block_dim": d,
+                   "kl_bits": bits, "prune_mode": mode,
+                   "units_per_candidate": float((hist * np.arange(65)).sum() / ncand),
+                   "unit_dims": 4, "candidates": float(ncand),
+                   "survivors_exact_per_block": float(a[68] / nb),
+                   "method": "tools/prune_stats.py on a -DCWQ_PRUNE_STATS build of libcwq.so "
+                             "(counters inside k_encode_prune; same inputs as bench.py --config "
+                             "c4 but a block sample)"}, f, indent=1)
+    print("wrote", path)
