@@ -985,21 +985,12 @@ __global__ void __launch_bounds__(256, 6) k_encode_prune_csr(
         // iteration would expose its latency every time); a new row reloads
         uint32_t u_nx = od[cb];
         while (__ballot(active) != 0ull) {
-#ifdef CWQ_NO_PREFETCH
-          const uint32_t u = od[cb + k];
-#else
           const uint32_t u = u_nx;
           u_nx = od[cb + (k + 1 < U ? k + 1 : U)];
-#endif
-          // round keys recomputed in SALU each iteration (opaque key): keeping
-          // all 20 live costs SGPRs the loop then spills into VGPR lanes
-          uint32_t kk0 = st.k0, kk1 = st.k1;
-          asm volatile("" : "+s"(kk0), "+s"(kk1));
-          const uint64_t blk = rb + u;
-          const U4 x = philox10_dev((uint32_t)blk, (uint32_t)(blk >> 32), st.c2, st.c3, kk0, kk1);
-          F4 z;
-          box_muller_screen(x.x, x.y, z.a, z.b);
-          box_muller_screen(x.z, x.w, z.c, z.d);
+          // this unit's constants and the next drop bound are loaded here,
+          // ahead of the opaque key move below, so their latency overlaps the
+          // Philox rounds (the compiler otherwise issues them after the
+          // transcendentals and waits on them at once)
           float2 e0, e1, e2, e3;
           if constexpr (decltype(REC)::value) {
             const float4 ra = rec[2 * (cb + k)], rb2 = rec[2 * (cb + k) + 1];
@@ -1014,6 +1005,16 @@ __global__ void __launch_bounds__(256, 6) k_encode_prune_csr(
             e2 = ab[jp + 2];
             e3 = ab[jp + 3];
           }
+          const float bnext = bp[cb + k + 1];
+          // round keys recomputed in SALU each iteration (opaque key): keeping
+          // all 20 live costs SGPRs the loop then spills into VGPR lanes
+          uint32_t kk0 = st.k0, kk1 = st.k1;
+          asm volatile("" : "+s"(kk0), "+s"(kk1));
+          const uint64_t blk = rb + u;
+          const U4 x = philox10_dev((uint32_t)blk, (uint32_t)(blk >> 32), st.c2, st.c3, kk0, kk1);
+          F4 z;
+          box_muller_screen(x.x, x.y, z.a, z.b);
+          box_muller_screen(x.z, x.w, z.c, z.d);
           const float a0 = __builtin_fmaf(e0.x, z.a, e0.y);
           const float a1 = __builtin_fmaf(e1.x, z.b, e1.y);
           const float a2 = __builtin_fmaf(e2.x, z.c, e2.y);
@@ -1027,7 +1028,7 @@ __global__ void __launch_bounds__(256, 6) k_encode_prune_csr(
           if (active) atomicAdd(&g_prune_stats[43], 1ull);
 #endif
           const bool complete = k == U;
-          const float upper = __builtin_fmaf(s, gc.x, bp[cb + k]);
+          const float upper = __builtin_fmaf(s, gc.x, bnext);
           const bool prune = !complete && (upper < tau);
           if (complete && active && upper >= tau) {  // may be the best: keep it
             const float lower =
@@ -1124,6 +1125,25 @@ __global__ void __launch_bounds__(256, 6) k_encode_prune_csr(
           float part = 0.0f;
           const uint32_t u = u_nx;
           u_nx = od[cb + (p + 16 < U ? p + 16 : U)];
+          // constants and the slot's next drop bound ahead of the Philox
+          // rounds, as in run (positions past U clamp to U: in the region)
+          const int kn = (k + 16 < U) ? k + 16 : U;
+          const float bnext = bp[cb + kn];
+          float2 e0, e1, e2, e3;
+          if constexpr (decltype(REC)::value) {
+            const int pc = p < U ? p : U;
+            const float4 ra = rec[2 * (cb + pc)], rb2 = rec[2 * (cb + pc) + 1];
+            e0 = float2{ra.x, ra.y};
+            e1 = float2{ra.z, ra.w};
+            e2 = float2{rb2.x, rb2.y};
+            e3 = float2{rb2.z, rb2.w};
+          } else {
+            const int jp = 4 * (int)(p < U ? u : 0u) - c + 4;
+            e0 = ab[jp];
+            e1 = ab[jp + 1];
+            e2 = ab[jp + 2];
+            e3 = ab[jp + 3];
+          }
           if (active && p < U) {
             uint32_t kk0 = st.k0, kk1 = st.k1;
             asm volatile("" : "+s"(kk0), "+s"(kk1));
@@ -1132,20 +1152,6 @@ __global__ void __launch_bounds__(256, 6) k_encode_prune_csr(
             F4 z;
             box_muller_screen(x.x, x.y, z.a, z.b);
             box_muller_screen(x.z, x.w, z.c, z.d);
-            float2 e0, e1, e2, e3;
-            if constexpr (decltype(REC)::value) {
-              const float4 ra = rec[2 * (cb + p)], rb2 = rec[2 * (cb + p) + 1];
-              e0 = float2{ra.x, ra.y};
-              e1 = float2{ra.z, ra.w};
-              e2 = float2{rb2.x, rb2.y};
-              e3 = float2{rb2.z, rb2.w};
-            } else {
-              const int jp = 4 * (int)u - c + 4;
-              e0 = ab[jp];
-              e1 = ab[jp + 1];
-              e2 = ab[jp + 2];
-              e3 = ab[jp + 3];
-            }
             const float a0 = __builtin_fmaf(e0.x, z.a, e0.y);
             const float a1 = __builtin_fmaf(e1.x, z.b, e1.y);
             const float a2 = __builtin_fmaf(e2.x, z.c, e2.y);
@@ -1159,9 +1165,9 @@ __global__ void __launch_bounds__(256, 6) k_encode_prune_csr(
           if (active && p < U) atomicAdd(&g_prune_stats[43], 1ull);
 #endif
           s = s + row16_sum_f32(part);
-          k = (k + 16 < U) ? k + 16 : U;
+          k = kn;
           const bool complete = k == U;
-          const float upper = __builtin_fmaf(s, gc.x, bp[cb + k]);
+          const float upper = __builtin_fmaf(s, gc.x, bnext);
           const bool prune = !complete && (upper < tau);
           if (complete && active && upper >= tau) {  // may be the best: keep it
             const float lower =
