@@ -887,9 +887,29 @@ __device__ __forceinline__ float exact_row_wave(
 #ifndef CWQ_CSR_COOP_MIN_D
 #define CWQ_CSR_COOP_MIN_D 256        // ... for blocks of at least this many dims
 #endif
+#ifndef CWQ_CSR_COOP_MIN_WAVES
+#define CWQ_CSR_COOP_MIN_WAVES 4      // waves/SIMD the cooperative kernel's registers allow
+#endif
+#ifndef CWQ_RUN_UPL
+#define CWQ_RUN_UPL 2                 // units per lane per iteration of a per-lane row
+#endif
+#ifndef CWQ_COOP_UPL
+#define CWQ_COOP_UPL 4                // units per lane per iteration of a cooperative row
+#endif
 
-template <bool STEP0>
-__global__ void __launch_bounds__(256, 6) k_encode_prune_csr(
+// element idx of base through an unsigned 32-bit byte offset (base + voffset)
+template <class T>
+__device__ __forceinline__ T ld_u32off(const T* base, uint32_t idx) {
+  return *(const T*)((const char*)base + (uint64_t)(idx * (uint32_t)sizeof(T)));
+}
+
+static_assert(CWQ_CSR_COOP_MIN_D <= CWQ_CSR_LDS_DIMS, "short rows of a cooperative launch use LDS");
+
+// COOP: the kernel of cooperative launches (few long rows; blocks of at least
+// coop_min_d dims walked by 16-lane slots, shorter ones per lane from LDS);
+// otherwise one row per lane for every block.
+template <bool STEP0, bool COOP>
+__global__ void __launch_bounds__(256, COOP ? CWQ_CSR_COOP_MIN_WAVES : 6) k_encode_prune_csr(
     const float* __restrict__ t_loc, const float* __restrict__ t_scale,
     const float* __restrict__ loc_s, const float* __restrict__ scale_s,
     const float* __restrict__ lognorm, const float* __restrict__ best,
@@ -980,53 +1000,78 @@ __global__ void __launch_bounds__(256, 6) k_encode_prune_csr(
         };
         start_row();
         int k = 0;
-        // the unit of the next visit position is loaded one iteration ahead
-        // (the Philox counter needs it first thing: a load at the top of the
-        // iteration would expose its latency every time); a new row reloads
-        uint32_t u_nx = od[cb];
-        while (__ballot(active) != 0ull) {
-          const uint32_t u = u_nx;
-          u_nx = od[cb + (k + 1 < U ? k + 1 : U)];
-          // this unit's constants and the next drop bound are loaded here,
-          // ahead of the opaque key move below, so their latency overlaps the
-          // Philox rounds (the compiler otherwise issues them after the
-          // transcendentals and waits on them at once)
-          float2 e0, e1, e2, e3;
-          if constexpr (decltype(REC)::value) {
-            const float4 ra = rec[2 * (cb + k)], rb2 = rec[2 * (cb + k) + 1];
-            e0 = float2{ra.x, ra.y};
-            e1 = float2{ra.z, ra.w};
-            e2 = float2{rb2.x, rb2.y};
-            e3 = float2{rb2.z, rb2.w};
-          } else {
-            const int jp = 4 * (int)u - c + 4;  // padded index of word 0
-            e0 = ab[jp];
-            e1 = ab[jp + 1];
-            e2 = ab[jp + 2];
-            e3 = ab[jp + 3];
+        // RUPL units per iteration (positions k .. k + RUPL - 1; a unit past
+        // the row end adds exactly 0: its a is forced to 0).  The units of the
+        // next positions are loaded one iteration ahead (the Philox counter
+        // needs them first thing: a load at the top of the iteration would
+        // expose its latency every time); a new row reloads.  Loads index
+        // their uniform base with an unsigned 32-bit byte offset.
+        constexpr int RUPL = COOP ? 1 : CWQ_RUN_UPL;  // the cooperative kernel: short rows only
+        uint32_t u_nx[RUPL];
+        auto load_units = [&](int p0) __attribute__((always_inline)) {
+#pragma unroll
+          for (int i = 0; i < RUPL; ++i) {
+            const int pp = p0 + i;
+            u_nx[i] = ld_u32off(od, (uint32_t)(cb + (pp < U ? pp : U)));
           }
-          const float bnext = bp[cb + k + 1];
+        };
+        load_units(0);
+        while (__ballot(active) != 0ull) {
+          uint32_t u[RUPL];
+#pragma unroll
+          for (int i = 0; i < RUPL; ++i) u[i] = u_nx[i];
+          load_units(k + RUPL);
+          // this iteration's constants and the next drop bound are loaded
+          // here, ahead of the opaque key move below, so their latency
+          // overlaps the Philox rounds (the compiler otherwise issues them
+          // after the transcendentals and waits on them at once)
+          float2 e[RUPL][4];
+#pragma unroll
+          for (int i = 0; i < RUPL; ++i) {
+            const int pp = k + i;
+            if constexpr (decltype(REC)::value) {
+              const uint32_t pc = (uint32_t)(cb + (pp < U ? pp : U));
+              const float4 ra = ld_u32off(rec, 2u * pc), rb2 = ld_u32off(rec, 2u * pc + 1u);
+              e[i][0] = float2{ra.x, ra.y};
+              e[i][1] = float2{ra.z, ra.w};
+              e[i][2] = float2{rb2.x, rb2.y};
+              e[i][3] = float2{rb2.z, rb2.w};
+            } else {
+              const uint32_t jp = (uint32_t)(4 * (int)(pp < U ? u[i] : 0u) - c + 4);
+              e[i][0] = ld_u32off(ab, jp);  // padded index of word 0
+              e[i][1] = ld_u32off(ab, jp + 1u);
+              e[i][2] = ld_u32off(ab, jp + 2u);
+              e[i][3] = ld_u32off(ab, jp + 3u);
+            }
+          }
+          const int kn = (k + RUPL < U) ? k + RUPL : U;
+          const float bnext = ld_u32off(bp, (uint32_t)(cb + kn));
           // round keys recomputed in SALU each iteration (opaque key): keeping
           // all 20 live costs SGPRs the loop then spills into VGPR lanes
           uint32_t kk0 = st.k0, kk1 = st.k1;
           asm volatile("" : "+s"(kk0), "+s"(kk1));
-          const uint64_t blk = rb + u;
-          const U4 x = philox10_dev((uint32_t)blk, (uint32_t)(blk >> 32), st.c2, st.c3, kk0, kk1);
-          F4 z;
-          box_muller_screen(x.x, x.y, z.a, z.b);
-          box_muller_screen(x.z, x.w, z.c, z.d);
-          const float a0 = __builtin_fmaf(e0.x, z.a, e0.y);
-          const float a1 = __builtin_fmaf(e1.x, z.b, e1.y);
-          const float a2 = __builtin_fmaf(e2.x, z.c, e2.y);
-          const float a3 = __builtin_fmaf(e3.x, z.d, e3.y);
-          s = __builtin_fmaf(-a0, a0, s);
-          s = __builtin_fmaf(-a1, a1, s);
-          s = __builtin_fmaf(-a2, a2, s);
-          s = __builtin_fmaf(-a3, a3, s);
-          k += 1;
+#pragma unroll
+          for (int i = 0; i < RUPL; ++i) {
+            const uint64_t blk = rb + u[i];
+            const U4 x =
+                philox10_dev((uint32_t)blk, (uint32_t)(blk >> 32), st.c2, st.c3, kk0, kk1);
+            F4 z;
+            box_muller_screen(x.x, x.y, z.a, z.b);
+            box_muller_screen(x.z, x.w, z.c, z.d);
+            const bool in = i == 0 || k + i < U;
+            const float a0 = in ? __builtin_fmaf(e[i][0].x, z.a, e[i][0].y) : 0.0f;
+            const float a1 = in ? __builtin_fmaf(e[i][1].x, z.b, e[i][1].y) : 0.0f;
+            const float a2 = in ? __builtin_fmaf(e[i][2].x, z.c, e[i][2].y) : 0.0f;
+            const float a3 = in ? __builtin_fmaf(e[i][3].x, z.d, e[i][3].y) : 0.0f;
+            s = __builtin_fmaf(-a0, a0, s);
+            s = __builtin_fmaf(-a1, a1, s);
+            s = __builtin_fmaf(-a2, a2, s);
+            s = __builtin_fmaf(-a3, a3, s);
 #ifdef CWQ_PRUNE_STATS
-          if (active) atomicAdd(&g_prune_stats[43], 1ull);
+            if (active && in) atomicAdd(&g_prune_stats[43], 1ull);
 #endif
+          }
+          k = kn;
           const bool complete = k == U;
           const float upper = __builtin_fmaf(s, gc.x, bnext);
           const bool prune = !complete && (upper < tau);
@@ -1055,7 +1100,7 @@ __global__ void __launch_bounds__(256, 6) k_encode_prune_csr(
             start_row();
             k = 0;
             s = 0.0f;
-            u_nx = od[cb];
+            load_units(0);
           }
           wnext += (uint32_t)__builtin_popcountll(m);
           active = r < r1;
@@ -1119,50 +1164,84 @@ __global__ void __launch_bounds__(256, 6) k_encode_prune_csr(
         };
         start_row();
         int k = 0;
-        uint32_t u_nx = od[cb + ((int)t < U ? (int)t : U)];  // one iteration ahead, as in run
+        // lane t takes visit positions k + t + 16 i, i < UPL: a slot advances
+        // CH = 16 UPL units per iteration.  The units of the next positions
+        // are loaded one iteration ahead, as in run.
+        constexpr int UPL = CWQ_COOP_UPL, CH = 16 * UPL;
+        // Loads index their (uniform) base with an unsigned 32-bit byte offset,
+        // so they address as base + voffset: no 64-bit address arithmetic in
+        // the loop.  Offsets stay far below 2^32 (a block's region holds
+        // d + 10 entries of at most 32 bytes).
+        uint32_t u_nx[UPL];
+        auto load_units = [&](int p0) __attribute__((always_inline)) {
+#pragma unroll
+          for (int i = 0; i < UPL; ++i) {
+            const int pp = p0 + 16 * i;
+            u_nx[i] = ld_u32off(od, (uint32_t)cb + (uint32_t)(pp < U ? pp : U));
+          }
+        };
+        load_units((int)t);
         while (__ballot(active) != 0ull) {
           const int p = k + (int)t;
           float part = 0.0f;
-          const uint32_t u = u_nx;
-          u_nx = od[cb + (p + 16 < U ? p + 16 : U)];
+          uint32_t u[UPL];
+#pragma unroll
+          for (int i = 0; i < UPL; ++i) u[i] = u_nx[i];
+          load_units(p + CH);
           // constants and the slot's next drop bound ahead of the Philox
           // rounds, as in run (positions past U clamp to U: in the region)
-          const int kn = (k + 16 < U) ? k + 16 : U;
-          const float bnext = bp[cb + kn];
-          float2 e0, e1, e2, e3;
-          if constexpr (decltype(REC)::value) {
-            const int pc = p < U ? p : U;
-            const float4 ra = rec[2 * (cb + pc)], rb2 = rec[2 * (cb + pc) + 1];
-            e0 = float2{ra.x, ra.y};
-            e1 = float2{ra.z, ra.w};
-            e2 = float2{rb2.x, rb2.y};
-            e3 = float2{rb2.z, rb2.w};
-          } else {
-            const int jp = 4 * (int)(p < U ? u : 0u) - c + 4;
-            e0 = ab[jp];
-            e1 = ab[jp + 1];
-            e2 = ab[jp + 2];
-            e3 = ab[jp + 3];
+          const int kn = (k + CH < U) ? k + CH : U;
+          const float bnext = ld_u32off(bp, (uint32_t)(cb + kn));
+          float2 e[UPL][4];
+#pragma unroll
+          for (int i = 0; i < UPL; ++i) {
+            const int pp = p + 16 * i;
+            if constexpr (decltype(REC)::value) {
+              const uint32_t pc = (uint32_t)(cb + (pp < U ? pp : U));
+              const float4 ra = ld_u32off(rec, 2u * pc), rb2 = ld_u32off(rec, 2u * pc + 1u);
+              e[i][0] = float2{ra.x, ra.y};
+              e[i][1] = float2{ra.z, ra.w};
+              e[i][2] = float2{rb2.x, rb2.y};
+              e[i][3] = float2{rb2.z, rb2.w};
+            } else {
+              const uint32_t jp = (uint32_t)(4 * (int)(pp < U ? u[i] : 0u) - c + 4);
+              e[i][0] = ld_u32off(ab, jp);
+              e[i][1] = ld_u32off(ab, jp + 1u);
+              e[i][2] = ld_u32off(ab, jp + 2u);
+              e[i][3] = ld_u32off(ab, jp + 3u);
+            }
           }
           if (active && p < U) {
             uint32_t kk0 = st.k0, kk1 = st.k1;
             asm volatile("" : "+s"(kk0), "+s"(kk1));
-            const uint64_t blk = rb + u;
-            const U4 x = philox10_dev((uint32_t)blk, (uint32_t)(blk >> 32), st.c2, st.c3, kk0, kk1);
-            F4 z;
-            box_muller_screen(x.x, x.y, z.a, z.b);
-            box_muller_screen(x.z, x.w, z.c, z.d);
-            const float a0 = __builtin_fmaf(e0.x, z.a, e0.y);
-            const float a1 = __builtin_fmaf(e1.x, z.b, e1.y);
-            const float a2 = __builtin_fmaf(e2.x, z.c, e2.y);
-            const float a3 = __builtin_fmaf(e3.x, z.d, e3.y);
-            part = -(a0 * a0);
-            part = __builtin_fmaf(-a1, a1, part);
-            part = __builtin_fmaf(-a2, a2, part);
-            part = __builtin_fmaf(-a3, a3, part);
+            // the UPL units are independent chains (ILP); a unit past the row
+            // end (its clamped constants may be anything) adds 0
+#pragma unroll
+            for (int i = 0; i < UPL; ++i) {
+              const uint64_t blk = rb + u[i];
+              const U4 x =
+                  philox10_dev((uint32_t)blk, (uint32_t)(blk >> 32), st.c2, st.c3, kk0, kk1);
+              F4 z;
+              box_muller_screen(x.x, x.y, z.a, z.b);
+              box_muller_screen(x.z, x.w, z.c, z.d);
+              const float a0 = __builtin_fmaf(e[i][0].x, z.a, e[i][0].y);
+              const float a1 = __builtin_fmaf(e[i][1].x, z.b, e[i][1].y);
+              const float a2 = __builtin_fmaf(e[i][2].x, z.c, e[i][2].y);
+              const float a3 = __builtin_fmaf(e[i][3].x, z.d, e[i][3].y);
+              float pu = -(a0 * a0);
+              pu = __builtin_fmaf(-a1, a1, pu);
+              pu = __builtin_fmaf(-a2, a2, pu);
+              pu = __builtin_fmaf(-a3, a3, pu);
+              if (i == 0)
+                part = pu;
+              else
+                part = part + (p + 16 * i < U ? pu : 0.0f);
+            }
           }
 #ifdef CWQ_PRUNE_STATS
-          if (active && p < U) atomicAdd(&g_prune_stats[43], 1ull);
+#pragma unroll
+          for (int i = 0; i < UPL; ++i)
+            if (active && p + 16 * i < U) atomicAdd(&g_prune_stats[43], 1ull);
 #endif
           s = s + row16_sum_f32(part);
           k = kn;
@@ -1195,7 +1274,7 @@ __global__ void __launch_bounds__(256, 6) k_encode_prune_csr(
             start_row();
             k = 0;
             s = 0.0f;
-            u_nx = od[cb + ((int)t < U ? (int)t : U)];
+            load_units((int)t);
           }
           wnext += (uint32_t)(__builtin_popcountll(m) >> 4);
           active = q < q1;
@@ -1214,13 +1293,19 @@ __global__ void __launch_bounds__(256, 6) k_encode_prune_csr(
       for (int pass = 0;; ++pass) {
         using NoRec = std::integral_constant<bool, false>;
         using Rec = std::integral_constant<bool, true>;
-        if (coop) {
-          if (in_lds)
-            run_coop(l_ab, l_bp, l_ord, nullptr, NoRec{});
-          else if (abp)
-            run_coop(nullptr, bpre + reg, ordu + reg, abp + 2 * reg, Rec{});
-          else
-            run_coop(sab + off + 8 * g, bpre + reg, ordu + reg, nullptr, NoRec{});
+        // each launch mode instantiates only its own loops (register
+        // allocation is per kernel: the largest loop sets every loop's budget)
+        if constexpr (COOP) {
+          if (coop) {
+            if (in_lds)
+              run_coop(l_ab, l_bp, l_ord, nullptr, NoRec{});
+            else if (abp)
+              run_coop(nullptr, bpre + reg, ordu + reg, abp + 2 * reg, Rec{});
+            else
+              run_coop(sab + off + 8 * g, bpre + reg, ordu + reg, nullptr, NoRec{});
+          } else {  // d < coop_min_d <= CWQ_CSR_LDS_DIMS: the constants are in LDS
+            run(l_ab, l_bp, l_ord, nullptr, NoRec{});
+          }
         } else if (in_lds)
           run(l_ab, l_bp, l_ord, nullptr, NoRec{});
         else if (abp)
@@ -1702,11 +1787,20 @@ static void launch_prune_csr(const EncodeArgs& a, int step, hipStream_t stream) 
                      (int64_t)CWQ_CSR_LDS_DIMS, coop_min_d);
   constexpr int64_t kGrid = 1 << 20;
   const unsigned grid = (unsigned)(ntiles < kGrid ? ntiles : kGrid);
-  hipLaunchKernelGGL((k_encode_prune_csr<STEP0>), dim3(grid), dim3(256), 0, stream, a.t_loc,
-                     a.t_scale, a.loc_s, a.scale_s, a.lognorm, a.out_sample, a.block_off, a.ud,
-                     ntiles, tpb, cpt, a.n_cand, a.seed, a.block_id_base, step,
-                     (const float2*)a.sab, (const float*)a.bpre, (const uint32_t*)a.ordu,
-                     (const float4*)a.grp, a.gtau, a.keys, coop_min_d, (const float4*)a.abp);
+  if (coop)
+    hipLaunchKernelGGL((k_encode_prune_csr<STEP0, true>), dim3(grid), dim3(256), 0, stream,
+                       a.t_loc, a.t_scale, a.loc_s, a.scale_s, a.lognorm, a.out_sample,
+                       a.block_off, a.ud, ntiles, tpb, cpt, a.n_cand, a.seed, a.block_id_base,
+                       step, (const float2*)a.sab, (const float*)a.bpre,
+                       (const uint32_t*)a.ordu, (const float4*)a.grp, a.gtau, a.keys,
+                       coop_min_d, (const float4*)a.abp);
+  else
+    hipLaunchKernelGGL((k_encode_prune_csr<STEP0, false>), dim3(grid), dim3(256), 0, stream,
+                       a.t_loc, a.t_scale, a.loc_s, a.scale_s, a.lognorm, a.out_sample,
+                       a.block_off, a.ud, ntiles, tpb, cpt, a.n_cand, a.seed, a.block_id_base,
+                       step, (const float2*)a.sab, (const float*)a.bpre,
+                       (const uint32_t*)a.ordu, (const float4*)a.grp, a.gtau, a.keys,
+                       coop_min_d, (const float4*)a.abp);
 }
 
 template <bool STEP0>

@@ -5,7 +5,7 @@
 set -e
 cd "$(dirname "$0")/.."
 CSRC=compression_without_quantization_amd/csrc
-OUT=tools/variants
+OUT=${VOUT:-tools/variants}
 FLAGS="--offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -fno-fast-math -fPIC -shared"
 declare -A V=(
   [base]=""
@@ -32,10 +32,24 @@ declare -A V=(
   [mask31]="-DCWQ_TAU_SHARE_MASK=31u"
   [cap512]="-DCWQ_SURVIVOR_CAP=512"
   [w7]="-DCWQ_PRUNE_MIN_WAVES=7"
+  [pf]="-DCWQ_COOP_REC_PREFETCH=1"
+  [upl2]="-DCWQ_COOP_UPL=2"
+  [upl2pf]="-DCWQ_COOP_UPL=2 -DCWQ_COOP_REC_PREFETCH=1"
+  [pfw5]="-DCWQ_COOP_REC_PREFETCH=1 -DCWQ_CSR_COOP_MIN_WAVES=5"
+  [upl2w5]="-DCWQ_COOP_UPL=2 -DCWQ_CSR_COOP_MIN_WAVES=5"
+  [upl2pfw4]="-DCWQ_COOP_UPL=2 -DCWQ_COOP_REC_PREFETCH=1 -DCWQ_CSR_COOP_MIN_WAVES=4"
+  [head]=prebuilt
+  [c4r2]="-DCWQ_COOP_UPL=4 -DCWQ_CSR_COOP_MIN_WAVES=4 -DCWQ_RUN_UPL=2"
+  [c4r1]="-DCWQ_COOP_UPL=4 -DCWQ_CSR_COOP_MIN_WAVES=4"
+  [c4r2m3]="-DCWQ_COOP_UPL=4 -DCWQ_CSR_COOP_MIN_WAVES=4 -DCWQ_RUN_UPL=2 -DCWQ_TAU_SHARE_MASK=7u"
+  [upl2w4]="-DCWQ_COOP_UPL=2 -DCWQ_CSR_COOP_MIN_WAVES=4"
+  [upl3w4]="-DCWQ_COOP_UPL=3 -DCWQ_CSR_COOP_MIN_WAVES=4"
+  [upl4w4]="-DCWQ_COOP_UPL=4 -DCWQ_CSR_COOP_MIN_WAVES=4"
+  [upl2w5m7]="-DCWQ_COOP_UPL=2 -DCWQ_CSR_COOP_MIN_WAVES=5 -DCWQ_TAU_SHARE_MASK=7u"
 )
 if [ "$1" = build ]; then
   mkdir -p $OUT
-  for k in "${!V[@]}"; do
+  for k in ${VARIANTS:-"${!V[@]}"}; do
     [ "${V[$k]}" = prebuilt ] && continue  # built by hand from an older commit
     hipcc $FLAGS ${V[$k]} -o $OUT/libcwq_$k.so $CSRC/cwq_kernels.hip $CSRC/cwq_importance.hip $CSRC/cwq_pln.hip $CSRC/cwq_capi.hip $CSRC/cwq_ac.cpp &
   done
