@@ -39,6 +39,7 @@ declare -A V=(
   [upl2w5]="-DCWQ_COOP_UPL=2 -DCWQ_CSR_COOP_MIN_WAVES=5"
   [upl2pfw4]="-DCWQ_COOP_UPL=2 -DCWQ_COOP_REC_PREFETCH=1 -DCWQ_CSR_COOP_MIN_WAVES=4"
   [head]=prebuilt
+  [split1]="-DCWQ_ENCODE_SPLIT=1"
   [c4r2]="-DCWQ_COOP_UPL=4 -DCWQ_CSR_COOP_MIN_WAVES=4 -DCWQ_RUN_UPL=2"
   [c4r1]="-DCWQ_COOP_UPL=4 -DCWQ_CSR_COOP_MIN_WAVES=4"
   [c4r2m3]="-DCWQ_COOP_UPL=4 -DCWQ_CSR_COOP_MIN_WAVES=4 -DCWQ_RUN_UPL=2 -DCWQ_TAU_SHARE_MASK=7u"
