@@ -1525,6 +1525,14 @@ __global__ void __launch_bounds__(256) k_decode(
 // sample move as float4 (coalesced across the wave).  Lanes map to blocks as
 // in k_encode_finalize_q4.  With n_steps == 1 the shard divisions are by 1.0f
 // (exact identities; skipped on a uniform branch).
+// A wave decodes a group of B = bpw * qpb blocks (<= 64) as qpb chunks of
+// bpw blocks, one lane per Philox block of a row (float4 I/O, coalesced).
+// Single-step codes: lane i computes the stream key of the group's block i
+// once (TF GenerateKey is itself a Philox-10 call, as costly as a row's
+// block) and each chunk takes its blocks' keys by lane shuffle, so a group
+// pays one key call per block instead of one per lane.  The next chunk's
+// inputs are loaded before the current chunk's arithmetic, so HBM reads stay
+// in flight while the exact Box-Muller runs.
 __global__ void __launch_bounds__(256) k_decode_q4(
     const int32_t* __restrict__ idx, const float4* __restrict__ p_loc,
     const float4* __restrict__ p_scale, uint32_t qpb, uint32_t bpw, int64_t nb, int n_steps,
@@ -1533,41 +1541,69 @@ __global__ void __launch_bounds__(256) k_decode_q4(
   __shared__ double logtab[32];
   fill_logtab(logtab);
   const Q4Lane L = q4_lane(qpb, bpw);
+  const uint32_t lane = threadIdx.x & 63u;
+  const int64_t B = (int64_t)bpw * qpb;
+  const int64_t ngroups = (nb + B - 1) / B;
   const int64_t nwaves = (int64_t)gridDim.x * 4;
   const bool unit = n_steps == 1;  // nst == sdiv == 1.0f
-  for (int64_t c = (int64_t)blockIdx.x * 4 + wave_id(); c * bpw < nb; c += nwaves) {
-    const int64_t g = c * bpw + L.lb;
-    if (!L.active || g >= nb) continue;
-    const int64_t t = g * qpb + L.q;
-    const float4 pl = p_loc[t], ps = p_scale[t];
-    float ls[4] = {pl.x, pl.y, pl.z, pl.w};
-    float ss[4] = {rho * ps.x, rho * ps.y, rho * ps.z, rho * ps.w};
-    if (!unit) {
+  for (int64_t grp = (int64_t)blockIdx.x * 4 + wave_id(); grp < ngroups; grp += nwaves) {
+    const int64_t gb0 = grp * B;
+    PhiloxStream kl{0u, 0u, 0u, 0u};
+    if (unit)  // lanes past the group (or nb) compute an unused key
+      kl = generate_key(step_seed(block_seed(seed, block_id_base + gb0 + lane), 0), 42);
+    // chunk inputs: the current ones and the next chunk's, loaded one ahead
+    float4 pl = float4{0.f, 0.f, 0.f, 0.f}, ps = pl;
+    int32_t n1 = 0;  // single-step index
+    auto load = [&](uint32_t j, float4& a, float4& b, int32_t& n) {
+      const int64_t g = gb0 + (int64_t)(j * bpw + L.lb);
+      if (L.active && g < nb) {
+        const int64_t t = g * qpb + L.q;
+        a = p_loc[t];
+        b = p_scale[t];
+        if (unit) n = idx[g];
+      }
+    };
+    load(0u, pl, ps, n1);
+    for (uint32_t j = 0; j < qpb; ++j) {
+      const uint32_t src = j * bpw + L.lb;  // the lane holding this block's key
+      const int64_t g = gb0 + (int64_t)src;
+      const PhiloxStream ku{(uint32_t)__shfl((int)kl.k0, (int)src, 64),
+                            (uint32_t)__shfl((int)kl.k1, (int)src, 64),
+                            (uint32_t)__shfl((int)kl.c2, (int)src, 64),
+                            (uint32_t)__shfl((int)kl.c3, (int)src, 64)};
+      const float4 cl = pl, cs = ps;
+      const int32_t cn = n1;
+      if (j + 1 < qpb) load(j + 1, pl, ps, n1);
+      if (!L.active || g >= nb) continue;
+      float ls[4] = {cl.x, cl.y, cl.z, cl.w};
+      float ss[4] = {rho * cs.x, rho * cs.y, rho * cs.z, rho * cs.w};
+      if (!unit) {
 #pragma unroll
-      for (int w = 0; w < 4; ++w) {
-        ls[w] = ls[w] / nst;
-        ss[w] = ss[w] / sdiv;
+        for (int w = 0; w < 4; ++w) {
+          ls[w] = ls[w] / nst;
+          ss[w] = ss[w] / sdiv;
+        }
       }
-    }
-    float v[4] = {0.0f, 0.0f, 0.0f, 0.0f};  // sample = tf.zeros (:143)
-    const int32_t sg = block_seed(seed, block_id_base + g);
-    for (int i = 0; i < n_steps; ++i) {
-      const int64_t n = idx[g * n_steps + i];
-      if (n < 0 || n >= n_cand) {
-        v[0] = v[1] = v[2] = v[3] = __builtin_nanf("");
-        continue;
-      }
-      const PhiloxStream st = generate_key(step_seed(sg, i), 42);
-      const F4 z = normal4_dev(st, (uint64_t)n * qpb + L.q, logtab);
-      const float zz[4] = {z.a, z.b, z.c, z.d};
+      float v[4] = {0.0f, 0.0f, 0.0f, 0.0f};  // sample = tf.zeros (:143)
+      const int32_t sg = block_seed(seed, block_id_base + g);
+      for (int i = 0; i < n_steps; ++i) {
+        const int64_t n = unit ? (int64_t)cn : (int64_t)idx[g * n_steps + i];
+        if (n < 0 || n >= n_cand) {
+          v[0] = v[1] = v[2] = v[3] = __builtin_nanf("");
+          continue;
+        }
+        const PhiloxStream st = unit ? ku : generate_key(step_seed(sg, i), 42);
+        const F4 z = normal4_dev(st, (uint64_t)n * qpb + L.q, logtab);
+        const float zz[4] = {z.a, z.b, z.c, z.d};
 #pragma unroll
-      for (int w = 0; w < 4; ++w) {
-        float s = ss[w] * zz[w];
-        s = ls[w] + s;
-        v[w] = v[w] + s;  // :153 tile(sample) + samples, row indices[i]
+        for (int w = 0; w < 4; ++w) {
+          float sv = ss[w] * zz[w];
+          sv = ls[w] + sv;
+          v[w] = v[w] + sv;  // :153 tile(sample) + samples, row indices[i]
+        }
       }
+      out_sample[g * qpb + L.q] = make_float4(v[0], v[1], v[2], v[3]);
     }
-    out_sample[t] = make_float4(v[0], v[1], v[2], v[3]);
   }
 }
 
@@ -2002,7 +2038,8 @@ hipError_t launch_decode(const int32_t* idx, const float* p_loc, const float* p_
   const float sdiv = (float)__builtin_sqrt((double)n_steps);
   if (q4_shape(block_off, ud) && aligned16(p_loc, p_scale, out_sample)) {
     const uint32_t qpb = (uint32_t)(ud / 4), bpw = 64u / qpb;
-    hipLaunchKernelGGL(k_decode_q4, dim3(grid_for(nb, 4 * (int64_t)bpw, 1u << 20)), dim3(256), 0,
+    const int64_t ngroups = (nb + (int64_t)bpw * qpb - 1) / ((int64_t)bpw * qpb);
+    hipLaunchKernelGGL(k_decode_q4, dim3(grid_for(ngroups, 4, 1u << 20)), dim3(256), 0,
                        stream, idx, (const float4*)p_loc, (const float4*)p_scale, qpb, bpw, nb,
                        n_steps, (int64_t)1 << n_bits, nst, sdiv, rho, seed, block_id_base,
                        (float4*)out_sample);
