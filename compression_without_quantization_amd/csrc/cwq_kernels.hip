@@ -890,6 +890,9 @@ __device__ __forceinline__ float exact_row_wave(
 #ifndef CWQ_CSR_COOP_MIN_WAVES
 #define CWQ_CSR_COOP_MIN_WAVES 4      // waves/SIMD the cooperative kernel's registers allow
 #endif
+#ifndef CWQ_CSR_RUN_MIN_WAVES
+#define CWQ_CSR_RUN_MIN_WAVES 6       // waves/SIMD the per-lane kernel's registers allow
+#endif
 #ifndef CWQ_RUN_UPL
 #define CWQ_RUN_UPL 2                 // units per lane per iteration of a per-lane row
 #endif
@@ -909,7 +912,7 @@ static_assert(CWQ_CSR_COOP_MIN_D <= CWQ_CSR_LDS_DIMS, "short rows of a cooperati
 // coop_min_d dims walked by 16-lane slots, shorter ones per lane from LDS);
 // otherwise one row per lane for every block.
 template <bool STEP0, bool COOP>
-__global__ void __launch_bounds__(256, COOP ? CWQ_CSR_COOP_MIN_WAVES : 6) k_encode_prune_csr(
+__global__ void __launch_bounds__(256, COOP ? CWQ_CSR_COOP_MIN_WAVES : CWQ_CSR_RUN_MIN_WAVES) k_encode_prune_csr(
     const float* __restrict__ t_loc, const float* __restrict__ t_scale,
     const float* __restrict__ loc_s, const float* __restrict__ scale_s,
     const float* __restrict__ lognorm, const float* __restrict__ best,

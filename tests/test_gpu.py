@@ -704,6 +704,11 @@ def test_uniform_odd_d_general_pruned(cwq, cwqlib, oracle, d, bits, nb):
     ([1500, 255, 256, 40], 13, 3, "normal"),     # coop and per-lane rows in one launch
     ([600] * 3, 14, 1, "flat"),                  # near-ties: survivor overflow, redo, exact
     ([700, 900], 12, 2, "heavy"),
+    # row lengths around the loops' unit strides (4 units per lane of a 16-lane
+    # slot: 64 units per iteration; 2 units per iteration of a per-lane row)
+    # and the LDS / visit-order-record boundary at 1024 dims
+    ([256, 257, 259, 255, 1021, 1024, 1025, 1027], 12, 2, "normal"),
+    ([1087, 1089, 4093, 513, 511, 7, 3, 1], 12, 2, "heavy"),
 ])
 def test_csr_cooperative_rows_vs_oracle(cwq, cwqlib, oracle, sizes, bits, n_steps, kind):
     rng = np.random.default_rng(sum(sizes) * bits)

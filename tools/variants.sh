@@ -39,6 +39,9 @@ declare -A V=(
   [upl2w5]="-DCWQ_COOP_UPL=2 -DCWQ_CSR_COOP_MIN_WAVES=5"
   [upl2pfw4]="-DCWQ_COOP_UPL=2 -DCWQ_COOP_REC_PREFETCH=1 -DCWQ_CSR_COOP_MIN_WAVES=4"
   [head]=prebuilt
+  [r3w5]="-DCWQ_RUN_UPL=3 -DCWQ_CSR_RUN_MIN_WAVES=5"
+  [r4w4]="-DCWQ_RUN_UPL=4 -DCWQ_CSR_RUN_MIN_WAVES=4"
+  [r2w5]="-DCWQ_RUN_UPL=2 -DCWQ_CSR_RUN_MIN_WAVES=5"
   [split1]="-DCWQ_ENCODE_SPLIT=1"
   [c4r2]="-DCWQ_COOP_UPL=4 -DCWQ_CSR_COOP_MIN_WAVES=4 -DCWQ_RUN_UPL=2"
   [c4r1]="-DCWQ_COOP_UPL=4 -DCWQ_CSR_COOP_MIN_WAVES=4"
