@@ -21,6 +21,7 @@ from .coded_importance_sampler import (code_grouped_importance_sample,
 from .misc import stateless_normal_sample
 from .pln import ProbabilisticLadderNetwork, build_empirical_dists
 from .parallel import gather_indices, shard_range
+from .streaming import encode_blocks_host
 
 __all__ = [
     "Normal", "code_greedy_sample", "decode_greedy_sample", "code_grouped_greedy_sample",
@@ -33,4 +34,5 @@ __all__ = [
     "code_grouped_importance_sample", "decode_grouped_importance_sample",
     "importance_encode_blocks", "importance_decode_blocks", "ArithmeticCoder",
     "write_bin_code", "read_bin_code", "ProbabilisticLadderNetwork", "build_empirical_dists",
+    "encode_blocks_host",
 ]

@@ -210,3 +210,28 @@ def test_bench_weak_scaling_two_ranks(cwq):
     assert line["n_gpus"] == 2 and line["scaling"] == "weak"
     assert line["config"]["blocks_total"] == 4096 and line["config"]["blocks_per_gpu"] == 2048
     assert line["parity"]["index_mismatches"] == 0
+
+
+@pytest.mark.parametrize("nb,d,chunk,n_steps,base", [
+    (1000, 32, 256, 1, 0),      # 4 chunks, the last one partial
+    (700, 8, 1000, 2, 5),       # one chunk larger than the job
+    (513, 16, 64, 1, 77),       # many chunks: both slots reused repeatedly
+    (3, 32, 1, 3, 0),           # one block per chunk
+])
+def test_encode_blocks_host_streamed_equals_one_call(cwq, nb, d, chunk, n_steps, base):
+    """encode_blocks_host (pinned staging, H2D / compute / D2H on three
+    streams, chunk c coded with block_id_base = base + c * chunk) equals one
+    encode_blocks call over all blocks, bit for bit."""
+    rng = np.random.default_rng(nb * d + chunk)
+    tl = rng.standard_normal(nb * d).astype(np.float32)
+    ts = rng.uniform(0.3, 0.9, nb * d).astype(np.float32)
+    pl = (0.1 * rng.standard_normal(nb * d)).astype(np.float32)
+    ps = rng.uniform(0.8, 1.2, nb * d).astype(np.float32)
+    bits = 12
+    gi, gs = cwq.encode_blocks(tl, ts, pl, ps, bits, n_steps, 42, block_dim=d,
+                               block_id_base=base)
+    hi, hs = cwq.encode_blocks_host(tl, ts, pl, ps, bits, n_steps, 42, d, block_id_base=base,
+                                    chunk_blocks=chunk)
+    assert hi.shape == (nb, n_steps) and hs.shape == (nb * d,)
+    assert np.array_equal(hi, gi.cpu().numpy())
+    assert np.array_equal(hs.view(np.uint32), gs.cpu().numpy().view(np.uint32))
