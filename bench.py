@@ -100,6 +100,8 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
+    ap.add_argument("--per-image", action="store_true",
+                    help="grouped configs: time one call per latent set only (no batched call)")
     ap.add_argument("--prune-mode", type=int, default=2, choices=(0, 1, 2),
                     help="0 unpruned, 1 exact pruning, 2 pruning + screening (default)")
     ap.add_argument("--scaling", choices=("strong", "weak"), default=None,
@@ -129,19 +131,38 @@ def grouped_main(args):
             lat.append((C.Normal(torch.from_numpy(q_loc).to(dev), torch.from_numpy(q_scale).to(dev)),
                         C.Normal(torch.from_numpy(p_loc).to(dev), torch.from_numpy(p_scale).to(dev))))
 
-    def step():
+    def step_single():  # one code_grouped_greedy_sample call per latent set
         out = []
         for target, proposal in lat:
             out.append(C.code_grouped_greedy_sample(None, target, proposal, n_steps, bits, 42))
         return out
-    for _ in range(args.warmup):
-        res = step()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        res = step()
-    torch.cuda.synchronize()
-    el = time.perf_counter() - t0
+
+    def step_batch():  # every latent set of the step in one batched call
+        return C.code_grouped_greedy_sample_batch(None, [t for t, _ in lat], [p for _, p in lat],
+                                                  n_steps, bits, 42)
+
+    def timed(step):
+        for _ in range(args.warmup):
+            step()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            res = step()
+        torch.cuda.synchronize()
+        return time.perf_counter() - t0, res
+
+    el_single, res = timed(step_single)
+    el = el_single
+    batched = None
+    if len(lat) > 1 and not args.per_image:
+        el, res_b = timed(step_batch)
+        same = all(list(a[2]) == list(b[2]) and a[1] == b[1] and
+                   np.array_equal(np.asarray(a[0]).view(np.uint32), np.asarray(b[0]).view(np.uint32))
+                   for a, b in zip(res, res_b))
+        batched = {"latent_sets_per_call": len(lat), "equal_to_single_calls": bool(same),
+                   "single_call_images_per_s": n_img * args.steps / el_single}
+        if not same:
+            raise SystemExit("bench.py: batched results differ from the single calls")
     groups = sum(len(r[2]) - 1 for r in res)
     bitlen = sum(len(r[1]) for r in res)
     line = {"metric": "images coded/s (grouped greedy pipeline)", "value": n_img * args.steps / el,
@@ -149,7 +170,11 @@ def grouped_main(args):
             "ms_per_step": el / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": "f32", "data": "synthetic PLN-like latents",
             "config": {"workload": desc, "groups_per_step": groups, "bits_per_step": bitlen,
-                       "groups_per_s": groups * args.steps / el}}
+                       "groups_per_s": groups * args.steps / el,
+                       "mode": ("code_grouped_greedy_sample_batch: every latent set of a step "
+                                "in one call" if batched else
+                                "one code_grouped_greedy_sample call per latent set"),
+                       "batched": batched}}
     print(json.dumps(line), flush=True)
 
 

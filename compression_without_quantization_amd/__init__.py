@@ -10,6 +10,7 @@ from .binary_io import (bitcode_to_indices, elias_delta_code, elias_delta_decode
                         write_bin_code)
 from .coding import ArithmeticCoder
 from .coded_greedy_sampler import (Normal, code_greedy_sample, code_grouped_greedy_sample,
+                                   code_grouped_greedy_sample_batch,
                                    decode, decode_blocks, decode_greedy_sample,
                                    decode_grouped_greedy_sample, encode, encode_blocks,
                                    encode_workspace_bytes, group_size_threshold, group_starts)
@@ -34,5 +35,5 @@ __all__ = [
     "code_grouped_importance_sample", "decode_grouped_importance_sample",
     "importance_encode_blocks", "importance_decode_blocks", "ArithmeticCoder",
     "write_bin_code", "read_bin_code", "ProbabilisticLadderNetwork", "build_empirical_dists",
-    "encode_blocks_host",
+    "encode_blocks_host", "code_grouped_greedy_sample_batch",
 ]

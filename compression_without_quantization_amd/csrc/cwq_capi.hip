@@ -12,6 +12,7 @@
 #include <time.h>
 #include <immintrin.h>
 
+#include <thread>
 #include <vector>
 
 #include "../../include/cwq.h"
@@ -317,7 +318,8 @@ int encode_impl(const float* t_loc, const float* t_scale, const float* p_loc,
                 const float* p_scale, const int64_t* block_off, int64_t ud, int64_t nb,
                 int64_t total_dims, int64_t max_block_dim, int n_bits, int n_steps, int32_t seed, float rho,
                 int64_t block_id_base, int32_t* out_idx, float* out_sample, void* workspace,
-                size_t workspace_bytes, const cwq_options* opts, void* stream) {
+                size_t workspace_bytes, const cwq_options* opts, void* stream,
+                const int32_t* block_seeds = nullptr) {
   int rc = check_common(n_bits, n_steps, nb);
   if (rc) return rc;
   cwq_options o;
@@ -349,6 +351,7 @@ int encode_impl(const float* t_loc, const float* t_scale, const float* p_loc,
   a.seed = seed;
   a.rho = rho;
   a.block_id_base = block_id_base;
+  a.seeds = block_seeds;
   a.out_idx = out_idx;
   a.out_sample = out_sample;
   char* w = (char*)workspace;
@@ -534,6 +537,33 @@ GroupedWs grouped_ws(int64_t D, int n_steps) {
 }
 thread_local std::vector<float> g_kl_host;
 thread_local std::vector<int32_t> g_idx_host;
+// :81-87, :288 (and binary_io.py:41-53) each of n indices as n_bits LSB-first
+// '0'/'1' chars; returns n * n_bits, or CWQ_ERR_INVALID for an index that does
+// not fit (to_bit_string raises there).
+int64_t write_bitcode(const int32_t* idx, int64_t n, int n_bits, char* o) {
+  static const struct ByteChars {  // byte value -> its 8 LSB-first '0'/'1' chars
+    uint64_t c[256];
+    ByteChars() {
+      for (int v = 0; v < 256; ++v) {
+        uint64_t w = 0;
+        for (int b = 0; b < 8; ++b) w |= (uint64_t)('0' + ((v >> b) & 1)) << (8 * b);
+        c[v] = w;
+      }
+    }
+  } kByteChars;
+  for (int64_t i = 0; i < n; ++i) {
+    const uint32_t v = (uint32_t)idx[i];
+    if (n_bits < 31 && (v >> n_bits) != 0)
+      return fail(CWQ_ERR_INVALID, "index %u does not fit %d bits", v, n_bits);
+    int b = 0;
+    for (; b + 8 <= n_bits; b += 8) {
+      memcpy(o, &kByteChars.c[(v >> b) & 0xffu], 8);
+      o += 8;
+    }
+    for (; b < n_bits; ++b) *o++ = (char)('0' + ((v >> b) & 1u));
+  }
+  return n * n_bits;
+}
 }  // namespace
 
 size_t cwq_code_grouped_greedy_workspace_size(int64_t D, int n_steps) {
@@ -650,27 +680,235 @@ int64_t cwq_code_grouped_greedy(const float* q_loc, const float* q_scale, const 
   if ((e = hipStreamSynchronize(s)) != hipSuccess) return hip_fail(e, "sync");
   lap("encode");
   // :81-87, :288 each index as n_bits_per_step LSB-first chars, steps then groups
-  static const struct ByteChars {  // byte value -> its 8 LSB-first '0'/'1' chars
-    uint64_t c[256];
-    ByteChars() {
-      for (int v = 0; v < 256; ++v) {
-        uint64_t w = 0;
-        for (int b = 0; b < 8; ++b) w |= (uint64_t)('0' + ((v >> b) & 1)) << (8 * b);
-        c[v] = w;
+  {
+    const int64_t nw = write_bitcode(g_idx_host.data(), G * n_steps, n_bits_per_step, bits_host);
+    if (nw < 0) return nw;
+  }
+  lap("bits");
+  cwq::set_error(CWQ_OK, "");
+  return G;
+}
+
+// ---------------------------------------------------------------------------
+// A batch of independent code_grouped_greedy_sample calls (the images of a
+// dataset, or both ladder levels of several images) in one call.  Item i is
+// dims [item_off[i], item_off[i+1]) of the concatenated inputs and is coded
+// exactly as cwq_code_grouped_greedy on that slice with seed seeds[i]: its
+// partition is its own (:207-252), its groups are numbered from 0 and group g
+// is coded with seeds[i] + g (:273-284).  All items share one
+// standardisation, one KL copy, ONE encode launch over every item's groups
+// (per-block seeds) and one destandardisation, so a batch of small items
+// fills the chip instead of paying a launch sequence and two host round trips
+// each.
+// ---------------------------------------------------------------------------
+namespace {
+struct BatchWs {
+  GroupedWs g;
+  size_t seeds, total;
+};
+BatchWs batch_ws(int64_t D, int n_steps) {
+  BatchWs l;
+  l.g = grouped_ws(D, n_steps);
+  l.seeds = l.g.total;
+  l.total = align_up(l.seeds + (size_t)(D > 0 ? D : 1) * 4, 256);
+  return l;
+}
+thread_local std::vector<int32_t> g_seed_host;
+thread_local std::vector<int64_t> g_offs_host;
+}  // namespace
+
+size_t cwq_code_grouped_greedy_batch_workspace_size(int64_t D, int n_steps) {
+  if (D < 0 || n_steps < 0) return 0;
+  return batch_ws(D, n_steps).total;
+}
+
+int64_t cwq_code_grouped_greedy_batch(
+    int64_t n_items, const int64_t* item_off, const float* q_loc, const float* q_scale,
+    const float* p_loc, const float* p_scale, int n_steps, int n_bits_per_step,
+    const int32_t* seeds, float rho, int64_t size_threshold, double n_nats, float* sample_host,
+    char* bits_host, int64_t bits_cap, int64_t* bits_off, int64_t* starts_host,
+    int64_t starts_cap, int64_t* n_starts, void* workspace, size_t workspace_bytes,
+    const cwq_options* opts, void* stream) {
+  {
+    cwq_options o;
+    const int rc0 = read_options(opts, &o);
+    if (rc0) return rc0;
+  }
+  if (n_items < 0 || n_steps < 1 || n_bits_per_step < 0 ||
+      n_bits_per_step > CWQ_MAX_BITS_PER_STEP)
+    return fail(CWQ_ERR_INVALID, "cwq_code_grouped_greedy_batch: bad sizes");
+  if (!item_off || !bits_off || !n_starts || (n_items > 0 && !seeds))
+    return fail(CWQ_ERR_INVALID, "cwq_code_grouped_greedy_batch: null pointer");
+  if (item_off[0] != 0) return fail(CWQ_ERR_INVALID, "item_off[0] must be 0");
+  for (int64_t i = 0; i < n_items; ++i)
+    if (item_off[i + 1] < item_off[i])
+      return fail(CWQ_ERR_INVALID, "item_off must be non-decreasing");
+  const int64_t D = item_off[n_items];
+  if (D > 0 && (!q_loc || !q_scale || !p_loc || !p_scale || !sample_host))
+    return fail(CWQ_ERR_INVALID, "cwq_code_grouped_greedy_batch: null pointer");
+  if (!starts_host || starts_cap < D + 2 * n_items)
+    return fail(CWQ_ERR_CAPACITY, "starts_cap must be >= D_total + 2 n_items");
+  const BatchWs bl = batch_ws(D, n_steps);
+  const GroupedWs& l = bl.g;
+  if (workspace_bytes < bl.total || !workspace)
+    return fail(CWQ_ERR_WORKSPACE, "workspace %zu bytes < required %zu", workspace_bytes,
+                bl.total);
+  hipStream_t s = (hipStream_t)stream;
+#ifdef CWQ_PHASE_TIMES  // tuning builds: per-phase host wall times to stderr
+  struct timespec ts0, ts1;
+  clock_gettime(CLOCK_MONOTONIC, &ts0);
+  auto lap = [&](const char* what) {
+    clock_gettime(CLOCK_MONOTONIC, &ts1);
+    fprintf(stderr, "[cwq batch] %-10s %8.1f us\n", what,
+            (ts1.tv_sec - ts0.tv_sec) * 1e6 + (ts1.tv_nsec - ts0.tv_nsec) * 1e-3);
+    ts0 = ts1;
+  };
+#else
+  auto lap = [](const char*) {};
+#endif
+  // fn(i) for every item, on up to 8 host threads when the batch is large
+  const int64_t nthr = std::min<int64_t>(
+      n_items,
+      std::max<int64_t>(1, std::min<int64_t>(8, (int64_t)std::thread::hardware_concurrency())));
+  auto for_items = [&](auto fn) {
+    auto work = [&](int64_t t) {
+      for (int64_t i = t; i < n_items; i += nthr) fn(i);
+    };
+    if (nthr <= 1 || item_off[n_items] < (1 << 16)) {
+      for (int64_t t = 0; t < nthr; ++t) work(t);
+      return;
+    }
+    std::vector<std::thread> pool;
+    for (int64_t t = 1; t < nthr; ++t) pool.emplace_back(work, t);
+    work(0);
+    for (auto& th : pool) th.join();
+  };
+  char* w = (char*)workspace;
+  float* t_loc = (float*)(w + l.t_loc);
+  float* t_scale = (float*)(w + l.t_scale);
+  float* kl = (float*)(w + l.kl);
+  float* zeros = (float*)(w + l.zeros);
+  float* ones = (float*)(w + l.ones);
+  float* sample = (float*)(w + l.sample);
+  float* out = (float*)(w + l.out);
+  int64_t* offs = (int64_t*)(w + l.offs);
+  int32_t* idx = (int32_t*)(w + l.idx);
+  int32_t* bseed = (int32_t*)(w + bl.seeds);
+  hipError_t e = hipSuccess;
+  int rc;
+  if (D > 0) {  // :193-210 for every item at once (elementwise)
+    if ((rc = cwq_standardise(q_loc, q_scale, p_loc, p_scale, D, t_loc, t_scale, stream)) < 0)
+      return rc;
+    if ((rc = cwq_kl_normal_normal(q_loc, q_scale, p_loc, p_scale, D, kl, stream)) < 0) return rc;
+    if ((e = hipMemsetAsync(zeros, 0, (size_t)D * 4, s)) != hipSuccess) return hip_fail(e, "memset");
+    if ((e = hipMemsetD32Async((hipDeviceptr_t)ones, 0x3f800000u, (size_t)D, s)) != hipSuccess)
+      return hip_fail(e, "memset");
+    g_kl_host.resize((size_t)D);
+    if ((e = hipMemcpyAsync(g_kl_host.data(), kl, (size_t)D * 4, hipMemcpyDeviceToHost, s)) !=
+        hipSuccess)
+      return hip_fail(e, "KL to host");
+    if ((e = hipStreamSynchronize(s)) != hipSuccess) return hip_fail(e, "sync");
+  }
+  lap("kl");
+  // :207-252 each item's own partition, item i's starts at item_off[i] + 2 i
+  // (room for its D_i + 2 entries); the items are independent, so several
+  // host threads partition them side by side
+  {
+    std::vector<int64_t> rcs((size_t)n_items, 0);
+    const float* klh = g_kl_host.data();  // thread_local: resolve here, not in the workers
+    for_items([&](int64_t i) {
+      const int64_t a = item_off[i], Di = item_off[i + 1] - a;
+      const int64_t n = group_starts_impl(Di > 0 ? klh + a : nullptr, Di, size_threshold, n_nats,
+                                          starts_host + a + 2 * i, Di + 2, false);
+      rcs[(size_t)i] = n;
+      n_starts[i] = n < 0 ? 0 : n;
+    });
+    for (int64_t i = 0; i < n_items; ++i)
+      if (rcs[(size_t)i] < 0)
+        return fail((int)rcs[(size_t)i], "cwq_code_grouped_greedy_batch: partition of item %lld",
+                    (long long)i);
+  }
+  lap("group");
+  // the items' groups concatenated into one CSR layout, seeds seeds[i] + g
+  // (item i's groups start at global group gfirst[i]), filled per item on the
+  // same host threads
+  std::vector<int64_t> gfirst((size_t)n_items + 1, 0);
+  std::vector<int64_t> imaxd((size_t)n_items, 0);
+  bits_off[0] = 0;
+  for (int64_t i = 0; i < n_items; ++i) {
+    const int64_t Gi = n_starts[i] - 1 > 0 ? n_starts[i] - 1 : 0;
+    gfirst[(size_t)i + 1] = gfirst[(size_t)i] + Gi;
+    bits_off[i + 1] = bits_off[i] + Gi * (int64_t)n_steps * n_bits_per_step;
+  }
+  const int64_t G = gfirst[(size_t)n_items], nbits = bits_off[n_items];
+  g_offs_host.resize((size_t)G + 1);
+  g_seed_host.resize((size_t)(G > 0 ? G : 1));
+  {
+    int64_t* go = g_offs_host.data();  // thread_local: resolve here, not in the workers
+    int32_t* gs = g_seed_host.data();
+    for_items([&](int64_t i) {
+      const int64_t a = item_off[i], g0 = gfirst[(size_t)i];
+      const int64_t* st = starts_host + a + 2 * i;
+      const int64_t Gi = gfirst[(size_t)i + 1] - g0;
+      int64_t md = 0;
+      for (int64_t g = 0; g < Gi; ++g) {
+        go[g0 + g] = a + st[g];
+        gs[g0 + g] = (int32_t)((uint32_t)seeds[i] + (uint32_t)g);  // :282, int32 wrap
+        const int64_t dg = st[g + 1] - st[g];
+        md = dg > md ? dg : md;
       }
-    }
-  } kByteChars;
-  char* o = bits_host;
-  for (int64_t i = 0; i < G * n_steps; ++i) {
-    const uint32_t v = (uint32_t)g_idx_host[(size_t)i];
-    if (n_bits_per_step < 31 && (v >> n_bits_per_step) != 0)
-      return fail(CWQ_ERR_INVALID, "index %u does not fit %d bits", v, n_bits_per_step);
-    int b = 0;
-    for (; b + 8 <= n_bits_per_step; b += 8) {
-      memcpy(o, &kByteChars.c[(v >> b) & 0xffu], 8);
-      o += 8;
-    }
-    for (; b < n_bits_per_step; ++b) *o++ = (char)('0' + ((v >> b) & 1u));
+      imaxd[(size_t)i] = md;
+    });
+  }
+  g_offs_host[(size_t)G] = D;
+  if (bits_cap < nbits || (nbits > 0 && !bits_host))
+    return fail(CWQ_ERR_CAPACITY, "cwq_code_grouped_greedy_batch: bits_cap %lld < %lld",
+                (long long)bits_cap, (long long)nbits);
+  if (G <= 0) {
+    if (D > 0 && (e = hipMemcpyAsync(sample_host, zeros, (size_t)D * 4, hipMemcpyDeviceToHost,
+                                     s)) != hipSuccess)
+      return hip_fail(e, "sample to host");
+    if ((e = hipStreamSynchronize(s)) != hipSuccess) return hip_fail(e, "sync");
+    cwq::set_error(CWQ_OK, "");
+    return 0;
+  }
+  int64_t maxd = 0;
+  for (int64_t i = 0; i < n_items; ++i) maxd = imaxd[(size_t)i] > maxd ? imaxd[(size_t)i] : maxd;
+  if ((e = hipMemcpyAsync(offs, g_offs_host.data(), (size_t)(G + 1) * 8, hipMemcpyHostToDevice,
+                          s)) != hipSuccess)
+    return hip_fail(e, "offsets to device");
+  if ((e = hipMemcpyAsync(bseed, g_seed_host.data(), (size_t)G * 4, hipMemcpyHostToDevice, s)) !=
+      hipSuccess)
+    return hip_fail(e, "seeds to device");
+  lap("layout");
+  // :273-284 every item's groups in one launch
+  if ((rc = encode_impl(t_loc, t_scale, zeros, ones, offs, 0, G, D, maxd, n_bits_per_step,
+                        n_steps, 0, rho, 0, idx, sample, w + l.enc, workspace_bytes - l.enc, opts,
+                        stream, bseed)) < 0)
+    return rc;
+  if ((rc = cwq_destandardise(sample, p_loc, p_scale, D, out, stream)) < 0) return rc;  // :292
+  g_idx_host.resize((size_t)(G * n_steps));
+  if ((e = hipMemcpyAsync(g_idx_host.data(), idx, (size_t)(G * n_steps) * 4,
+                          hipMemcpyDeviceToHost, s)) != hipSuccess)
+    return hip_fail(e, "indices to host");
+  if ((e = hipMemcpyAsync(sample_host, out, (size_t)D * 4, hipMemcpyDeviceToHost, s)) !=
+      hipSuccess)
+    return hip_fail(e, "sample to host");
+  if ((e = hipStreamSynchronize(s)) != hipSuccess) return hip_fail(e, "sync");
+  lap("encode");
+  // :81-87, :288 the items' bitcodes at bits_off[i] (items are consecutive in
+  // the group order), items side by side on host threads as the partitions
+  {
+    std::vector<int64_t> rcs((size_t)n_items, 0);
+    const int32_t* idh = g_idx_host.data();  // thread_local: resolve here, not in the workers
+    for_items([&](int64_t i) {
+      rcs[(size_t)i] = write_bitcode(idh + gfirst[(size_t)i] * n_steps,
+                                     (gfirst[(size_t)i + 1] - gfirst[(size_t)i]) * n_steps,
+                                     n_bits_per_step, bits_host + bits_off[i]);
+    });
+    for (int64_t i = 0; i < n_items; ++i)
+      if (rcs[(size_t)i] < 0) return fail((int)rcs[(size_t)i], "index does not fit %d bits",
+                                          n_bits_per_step);
   }
   lap("bits");
   cwq::set_error(CWQ_OK, "");

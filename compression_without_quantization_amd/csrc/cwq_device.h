@@ -198,6 +198,19 @@ __device__ __forceinline__ int32_t block_seed(int32_t seed, int64_t block_id) {
   return (int32_t)((uint32_t)seed + (uint32_t)block_id);
 }
 
+// The encoders' block seeds: block g of a launch is coded with seed
+// `seed + base + g` (coded_greedy_sampler.py:282), or with per_block[g] when
+// the launch codes several independent jobs at once (a batch of images, each
+// numbering its groups from 0 with its own seed).
+struct SeedSpec {
+  int32_t seed;
+  int64_t base;
+  const int32_t* per_block;  // device [nb] or nullptr
+  __device__ __forceinline__ int32_t of(int64_t g) const {
+    return per_block ? per_block[g] : block_seed(seed, base + g);
+  }
+};
+
 __device__ __forceinline__ uint32_t ord_f32(float v) {
   const uint32_t b = f2u(v);
   return (b & 0x80000000u) ? ~b : (b | 0x80000000u);

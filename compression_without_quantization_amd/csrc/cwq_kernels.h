@@ -34,6 +34,7 @@ struct EncodeArgs {
   int32_t seed;
   float rho;
   int64_t block_id_base;
+  const int32_t* seeds;      // device [nb] per-block seeds, or nullptr: seed + block_id_base + g
   int32_t* out_idx;
   float* out_sample;
   // workspace

@@ -78,7 +78,7 @@ __global__ void __launch_bounds__(256) k_encode_eval(
     const float* __restrict__ loc_s, const float* __restrict__ scale_s,
     const float* __restrict__ lognorm, const float* __restrict__ best,
     const int64_t* __restrict__ block_off, int64_t ud, int64_t ntiles, int64_t tiles_per_block,
-    int64_t cand_per_tile, int64_t n_cand, int32_t seed, int64_t block_id_base, int32_t step,
+    int64_t cand_per_tile, int64_t n_cand, SeedSpec sd, int32_t step,
     unsigned long long* __restrict__ keys) {
   __shared__ double logtab[32];
   __shared__ unsigned long long wkey[4];
@@ -93,7 +93,7 @@ __global__ void __launch_bounds__(256) k_encode_eval(
     const int64_t n0 = tt * cand_per_tile;
     const int64_t n1 = (n0 + cand_per_tile < n_cand) ? n0 + cand_per_tile : n_cand;
     const PhiloxStream st =
-        generate_key(step_seed(block_seed(seed, block_id_base + g), step), 42);
+        generate_key(step_seed(sd.of(g), step), 42);
     const int align = (int)(((uint64_t)(n0 + wv) * (uint64_t)sp.d) & 3u);
 
     uint64_t bestk = 0;
@@ -214,8 +214,8 @@ __global__ void __launch_bounds__(256, CWQ_PRUNE_MIN_WAVES) k_encode_prune(
     const float* __restrict__ t_loc, const float* __restrict__ t_scale,
     const float* __restrict__ loc_s, const float* __restrict__ scale_s,
     const float* __restrict__ lognorm, const float* __restrict__ best, int64_t ntiles,
-    int64_t tiles_per_block, int64_t cand_per_tile, int64_t n_cand, int32_t seed,
-    int64_t block_id_base, int32_t step, int allow_screen, unsigned long long* __restrict__ keys) {
+    int64_t tiles_per_block, int64_t cand_per_tile, int64_t n_cand, SeedSpec sd, int32_t step,
+    int allow_screen, unsigned long long* __restrict__ keys) {
   static_assert(D % 8 == 0 && D >= 8 && D <= 64, "pruned path: D % 8 == 0, D <= 64");
   constexpr int G = D / 4;
   constexpr int NF = STEP0 ? 6 : 7;  // loc_s, scale_s, mu, sigma, c, 1/sigma[, best]
@@ -252,7 +252,7 @@ __global__ void __launch_bounds__(256, CWQ_PRUNE_MIN_WAVES) k_encode_prune(
     const int64_t n0 = tt * cand_per_tile;
     const int64_t n1 = (n0 + cand_per_tile < n_cand) ? n0 + cand_per_tile : n_cand;
     const PhiloxStream st =
-        generate_key(step_seed(block_seed(seed, block_id_base + g), step), 42);
+        generate_key(step_seed(sd.of(g), step), 42);
 
     // (a) expected deficit of dim j under the proposal shard:
     //     E[0.5((T - mu)/sigma)^2], T ~ N(best + loc_s, scale_s^2)
@@ -917,7 +917,7 @@ __global__ void __launch_bounds__(256, COOP ? CWQ_CSR_COOP_MIN_WAVES : CWQ_CSR_R
     const float* __restrict__ loc_s, const float* __restrict__ scale_s,
     const float* __restrict__ lognorm, const float* __restrict__ best,
     const int64_t* __restrict__ block_off, int64_t ud, int64_t ntiles, int64_t tiles_per_block,
-    int64_t cand_per_tile, int64_t n_cand, int32_t seed, int64_t block_id_base, int32_t step,
+    int64_t cand_per_tile, int64_t n_cand, SeedSpec sd, int32_t step,
     const float2* __restrict__ sab, const float* __restrict__ bpre,
     const uint32_t* __restrict__ ordu, const float4* __restrict__ grp,
     uint32_t* __restrict__ gtau, unsigned long long* __restrict__ keys, int64_t coop_min_d,
@@ -951,7 +951,7 @@ __global__ void __launch_bounds__(256, COOP ? CWQ_CSR_COOP_MIN_WAVES : CWQ_CSR_R
     const int64_t n1 = (n0 + cand_per_tile < n_cand) ? n0 + cand_per_tile : n_cand;
     if (n1 <= n0) continue;  // empty tile (the launcher sizes tiles so there are none)
     const PhiloxStream st =
-        generate_key(step_seed(block_seed(seed, block_id_base + g), step), 42);
+        generate_key(step_seed(sd.of(g), step), 42);
     const float4 gc = grp[g];
     const bool in_lds = d <= CWQ_CSR_LDS_DIMS;
     const int64_t reg = off + 12 * g, cs = csr_cls_stride(d);
@@ -1402,8 +1402,8 @@ __device__ __forceinline__ uint32_t key_index(uint64_t key) {
 
 __global__ void __launch_bounds__(256) k_encode_finalize(
     const float* __restrict__ loc_s, const float* __restrict__ scale_s,
-    const int64_t* __restrict__ block_off, int64_t ud, int64_t nb, int32_t seed,
-    int64_t block_id_base, int32_t step, int n_steps,
+    const int64_t* __restrict__ block_off, int64_t ud, int64_t nb, SeedSpec sd, int32_t step,
+    int n_steps,
     const unsigned long long* __restrict__ keys, int32_t* __restrict__ out_idx,
     float* __restrict__ out_sample) {
   __shared__ double logtab[32];
@@ -1421,7 +1421,7 @@ __global__ void __launch_bounds__(256) k_encode_finalize(
     const int64_t d = block_off ? block_off[g + 1] - off : ud;
     const uint32_t idx = key_index(keys[g]);
     const PhiloxStream st =
-        generate_key(step_seed(block_seed(seed, block_id_base + g), step), 42);
+        generate_key(step_seed(sd.of(g), step), 42);
     const uint64_t k = (uint64_t)idx * (uint64_t)d + (uint64_t)(i - off);
     const F4 z = normal4_dev(st, k >> 2, logtab);
     const uint32_t w = (uint32_t)(k & 3u);
@@ -1450,7 +1450,7 @@ __device__ __forceinline__ Q4Lane q4_lane(uint32_t qpb, uint32_t bpw) {
 
 __global__ void __launch_bounds__(256) k_encode_finalize_q4(
     const float4* __restrict__ loc_s, const float4* __restrict__ scale_s, uint32_t qpb,
-    uint32_t bpw, int64_t nb, int32_t seed, int64_t block_id_base, int32_t step, int n_steps,
+    uint32_t bpw, int64_t nb, SeedSpec sd, int32_t step, int n_steps,
     const unsigned long long* __restrict__ keys, int32_t* __restrict__ out_idx,
     float4* __restrict__ out_sample) {
   __shared__ double logtab[32];
@@ -1465,7 +1465,7 @@ __global__ void __launch_bounds__(256) k_encode_finalize_q4(
     const uint32_t idx = (key >> 32) > kArgmaxClampOrd ? argmax_key_index(key) : 0u;
     if (L.q == 0) out_idx[g * n_steps + step] = (int32_t)idx;
     const PhiloxStream st =
-        generate_key(step_seed(block_seed(seed, block_id_base + g), step), 42);
+        generate_key(step_seed(sd.of(g), step), 42);
     const F4 z = normal4_dev(st, (uint64_t)idx * qpb + L.q, logtab);
     const float4 l = loc_s[t], sc = scale_s[t];
     float4 b = out_sample[t];
@@ -1745,6 +1745,10 @@ __global__ void __launch_bounds__(256) k_selftest_div(const float* __restrict__ 
 // Host-side launchers.
 // ---------------------------------------------------------------------------
 
+static SeedSpec seeds_of(const EncodeArgs& a) {
+  return SeedSpec{a.seed, a.block_id_base, a.seeds};
+}
+
 // The float4 lane-per-Philox-block kernels: uniform d % 4 == 0, d <= 256.
 static bool q4_shape(const int64_t* block_off, int64_t ud) {
   return block_off == nullptr && ud > 0 && ud % 4 == 0 && ud <= 256;
@@ -1771,8 +1775,8 @@ static void launch_eval_t(const EncodeArgs& a, int step, hipStream_t stream) {
   const unsigned grid = (unsigned)(ntiles < (1LL << 30) ? ntiles : (1LL << 30));
   hipLaunchKernelGGL((k_encode_eval<DC, STEP0>), dim3(grid), dim3(256), 0, stream, a.t_loc,
                      a.t_scale, a.loc_s, a.scale_s, a.lognorm, a.out_sample, a.block_off, a.ud,
-                     ntiles, a.tiles_per_block, a.cand_per_tile, a.n_cand, a.seed,
-                     a.block_id_base, step, a.keys);
+                     ntiles, a.tiles_per_block, a.cand_per_tile, a.n_cand, seeds_of(a),
+                     step, a.keys);
 }
 
 template <int D, bool STEP0>
@@ -1788,7 +1792,7 @@ static void launch_prune_t(const EncodeArgs& a, int step, hipStream_t stream) {
   const unsigned grid = (unsigned)(ntiles < kPruneGrid ? ntiles : kPruneGrid);
   hipLaunchKernelGGL((k_encode_prune<D, STEP0>), dim3(grid), dim3(256), 0, stream, a.t_loc,
                      a.t_scale, a.loc_s, a.scale_s, a.lognorm, a.out_sample, ntiles,
-                     a.tiles_per_block, a.cand_per_tile, a.n_cand, a.seed, a.block_id_base, step,
+                     a.tiles_per_block, a.cand_per_tile, a.n_cand, seeds_of(a), step,
                      a.prune >= 2 ? 1 : 0, a.keys);
 }
 
@@ -1829,14 +1833,14 @@ static void launch_prune_csr(const EncodeArgs& a, int step, hipStream_t stream) 
   if (coop)
     hipLaunchKernelGGL((k_encode_prune_csr<STEP0, true>), dim3(grid), dim3(256), 0, stream,
                        a.t_loc, a.t_scale, a.loc_s, a.scale_s, a.lognorm, a.out_sample,
-                       a.block_off, a.ud, ntiles, tpb, cpt, a.n_cand, a.seed, a.block_id_base,
+                       a.block_off, a.ud, ntiles, tpb, cpt, a.n_cand, seeds_of(a),
                        step, (const float2*)a.sab, (const float*)a.bpre,
                        (const uint32_t*)a.ordu, (const float4*)a.grp, a.gtau, a.keys,
                        coop_min_d, (const float4*)a.abp);
   else
     hipLaunchKernelGGL((k_encode_prune_csr<STEP0, false>), dim3(grid), dim3(256), 0, stream,
                        a.t_loc, a.t_scale, a.loc_s, a.scale_s, a.lognorm, a.out_sample,
-                       a.block_off, a.ud, ntiles, tpb, cpt, a.n_cand, a.seed, a.block_id_base,
+                       a.block_off, a.ud, ntiles, tpb, cpt, a.n_cand, seeds_of(a),
                        step, (const float2*)a.sab, (const float*)a.bpre,
                        (const uint32_t*)a.ordu, (const float4*)a.grp, a.gtau, a.keys,
                        coop_min_d, (const float4*)a.abp);
@@ -1904,11 +1908,11 @@ static hipError_t encode_steps(const EncodeArgs& a, hipStream_t stream, bool eve
       const uint32_t qpb = (uint32_t)(a.ud / 4), bpw = 64u / qpb;
       hipLaunchKernelGGL(k_encode_finalize_q4, dim3(grid_for(a.nb, 4 * (int64_t)bpw, 1u << 20)),
                          dim3(256), 0, stream, (const float4*)a.loc_s, (const float4*)a.scale_s,
-                         qpb, bpw, a.nb, a.seed, a.block_id_base, s, a.n_steps, a.keys,
+                         qpb, bpw, a.nb, seeds_of(a), s, a.n_steps, a.keys,
                          a.out_idx, (float4*)a.out_sample);
     } else {
       hipLaunchKernelGGL(k_encode_finalize, dim3(fgrid_dims), dim3(256), 0, stream, a.loc_s,
-                         a.scale_s, a.block_off, a.ud, a.nb, a.seed, a.block_id_base, s,
+                         a.scale_s, a.block_off, a.ud, a.nb, seeds_of(a), s,
                          a.n_steps, a.keys, a.out_idx, a.out_sample);
     }
     e = hipGetLastError();
@@ -2004,6 +2008,7 @@ hipError_t launch_encode(const EncodeArgs& a, hipStream_t stream) {
     p.block_off = a.block_off + g0;
     p.nb = g1 - g0;
     p.block_id_base = a.block_id_base + g0;
+    if (a.seeds) p.seeds = a.seeds + g0;
     p.keys = a.keys + g0;
     p.out_idx = a.out_idx + g0 * a.n_steps;
     if (a.sab) p.sab = a.sab + 8 * g0;

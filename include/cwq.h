@@ -24,6 +24,7 @@
  *                                   (host-side sequential partition)
  *   cwq_code_grouped_greedy      <- code/coded_greedy_sampler.py:170-296
  *                                   (the whole grouped coder in one call)
+ *   cwq_code_grouped_greedy_batch <- the same, once per item of a batch
  *
  * Conventions
  *   - All float/index pointers are DEVICE pointers (hipMalloc / torch cuda
@@ -189,6 +190,31 @@ int64_t cwq_code_grouped_greedy(const float* q_loc, const float* q_scale, const 
                                 char* bits_host, int64_t bits_cap, int64_t* starts_host,
                                 int64_t starts_cap, double* kl_sum_out, void* workspace,
                                 size_t workspace_bytes, const cwq_options* opts, void* stream);
+
+/* A batch of independent code_grouped_greedy_sample calls (coded_greedy_sampler.py:170-296
+ * once per item: the images of a dataset, or the ladder levels of several
+ * images) in one call.  Item i is dims [item_off[i], item_off[i+1]) of the
+ * concatenated DEVICE q_* / p_* (item_off: HOST int64 [n_items + 1], item_off[0]
+ * == 0) and is coded exactly as cwq_code_grouped_greedy on that slice with seed
+ * seeds[i] (HOST int32 [n_items]): its own partition (:207-252), its groups
+ * numbered from 0 and coded with seeds[i] + g (:273-284).  One standardisation,
+ * one KL copy, ONE encode launch over every item's groups (per-block seeds) and
+ * one destandardisation serve all items; the host partitions and bitcodes of
+ * the items run on up to 8 host threads.  HOST outputs: sample_host
+ * [D_total]; item i's bitcode at bits_host[bits_off[i], bits_off[i+1])
+ * (bits_off: HOST int64 [n_items + 1], written); item i's group_start_indices
+ * (local, incl. its trailing D_i): n_starts[i] entries (HOST int64 [n_items],
+ * written) at starts_host + item_off[i] + 2 i (starts_cap >= D_total + 2
+ * n_items).  Returns the total number of groups, or a negative error code.
+ * Synchronises twice. */
+size_t cwq_code_grouped_greedy_batch_workspace_size(int64_t D_total, int n_steps);
+int64_t cwq_code_grouped_greedy_batch(
+    int64_t n_items, const int64_t* item_off, const float* q_loc, const float* q_scale,
+    const float* p_loc, const float* p_scale, int n_steps, int n_bits_per_step,
+    const int32_t* seeds, float rho, int64_t size_threshold, double n_nats, float* sample_host,
+    char* bits_host, int64_t bits_cap, int64_t* bits_off, int64_t* starts_host,
+    int64_t starts_cap, int64_t* n_starts, void* workspace, size_t workspace_bytes,
+    const cwq_options* opts, void* stream);
 
 /* ---- Importance sampler (code/coded_importance_sampler.py) ------------- */
 /* Workspace bytes for cwq_importance_encode. */

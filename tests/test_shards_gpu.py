@@ -177,6 +177,58 @@ def test_c3_image_set(cwq, oracle):
                 assert np.array_equal(_u32(sample), _u32(ws)), f"image {i} level {li} sample"
 
 
+def test_c3_batch_equals_per_image_calls(cwq):
+    """code_grouped_greedy_sample_batch over C3's 48 latent sets (24 images x 2
+    levels, one encode launch over every image's groups with per-group seeds)
+    equals 48 code_grouped_greedy_sample calls: groups, bitcode, sample bits."""
+    from compression_without_quantization_amd.synthetic import make_latents
+    cwq.coded_greedy_sampler.VERBOSE = False
+    tg, pr = [], []
+    for i in range(24):
+        for li, D in enumerate((32 * 48 * 128, 8 * 12 * 24)):
+            q_loc, q_scale, p_loc, p_scale = make_latents(D, seed=1000 * i + li)
+            tg.append(cwq.Normal(q_loc, q_scale))
+            pr.append(cwq.Normal(p_loc, p_scale))
+    got = cwq.code_grouped_greedy_sample_batch(None, tg, pr, 1, 8, 42)
+    assert len(got) == 48
+    for k in (0, 1, 2, 17, 46, 47):
+        sample, bitcode, starts = cwq.code_grouped_greedy_sample(None, tg[k], pr[k], 1, 8, 42)
+        bs, bb, bst = got[k]
+        assert isinstance(bst, np.ndarray) and bst.tolist() == starts, k
+        assert bb == bitcode, k
+        assert np.array_equal(_u32(bs), _u32(sample)), k
+
+
+@pytest.mark.parametrize("sizes,seeds,bits,n_steps", [
+    ([3000, 1, 20000, 257, 4096], [42, -7, 2 ** 31 - 3, 0, -2 ** 31], 8, 1),
+    ([5000, 300, 6000], [1, 2, 3], 14, 3),   # multi-step: the forked stream parts
+    ([2, 1, 3], 9, 6, 2),                    # tiny items, one seed for all
+])
+def test_grouped_batch_equals_single_calls(cwq, sizes, seeds, bits, n_steps):
+    """Per-item seeds (int32 wrap-around included), items of 1 dim, and
+    multi-step batches whose launch forks onto the library streams: each item's
+    result equals code_grouped_greedy_sample on that item alone."""
+    cwq.coded_greedy_sampler.VERBOSE = False
+    rng = np.random.default_rng(sum(sizes) + bits)
+    tg, pr = [], []
+    for D in sizes:
+        pl = (0.1 * rng.standard_normal(D)).astype(np.float32)
+        ps = rng.uniform(0.8, 1.2, D).astype(np.float32)
+        ql = (pl + ps * rng.standard_normal(D) * 0.7).astype(np.float32)
+        qs = (ps * rng.uniform(0.3, 1.0, D)).astype(np.float32)
+        tg.append(cwq.Normal(torch.from_numpy(ql).cuda(), torch.from_numpy(qs).cuda()))
+        pr.append(cwq.Normal(torch.from_numpy(pl).cuda(), torch.from_numpy(ps).cuda()))
+    got = cwq.code_grouped_greedy_sample_batch(None, tg, pr, n_steps, bits, seeds)
+    sl = seeds if isinstance(seeds, list) else [seeds] * len(sizes)
+    for k in range(len(sizes)):
+        sample, bitcode, starts = cwq.code_grouped_greedy_sample(None, tg[k], pr[k], n_steps,
+                                                                 bits, sl[k])
+        bs, bb, bst = got[k]
+        assert isinstance(bst, np.ndarray) and bst.tolist() == starts, k
+        assert bb == bitcode, k
+        assert np.array_equal(_u32(bs), _u32(sample)), k
+
+
 def _bench(args, timeout=300):
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
     r = subprocess.run([sys.executable, "-u", os.path.join(REPO, "bench.py")] + args,
