@@ -1931,7 +1931,7 @@ static hipError_t encode_steps(const EncodeArgs& a, hipStream_t stream, bool eve
 #define CWQ_ENCODE_SPLIT 3  // most parts a multi-step CSR encode forks into
 #endif
 namespace {
-constexpr int kMaxSplit = 3;
+constexpr int kMaxSplit = CWQ_ENCODE_SPLIT > 3 ? CWQ_ENCODE_SPLIT : 3;
 constexpr int kMaxDevices = 16;
 struct ForkStreams {
   bool ok = false;
@@ -1996,7 +1996,10 @@ hipError_t launch_encode(const EncodeArgs& a, hipStream_t stream) {
   // long rows (the cooperative mode) overlap best in three parts, others in two
   // (tools/stream_overlap.py).
   const bool few_rows = a.nb * a.n_cand < (int64_t)CWQ_CSR_COOP_ROWS_PER_LANE * 1536 * 256;
-  int k = few_rows ? 3 : 2;
+#ifndef CWQ_SPLIT_FEW
+#define CWQ_SPLIT_FEW 3  // parts of a cooperative (few long rows) launch
+#endif
+  int k = few_rows ? CWQ_SPLIT_FEW : 2;
   k = k < CWQ_ENCODE_SPLIT ? k : CWQ_ENCODE_SPLIT;
   k = (int64_t)k < a.nb ? k : (int)a.nb;
   if (a.ev_start && (e = hipEventRecord((hipEvent_t)a.ev_start, stream)) != hipSuccess) return e;

@@ -39,6 +39,11 @@ declare -A V=(
   [upl2w5]="-DCWQ_COOP_UPL=2 -DCWQ_CSR_COOP_MIN_WAVES=5"
   [upl2pfw4]="-DCWQ_COOP_UPL=2 -DCWQ_COOP_REC_PREFETCH=1 -DCWQ_CSR_COOP_MIN_WAVES=4"
   [head]=prebuilt
+  [sf2]="-DCWQ_SPLIT_FEW=2"
+  [sf4]="-DCWQ_SPLIT_FEW=4 -DCWQ_ENCODE_SPLIT=4"
+  [ct3k]="-DCWQ_CSR_COOP_TILES=3072"
+  [ct12k]="-DCWQ_CSR_COOP_TILES=12288"
+  [ct256]="-DCWQ_CSR_COOP_TILE=256"
   [r3w5]="-DCWQ_RUN_UPL=3 -DCWQ_CSR_RUN_MIN_WAVES=5"
   [r4w4]="-DCWQ_RUN_UPL=4 -DCWQ_CSR_RUN_MIN_WAVES=4"
   [r2w5]="-DCWQ_RUN_UPL=2 -DCWQ_CSR_RUN_MIN_WAVES=5"
