@@ -43,14 +43,15 @@ int hip_fail(hipError_t e, const char* where) {
 size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
 
 struct WsLayout {
-  size_t keys, loc_s, scale_s, lognorm, sab, bpre, ordu, grp, gtau, abp, total;
+  size_t keys, loc_s, scale_s, lognorm, sab, bpre, ordu, grp, gtau, abp, slist, total;
   bool csr;   // has the general pruned kernel's arrays
   bool recs;  // ... and the visit-order records of blocks longer than CWQ_CSR_LDS_DIMS
 };
 
 // Blocks the uniform fast pruned kernel takes (d % 8 == 0, 8 <= d <= 64) need
 // only keys + the per-dim shard constants; everything else (CSR, other d) also
-// gets the general pruned kernel's screening constants (16 B/dim + 180 B/block),
+// gets the general pruned kernel's screening constants and the screened small-candidate
+// path's survivor slots (16 B/dim + 244 B/block),
 // and, when some block may exceed CWQ_CSR_LDS_DIMS dims, its visit-order
 // records (32 B/dim + 384 B/block).
 bool uniform_fast(int64_t d) { return d % 8 == 0 && d >= 8 && d <= 64; }
@@ -68,8 +69,10 @@ WsLayout ws_layout(int64_t nb, int64_t total_dims, bool csr, bool recs) {
   o = align_up(o + (size_t)total_dims * 4, 256);
   l.csr = csr;
   l.recs = csr && recs;
-  l.sab = l.bpre = l.ordu = l.grp = l.gtau = l.abp = o;
+  l.sab = l.bpre = l.ordu = l.grp = l.gtau = l.abp = l.slist = o;
   if (csr) {
+    l.slist = o;  // the screened small-candidate path's survivor slots (8 B each)
+    o = align_up(o + (size_t)nb * CWQ_SLIST_PER_BLOCK * 8, 256);
     l.sab = o;
     o = align_up(o + (size_t)(total_dims + 8 * nb) * 8, 256);
     l.bpre = o;
@@ -369,6 +372,7 @@ int encode_impl(const float* t_loc, const float* t_scale, const float* p_loc,
 #else
   a.abp = l.recs ? (float4*)(w + l.abp) : nullptr;
 #endif
+  a.slist = l.csr ? (uint2*)(w + l.slist) : nullptr;
   a.ev_start = o.eval_start_event;
   a.ev_stop = o.eval_stop_event;
   hipError_t e = cwq::launch_encode(a, (hipStream_t)stream);

@@ -21,6 +21,20 @@ __device__ __forceinline__ uint32_t wave_id() {
   return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
 }
 
+__device__ __forceinline__ double wave_sum_f64(double v) {  // full exec mask
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+__device__ __forceinline__ double wave_max_f64(double v) {  // full exec mask
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) {
+    const double o = __shfl_xor(v, off, 64);
+    v = o > v ? o : v;
+  }
+  return v;
+}
+
 __device__ __forceinline__ uint64_t wave_max_u64(uint64_t v) {
 #pragma unroll
   for (int off = 32; off >= 1; off >>= 1) {

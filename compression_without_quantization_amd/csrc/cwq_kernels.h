@@ -51,10 +51,15 @@ struct EncodeArgs {
   uint32_t* gtau;            // [nb] per-block shared threshold (ord)
   float4* abp;               // [2 (total_dims + 12 nb)] visit-order (sa, sb) records of the
                              // blocks longer than CWQ_CSR_LDS_DIMS; nullptr if none are
+  uint2* slist;              // screened small-candidate path: CWQ_SLIST_PER_BLOCK
+                             // (row, upper bits) survivor slots per block; the
+                             // per-block counts live in ordu[off + 12 g]
   // optional profiling events around the eval launches (hipEvent_t)
   void* ev_start;
   void* ev_stop;
 };
+
+#define CWQ_SLIST_PER_BLOCK 8
 
 hipError_t launch_encode(const EncodeArgs& a, hipStream_t stream);
 hipError_t launch_decode(const int32_t* idx, const float* p_loc, const float* p_scale,

@@ -1375,6 +1375,259 @@ __global__ void __launch_bounds__(256, COOP ? CWQ_CSR_COOP_MIN_WAVES : CWQ_CSR_R
 }
 
 // ---------------------------------------------------------------------------
+// Screened encoder for few candidates (64 <= 2^b < 4096, CSR or uniform d the
+// fast kernel does not take): C2/C3's 8-bit groups of ~5 dims.  Every
+// candidate is screened -- k_csr_prep's bound with the row summed
+// sequentially in natural order, no pruning -- and only survivors are scored
+// exactly, densely, in a separate pass:
+//   k_small_prep      per block (a lane each for short blocks): per-dim (sA, sB)
+//                     into sab, the block's (c1, c2, As, Pq) into grp (c1 == 0:
+//                     the block is scored exactly), its full-row bound B and
+//                     stream key into bpre[off + 12 g ...]; gtau = -inf; the
+//                     survivor count = 0.
+//   k_small_screen    a wave per tile, its rows n = r (mod 4) one alignment
+//                     class at a time: screened value s of each row; tau = the wave's
+//                     best lower bound fma(s, c2, As) - Pq sqrt(-s); rows whose
+//                     upper bound fma(s, c1, B) reaches tau take one of the
+//                     block's CWQ_SLIST_PER_BLOCK slots; tau is published to
+//                     gtau[g].  Full slots mark the block exact.
+//   k_small_survivors listed rows still reaching gtau[g], scored exactly one
+//                     per lane; then every candidate of the blocks marked exact.
+// The exact pass costs about 3x a screened row (f64 Box-Muller against the
+// hardware transcendentals); survivors are ~1 per block, so the step costs
+// about a third of scoring every candidate exactly.
+// ---------------------------------------------------------------------------
+#ifndef CWQ_SMALL_MIN_CAND
+#define CWQ_SMALL_MIN_CAND 64  // fewer candidates: the exact kernel (screening would not pay)
+#endif
+
+// A wave prepares 64 consecutive blocks: lane i block i when it has at most
+// kSmallLaneD dims (C2's groups: ~5), sequentially; longer blocks afterwards
+// with the whole wave, lanes over dims.  The block's stream key for this step
+// (a Philox-10 call) is stored too, so the screening rows do not repeat it.
+constexpr int64_t kSmallLaneD = 32;
+
+template <bool STEP0>
+__global__ void __launch_bounds__(256) k_small_prep(
+    const float* __restrict__ t_loc, const float* __restrict__ t_scale,
+    const float* __restrict__ loc_s, const float* __restrict__ scale_s,
+    const float* __restrict__ lognorm, const float* __restrict__ best,
+    const int64_t* __restrict__ block_off, int64_t ud, int64_t nb, SeedSpec sd, int32_t step,
+    float2* __restrict__ sab, float* __restrict__ bpre, float4* __restrict__ grp,
+    uint32_t* __restrict__ gtau, uint32_t* __restrict__ scnt) {
+  const uint32_t lane = threadIdx.x & 63u;
+  const int64_t nwaves = (int64_t)gridDim.x * 4;
+  struct Sums {
+    double sm = 0.0, sa = 0.0, sk = 0.0, s2 = 0.0, cs = 0.0, mx = 0.0;
+    int ok = 1;
+  };
+  auto dim = [&](Sums& u, int64_t off, int64_t g, int64_t j) {
+    const CsrDim o = csr_dim<STEP0>(loc_s[off + j], scale_s[off + j], t_loc[off + j],
+                                    t_scale[off + j], lognorm[off + j],
+                                    STEP0 ? 0.0f : best[off + j]);
+    sab[off + 8 * g + 4 + j] = float2{o.sa, o.sb};  // k_csr_prep's padded layout
+    u.sm += o.M;
+    u.sa += __builtin_fabs(o.M);
+    u.sk += __builtin_fabs(o.M) + o.M;
+    u.s2 += (double)o.A * (double)o.A;
+    u.cs += (double)o.C;
+    u.mx = (double)o.A > u.mx ? (double)o.A : u.mx;
+    u.ok &= o.ok ? 1 : 0;
+  };
+  // as k_csr_prep: gamma at the larger depth of the two float sums, the
+  // screening sum (sequential over the row here: h = d) and the exact
+  // Eigen-order row value (h <= d/8 + 8)
+  auto finish = [&](const Sums& u, int64_t off, int64_t g, int64_t d) {
+    const double h_s = (double)d, h_e = (double)d / 8.0 + 8.0;
+    const double gam = 1.01 * ((h_s > h_e ? h_s : h_e) + 1.0) * 0x1p-24;
+    const double sl = (3.0 * gam + 0x1p-20) * (__builtin_fabs(u.sm) + u.sa + u.sk) + 0x1p-126;
+    const float bf = round_up_f32(u.sm + u.cs * (1.0 + 0x1p-20) + sl);
+    const float c1 = round_dn_f32(1.0 - 3.0 * gam - 0x1p-22);
+    const float c2 = round_up_f32(1.0 + 3.0 * gam + 0x1p-14);
+    const float as = round_dn_f32(u.sm - sl - 1.01 * u.s2 * (1.0 + 0x1p-11));
+    const float pq = round_up_f32(2.01 * u.mx * __builtin_sqrt((double)(d > 0 ? d : 1)) *
+                                  (1.0 + 0x1p-11));
+    const bool fin = as - as == 0.0f && pq - pq == 0.0f && bf - bf == 0.0f;
+    grp[g] = (u.ok && fin && d > 0) ? float4{c1, c2, as, pq} : float4{0.f, 0.f, 0.f, 0.f};
+    float* bg = bpre + off + 12 * g;  // [0] the full-row bound, [1..4] the stream key
+    bg[0] = bf;
+    const PhiloxStream st = generate_key(step_seed(sd.of(g), step), 42);
+    bg[1] = u2f(st.k0);
+    bg[2] = u2f(st.k1);
+    bg[3] = u2f(st.c2);
+    bg[4] = u2f(st.c3);
+    scnt[off + 12 * g] = 0u;
+    gtau[g * CWQ_CSR_GTAU_STRIDE] = ord_f32(-__builtin_inff());
+  };
+  for (int64_t gb = ((int64_t)blockIdx.x * 4 + wave_id()) * 64; gb < nb; gb += nwaves * 64) {
+    const int64_t g = gb + lane;
+    bool longb = false;
+    if (g < nb) {
+      const BlockSpan sp = block_span(block_off, ud, g);
+      if (sp.d <= kSmallLaneD) {
+        Sums u;
+        for (int64_t j = 0; j < sp.d; ++j) dim(u, sp.off, g, j);
+        finish(u, sp.off, g, sp.d);
+      } else {
+        longb = true;
+      }
+    }
+    for (uint64_t m = __ballot(longb); m != 0ull; m &= m - 1ull) {  // the long blocks, a wave each
+      const int64_t gl = gb + (int64_t)__builtin_ctzll(m);
+      const BlockSpan sp = block_span(block_off, ud, gl);
+      Sums u;
+      for (int64_t j = lane; j < sp.d; j += 64) dim(u, sp.off, gl, j);
+      const bool all_ok = __ballot(u.ok == 0) == 0ull;
+      u.sm = wave_sum_f64(u.sm);
+      u.sa = wave_sum_f64(u.sa);
+      u.sk = wave_sum_f64(u.sk);
+      u.s2 = wave_sum_f64(u.s2);
+      u.cs = wave_sum_f64(u.cs);
+      u.mx = wave_max_f64(u.mx);
+      u.ok = all_ok ? 1 : 0;
+      if (lane == 0) finish(u, sp.off, gl, sp.d);
+    }
+  }
+}
+
+template <bool STEP0>
+__global__ void __launch_bounds__(256) k_small_screen(
+    const int64_t* __restrict__ block_off, int64_t ud, int64_t ntiles, int64_t tiles_per_block,
+    int64_t cand_per_tile, int64_t n_cand, SeedSpec sd, int32_t step,
+    const float2* __restrict__ sab, const float* __restrict__ bpre, float4* __restrict__ grp,
+    uint32_t* __restrict__ gtau, uint32_t* __restrict__ scnt, uint2* __restrict__ slist) {
+  const uint32_t lane = threadIdx.x & 63u;
+  const int64_t nwaves = (int64_t)gridDim.x * 4;
+  // a wave takes a whole tile, its four alignment classes r = n mod 4 one
+  // after the other (the block's loads, key and threshold once per tile)
+  for (int64_t tile = (int64_t)blockIdx.x * 4 + wave_id(); tile < ntiles; tile += nwaves) {
+    const int64_t g = tiles_per_block == 1 ? tile : tile / tiles_per_block;
+    const int64_t tt = tile - g * tiles_per_block;
+    const float4 gc = grp[g];
+    if (gc.x == 0.0f) continue;  // scored exactly by k_small_survivors
+    const BlockSpan sp = block_span(block_off, ud, g);
+    const int64_t off = sp.off;
+    const int d = (int)sp.d;
+    const int64_t n0 = tt * cand_per_tile;
+    const int64_t n1 = (n0 + cand_per_tile < n_cand) ? n0 + cand_per_tile : n_cand;
+    const float* bg = bpre + off + 12 * g;  // k_small_prep: bound, then the stream key
+    const float bf = bg[0];
+    const PhiloxStream st{f2u(bg[1]), f2u(bg[2]), f2u(bg[3]), f2u(bg[4])};
+    const float2* ab = sab + off + 8 * g + 4;
+    float tau = unord_f32(__hip_atomic_load(&gtau[g * CWQ_CSR_GTAU_STRIDE], __ATOMIC_RELAXED,
+                                            __HIP_MEMORY_SCOPE_AGENT));
+    // rows n0 + r + 4 lane + 256 k: the same (r, k) for every lane
+    // (wave-uniform trip counts), so tau is shared through the wave after
+    // each round, and n d mod 4 is the same in every lane
+    for (int64_t r = 0; r < 4 && n0 + r < n1; ++r)
+    for (int64_t k = 0, rounds = (n1 - n0 - r + 255) / 256; k < rounds; ++k) {
+      const int64_t n = n0 + r + 4 * (int64_t)lane + 256 * k;
+      const bool valid = n < n1;
+      float s = 0.0f;
+      if (valid) {
+        const uint64_t k0 = (uint64_t)n * (uint64_t)d;
+        F4 z = {0.f, 0.f, 0.f, 0.f};
+        for (int j = 0; j < d; ++j) {  // natural order, sequential sum (h = d)
+          const uint64_t kk = k0 + (uint64_t)j;
+          const int w = (int)(kk & 3u);  // wave-uniform: n = r (mod 4) for every lane
+          if (w == 0 || j == 0) {
+            const uint64_t blk = kk >> 2;
+            const U4 x = philox10_dev((uint32_t)blk, (uint32_t)(blk >> 32), st.c2, st.c3, st.k0,
+                                      st.k1);
+            box_muller_screen(x.x, x.y, z.a, z.b);
+            box_muller_screen(x.z, x.w, z.c, z.d);
+          }
+          const float zz = w == 0 ? z.a : (w == 1 ? z.b : (w == 2 ? z.c : z.d));
+          const float2 e = ab[j];
+          const float a = __builtin_fmaf(e.x, zz, e.y);
+          s = __builtin_fmaf(-a, a, s);
+        }
+      }
+      const float upper = __builtin_fmaf(s, gc.x, bf);
+      const float lower = valid ? __builtin_fmaf(s, gc.y, gc.z) - gc.w * __builtin_amdgcn_sqrtf(-s)
+                                : -__builtin_inff();
+      tau = fmaxf(tau, wave_max_f32(lower));
+      const bool push = valid && upper >= tau;
+      const uint64_t m = __ballot(push);
+      if (m) {
+        const uint32_t cnt = (uint32_t)__builtin_popcountll(m);
+        // the block's own slots (a global counter serialised every wave)
+        uint32_t base = 0;
+        if (lane == 0) base = atomicAdd(&scnt[off + 12 * g], cnt);
+        base = (uint32_t)__shfl((int)base, 0, 64);
+        const uint32_t rank = __builtin_amdgcn_mbcnt_hi(
+            (uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+        if (push) {
+          const uint32_t slot = base + rank;
+          if (slot < CWQ_SLIST_PER_BLOCK)
+            slist[CWQ_SLIST_PER_BLOCK * g + slot] = uint2{(uint32_t)n, f2u(upper)};
+        }
+        if (base + cnt > CWQ_SLIST_PER_BLOCK && lane == 0)  // slots full: score the block exactly
+          __hip_atomic_store(reinterpret_cast<uint32_t*>(&grp[g].x), 0u, __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+    if (lane == 0) atomicMax(&gtau[g * CWQ_CSR_GTAU_STRIDE], ord_f32(tau));
+  }
+}
+
+template <bool STEP0>
+__global__ void __launch_bounds__(256) k_small_survivors(
+    const float* __restrict__ t_loc, const float* __restrict__ t_scale,
+    const float* __restrict__ loc_s, const float* __restrict__ scale_s,
+    const float* __restrict__ lognorm, const float* __restrict__ best,
+    const int64_t* __restrict__ block_off, int64_t ud, int64_t nb, int64_t n_cand, SeedSpec sd,
+    int32_t step, const float4* __restrict__ grp, const uint32_t* __restrict__ gtau,
+    const uint32_t* __restrict__ scnt, const uint2* __restrict__ slist,
+    unsigned long long* __restrict__ keys) {
+  __shared__ double logtab[32];
+  fill_logtab(logtab);
+  const uint32_t lane = threadIdx.x & 63u;
+  const int64_t nthr = (int64_t)gridDim.x * blockDim.x;
+  // listed rows, one slot per thread (blocks and alignments differ from lane
+  // to lane)
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+       i < CWQ_SLIST_PER_BLOCK * nb; i += nthr) {
+    const int64_t g = i / CWQ_SLIST_PER_BLOCK;
+    const uint32_t slot = (uint32_t)(i - g * CWQ_SLIST_PER_BLOCK);
+    if (grp[g].x == 0.0f) continue;  // scored exactly below
+    const BlockSpan sp = block_span(block_off, ud, g);
+    if (slot >= scnt[sp.off + 12 * g]) continue;
+    const uint2 e = slist[i];
+    const int64_t n = (int64_t)e.x;
+    if (u2f(e.y) < unord_f32(gtau[g * CWQ_CSR_GTAU_STRIDE])) continue;
+    const PhiloxStream st = generate_key(step_seed(sd.of(g), step), 42);
+    const float v = eval_row<0, STEP0>(st, (uint64_t)n * (uint64_t)sp.d, sp.d,
+                                       (int)(((uint64_t)n * (uint64_t)sp.d) & 3u),
+                                       loc_s + sp.off, scale_s + sp.off, t_loc + sp.off,
+                                       t_scale + sp.off, lognorm + sp.off,
+                                       STEP0 ? nullptr : best + sp.off, logtab);
+    atomicMax(&keys[g], (unsigned long long)argmax_key(v, (uint32_t)n));
+  }
+  // blocks whose constants failed the gate, or whose survivors overflowed
+  const int64_t nwaves = (int64_t)gridDim.x * 4;
+  for (int64_t g = (int64_t)blockIdx.x * 4 + wave_id(); g < nb; g += nwaves) {
+    if (grp[g].x != 0.0f) continue;
+    const BlockSpan sp = block_span(block_off, ud, g);
+    const PhiloxStream st = generate_key(step_seed(sd.of(g), step), 42);
+    uint64_t bestk = 0;
+    for (int r = 0; r < 4; ++r) {  // rows n = r (mod 4): one alignment class per pass
+      const int align = (int)(((uint64_t)r * (uint64_t)sp.d) & 3u);
+      for (int64_t n = r + 4 * (int64_t)lane; n < n_cand; n += 256) {
+        const float v = eval_row<0, STEP0>(st, (uint64_t)n * (uint64_t)sp.d, sp.d, align,
+                                           loc_s + sp.off, scale_s + sp.off, t_loc + sp.off,
+                                           t_scale + sp.off, lognorm + sp.off,
+                                           STEP0 ? nullptr : best + sp.off, logtab);
+        const uint64_t k = argmax_key(v, (uint32_t)n);
+        bestk = k > bestk ? k : bestk;
+      }
+    }
+    bestk = wave_max_u64(bestk);
+    if (lane == 0 && bestk) atomicMax(&keys[g], (unsigned long long)bestk);
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Encoder, end of a step: index -> out_idx; best += winning candidate (:63).
 // General shapes (CSR groups, uniform d the float4 kernel does not take): one
 // thread per flat dim i, which finds its block by binary search in block_off
@@ -1847,6 +2100,25 @@ static void launch_prune_csr(const EncodeArgs& a, int step, hipStream_t stream) 
 }
 
 template <bool STEP0>
+static void launch_small(const EncodeArgs& a, int step, hipStream_t stream) {
+  const int64_t ntiles = a.nb * a.tiles_per_block;
+  hipLaunchKernelGGL((k_small_prep<STEP0>), dim3(grid_for(a.nb, 4 * 64, 16384)), dim3(256), 0,
+                     stream, a.t_loc, a.t_scale, a.loc_s, a.scale_s, a.lognorm, a.out_sample,
+                     a.block_off, a.ud, a.nb, seeds_of(a), step, a.sab, a.bpre, a.grp, a.gtau,
+                     a.ordu);
+  hipLaunchKernelGGL((k_small_screen<STEP0>), dim3(grid_for(ntiles, 4, 1u << 20)),
+                     dim3(256), 0, stream, a.block_off, a.ud, ntiles, a.tiles_per_block,
+                     a.cand_per_tile, a.n_cand, seeds_of(a), step, (const float2*)a.sab,
+                     (const float*)a.bpre, a.grp, a.gtau, a.ordu, a.slist);
+  hipLaunchKernelGGL((k_small_survivors<STEP0>), dim3(grid_for(CWQ_SLIST_PER_BLOCK * a.nb, 256,
+                                                               4096)),
+                     dim3(256), 0, stream, a.t_loc, a.t_scale, a.loc_s, a.scale_s, a.lognorm,
+                     a.out_sample, a.block_off, a.ud, a.nb, a.n_cand, seeds_of(a), step,
+                     (const float4*)a.grp, (const uint32_t*)a.gtau, (const uint32_t*)a.ordu,
+                     (const uint2*)a.slist, a.keys);
+}
+
+template <bool STEP0>
 static void launch_eval_dc(const EncodeArgs& a, int step, hipStream_t stream) {
   // pruned path: uniform D % 8 == 0, D <= 64, Philox block index n*D/4 < 2^32
   if (a.block_off == nullptr && a.prune && a.ud % 8 == 0 && a.ud >= 8 && a.ud <= 64 &&
@@ -1866,6 +2138,10 @@ static void launch_eval_dc(const EncodeArgs& a, int step, hipStream_t stream) {
   // general pruned path (screening): CSR or other uniform d, >= 4096 candidates
   if (a.prune >= 2 && a.sab != nullptr && a.n_cand >= 4096)
     return launch_prune_csr<STEP0>(a, step, stream);
+  // screened small-candidate path (k_small_*): few candidates per block
+  if (a.prune >= 2 && a.sab != nullptr && a.slist != nullptr && a.ordu != nullptr &&
+      a.n_cand >= CWQ_SMALL_MIN_CAND)
+    return launch_small<STEP0>(a, step, stream);
   if (a.block_off == nullptr) {
     switch (a.ud) {
       case 8: return launch_eval_t<8, STEP0>(a, step, stream);
@@ -2020,6 +2296,7 @@ hipError_t launch_encode(const EncodeArgs& a, hipStream_t stream) {
     if (a.grp) p.grp = a.grp + g0;
     if (a.gtau) p.gtau = a.gtau + g0 * CWQ_CSR_GTAU_STRIDE;
     if (a.abp) p.abp = a.abp + 2 * 12 * g0;
+    if (a.slist) p.slist = a.slist + CWQ_SLIST_PER_BLOCK * g0;
     if ((e = hipStreamWaitEvent(f->s[i], f->fork, 0)) != hipSuccess) break;
     forked = i + 1;
     e = encode_steps(p, f->s[i], false);

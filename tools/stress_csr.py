@@ -7,7 +7,7 @@ constants read from global memory (d > 1024), the 2- and 3-stream step splits,
 near-tie (low-rate) inputs, per-lane rows of long groups (constants in global
 memory) and groups past the sorted-order limit (8189 dims).  Prints one line per trial; exits 1 on a mismatch.
 
-Usage: python tools/stress_csr.py [trials] [first_seed] [max_seconds]
+Usage: [STRESS_BITS=lo,hi] python tools/stress_csr.py [trials] [first_seed] [max_seconds]
 """
 import os
 import sys
@@ -42,6 +42,9 @@ def inputs(rng, n, kind):
 
 
 VERBOSE = bool(os.environ.get("STRESS_VERBOSE"))
+# bits per step drawn from [BITS_LO, BITS_HI]: 12-16 reach the general pruned
+# kernel (>= 4096 candidates); STRESS_BITS=6,11 the screened small-candidate path
+BITS_LO, BITS_HI = (int(v) for v in os.environ.get("STRESS_BITS", "12,16").split(","))
 
 
 def encode(lib, tl, ts, pl, ps, off, bits, n_steps, seed, rho, mode):
@@ -86,7 +89,7 @@ def main():
             sizes[0] = 1
         off = np.concatenate([[0], np.cumsum(sizes)]).astype(np.int64)
         D = int(off[-1])
-        bits = int(rng.integers(12, 17))
+        bits = int(rng.integers(BITS_LO, BITS_HI + 1))
         n_steps = int(rng.integers(1, 4))
         rho = float(rng.choice([1.0, 0.7, 1.3]))
         seed = int(rng.integers(-2 ** 31, 2 ** 31 - 1))
