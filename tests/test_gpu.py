@@ -660,6 +660,52 @@ def test_csr_pruned_adversarial(cwq, cwqlib, oracle, kind):
         _assert_bits_equal(gs, ws, f"csr {kind} mode {mode}")
 
 
+@pytest.mark.parametrize("kind", ["normal", "far_locs", "huge_locs", "tiny_locs", "flat",
+                                  "posterior_is_prior", "inf_scale", "zero_scale", "nan_scale",
+                                  "nan_loc_one_dim"])
+@pytest.mark.parametrize("bits,n_steps", [(6, 1), (8, 2), (11, 1)])
+def test_small_path_adversarial(cwq, cwqlib, oracle, kind, bits, n_steps):
+    """The screened small-candidate path (64 <= 2^b < 4096) on
+    ragged groups (an empty one included): near-ties everywhere overflow the
+    per-block survivor slots (exact fallback), non-finite or out-of-range
+    constants fail the gate (exact fallback); every mode equals the oracle."""
+    rng = np.random.default_rng(sum(map(ord, kind)) + bits)
+    sizes = [3, 20, 1, 45, 0, 7, 64, 130]
+    off = np.concatenate([[0], np.cumsum(sizes)]).astype(np.int64)
+    D = int(off[-1])
+    pl = (0.2 * rng.standard_normal(D)).astype(np.float32)
+    ps = rng.uniform(0.5, 2.0, D).astype(np.float32)
+    tl = (pl + ps * rng.standard_normal(D) * 0.8).astype(np.float32)
+    ts = (ps * rng.uniform(0.3, 1.0, D)).astype(np.float32)
+    if kind == "far_locs":
+        tl = (rng.standard_normal(D) * 40).astype(np.float32)
+    elif kind == "huge_locs":
+        tl = (rng.standard_normal(D) * 1e30).astype(np.float32)
+        pl = (rng.standard_normal(D) * 1e30).astype(np.float32)
+    elif kind == "tiny_locs":
+        ts = (rng.uniform(0.3, 1.0, D) * 1e-20).astype(np.float32)
+        tl = (rng.standard_normal(D) * 1e-20).astype(np.float32)
+    elif kind == "flat":
+        ts = np.full(D, 1e3, np.float32)
+        tl = np.zeros(D, np.float32)
+    elif kind == "posterior_is_prior":
+        tl, ts = pl.copy(), ps.copy()
+    elif kind == "inf_scale":
+        ts[5] = np.inf
+    elif kind == "zero_scale":
+        ts[30] = 0.0
+        tl[30] = pl[30]
+    elif kind == "nan_scale":
+        ts[:] = np.nan
+    elif kind == "nan_loc_one_dim":
+        tl[40] = np.nan
+    wi, ws = oracle.greedy_encode(tl, ts, pl, ps, off, bits, n_steps, 5)
+    for mode in (0, 2):
+        gi, gs = _csr_encode(cwq, cwqlib, tl, ts, pl, ps, off, bits, n_steps, 5, 1.0, mode)
+        assert np.array_equal(gi, wi), (kind, bits, mode)
+        _assert_bits_equal(gs, ws, f"small path {kind} bits {bits} mode {mode}")
+
+
 @pytest.mark.parametrize("trial", range(12))
 def test_csr_random_stress(cwq, cwqlib, trial):
     """Random ragged layouts (empty groups included) and odd uniform d, heavy-
