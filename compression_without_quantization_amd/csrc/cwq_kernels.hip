@@ -1789,7 +1789,10 @@ __global__ void __launch_bounds__(256) k_decode(
 // pays one key call per block instead of one per lane.  The next chunk's
 // inputs are loaded before the current chunk's arithmetic, so HBM reads stay
 // in flight while the exact Box-Muller runs.
-__global__ void __launch_bounds__(256) k_decode_q4(
+#ifndef CWQ_DECODE_MIN_WAVES
+#define CWQ_DECODE_MIN_WAVES 1  // waves/SIMD the decoder's registers must allow (tuning)
+#endif
+__global__ void __launch_bounds__(256, CWQ_DECODE_MIN_WAVES) k_decode_q4(
     const int32_t* __restrict__ idx, const float4* __restrict__ p_loc,
     const float4* __restrict__ p_scale, uint32_t qpb, uint32_t bpw, int64_t nb, int n_steps,
     int64_t n_cand, float nst, float sdiv, float rho, int32_t seed, int64_t block_id_base,

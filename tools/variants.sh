@@ -39,6 +39,8 @@ declare -A V=(
   [upl2w5]="-DCWQ_COOP_UPL=2 -DCWQ_CSR_COOP_MIN_WAVES=5"
   [upl2pfw4]="-DCWQ_COOP_UPL=2 -DCWQ_COOP_REC_PREFETCH=1 -DCWQ_CSR_COOP_MIN_WAVES=4"
   [head]=prebuilt
+  [dw6]="-DCWQ_DECODE_MIN_WAVES=6"
+  [dw8]="-DCWQ_DECODE_MIN_WAVES=8"
   [sf2]="-DCWQ_SPLIT_FEW=2"
   [sf4]="-DCWQ_SPLIT_FEW=4 -DCWQ_ENCODE_SPLIT=4"
   [ct3k]="-DCWQ_CSR_COOP_TILES=3072"
