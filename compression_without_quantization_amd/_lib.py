@@ -67,7 +67,7 @@ SIGNATURES = {
     "cwq_code_grouped_greedy": (c_i64, [c_vp, c_vp, c_vp, c_vp, c_i64, c_int, c_int, c_i32, c_f32,
                                         c_i64, c_f64, c_vp, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp,
                                         c_size, c_opts, c_vp]),
-    "cwq_code_grouped_greedy_batch_workspace_size": (c_size, [c_i64, c_int]),
+    "cwq_code_grouped_greedy_batch_workspace_size": (c_size, [c_i64, c_i64, c_int]),
     "cwq_code_grouped_greedy_batch": (c_i64, [c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int,
                                               c_vp, c_f32, c_i64, c_f64, c_vp, c_vp, c_i64, c_vp,
                                               c_vp, c_i64, c_vp, c_vp, c_size, c_opts, c_vp]),

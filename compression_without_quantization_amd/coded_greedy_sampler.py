@@ -414,7 +414,7 @@ def code_grouped_greedy_sample_batch(sess, targets, proposals, n_steps, n_bits_p
     n_steps, n_bits_per_step = int(n_steps), int(n_bits_per_step)
     n_bits_per_group = n_bits_per_step * n_steps
     seeds32 = np.array([np.int32(np.uint32(x & 0xFFFFFFFF)) for x in seeds], dtype=np.int32)
-    need = int(lib.cwq_code_grouped_greedy_batch_workspace_size(D, n_steps))
+    need = int(lib.cwq_code_grouped_greedy_batch_workspace_size(D, n_items, n_steps))
     ws = torch.empty(max(need, 1), dtype=torch.uint8, device=dev)
     sample_h = np.empty(max(D, 1), dtype=np.float32)
     bits_cap = (D + n_items) * n_bits_per_group

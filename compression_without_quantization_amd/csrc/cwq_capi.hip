@@ -517,7 +517,9 @@ namespace {
 struct GroupedWs {
   size_t t_loc, t_scale, kl, zeros, ones, sample, out, offs, idx, enc, total;
 };
-GroupedWs grouped_ws(int64_t D, int n_steps) {
+// D dims in at most max_groups groups (a partition of D dims has at most D + 1:
+// the reference's forced boundary at D - 1 can leave an empty first group)
+GroupedWs grouped_ws(int64_t D, int n_steps, int64_t max_groups) {
   GroupedWs l;
   size_t o = 0;
   auto take = [&](size_t bytes) {
@@ -533,9 +535,10 @@ GroupedWs grouped_ws(int64_t D, int n_steps) {
   l.ones = take(fd);
   l.sample = take(fd);
   l.out = take(fd);
-  l.offs = take((size_t)(D + 2) * 8);
-  l.idx = take((size_t)(D > 0 ? D : 1) * (size_t)(n_steps > 0 ? n_steps : 1) * 4);
-  l.enc = take(ws_layout_csr(D, D, D).total);
+  const int64_t G = max_groups > 1 ? max_groups : 1;
+  l.offs = take((size_t)(G + 1) * 8);
+  l.idx = take((size_t)G * (size_t)(n_steps > 0 ? n_steps : 1) * 4);
+  l.enc = take(ws_layout_csr(G, D, D).total);
   l.total = o;
   return l;
 }
@@ -572,7 +575,7 @@ int64_t write_bitcode(const int32_t* idx, int64_t n, int n_bits, char* o) {
 
 size_t cwq_code_grouped_greedy_workspace_size(int64_t D, int n_steps) {
   if (D < 0 || n_steps < 0) return 0;
-  return grouped_ws(D, n_steps).total;
+  return grouped_ws(D, n_steps, D + 1).total;
 }
 
 int64_t cwq_code_grouped_greedy(const float* q_loc, const float* q_scale, const float* p_loc,
@@ -593,7 +596,7 @@ int64_t cwq_code_grouped_greedy(const float* q_loc, const float* q_scale, const 
     return fail(CWQ_ERR_INVALID, "cwq_code_grouped_greedy: null pointer");
   if (!starts_host || starts_cap < D + 2)
     return fail(CWQ_ERR_CAPACITY, "cwq_code_grouped_greedy: starts_cap must be >= D + 2");
-  const GroupedWs l = grouped_ws(D, n_steps);
+  const GroupedWs l = grouped_ws(D, n_steps, D + 1);
   if (workspace_bytes < l.total || !workspace)
     return fail(CWQ_ERR_WORKSPACE, "workspace %zu bytes < required %zu", workspace_bytes,
                 l.total);
@@ -710,20 +713,21 @@ struct BatchWs {
   GroupedWs g;
   size_t seeds, total;
 };
-BatchWs batch_ws(int64_t D, int n_steps) {
+BatchWs batch_ws(int64_t D, int64_t n_items, int n_steps) {
   BatchWs l;
-  l.g = grouped_ws(D, n_steps);
+  const int64_t G = D + (n_items > 0 ? n_items : 0);  // at most D_i + 1 groups per item
+  l.g = grouped_ws(D, n_steps, G);
   l.seeds = l.g.total;
-  l.total = align_up(l.seeds + (size_t)(D > 0 ? D : 1) * 4, 256);
+  l.total = align_up(l.seeds + (size_t)(G > 0 ? G : 1) * 4, 256);
   return l;
 }
 thread_local std::vector<int32_t> g_seed_host;
 thread_local std::vector<int64_t> g_offs_host;
 }  // namespace
 
-size_t cwq_code_grouped_greedy_batch_workspace_size(int64_t D, int n_steps) {
-  if (D < 0 || n_steps < 0) return 0;
-  return batch_ws(D, n_steps).total;
+size_t cwq_code_grouped_greedy_batch_workspace_size(int64_t D, int64_t n_items, int n_steps) {
+  if (D < 0 || n_items < 0 || n_steps < 0) return 0;
+  return batch_ws(D, n_items, n_steps).total;
 }
 
 int64_t cwq_code_grouped_greedy_batch(
@@ -752,7 +756,7 @@ int64_t cwq_code_grouped_greedy_batch(
     return fail(CWQ_ERR_INVALID, "cwq_code_grouped_greedy_batch: null pointer");
   if (!starts_host || starts_cap < D + 2 * n_items)
     return fail(CWQ_ERR_CAPACITY, "starts_cap must be >= D_total + 2 n_items");
-  const BatchWs bl = batch_ws(D, n_steps);
+  const BatchWs bl = batch_ws(D, n_items, n_steps);
   const GroupedWs& l = bl.g;
   if (workspace_bytes < bl.total || !workspace)
     return fail(CWQ_ERR_WORKSPACE, "workspace %zu bytes < required %zu", workspace_bytes,

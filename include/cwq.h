@@ -207,7 +207,8 @@ int64_t cwq_code_grouped_greedy(const float* q_loc, const float* q_scale, const 
  * written) at starts_host + item_off[i] + 2 i (starts_cap >= D_total + 2
  * n_items).  Returns the total number of groups, or a negative error code.
  * Synchronises twice. */
-size_t cwq_code_grouped_greedy_batch_workspace_size(int64_t D_total, int n_steps);
+size_t cwq_code_grouped_greedy_batch_workspace_size(int64_t D_total, int64_t n_items,
+                                                    int n_steps);
 int64_t cwq_code_grouped_greedy_batch(
     int64_t n_items, const int64_t* item_off, const float* q_loc, const float* q_scale,
     const float* p_loc, const float* p_scale, int n_steps, int n_bits_per_step,

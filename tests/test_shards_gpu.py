@@ -203,6 +203,7 @@ def test_c3_batch_equals_per_image_calls(cwq):
     ([3000, 1, 20000, 257, 4096], [42, -7, 2 ** 31 - 3, 0, -2 ** 31], 8, 1),
     ([5000, 300, 6000], [1, 2, 3], 14, 3),   # multi-step: the forked stream parts
     ([2, 1, 3], 9, 6, 2),                    # tiny items, one seed for all
+    ([0, 5, 0, 0, 700], [3, 4, 5, 6, 7], 8, 1),  # empty items (one empty group each)
 ])
 def test_grouped_batch_equals_single_calls(cwq, sizes, seeds, bits, n_steps):
     """Per-item seeds (int32 wrap-around included), items of 1 dim, and
@@ -219,6 +220,7 @@ def test_grouped_batch_equals_single_calls(cwq, sizes, seeds, bits, n_steps):
         tg.append(cwq.Normal(torch.from_numpy(ql).cuda(), torch.from_numpy(qs).cuda()))
         pr.append(cwq.Normal(torch.from_numpy(pl).cuda(), torch.from_numpy(ps).cuda()))
     got = cwq.code_grouped_greedy_sample_batch(None, tg, pr, n_steps, bits, seeds)
+    assert cwq.code_grouped_greedy_sample_batch(None, [], [], n_steps, bits, seeds) == []
     sl = seeds if isinstance(seeds, list) else [seeds] * len(sizes)
     for k in range(len(sizes)):
         sample, bitcode, starts = cwq.code_grouped_greedy_sample(None, tg[k], pr[k], n_steps,
