@@ -287,7 +287,10 @@ def _uniform_encode(cwq, cwqlib, tl, ts, pl, ps, d, bits, n_steps, seed, rho, mo
 @pytest.mark.parametrize("d,bits,n_steps,nb,rho", [
     (8, 4, 1, 64, 1.0), (8, 12, 1, 16, 1.0), (16, 14, 1, 8, 1.0), (24, 10, 2, 12, 1.0),
     (32, 16, 1, 6, 1.0), (32, 9, 3, 10, 0.8), (40, 11, 1, 8, 1.0), (64, 13, 1, 4, 1.0),
-    (16, 20, 1, 1, 1.0)])
+    # 2^20+ candidates (many tiles per block, tau close to the best row):
+    # multi-step (best carried), rho, group counts G = d / 4 from 2 to 16
+    (16, 20, 1, 1, 1.0), (8, 20, 1, 3, 1.0), (16, 21, 2, 2, 0.9), (24, 20, 1, 2, 1.0),
+    (32, 20, 3, 2, 1.0), (64, 20, 1, 1, 1.0), (16, 22, 1, 2, 1.0)])
 def test_pruned_matches_unpruned_and_oracle(cwq, cwqlib, oracle, d, bits, n_steps, nb, rho):
     from compression_without_quantization_amd.synthetic import make_blocks
     b = make_blocks(nb, d, bits, seed=77 + d + bits)
@@ -310,8 +313,31 @@ def test_pruned_matches_unpruned_and_oracle(cwq, cwqlib, oracle, d, bits, n_step
                                   "nan_loc_one_dim", "far_locs", "huge_locs", "tiny_locs"])
 @pytest.mark.parametrize("mode", [1, 2])
 def test_pruned_adversarial(cwq, cwqlib, oracle, kind, mode):
-    rng = np.random.default_rng(sum(map(ord, kind)))
     nb, d, bits = 6, 16, 10
+    tl, ts, pl, ps = _adversarial_inputs(kind, nb, d)
+    i1, s1 = _uniform_encode(cwq, cwqlib, tl, ts, pl, ps, d, bits, 1, 42, 1.0, mode)
+    wi, ws = oracle.greedy_encode(tl, ts, pl, ps, np.arange(nb + 1) * d, bits, 1, 42)
+    assert np.array_equal(i1, wi)
+    _assert_bits_equal(s1, ws, kind)
+
+
+@pytest.mark.parametrize("kind", ["posterior_is_prior", "tiny_scales", "huge_scales",
+                                  "inf_scale", "zero_scale", "mixed_sign_norm", "nan_scale",
+                                  "nan_loc_one_dim", "far_locs", "huge_locs", "tiny_locs"])
+def test_pruned_adversarial_high_rate(cwq, cwqlib, kind):
+    """The same inputs with 2^20 candidates (16 tiles per block; the
+    survivor list overflows on the near-tie inputs): the screened pass equals
+    the unpruned kernel, which the 10-bit test above pins to the oracle."""
+    nb, d, bits = 3, 16, 20
+    tl, ts, pl, ps = _adversarial_inputs(kind, nb, d)
+    i0, s0 = _uniform_encode(cwq, cwqlib, tl, ts, pl, ps, d, bits, 1, 42, 1.0, 0)
+    i2, s2 = _uniform_encode(cwq, cwqlib, tl, ts, pl, ps, d, bits, 1, 42, 1.0, 2)
+    assert np.array_equal(i2, i0)
+    _assert_bits_equal(s2, s0, kind)
+
+
+def _adversarial_inputs(kind, nb, d):
+    rng = np.random.default_rng(sum(map(ord, kind)))
     pl = rng.standard_normal(nb * d).astype(np.float32)
     ps = rng.uniform(0.5, 2, nb * d).astype(np.float32)
     tl = pl.copy()
@@ -346,10 +372,7 @@ def test_pruned_adversarial(cwq, cwqlib, oracle, kind, mode):
         ps = (ps * 1e-30).astype(np.float32)
         tl = (pl + 0.5 * ps * rng.standard_normal(nb * d)).astype(np.float32)
         ts = (0.7 * ps).astype(np.float32)
-    i1, s1 = _uniform_encode(cwq, cwqlib, tl, ts, pl, ps, d, bits, 1, 42, 1.0, mode)
-    wi, ws = oracle.greedy_encode(tl, ts, pl, ps, np.arange(nb + 1) * d, bits, 1, 42)
-    assert np.array_equal(i1, wi)
-    _assert_bits_equal(s1, ws, kind)
+    return tl, ts, pl, ps
 
 
 def test_screen_tables_within_bounds(cwq, cwqlib):
