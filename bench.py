@@ -573,7 +573,10 @@ def main():
                 "hbm_note": "achieved/peak/frac/traffic are the HBM figures the north star "
                             "asks for; the kernel is bound by VALU issue (Philox + "
                             "Box-Muller per candidate), see `valu` and DESIGN.md 4",
-                "kernel": (f"k_encode_prune<{d},true>" if fast else "k_encode_eval"),
+                # third argument: tiles run block-interleaved when a block spans
+                # several tiles (fewer than 16,384 blocks, csrc choose_tiling)
+                "kernel": (f"k_encode_prune<{d},true,{'true' if 0 < nb < 16384 else 'false'}>"
+                           if fast else "k_encode_eval"),
                 "kernel_ms": round(eval_ms, 3),
                 "algorithmic_bytes_per_launch": bytes_per_launch,
                 "valu": {"unit": "candidate-dims/s",

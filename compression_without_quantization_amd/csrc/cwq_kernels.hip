@@ -209,7 +209,7 @@ __device__ unsigned long long g_dbg_best[kDbgBlocks];
 __device__ int g_seed_tau;
 #endif
 
-template <int D, bool STEP0>
+template <int D, bool STEP0, bool INTER>
 __global__ void __launch_bounds__(256, CWQ_PRUNE_MIN_WAVES) k_encode_prune(
     const float* __restrict__ t_loc, const float* __restrict__ t_scale,
     const float* __restrict__ loc_s, const float* __restrict__ scale_s,
@@ -240,14 +240,20 @@ __global__ void __launch_bounds__(256, CWQ_PRUNE_MIN_WAVES) k_encode_prune(
   const uint32_t wv = wave_id();
   const uint32_t lane = threadIdx.x & 63u;
 
+  // INTER (several tiles per block, high rates): tiles run block-interleaved
+  // (tile t is tile t / nb of block t % nb), so a block's later tiles start
+  // after its first ones have finished and begin from the exact best value
+  // they left in keys[g] instead of from -inf
+  constexpr bool inter = INTER;
+  const int64_t nbt = INTER ? ntiles / tiles_per_block : 0;
   for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
     // thread index re-derived per tile behind an opaque move: the per-thread
     // addresses below are then recomputed (cheap) instead of hoisted out of the
     // tile loop and spilled under the 6-waves/SIMD register budget
     uint32_t tid = threadIdx.x;
     asm volatile("" : "+v"(tid));
-    const int64_t g = tile / tiles_per_block;
-    const int64_t tt = tile - g * tiles_per_block;
+    const int64_t g = inter ? tile % nbt : tile / tiles_per_block;
+    const int64_t tt = inter ? tile / nbt : tile - g * tiles_per_block;
     const int64_t off = g * D;
     const int64_t n0 = tt * cand_per_tile;
     const int64_t n1 = (n0 + cand_per_tile < n_cand) ? n0 + cand_per_tile : n_cand;
@@ -369,7 +375,13 @@ __global__ void __launch_bounds__(256, CWQ_PRUNE_MIN_WAVES) k_encode_prune(
         scr_pq = round_up_f32(2.01 * amax * __builtin_sqrt((double)D) * (1.0 + 0x1p-11));
       }
       if (kb == 0) {
-        tau_ord = ord_f32(-__builtin_inff());
+        uint32_t t0 = ord_f32(-__builtin_inff());
+        if (inter) {  // an actual row's exact value: no larger than the block's best
+          const unsigned long long kv =
+              __hip_atomic_load(&keys[g], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if ((uint32_t)(kv >> 32) > kArgmaxClampOrd) t0 = (uint32_t)(kv >> 32);
+        }
+        tau_ord = t0;
 #ifdef CWQ_PRUNE_STATS
         if (g_seed_tau && g < kDbgBlocks && (g_dbg_best[g] >> 32) > kArgmaxClampOrd)
           tau_ord = (uint32_t)(g_dbg_best[g] >> 32);
@@ -2046,10 +2058,19 @@ static void launch_prune_t(const EncodeArgs& a, int step, hipStream_t stream) {
   constexpr int64_t kPruneGrid = CWQ_PRUNE_GRID;
   const int64_t ntiles = a.nb * a.tiles_per_block;
   const unsigned grid = (unsigned)(ntiles < kPruneGrid ? ntiles : kPruneGrid);
-  hipLaunchKernelGGL((k_encode_prune<D, STEP0>), dim3(grid), dim3(256), 0, stream, a.t_loc,
-                     a.t_scale, a.loc_s, a.scale_s, a.lognorm, a.out_sample, ntiles,
-                     a.tiles_per_block, a.cand_per_tile, a.n_cand, seeds_of(a), step,
-                     a.prune >= 2 ? 1 : 0, a.keys);
+#ifndef CWQ_TILE_INTERLEAVE
+#define CWQ_TILE_INTERLEAVE 1
+#endif
+  if (CWQ_TILE_INTERLEAVE && a.tiles_per_block > 1)
+    hipLaunchKernelGGL((k_encode_prune<D, STEP0, true>), dim3(grid), dim3(256), 0, stream,
+                       a.t_loc, a.t_scale, a.loc_s, a.scale_s, a.lognorm, a.out_sample, ntiles,
+                       a.tiles_per_block, a.cand_per_tile, a.n_cand, seeds_of(a), step,
+                       a.prune >= 2 ? 1 : 0, a.keys);
+  else
+    hipLaunchKernelGGL((k_encode_prune<D, STEP0, false>), dim3(grid), dim3(256), 0, stream,
+                       a.t_loc, a.t_scale, a.loc_s, a.scale_s, a.lognorm, a.out_sample, ntiles,
+                       a.tiles_per_block, a.cand_per_tile, a.n_cand, seeds_of(a), step,
+                       a.prune >= 2 ? 1 : 0, a.keys);
 }
 
 template <bool STEP0>

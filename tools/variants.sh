@@ -39,6 +39,7 @@ declare -A V=(
   [upl2w5]="-DCWQ_COOP_UPL=2 -DCWQ_CSR_COOP_MIN_WAVES=5"
   [upl2pfw4]="-DCWQ_COOP_UPL=2 -DCWQ_COOP_REC_PREFETCH=1 -DCWQ_CSR_COOP_MIN_WAVES=4"
   [head]=prebuilt
+  [noint]="-DCWQ_TILE_INTERLEAVE=0"
   [dw6]="-DCWQ_DECODE_MIN_WAVES=6"
   [dw8]="-DCWQ_DECODE_MIN_WAVES=8"
   [sf2]="-DCWQ_SPLIT_FEW=2"
