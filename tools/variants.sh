@@ -40,6 +40,9 @@ declare -A V=(
   [upl2pfw4]="-DCWQ_COOP_UPL=2 -DCWQ_COOP_REC_PREFETCH=1 -DCWQ_CSR_COOP_MIN_WAVES=4"
   [head]=prebuilt
   [noint]="-DCWQ_TILE_INTERLEAVE=0"
+  [noperm]="-DCWQ_IMP_PERMUTE=0"
+  [ig0]="-DCWQ_IMP_GTAU_MASK=0u"
+  [ig255]="-DCWQ_IMP_GTAU_MASK=255u"
   [dw6]="-DCWQ_DECODE_MIN_WAVES=6"
   [dw8]="-DCWQ_DECODE_MIN_WAVES=8"
   [sf2]="-DCWQ_SPLIT_FEW=2"
