@@ -8,8 +8,11 @@ mkdir -p gpurun_out
 timeout -k 10 900 python -u -m pytest tests -x -q -m gpu --timeout 300 --timeout-method thread > gpurun_out/t_all.log 2>&1 && tail -1 gpurun_out/t_all.log && \
 timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 && tail -1 gpurun_out/smoke.log && \
 timeout -k 10 600 python -u bench.py > gpurun_out/b_c4.log 2>&1 && tail -1 gpurun_out/b_c4.log && \
-for c in c5 c1 c2 c2cli c2low c3 i1 i2 pln pln_is; do
+for c in c5 c2cli c2low i1 pln; do
   timeout -k 10 300 python -u bench.py --config $c --steps 3 --warmup 1 > gpurun_out/b_$c.log 2>&1 || exit 1
+done && \
+for c in c1 c2 c3 i2 pln_is; do  # short steps: more of them (host and launch jitter)
+  timeout -k 10 300 python -u bench.py --config $c --steps 20 --warmup 2 > gpurun_out/b_$c.log 2>&1 || exit 1
 done && \
 timeout -k 10 300 python -u -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 2 --warmup 1 --blocks 65536 > gpurun_out/b_torchrun2.log 2>&1 && tail -1 gpurun_out/b_torchrun2.log && \
 bash tools/profile.sh $TAG --config c4
