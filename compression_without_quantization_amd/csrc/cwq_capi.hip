@@ -43,7 +43,7 @@ int hip_fail(hipError_t e, const char* where) {
 size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
 
 struct WsLayout {
-  size_t keys, loc_s, scale_s, lognorm, sab, bpre, ordu, grp, gtau, abp, slist, total;
+  size_t keys, loc_s, scale_s, lognorm, sab, cdim, bpre, ordu, grp, gtau, abp, slist, total;
   bool csr;   // has the general pruned kernel's arrays
   bool recs;  // ... and the visit-order records of blocks longer than CWQ_CSR_LDS_DIMS
 };
@@ -51,7 +51,7 @@ struct WsLayout {
 // Blocks the uniform fast pruned kernel takes (d % 8 == 0, 8 <= d <= 64) need
 // only keys + the per-dim shard constants; everything else (CSR, other d) also
 // gets the general pruned kernel's screening constants and the screened small-candidate
-// path's survivor slots (16 B/dim + 244 B/block),
+// path's survivor slots (20 B/dim + 244 B/block),
 // and, when some block may exceed CWQ_CSR_LDS_DIMS dims, its visit-order
 // records (32 B/dim + 384 B/block).
 bool uniform_fast(int64_t d) { return d % 8 == 0 && d >= 8 && d <= 64; }
@@ -69,12 +69,14 @@ WsLayout ws_layout(int64_t nb, int64_t total_dims, bool csr, bool recs) {
   o = align_up(o + (size_t)total_dims * 4, 256);
   l.csr = csr;
   l.recs = csr && recs;
-  l.sab = l.bpre = l.ordu = l.grp = l.gtau = l.abp = l.slist = o;
+  l.sab = l.cdim = l.bpre = l.ordu = l.grp = l.gtau = l.abp = l.slist = o;
   if (csr) {
     l.slist = o;  // the screened small-candidate path's survivor slots (8 B each)
     o = align_up(o + (size_t)nb * CWQ_SLIST_PER_BLOCK * 8, 256);
     l.sab = o;
     o = align_up(o + (size_t)(total_dims + 8 * nb) * 8, 256);
+    l.cdim = o;
+    o = align_up(o + (size_t)total_dims * 4, 256);
     l.bpre = o;
     o = align_up(o + (size_t)(total_dims + 12 * nb) * 4, 256);
     l.ordu = o;
@@ -363,6 +365,7 @@ int encode_impl(const float* t_loc, const float* t_scale, const float* p_loc,
   a.scale_s = (float*)(w + l.scale_s);
   a.lognorm = (float*)(w + l.lognorm);
   a.sab = l.csr ? (float2*)(w + l.sab) : nullptr;
+  a.cdim = l.csr ? (float*)(w + l.cdim) : nullptr;
   a.bpre = l.csr ? (float*)(w + l.bpre) : nullptr;
   a.ordu = l.csr ? (uint32_t*)(w + l.ordu) : nullptr;
   a.grp = l.csr ? (float4*)(w + l.grp) : nullptr;

@@ -45,6 +45,7 @@ struct EncodeArgs {
   // screening constants of the general pruned kernel (k_encode_prune_csr);
   // nullptr when the workspace was sized without them
   float2* sab;               // [total_dims + 8 nb] (sA, sB), 4 zero pads either side per block
+  float* cdim;               // [total_dims] C_j of the screening bound (k_csr_prep scratch)
   float* bpre;               // [total_dims + 12 nb] drop bounds per visit position (k_csr_prep)
   uint32_t* ordu;            // [total_dims + 12 nb] unit visited at each position
   float4* grp;               // [nb] (c1, c2, As, Pq); c1 == 0: block not screened

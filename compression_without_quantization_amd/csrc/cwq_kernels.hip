@@ -628,13 +628,17 @@ __host__ __device__ __forceinline__ int64_t csr_cls_stride(int64_t d) { return (
 constexpr int64_t kCsrSortUnits = 2048;  // sorted if U_3 <= this (d <= 8189); else natural order
 
 // Per block: the per-dim constants and sums, then for each alignment class
-// its sorted visit order and drop bounds.  The per-dim constants are
-// recomputed where a unit needs them rather than cached in LDS: a prep
-// workgroup with a large LDS footprint cannot start on a CU that the other
-// streams' scoring kernels occupy (measured: +10% on the multi-step coders).  With few blocks the four classes go to four workgroups
-// (blockIdx.y), each recomputing the block's sums, so the sorts run side by
-// side; the blockIdx.y == 0 workgroup also writes the natural-order (sa, sb)
-// array and the block's gate constants.
+// its sorted visit order and drop bounds.  Each dim's constants are computed
+// once (double arithmetic) into sab (sA, sB) and cdim (C_j) in global memory,
+// where the class passes read them back; the prep workgroup keeps a small LDS
+// footprint, so it can start on a CU that the other streams' scoring kernels
+// occupy.  With few blocks the four classes go to four workgroups
+// (blockIdx.y), each computing the block's constants and sums (identical
+// values, so their stores to sab / cdim agree), so the sorts run side by
+// side; the blockIdx.y == 0 workgroup also writes sab's zero pads and the
+// block's gate constants.  Sums and the drop-bound prefix sums are wave
+// reductions / scans (a few barriers per block); classes of <= 256 units are
+// ordered by a rank sort (one barrier), longer ones by a bitonic sort.
 // Blocks longer than lds_dims (whose constants the scoring kernel reads from
 // global memory, not LDS) also get abp: for visit position k of class c the
 // (sa, sb) of unit ord[k]'s four words in one 32-byte record, so the scoring
@@ -645,13 +649,15 @@ __global__ void __launch_bounds__(256) k_csr_prep(
     const float* __restrict__ loc_s, const float* __restrict__ scale_s,
     const float* __restrict__ lognorm, const float* __restrict__ best,
     const int64_t* __restrict__ block_off, int64_t ud, int64_t nb, float2* __restrict__ sab,
-    float* __restrict__ bpre, uint32_t* __restrict__ ordu, float4* __restrict__ grp,
-    uint32_t* __restrict__ gtau, float4* __restrict__ abp, int64_t lds_dims,
-    int64_t coop_min_d) {
-  __shared__ double red[256];
-  __shared__ double scan[256];
+    float* __restrict__ cdim, float* __restrict__ bpre, uint32_t* __restrict__ ordu,
+    float4* __restrict__ grp, uint32_t* __restrict__ gtau, float4* __restrict__ abp,
+    int64_t lds_dims, int64_t coop_min_d) {
+  __shared__ double red[5][4];
+  __shared__ double wscan[4];
+  __shared__ double ucs[256];  // classes of <= 256 units: unit u's C sum
   __shared__ unsigned long long skey[kCsrSortUnits];
   const int tid = threadIdx.x;
+  const int lane = tid & 63, wv = tid >> 6;
   // gridDim.y == 4: one class per workgroup (few blocks: the four sorts run
   // side by side); gridDim.y == 1: one workgroup walks all four classes (many
   // blocks: the per-dim constants are computed once per block, not per class)
@@ -659,20 +665,20 @@ __global__ void __launch_bounds__(256) k_csr_prep(
   for (int64_t g = blockIdx.x; g < nb; g += gridDim.x) {
     const BlockSpan sp = block_span(block_off, ud, g);
     const int64_t off = sp.off, d = sp.d;
-    auto dim = [&](int64_t j) {
-      return csr_dim<STEP0>(loc_s[off + j], scale_s[off + j], t_loc[off + j], t_scale[off + j],
-                            lognorm[off + j], STEP0 ? 0.0f : best[off + j]);
-    };
     double sm = 0.0, sa = 0.0, sk = 0.0, s2 = 0.0, mx = 0.0;
     int ok = 1;
     float2* sabg = sab + off + 8 * g + 4;  // 4 zero pads either side (partial units)
+    float* cg = cdim + off;
     if (lead && tid < 4) {
       sabg[tid - 4] = float2{0.f, 0.f};
       sabg[d + tid] = float2{0.f, 0.f};
     }
     for (int64_t j = tid; j < d; j += 256) {
-      const CsrDim o = dim(j);
-      if (lead) sabg[j] = float2{o.sa, o.sb};
+      const CsrDim o =
+          csr_dim<STEP0>(loc_s[off + j], scale_s[off + j], t_loc[off + j], t_scale[off + j],
+                         lognorm[off + j], STEP0 ? 0.0f : best[off + j]);
+      sabg[j] = float2{o.sa, o.sb};
+      cg[j] = o.C;
       sm += o.M;
       sa += __builtin_fabs(o.M);
       sk += __builtin_fabs(o.M) + o.M;
@@ -680,17 +686,31 @@ __global__ void __launch_bounds__(256) k_csr_prep(
       mx = (double)o.A > mx ? (double)o.A : mx;
       ok &= o.ok ? 1 : 0;
     }
-    const bool all_ok = __syncthreads_and(ok) != 0;
-    const double SM = block_sum_d(sm, red), SA = block_sum_d(sa, red);
-    const double SK = block_sum_d(sk, red), S2 = block_sum_d(s2, red);
-    red[tid] = mx;
-    __syncthreads();
-    for (int w = 128; w > 0; w >>= 1) {
-      if (tid < w) red[tid] = red[tid + w] > red[tid] ? red[tid + w] : red[tid];
-      __syncthreads();
+    sm = wave_sum_f64(sm);
+    sa = wave_sum_f64(sa);
+    sk = wave_sum_f64(sk);
+    s2 = wave_sum_f64(s2);
+    mx = wave_max_f64(mx);
+    if (lane == 0) {
+      red[0][wv] = sm;
+      red[1][wv] = sa;
+      red[2][wv] = sk;
+      red[3][wv] = s2;
+      red[4][wv] = mx;
     }
-    const double MX = red[0];
-    __syncthreads();
+    // the sab / cdim stores are read back below by other threads: wait for
+    // them to complete (they write through to L2) and read them with
+    // agent-scope loads, which bypass the CU's L1 (a line another block's
+    // workgroup on this CU filled earlier may hold this block's previous-step
+    // values at its edges)
+    __threadfence_block();
+    const bool all_ok = __syncthreads_and(ok) != 0;
+    const double SM = ((red[0][0] + red[0][1]) + red[0][2]) + red[0][3];
+    const double SA = ((red[1][0] + red[1][1]) + red[1][2]) + red[1][3];
+    const double SK = ((red[2][0] + red[2][1]) + red[2][2]) + red[2][3];
+    const double S2 = ((red[3][0] + red[3][1]) + red[3][2]) + red[3][3];
+    double MX = red[4][0];
+    for (int w = 1; w < 4; ++w) MX = red[4][w] > MX ? red[4][w] : MX;
     // Float summation error of depth h: gamma_h = 1.01 (h + 1) 2^-24 bounds
     // |fl(sum) - sum| / sum|x| for any summation tree in which every term
     // passes through at most h roundings.  Two sums of d terms enter the
@@ -698,21 +718,22 @@ __global__ void __launch_bounds__(256) k_csr_prep(
     // rows: 4 in-lane + 4 butterfly + one per 16-unit chunk, <= 16 + d/64) and
     // the exact Eigen-order row value (8 strided accumulators, predux, tail:
     // <= d/8 + 8).  gamma is taken at the larger depth.  The additive margin
-    // 2^-20 covers the float rounding of B_k and of the tests' fma (u |B_k|);
-    // u |s| is covered by the 2^-22 / 2^-14 terms of c1 / c2.
+    // 2^-20 covers the float rounding of B_k and of the tests' fma (u |B_k|)
+    // and the double roundings of the sums here; u |s| is covered by the
+    // 2^-22 / 2^-14 terms of c1 / c2.
     const bool coop_blk = d >= coop_min_d;
     const double h_s = coop_blk ? 16.0 + (double)d / 64.0 : (double)d;
     const double h_e = (double)d / 8.0 + 8.0;
     const double gam = 1.01 * ((h_s > h_e ? h_s : h_e) + 1.0) * 0x1p-24;
     const double sl = (3.0 * gam + 0x1p-20) * (__builtin_fabs(SM) + SA + SK) + 0x1p-126;
     const int64_t reg = off + 12 * g, cs = csr_cls_stride(d);
-    auto consts = [&](int64_t j, float& xa, float& xb, float& xc) {
-      const CsrDim o = dim(j);
-      xa = o.sa;
-      xb = o.sb;
-      xc = o.C;
-    };
     const bool recs = abp != nullptr && d > lds_dims;
+    auto sab_at = [&](int64_t j) {
+      const unsigned long long v = __hip_atomic_load(
+          reinterpret_cast<unsigned long long*>(sabg + j), __ATOMIC_RELAXED,
+          __HIP_MEMORY_SCOPE_AGENT);
+      return float2{u2f((uint32_t)v), u2f((uint32_t)(v >> 32))};
+    };
     for (int c = (int)blockIdx.y; c < 4; c += (int)gridDim.y) {
       // word t of unit u of class c is dim 4u - c + t (absent outside [0, d));
       // unit u: its sum of C_j and its expected sum of a_j^2 - C_j
@@ -722,29 +743,45 @@ __global__ void __launch_bounds__(256) k_csr_prep(
         for (int t = 0; t < 4; ++t) {
           const int64_t j = 4 * u - c + t;
           if (j >= 0 && j < d) {
-            float xa, xb, xc;
-            consts(j, xa, xb, xc);
+            const float2 ab = sab_at(j);
+            const float xc = u2f(__hip_atomic_load(reinterpret_cast<uint32_t*>(cg + j),
+                                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
             csum += (double)xc;
-            gain += (double)xa * (double)xa * (0.5 / 0.6931471805599453) +
-                    (double)xb * (double)xb - (double)xc;
+            gain += (double)ab.x * (double)ab.x * (0.5 / 0.6931471805599453) +
+                    (double)ab.y * (double)ab.y - (double)xc;
           }
         }
       };
+      auto key_of = [&](int64_t u) {
+        double cu, gu;
+        unit(u, cu, gu);
+        const float gf = (float)(gu > 0.0 ? gu : 0.0);
+        return ((unsigned long long)ord_f32(gf) << 32) | (0xffffffffull - (uint64_t)u);
+      };
       const int64_t U = (d + c + 3) / 4;
       const bool sorted = all_ok && U <= kCsrSortUnits;
-      if (sorted) {  // bitonic sort of (gain desc, u asc) keys
+      const bool small = U <= 256;  // one unit per thread: its C sum kept in LDS
+      if (sorted && small) {  // rank sort of (gain desc, u asc) keys: keys are distinct
+        unsigned long long key = 0ull;
+        if (tid < U) {
+          double cu, gu;
+          unit(tid, cu, gu);
+          ucs[tid] = cu;
+          const float gf = (float)(gu > 0.0 ? gu : 0.0);
+          key = ((unsigned long long)ord_f32(gf) << 32) | (0xffffffffull - (uint64_t)tid);
+          skey[tid] = key;
+        }
+        __syncthreads();
+        int r = 0;
+        if (tid < U)
+          for (int i = 0; i < (int)U; ++i) r += skey[i] > key ? 1 : 0;
+        __syncthreads();
+        if (tid < U) skey[r] = key;
+        __syncthreads();
+      } else if (sorted) {  // bitonic sort of (gain desc, u asc) keys
         int64_t P = 1;
         while (P < U) P <<= 1;
-        for (int64_t u = tid; u < P; u += 256) {
-          unsigned long long key = 0ull;
-          if (u < U) {
-            double cu, gu;
-            unit(u, cu, gu);
-            const float gf = (float)(gu > 0.0 ? gu : 0.0);
-            key = ((unsigned long long)ord_f32(gf) << 32) | (0xffffffffull - (uint64_t)u);
-          }
-          skey[u] = key;
-        }
+        for (int64_t u = tid; u < P; u += 256) skey[u] = u < U ? key_of(u) : 0ull;
         __syncthreads();
         for (int64_t k = 2; k <= P; k <<= 1) {
           for (int64_t jj = k >> 1; jj > 0; jj >>= 1) {
@@ -770,34 +807,42 @@ __global__ void __launch_bounds__(256) k_csr_prep(
         int64_t u = k;
         if (sorted && k < U) u = (int64_t)(0xffffffffull - (skey[k] & 0xffffffffull));
         double cu = 0.0, gu;
-        if (all_ok && k < U) unit(u, cu, gu);
+        if (all_ok && k < U) {
+          if (sorted && small)
+            cu = ucs[u];
+          else
+            unit(u, cu, gu);
+        }
         if (recs && k < U) {  // the unit's four (sa, sb), zero for absent words
           float e[8];
           for (int t = 0; t < 4; ++t) {
             const int64_t j = 4 * u - c + t;
-            float xa = 0.f, xb = 0.f, xc;
-            if (j >= 0 && j < d) consts(j, xa, xb, xc);
-            e[2 * t] = xa;
-            e[2 * t + 1] = xb;
+            float2 ab = float2{0.f, 0.f};
+            if (j >= 0 && j < d) ab = sab_at(j);
+            e[2 * t] = ab.x;
+            e[2 * t + 1] = ab.y;
           }
-          float4* r = abp + 2 * (reg + c * cs + k);
-          r[0] = float4{e[0], e[1], e[2], e[3]};
-          r[1] = float4{e[4], e[5], e[6], e[7]};
+          float4* rr = abp + 2 * (reg + c * cs + k);
+          rr[0] = float4{e[0], e[1], e[2], e[3]};
+          rr[1] = float4{e[4], e[5], e[6], e[7]};
         }
-        scan[tid] = cu;
+        double v = cu;  // inclusive scan: in the wave, then across the four waves
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+          const double t = __shfl_up(v, (unsigned)o, 64);
+          if (lane >= o) v += t;
+        }
+        if (lane == 63) wscan[wv] = v;
         __syncthreads();
-        for (int w = 1; w < 256; w <<= 1) {  // inclusive scan
-          const double v = tid >= w ? scan[tid - w] : 0.0;
-          __syncthreads();
-          scan[tid] += v;
-          __syncthreads();
-        }
-        const double excl = carry + scan[tid] - cu;
+        double pre = 0.0;
+        for (int w = 0; w < wv; ++w) pre += wscan[w];
+        const double total = ((wscan[0] + wscan[1]) + wscan[2]) + wscan[3];
+        const double excl = carry + (pre + v) - cu;
         if (k <= U) {
           bpre[reg + c * cs + k] = round_up_f32(SM + excl * (1.0 + 0x1p-20) + sl);
           ordu[reg + c * cs + k] = (uint32_t)(k < U ? u : 0);
         }
-        carry += scan[255];
+        carry += total;
         __syncthreads();
       }
     }
@@ -2103,8 +2148,8 @@ static void launch_prune_csr(const EncodeArgs& a, int step, hipStream_t stream) 
   const unsigned cls_wgs = a.nb <= CWQ_PREP_SPLIT_MAX_NB ? 4 : 1;
   hipLaunchKernelGGL((k_csr_prep<STEP0>), dim3(grid_for(a.nb, 1, 65536), cls_wgs), dim3(256), 0,
                      stream, a.t_loc, a.t_scale, a.loc_s, a.scale_s, a.lognorm, a.out_sample,
-                     a.block_off, a.ud, a.nb, a.sab, a.bpre, a.ordu, a.grp, a.gtau, a.abp,
-                     (int64_t)CWQ_CSR_LDS_DIMS, coop_min_d);
+                     a.block_off, a.ud, a.nb, a.sab, a.cdim, a.bpre, a.ordu, a.grp, a.gtau,
+                     a.abp, (int64_t)CWQ_CSR_LDS_DIMS, coop_min_d);
   constexpr int64_t kGrid = 1 << 20;
   const unsigned grid = (unsigned)(ntiles < kGrid ? ntiles : kGrid);
   if (coop)

@@ -40,6 +40,7 @@ declare -A V=(
   [upl2pfw4]="-DCWQ_COOP_UPL=2 -DCWQ_COOP_REC_PREFETCH=1 -DCWQ_CSR_COOP_MIN_WAVES=4"
   [head]=prebuilt
   [noint]="-DCWQ_TILE_INTERLEAVE=0"
+  [psplit0]="-DCWQ_PREP_SPLIT_MAX_NB=0"
   [noperm]="-DCWQ_IMP_PERMUTE=0"
   [ig0]="-DCWQ_IMP_GTAU_MASK=0u"
   [ig255]="-DCWQ_IMP_GTAU_MASK=255u"
