@@ -32,12 +32,8 @@ declare -A V=(
   [mask31]="-DCWQ_TAU_SHARE_MASK=31u"
   [cap512]="-DCWQ_SURVIVOR_CAP=512"
   [w7]="-DCWQ_PRUNE_MIN_WAVES=7"
-  [pf]="-DCWQ_COOP_REC_PREFETCH=1"
   [upl2]="-DCWQ_COOP_UPL=2"
-  [upl2pf]="-DCWQ_COOP_UPL=2 -DCWQ_COOP_REC_PREFETCH=1"
-  [pfw5]="-DCWQ_COOP_REC_PREFETCH=1 -DCWQ_CSR_COOP_MIN_WAVES=5"
   [upl2w5]="-DCWQ_COOP_UPL=2 -DCWQ_CSR_COOP_MIN_WAVES=5"
-  [upl2pfw4]="-DCWQ_COOP_UPL=2 -DCWQ_COOP_REC_PREFETCH=1 -DCWQ_CSR_COOP_MIN_WAVES=4"
   [head]=prebuilt
   [noint]="-DCWQ_TILE_INTERLEAVE=0"
   [psplit0]="-DCWQ_PREP_SPLIT_MAX_NB=0"
