@@ -1442,8 +1442,8 @@ __global__ void __launch_bounds__(256, COOP ? CWQ_CSR_COOP_MIN_WAVES : CWQ_CSR_R
 //                     the block is scored exactly), its full-row bound B and
 //                     stream key into bpre[off + 12 g ...]; gtau = -inf; the
 //                     survivor count = 0.
-//   k_small_screen    a wave per tile, its rows n = r (mod 4) one alignment
-//                     class at a time: screened value s of each row; tau = the wave's
+//   k_small_screen    a wave per tile, each lane 4 consecutive rows at a time
+//                     (d whole Philox blocks): screened value s of each row; tau = the wave's
 //                     best lower bound fma(s, c2, As) - Pq sqrt(-s); rows whose
 //                     upper bound fma(s, c1, B) reaches tau take one of the
 //                     block's CWQ_SLIST_PER_BLOCK slots; tau is published to
@@ -1555,8 +1555,8 @@ __global__ void __launch_bounds__(256) k_small_screen(
     uint32_t* __restrict__ gtau, uint32_t* __restrict__ scnt, uint2* __restrict__ slist) {
   const uint32_t lane = threadIdx.x & 63u;
   const int64_t nwaves = (int64_t)gridDim.x * 4;
-  // a wave takes a whole tile, its four alignment classes r = n mod 4 one
-  // after the other (the block's loads, key and threshold once per tile)
+  // a wave takes a whole tile (the block's loads, key and threshold once per
+  // tile), 256 rows per round
   for (int64_t tile = (int64_t)blockIdx.x * 4 + wave_id(); tile < ntiles; tile += nwaves) {
     const int64_t g = tiles_per_block == 1 ? tile : tile / tiles_per_block;
     const int64_t tt = tile - g * tiles_per_block;
@@ -1573,55 +1573,70 @@ __global__ void __launch_bounds__(256) k_small_screen(
     const float2* ab = sab + off + 8 * g + 4;
     float tau = unord_f32(__hip_atomic_load(&gtau[g * CWQ_CSR_GTAU_STRIDE], __ATOMIC_RELAXED,
                                             __HIP_MEMORY_SCOPE_AGENT));
-    // rows n0 + r + 4 lane + 256 k: the same (r, k) for every lane
-    // (wave-uniform trip counts), so tau is shared through the wave after
-    // each round, and n d mod 4 is the same in every lane
-    for (int64_t r = 0; r < 4 && n0 + r < n1; ++r)
-    for (int64_t k = 0, rounds = (n1 - n0 - r + 255) / 256; k < rounds; ++k) {
-      const int64_t n = n0 + r + 4 * (int64_t)lane + 256 * k;
-      const bool valid = n < n1;
-      float s = 0.0f;
-      if (valid) {
-        const uint64_t k0 = (uint64_t)n * (uint64_t)d;
-        F4 z = {0.f, 0.f, 0.f, 0.f};
-        for (int j = 0; j < d; ++j) {  // natural order, sequential sum (h = d)
-          const uint64_t kk = k0 + (uint64_t)j;
-          const int w = (int)(kk & 3u);  // wave-uniform: n = r (mod 4) for every lane
-          if (w == 0 || j == 0) {
-            const uint64_t blk = kk >> 2;
-            const U4 x = philox10_dev((uint32_t)blk, (uint32_t)(blk >> 32), st.c2, st.c3, st.k0,
-                                      st.k1);
-            box_muller_screen(x.x, x.y, z.a, z.b);
-            box_muller_screen(x.z, x.w, z.c, z.d);
-          }
-          const float zz = w == 0 ? z.a : (w == 1 ? z.b : (w == 2 ? z.c : z.d));
+    // lane span m: rows n0 + 4 (lane + 64 m) + q, q = 0..3.  n0 is a multiple
+    // of 4 (tiles are multiples of 256 candidates), so a span's 4d words are
+    // exactly Philox blocks [n d / 4, n d / 4 + d): every block is computed
+    // once (a row alone would start and end inside blocks its neighbours also
+    // compute), and the dim index of each word is the same in every lane, so
+    // the per-dim constants are wave-uniform loads.
+    for (int64_t m0 = 0; n0 + 256 * m0 < n1; ++m0) {
+      const int64_t ns = n0 + 4 * ((int64_t)lane + 64 * m0);
+      const uint64_t b0 = (uint64_t)ns * (uint64_t)d / 4u;
+      float rs0 = 0.0f, rs1 = 0.0f, rs2 = 0.0f, rs3 = 0.0f;  // the span's four row sums
+      float cur = 0.0f;  // natural order, sequential sum (h = d), as k_small_prep's bound
+      int j = 0, q = 0;
+      for (int b = 0; b < d; ++b) {
+        const uint64_t blk = b0 + (uint64_t)b;
+        const U4 x = philox10_dev((uint32_t)blk, (uint32_t)(blk >> 32), st.c2, st.c3, st.k0,
+                                  st.k1);
+        float z[4];
+        box_muller_screen(x.x, x.y, z[0], z[1]);
+        box_muller_screen(x.z, x.w, z[2], z[3]);
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
           const float2 e = ab[j];
-          const float a = __builtin_fmaf(e.x, zz, e.y);
-          s = __builtin_fmaf(-a, a, s);
+          const float a = __builtin_fmaf(e.x, z[t], e.y);
+          cur = __builtin_fmaf(-a, a, cur);
+          if (++j == d) {  // wave-uniform: a row of the span is complete
+            if (q == 0) rs0 = cur;
+            else if (q == 1) rs1 = cur;
+            else if (q == 2) rs2 = cur;
+            else rs3 = cur;
+            cur = 0.0f;
+            j = 0;
+            ++q;
+          }
         }
       }
-      const float upper = __builtin_fmaf(s, gc.x, bf);
-      const float lower = valid ? __builtin_fmaf(s, gc.y, gc.z) - gc.w * __builtin_amdgcn_sqrtf(-s)
-                                : -__builtin_inff();
-      tau = fmaxf(tau, wave_max_f32(lower));
-      const bool push = valid && upper >= tau;
-      const uint64_t m = __ballot(push);
-      if (m) {
-        const uint32_t cnt = (uint32_t)__builtin_popcountll(m);
-        // the block's own slots (a global counter serialised every wave)
-        uint32_t base = 0;
-        if (lane == 0) base = atomicAdd(&scnt[off + 12 * g], cnt);
-        base = (uint32_t)__shfl((int)base, 0, 64);
-        const uint32_t rank = __builtin_amdgcn_mbcnt_hi(
-            (uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-        if (push) {
-          const uint32_t slot = base + rank;
-          if (slot < CWQ_SLIST_PER_BLOCK)
-            slist[CWQ_SLIST_PER_BLOCK * g + slot] = uint2{(uint32_t)n, f2u(upper)};
+#pragma unroll
+      for (int qq = 0; qq < 4; ++qq) {
+        const float sv = qq == 0 ? rs0 : (qq == 1 ? rs1 : (qq == 2 ? rs2 : rs3));
+        const int64_t n = ns + qq;
+        const bool valid = n < n1;
+        const float upper = __builtin_fmaf(sv, gc.x, bf);
+        const float lower = valid ? __builtin_fmaf(sv, gc.y, gc.z) -
+                                        gc.w * __builtin_amdgcn_sqrtf(-sv)
+                                  : -__builtin_inff();
+        tau = fmaxf(tau, wave_max_f32(lower));
+        const bool push = valid && upper >= tau;
+        const uint64_t m = __ballot(push);
+        if (m) {
+          const uint32_t cnt = (uint32_t)__builtin_popcountll(m);
+          // the block's own slots (a global counter serialised every wave)
+          uint32_t base = 0;
+          if (lane == 0) base = atomicAdd(&scnt[off + 12 * g], cnt);
+          base = (uint32_t)__shfl((int)base, 0, 64);
+          const uint32_t rank = __builtin_amdgcn_mbcnt_hi(
+              (uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+          if (push) {
+            const uint32_t slot = base + rank;
+            if (slot < CWQ_SLIST_PER_BLOCK)
+              slist[CWQ_SLIST_PER_BLOCK * g + slot] = uint2{(uint32_t)n, f2u(upper)};
+          }
+          if (base + cnt > CWQ_SLIST_PER_BLOCK && lane == 0)  // slots full: score the block exactly
+            __hip_atomic_store(reinterpret_cast<uint32_t*>(&grp[g].x), 0u, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
         }
-        if (base + cnt > CWQ_SLIST_PER_BLOCK && lane == 0)  // slots full: score the block exactly
-          __hip_atomic_store(reinterpret_cast<uint32_t*>(&grp[g].x), 0u, __ATOMIC_RELAXED,
-                             __HIP_MEMORY_SCOPE_AGENT);
       }
     }
     if (lane == 0) atomicMax(&gtau[g * CWQ_CSR_GTAU_STRIDE], ord_f32(tau));
