@@ -11,8 +11,9 @@ timeout -k 10 600 python -u bench.py > gpurun_out/b_c4.log 2>&1 && tail -1 gpuru
 for c in c5 c2cli c2low i1 pln; do
   timeout -k 10 300 python -u bench.py --config $c --steps 3 --warmup 1 > gpurun_out/b_$c.log 2>&1 || exit 1
 done && \
-for c in c1 c2 c3 i2 pln_is; do  # short steps: more of them (host and launch jitter)
+for c in c1 c3 i2 pln_is; do  # short steps: more of them (host and launch jitter)
   timeout -k 10 300 python -u bench.py --config $c --steps 20 --warmup 2 > gpurun_out/b_$c.log 2>&1 || exit 1
 done && \
+timeout -k 10 300 python -u bench.py --config c2 --steps 100 --warmup 5 > gpurun_out/b_c2.log 2>&1 && \
 timeout -k 10 300 python -u -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 2 --warmup 1 --blocks 65536 > gpurun_out/b_torchrun2.log 2>&1 && tail -1 gpurun_out/b_torchrun2.log && \
 bash tools/profile.sh $TAG --config c4
