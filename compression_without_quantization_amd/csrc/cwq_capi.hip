@@ -12,6 +12,9 @@
 #include <time.h>
 #include <immintrin.h>
 
+#include <atomic>
+#include <sched.h>
+#include <stdlib.h>
 #include <thread>
 #include <vector>
 
@@ -724,6 +727,24 @@ BatchWs batch_ws(int64_t D, int64_t n_items, int n_steps) {
   l.total = align_up(l.seeds + (size_t)(G > 0 ? G : 1) * 4, 256);
   return l;
 }
+// Host threads for the per-item phases: CWQ_HOST_THREADS if set, else the
+// CPUs this process may run on, at most 8.  (On the GPU boxes, whose cgroup
+// quota is 16 CPUs, 12 or 16 threads sporadically ran C3 2.5x slower: the
+// quota's throttling; 4 and 8 were steady at 9-10 ms per 24 images.)
+int64_t host_threads() {
+  static const int64_t n = [] {
+    if (const char* e = getenv("CWQ_HOST_THREADS")) {
+      const long v = strtol(e, nullptr, 10);
+      if (v >= 1) return (int64_t)v;
+    }
+    cpu_set_t set;
+    int64_t c = 0;
+    if (sched_getaffinity(0, sizeof(set), &set) == 0) c = CPU_COUNT(&set);
+    if (c < 1) c = (int64_t)std::thread::hardware_concurrency();
+    return std::max<int64_t>(1, std::min<int64_t>(8, c));
+  }();
+  return n;
+}
 thread_local std::vector<int32_t> g_seed_host;
 thread_local std::vector<int64_t> g_offs_host;
 }  // namespace
@@ -777,21 +798,22 @@ int64_t cwq_code_grouped_greedy_batch(
 #else
   auto lap = [](const char*) {};
 #endif
-  // fn(i) for every item, on up to 8 host threads when the batch is large
-  const int64_t nthr = std::min<int64_t>(
-      n_items,
-      std::max<int64_t>(1, std::min<int64_t>(8, (int64_t)std::thread::hardware_concurrency())));
+  // fn(i) for every item, on up to host_threads() threads when the batch is large
+  const int64_t nthr = std::min<int64_t>(n_items, host_threads());
   auto for_items = [&](auto fn) {
-    auto work = [&](int64_t t) {
-      for (int64_t i = t; i < n_items; i += nthr) fn(i);
-    };
     if (nthr <= 1 || item_off[n_items] < (1 << 16)) {
-      for (int64_t t = 0; t < nthr; ++t) work(t);
+      for (int64_t i = 0; i < n_items; ++i) fn(i);
       return;
     }
+    // items handed out one at a time (sizes differ by orders of magnitude:
+    // both ladder levels of an image alternate in a batch)
+    std::atomic<int64_t> next{0};
+    auto work = [&]() {
+      for (int64_t i = next++; i < n_items; i = next++) fn(i);
+    };
     std::vector<std::thread> pool;
-    for (int64_t t = 1; t < nthr; ++t) pool.emplace_back(work, t);
-    work(0);
+    for (int64_t t = 1; t < nthr; ++t) pool.emplace_back(work);
+    work();
     for (auto& th : pool) th.join();
   };
   char* w = (char*)workspace;
