@@ -2109,11 +2109,13 @@ static void launch_eval_t(const EncodeArgs& a, int step, hipStream_t stream) {
 
 template <int D, bool STEP0>
 static void launch_prune_t(const EncodeArgs& a, int step, hipStream_t stream) {
-  // persistent-style grid: 256 CUs x 6 resident workgroups x 64; each workgroup
-  // loops over tiles (per-workgroup setup, e.g. register spill slots written
-  // once at entry, is paid thousands of times less often than one per tile)
+  // grid of 256 CUs x 6 resident workgroups x 256; each workgroup loops over
+  // its tiles (C4: 2.5 each).  Many more workgroups than resident slots keep
+  // the SIMDs busy while a workgroup sets up its next tile: 1,536 (exactly
+  // resident) was 15% slower on C4, 12,288 2%, 98,304 0.5%; one tile per
+  // workgroup (1M) 0.5% (tools/variants.sh pg*)
 #ifndef CWQ_PRUNE_GRID
-#define CWQ_PRUNE_GRID (256 * 6 * 64)
+#define CWQ_PRUNE_GRID (256 * 6 * 256)
 #endif
   constexpr int64_t kPruneGrid = CWQ_PRUNE_GRID;
   const int64_t ntiles = a.nb * a.tiles_per_block;

@@ -36,6 +36,10 @@ declare -A V=(
   [upl2w5]="-DCWQ_COOP_UPL=2 -DCWQ_CSR_COOP_MIN_WAVES=5"
   [head]=prebuilt
   [noint]="-DCWQ_TILE_INTERLEAVE=0"
+  [pg1536]="-DCWQ_PRUNE_GRID=1536"
+  [pg12k]="-DCWQ_PRUNE_GRID=12288"
+  [pg98k]="-DCWQ_PRUNE_GRID=98304"
+  [pg1m]="-DCWQ_PRUNE_GRID=1048576"
   [psplit0]="-DCWQ_PREP_SPLIT_MAX_NB=0"
   [noperm]="-DCWQ_IMP_PERMUTE=0"
   [ig0]="-DCWQ_IMP_GTAU_MASK=0u"
