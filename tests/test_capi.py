@@ -85,3 +85,20 @@ def test_group_starts_host(cwqlib):
                                 starts.ctypes.data, 16)
     # n_nats = 0.386: dim0 alone (0.5 >= n_nats at idx 0 -> duplicate 0) ...
     assert list(starts[:n]) == [0, 0, 1, 2, 3, 4, 5]
+
+
+def test_missing_library_fails_loudly(tmp_path):
+    """No CPU fallback: with the library absent the product path raises on
+    first use instead of routing anywhere else."""
+    import subprocess
+    import sys
+    code = ("import numpy as np, compression_without_quantization_amd as C\n"
+            "try:\n"
+            "    C.encode_blocks(np.zeros(4, np.float32), np.ones(4, np.float32),\n"
+            "                    np.zeros(4, np.float32), np.ones(4, np.float32), 4, 1, 0)\n"
+            "except (ImportError, OSError) as e:\n"
+            "    print('raised', type(e).__name__)\n")
+    env = dict(os.environ, CWQ_LIB_PATH=str(tmp_path / "absent" / "libcwq.so"))
+    out = subprocess.run([sys.executable, "-c", code], cwd=REPO, env=env,
+                         capture_output=True, text=True, timeout=120)
+    assert "raised" in out.stdout, (out.stdout, out.stderr)
