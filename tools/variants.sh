@@ -32,6 +32,8 @@ declare -A V=(
   [mask31]="-DCWQ_TAU_SHARE_MASK=31u"
   [cap512]="-DCWQ_SURVIVOR_CAP=512"
   [w7]="-DCWQ_PRUNE_MIN_WAVES=7"
+  [w5]="-DCWQ_PRUNE_MIN_WAVES=5"
+  [w8]="-DCWQ_PRUNE_MIN_WAVES=8"
   [upl2]="-DCWQ_COOP_UPL=2"
   [upl2w5]="-DCWQ_COOP_UPL=2 -DCWQ_CSR_COOP_MIN_WAVES=5"
   [head]=prebuilt
