@@ -91,11 +91,19 @@ SIGNATURES = {
     "cwq_selftest_logf": (c_int, [c_vp, c_i64, c_vp, c_vp]),
     "cwq_selftest_wave_max": (c_int, [c_vp, c_i64, c_vp, c_vp]),
     "cwq_selftest_div": (c_int, [c_vp, c_vp, c_i64, c_vp, c_vp]),
-    "cwq_debug_prune_stats": (c_int, [c_vp, c_int]),
     "cwq_pln_posterior": (c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, c_f32, c_vp, c_vp, c_vp]),
     "cwq_permute_gather": (c_int, [c_vp, c_i64, c_i64, c_vp, c_vp, c_vp]),
     "cwq_permute_scatter": (c_int, [c_vp, c_i64, c_i64, c_vp, c_vp, c_vp]),
 }
+
+# Tools-only entry points (csrc/cwq_debug.h, not in include/cwq.h).
+TOOL_SIGNATURES = {
+    "cwq_debug_prune_stats": (c_int, [c_vp, c_int]),
+}
+
+# CWQ_ABI_VERSION of the include/cwq.h these signatures mirror: a library
+# reporting another version has other argument lists and is refused.
+ABI_VERSION = (0 << 16) | 2
 
 _lib = None
 
@@ -114,9 +122,15 @@ def load():
             f"{LIB_PATH} not found: build the HIP extension first "
             "(python -c 'import __graft_entry__ as g; g.build()')")
     lib = ctypes.CDLL(LIB_PATH)
-    for name, (res, args) in SIGNATURES.items():
-        if os.environ.get("CWQ_LIB_PATH") and not hasattr(lib, name):
-            continue  # an older tuning build (tools/variants.sh) may lack newer entry points
+    lib.cwq_version.restype = c_int
+    lib.cwq_version.argtypes = []
+    ver = lib.cwq_version()
+    if ver != ABI_VERSION:
+        raise ImportError(f"{LIB_PATH} has ABI version {ver >> 16}.{ver & 0xffff}, these "
+                          f"bindings need {ABI_VERSION >> 16}.{ABI_VERSION & 0xffff}: rebuild it")
+    for name, (res, args) in list(SIGNATURES.items()) + list(TOOL_SIGNATURES.items()):
+        if not hasattr(lib, name):
+            raise ImportError(f"{LIB_PATH} does not export {name}: rebuild it")
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args

@@ -186,34 +186,59 @@ def write_bin_code(code, path, extras=None, extra_var_bits=None, var_length_extr
         f.write(bytes(out))
 
 
+class _ByteCursor:
+    """Sequential reader over a .miracle file's bytes (every section of the
+    container starts on a byte boundary, binary_io.py:69-133)."""
+
+    def __init__(self, data):
+        self.data = data
+        self.pos = 0
+
+    def take(self, n):
+        if n < 0 or self.pos + n > len(self.data):
+            raise ValueError(f"truncated .miracle file: {n} bytes wanted at byte {self.pos} "
+                             f"of {len(self.data)}")
+        out = self.data[self.pos:self.pos + n]
+        self.pos += n
+        return out
+
+    def uint(self, n):
+        """n-byte big-endian unsigned integer."""
+        return int.from_bytes(self.take(n), "big")
+
+    def bits(self, nbits):
+        """The next ceil(nbits / 8) bytes as nbits MSB-first '0'/'1' flags (uint8)."""
+        raw = np.frombuffer(self.take(-(-nbits // 8)), dtype=np.uint8)
+        return np.unpackbits(raw)[:nbits]
+
+
+def _chars(flags):
+    return (flags + ord("0")).astype(np.uint8).tobytes().decode("ascii")
+
+
 def read_bin_code(path, num_extras=0, num_extra_var_bits=0, num_var_length_extras=0,
                   extras_bytes=4, extra_bytes=2):
     """binary_io.py:135-197 -> (remaining message bits incl. padding, extras,
-    extra_var_bits, var_length_extras)."""
+    extra_var_bits, var_length_extras).
+
+    Parsed section by section from the file's bytes: ``extras_bytes``-byte
+    big-endian extras; for each variable bit string an ``extra_bytes``-byte bit
+    length and its bits, padded to a byte; for each integer list an
+    ``extra_bytes``-byte length, a one-byte width w and its w-bit LSB-first
+    values, padded to a byte; the rest of the file is the message."""
     with open(path, "rb") as f:
-        raw = np.frombuffer(f.read(), dtype=np.uint8)
-    compressed = (np.unpackbits(raw) + ord("0")).tobytes().decode("ascii") if raw.size else ""
-    extra_bits = compressed[:num_extras * extras_bytes * 8]
-    compressed = compressed[num_extras * extras_bytes * 8:]
-    extras = [int('0b' + extra_bits[s:s + extras_bytes * 8], 2)
-              for s in range(0, num_extras * extras_bytes * 8, extras_bytes * 8)]
+        cur = _ByteCursor(f.read())
+    extras = [cur.uint(extras_bytes) for _ in range(num_extras)]
     extra_var_bits = []
     for _ in range(num_extra_var_bits):
-        bits_length = int('0b' + compressed[:extra_bytes * 8], 2)
-        compressed = compressed[extra_bytes * 8:]
-        bytes_to_read = bits_length // 8 + (1 if bits_length % 8 else 0)
-        extra_var_bits.append(compressed[:bits_length])
-        compressed = compressed[bytes_to_read * 8:]
+        extra_var_bits.append(_chars(cur.bits(cur.uint(extra_bytes))))
     var_length_extras = []
     for _ in range(num_var_length_extras):
-        extra_length = int('0b' + compressed[:extra_bytes * 8], 2)
-        extra_bit_size = int('0b' + compressed[extra_bytes * 8:(extra_bytes + 1) * 8], 2)
-        compressed = compressed[(extra_bytes + 1) * 8:]
-        bytes_to_read = extra_bit_size * extra_length // 8
-        if extra_bit_size * extra_length % 8 != 0:
-            bytes_to_read += 1
-        extra = [from_bit_string(compressed[s:s + extra_bit_size])
-                 for s in range(0, bytes_to_read * 8, extra_bit_size)]
-        compressed = compressed[bytes_to_read * 8:]
-        var_length_extras.append(extra[:extra_length])
-    return compressed, extras, extra_var_bits, var_length_extras
+        n, w = cur.uint(extra_bytes), cur.uint(1)
+        if w == 0:  # the reference's slicing loop has step 0 here (ValueError)
+            raise ValueError("integer list of bit width 0")
+        flags = cur.bits(n * w).astype(np.int64).reshape(n, w)
+        weights = np.int64(1) << np.arange(w, dtype=np.int64)  # LSB first (from_bit_string)
+        var_length_extras.append([int(v) for v in (flags * weights).sum(axis=1)])
+    rest = cur.bits(8 * (len(cur.data) - cur.pos))
+    return _chars(rest), extras, extra_var_bits, var_length_extras

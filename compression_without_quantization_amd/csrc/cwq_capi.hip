@@ -19,6 +19,7 @@
 #include <vector>
 
 #include "../../include/cwq.h"
+#include "cwq_debug.h"
 #include "cwq_kernels.h"
 
 namespace {
@@ -55,8 +56,10 @@ struct WsLayout {
 // only keys + the per-dim shard constants; everything else (CSR, other d) also
 // gets the general pruned kernel's screening constants and the screened small-candidate
 // path's survivor slots (20 B/dim + 244 B/block),
-// and, when some block may exceed CWQ_CSR_LDS_DIMS dims, its visit-order
-// records (32 B/dim + 384 B/block).
+// and, when some block may exceed CWQ_CSR_LDS_DIMS dims, the visit-order
+// records of the long blocks (32 B/dim + 384 B per CWQ_CSR_LDS_DIMS + 1 dims,
+// csr_rec_entries: short blocks take no room, so a grouped call sized for
+// D + 1 possible groups does not pay 384 B for each).
 bool uniform_fast(int64_t d) { return d % 8 == 0 && d >= 8 && d <= 64; }
 
 WsLayout ws_layout(int64_t nb, int64_t total_dims, bool csr, bool recs) {
@@ -90,7 +93,7 @@ WsLayout ws_layout(int64_t nb, int64_t total_dims, bool csr, bool recs) {
     o = align_up(o + (size_t)nb * 4 * CWQ_CSR_GTAU_STRIDE, 256);
     if (l.recs) {
       l.abp = o;
-      o = align_up(o + (size_t)(total_dims + 12 * nb) * 32, 256);
+      o = align_up(o + (size_t)cwq::csr_rec_entries(total_dims) * 32, 256);
     }
   }
   l.total = o;
@@ -394,7 +397,7 @@ int set_error(int code, const char* msg) { return fail(code, "%s", msg); }
 
 extern "C" {
 
-int cwq_version(void) { return (0 << 16) | 1; }
+int cwq_version(void) { return CWQ_ABI_VERSION; }
 
 const char* cwq_last_error(void) { return g_err; }
 
@@ -811,8 +814,14 @@ int64_t cwq_code_grouped_greedy_batch(
     auto work = [&]() {
       for (int64_t i = next++; i < n_items; i = next++) fn(i);
     };
+    // thread creation may fail (pids cgroup, RLIMIT_NPROC): the exception must
+    // not cross the C ABI, so the threads that did start and this one share
+    // the items, down to the calling thread alone
     std::vector<std::thread> pool;
-    for (int64_t t = 1; t < nthr; ++t) pool.emplace_back(work);
+    try {
+      for (int64_t t = 1; t < nthr; ++t) pool.emplace_back(work);
+    } catch (...) {
+    }
     work();
     for (auto& th : pool) th.join();
   };

@@ -17,6 +17,18 @@ int set_error(int code, const char* msg);
                                // screening constants in LDS (longer: abp records)
 #endif
 
+// First entry of a long block's visit-order records (abp, 32 B per entry) for a
+// block at absolute dim offset off.  Only blocks of more than CWQ_CSR_LDS_DIMS
+// dims have records, and two of them start at least CWQ_CSR_LDS_DIMS + 1 dims
+// apart, so each gets a disjoint region of d + 12 entries here and the array
+// needs csr_rec_entries(total_dims) entries however many short blocks there are.
+__host__ __device__ inline int64_t csr_rec_base(int64_t off) {
+  return off + 12 * (off / (CWQ_CSR_LDS_DIMS + 1));
+}
+__host__ __device__ inline int64_t csr_rec_entries(int64_t total_dims) {
+  return total_dims + 12 * (total_dims / (CWQ_CSR_LDS_DIMS + 1) + 1);
+}
+
 struct EncodeArgs {
   const float* t_loc;
   const float* t_scale;

@@ -822,7 +822,7 @@ __global__ void __launch_bounds__(256) k_csr_prep(
             e[2 * t] = ab.x;
             e[2 * t + 1] = ab.y;
           }
-          float4* rr = abp + 2 * (reg + c * cs + k);
+          float4* rr = abp + 2 * (csr_rec_base(off) + c * cs + k);
           rr[0] = float4{e[0], e[1], e[2], e[3]};
           rr[1] = float4{e[4], e[5], e[6], e[7]};
         }
@@ -1360,7 +1360,7 @@ __global__ void __launch_bounds__(256, COOP ? CWQ_CSR_COOP_MIN_WAVES : CWQ_CSR_R
             if (in_lds)
               run_coop(l_ab, l_bp, l_ord, nullptr, NoRec{});
             else if (abp)
-              run_coop(nullptr, bpre + reg, ordu + reg, abp + 2 * reg, Rec{});
+              run_coop(nullptr, bpre + reg, ordu + reg, abp + 2 * csr_rec_base(off), Rec{});
             else
               run_coop(sab + off + 8 * g, bpre + reg, ordu + reg, nullptr, NoRec{});
           } else {  // d < coop_min_d <= CWQ_CSR_LDS_DIMS: the constants are in LDS
@@ -1369,7 +1369,7 @@ __global__ void __launch_bounds__(256, COOP ? CWQ_CSR_COOP_MIN_WAVES : CWQ_CSR_R
         } else if (in_lds)
           run(l_ab, l_bp, l_ord, nullptr, NoRec{});
         else if (abp)
-          run(nullptr, bpre + reg, ordu + reg, abp + 2 * reg, Rec{});
+          run(nullptr, bpre + reg, ordu + reg, abp + 2 * csr_rec_base(off), Rec{});
         else
           run(sab + off + 8 * g, bpre + reg, ordu + reg, nullptr, NoRec{});
         __syncthreads();
@@ -2381,7 +2381,7 @@ hipError_t launch_encode(const EncodeArgs& a, hipStream_t stream) {
     if (a.ordu) p.ordu = a.ordu + 12 * g0;
     if (a.grp) p.grp = a.grp + g0;
     if (a.gtau) p.gtau = a.gtau + g0 * CWQ_CSR_GTAU_STRIDE;
-    if (a.abp) p.abp = a.abp + 2 * 12 * g0;
+    // abp is indexed by absolute dim offset alone (csr_rec_base): unshifted
     if (a.slist) p.slist = a.slist + CWQ_SLIST_PER_BLOCK * g0;
     if ((e = hipStreamWaitEvent(f->s[i], f->fork, 0)) != hipSuccess) break;
     forked = i + 1;

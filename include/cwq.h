@@ -63,7 +63,12 @@ extern "C" {
 
 #define CWQ_MAX_BITS_PER_STEP 30
 
-/* Library version, (major << 16) | minor. */
+/* ABI version, (major << 16) | minor.  0.2: per-call cwq_options before the
+ * stream in the encoders, a max_block_dim argument to
+ * cwq_greedy_encode_workspace_size, no process-wide tuning setters.  Bindings
+ * must refuse a library whose cwq_version() differs from the header they were
+ * written against. */
+#define CWQ_ABI_VERSION ((0 << 16) | 2)
 int cwq_version(void);
 
 /* Thread-local description of the last error ("" if none). */
@@ -99,7 +104,8 @@ typedef struct cwq_options {
  * holding total_dims dims in all, none longer than max_block_dim: the argmax
  * keys and per-dim shard constants plus the general pruned kernel's per-step
  * screening constants (20 B/dim + 244 B/block) and, when max_block_dim > 1024,
- * their visit-order copies for the long blocks (32 B/dim + 384 B/block).  A
+ * their visit-order copies for the long blocks (32 B/dim + 384 B per 1025
+ * dims).  A
  * CSR call given less returns CWQ_ERR_WORKSPACE (it never silently falls back
  * to a slower kernel). */
 size_t cwq_greedy_encode_workspace_size(int64_t nb, int64_t total_dims, int64_t max_block_dim);
@@ -325,15 +331,6 @@ int cwq_selftest_div(const float* a, const float* b, int64_t n, float* out, void
  * shares its threshold with. */
 int cwq_selftest_wave_max(const float* x, int64_t n_waves, float* out, void* stream);
 
-/* Tuning counters of the pruned encoder, filled only by builds compiled with
- * -DCWQ_PRUNE_STATS (tools/prune_stats.py); returns 1 there, 0 (and zeros)
- * otherwise.  out72[k] = candidates finished after k units (k <= 64),
- * [65] completed rows, [66] survivors pushed, [67] tiles on the screening pass,
- * [68] survivors re-evaluated exactly at tile end, [69] in-loop exact evaluations.
- * flags: bit 0 resets the counters; bit 1 / bit 2 switch the "oracle tau"
- * experiment on / off (later launches start each tile at the best value the
- * last launch found for it). */
-int cwq_debug_prune_stats(unsigned long long* out72, int flags);
 
 
 /* ---- PLN image codec plumbing (csrc/cwq_pln.hip) ----

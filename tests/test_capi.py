@@ -102,3 +102,25 @@ def test_missing_library_fails_loudly(tmp_path):
     out = subprocess.run([sys.executable, "-c", code], cwd=REPO, env=env,
                          capture_output=True, text=True, timeout=120)
     assert "raised" in out.stdout, (out.stdout, out.stderr)
+
+
+def test_abi_version_checked(cwqlib, tmp_path):
+    """The header's CWQ_ABI_VERSION, the bindings' and the library's agree, and
+    a library reporting another version is refused at load time even when
+    selected through CWQ_LIB_PATH (its argument lists would differ)."""
+    import subprocess
+    import sys
+    with open(os.path.join(REPO, "include", "cwq.h")) as f:
+        m = re.search(r"#define CWQ_ABI_VERSION \(\((\d+) << 16\) \| (\d+)\)", f.read())
+    assert m, "CWQ_ABI_VERSION missing from include/cwq.h"
+    hdr = (int(m.group(1)) << 16) | int(m.group(2))
+    assert hdr == _lib.ABI_VERSION == cwqlib.cwq_version()
+    src = tmp_path / "old.c"
+    src.write_text("int cwq_version(void) { return 1; }\n")
+    so = tmp_path / "libold.so"
+    subprocess.check_call(["gcc", "-shared", "-fPIC", "-o", str(so), str(src)])
+    code = ("from compression_without_quantization_amd import _lib\n"
+            "try:\n    _lib.load()\nexcept ImportError as e:\n    print('refused', e)\n")
+    r = subprocess.run([sys.executable, "-c", code], cwd=REPO, capture_output=True, text=True,
+                       env=dict(os.environ, CWQ_LIB_PATH=str(so)), timeout=120)
+    assert "refused" in r.stdout and "ABI version 0.1" in r.stdout, r.stdout + r.stderr

@@ -104,3 +104,31 @@ def test_bin_code_roundtrip_and_layout(tmp_path):
     assert to_bit_string(3, 8) == "11000000"
     with pytest.raises(Exception, match="bitlength associated"):
         write_bin_code("1", str(p), var_length_extras=[[1]], var_length_bits=None)
+
+
+def test_bin_code_random_sections_roundtrip(tmp_path):
+    """read_bin_code's byte-cursor parser inverts write_bin_code on random
+    containers: empty and odd-length bit strings, 1..24-bit integer lists
+    (lengths 0..40, so padding ends mid-byte and on a byte), an empty message;
+    a truncated file raises instead of returning short sections."""
+    rng = np.random.default_rng(11)
+    p = tmp_path / "r.miracle"
+    for trial in range(60):
+        ne, nv, nl = (int(x) for x in rng.integers(0, 4, 3))
+        extras = [int(x) for x in rng.integers(0, 2**32, ne, dtype=np.uint64)]
+        evb = [''.join(rng.choice(['0', '1'], int(rng.integers(0, 70)))) for _ in range(nv)]
+        vlb = [int(x) for x in rng.integers(1, 25, nl)]
+        vle = [[int(v) for v in rng.integers(0, 2**w, int(rng.integers(0, 41)))] for w in vlb]
+        code = ''.join(rng.choice(['0', '1'], int(rng.integers(0, 200))))
+        write_bin_code(code, str(p), extras=extras, extra_var_bits=evb, var_length_extras=vle,
+                       var_length_bits=vlb)
+        msg, ex, vb, vl = read_bin_code(str(p), num_extras=ne, num_extra_var_bits=nv,
+                                        num_var_length_extras=nl)
+        assert ex == extras and vb == evb and vl == vle, trial
+        assert msg[:len(code)] == code and set(msg[len(code):]) <= {"0"} and len(msg) % 8 == 0
+        assert len(msg) - len(code) < 8
+    write_bin_code("1", str(p), extra_var_bits=["1" * 40])
+    raw = p.read_bytes()
+    p.write_bytes(raw[:4])  # 2-byte length 40, then only 2 of its 5 bytes
+    with pytest.raises(ValueError, match="truncated"):
+        read_bin_code(str(p), num_extra_var_bits=1)

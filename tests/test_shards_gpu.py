@@ -273,8 +273,9 @@ def test_bench_weak_scaling_two_ranks(cwq):
     (3, 32, 1, 3, 0),           # one block per chunk
 ])
 def test_encode_blocks_host_streamed_equals_one_call(cwq, nb, d, chunk, n_steps, base):
-    """encode_blocks_host (pinned staging, H2D / compute / D2H on three
-    streams, chunk c coded with block_id_base = base + c * chunk) equals one
+    """encode_blocks_host (copies straight from and to the caller's pageable
+    arrays on a copy stream, coding on the compute stream, two device buffer
+    slots; chunk c coded with block_id_base = base + c * chunk) equals one
     encode_blocks call over all blocks, bit for bit."""
     rng = np.random.default_rng(nb * d + chunk)
     tl = rng.standard_normal(nb * d).astype(np.float32)
