@@ -102,6 +102,9 @@ def parse():
     ap.add_argument("--no-e2e", action="store_true")
     ap.add_argument("--per-image", action="store_true",
                     help="grouped configs: time one call per latent set only (no batched call)")
+    ap.add_argument("--batch-only", action="store_true",
+                    help="grouped configs of several latent sets: time the batched call only "
+                         "(profiling runs: every scoring dispatch belongs to it)")
     ap.add_argument("--prune-mode", type=int, default=2, choices=(0, 1, 2),
                     help="0 unpruned, 1 exact pruning, 2 pruning + screening (default)")
     ap.add_argument("--scaling", choices=("strong", "weak"), default=None,
@@ -115,7 +118,11 @@ def parse():
 def grouped_main(args):
     """C2/C3: the whole grouped pipeline per image (code_grouped_greedy_sample):
     standardise + KL on the GPU, host grouping, encode, bitcode.  Synthetic
-    PLN-like latents (no Kodak images or checkpoints offline)."""
+    PLN-like latents (no Kodak images or checkpoints offline).  The line's
+    roofline prices the candidate-scoring launches (HIP events recorded by the
+    library around them, every call of the timed steps), cpu_baseline the
+    oracle on image 0's latent sets (a prefix of its groups where the whole set
+    would take too long)."""
     import compression_without_quantization_amd.coded_greedy_sampler as S
     from compression_without_quantization_amd.synthetic import make_latents
     S.VERBOSE = False
@@ -124,47 +131,107 @@ def grouped_main(args):
     bpd = GROUPED[args.config][5] if len(GROUPED[args.config]) > 5 else 1.1
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
-    lat = []
+    lat, lat_np = [], []
     for i in range(n_img):
         for li, D in enumerate(dims):
             q_loc, q_scale, p_loc, p_scale = make_latents(D, bits_per_dim=bpd, seed=1000 * i + li)
+            if i == 0:
+                lat_np.append((q_loc, q_scale, p_loc, p_scale))
             lat.append((C.Normal(torch.from_numpy(q_loc).to(dev), torch.from_numpy(q_scale).to(dev)),
                         C.Normal(torch.from_numpy(p_loc).to(dev), torch.from_numpy(p_scale).to(dev))))
+    evq = []  # (start, stop) event pairs of the timed calls
 
-    def step_single():  # one code_grouped_greedy_sample call per latent set
+    def ev():
+        if evq is None:
+            return None
+        a = torch.cuda.Event(enable_timing=True)
+        b = torch.cuda.Event(enable_timing=True)
+        a.record()
+        b.record()  # materialise the hipEvent_t handles
+        evq.append((a, b))
+        return (a.cuda_event, b.cuda_event)
+
+    def step_single(timed_events=False):  # one code_grouped_greedy_sample call per latent set
         out = []
         for target, proposal in lat:
-            out.append(C.code_grouped_greedy_sample(None, target, proposal, n_steps, bits, 42))
+            out.append(C.code_grouped_greedy_sample(None, target, proposal, n_steps, bits, 42,
+                                                    eval_events=ev() if timed_events else None))
         return out
 
-    def step_batch():  # every latent set of the step in one batched call
+    def step_batch(timed_events=False):  # every latent set of the step in one batched call
         return C.code_grouped_greedy_sample_batch(None, [t for t, _ in lat], [p for _, p in lat],
-                                                  n_steps, bits, 42)
+                                                  n_steps, bits, 42,
+                                                  eval_events=ev() if timed_events else None)
 
     def timed(step):
         for _ in range(args.warmup):
             step()
         torch.cuda.synchronize()
+        evq.clear()
         t0 = time.perf_counter()
         for _ in range(args.steps):
-            res = step()
+            res = step(True)
         torch.cuda.synchronize()
-        return time.perf_counter() - t0, res
+        el = time.perf_counter() - t0
+        kms = sum(a.elapsed_time(b) for a, b in evq) / max(args.steps, 1)
+        return el, res, kms
 
-    el_single, res = timed(step_single)
-    el = el_single
-    batched = None
-    if len(lat) > 1 and not args.per_image:
-        el, res_b = timed(step_batch)
+    batch = len(lat) > 1 and not args.per_image
+    if batch and args.batch_only:
+        el, res, kernel_ms = timed(step_batch)
+        batched = {"latent_sets_per_call": len(lat), "equal_to_single_calls": None,
+                   "single_call_images_per_s": None}
+    else:
+        el_single, res, kms_single = timed(step_single)
+        el, kernel_ms = el_single, kms_single
+        batched = None
+    if batch and not args.batch_only:
+        el, res_b, kernel_ms = timed(step_batch)
         same = all(list(a[2]) == list(b[2]) and a[1] == b[1] and
                    np.array_equal(np.asarray(a[0]).view(np.uint32), np.asarray(b[0]).view(np.uint32))
                    for a, b in zip(res, res_b))
         batched = {"latent_sets_per_call": len(lat), "equal_to_single_calls": bool(same),
-                   "single_call_images_per_s": n_img * args.steps / el_single}
+                   "single_call_images_per_s": n_img * args.steps / el_single,
+                   "single_call_scoring_kernel_ms": round(kms_single, 4)}
         if not same:
             raise SystemExit("bench.py: batched results differ from the single calls")
     groups = sum(len(r[2]) - 1 for r in res)
     bitlen = sum(len(r[1]) for r in res)
+    D_step = sum(int(t.loc.numel()) for t, _ in lat)
+    # SURVEY.md 8(d) per group: 16 d (four f32 inputs) + 4 n_steps (indices) + 4 d (sample)
+    alg = 20 * D_step + 4 * groups * n_steps
+    cand_dims = (1 << bits) * n_steps * D_step
+    achieved = alg / (kernel_ms * 1e-3) / 1e9
+    traffic = valu = None
+    tf = os.path.join(REPO, "profiles", f"traffic_{args.config}.json")
+    if os.path.exists(tf):
+        with open(tf) as f:
+            tj = json.load(f)
+        if tj.get("blocks") == groups:
+            traffic = tj.get("hbm_bytes_per_launch")
+            valu = tj.get("valu")
+    small = 64 <= (1 << bits) < 4096
+    roofline = {"bound": "valu", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS,
+                "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                "hbm_note": "achieved/peak/frac/traffic price the scoring launches' algorithmic "
+                            "bytes (20 d + 4 n_steps per group) against HBM, as the north star "
+                            "asks; the launches are bound by VALU issue (Philox + Box-Muller "
+                            "per candidate), see `valu` and DESIGN.md 5c/5d",
+                "kernel": ("k_small_prep + k_small_screen + k_small_survivors" if small else
+                           "k_csr_prep + k_encode_prune_csr (+ finalize between steps)"),
+                "kernel_ms": round(kernel_ms, 4),
+                "kernel_timing": "HIP events the library records on the call's stream around "
+                                 "its candidate-scoring launches, summed over the calls of a step",
+                "algorithmic_bytes_per_launch": alg,
+                "valu": {"unit": "candidate-dims/s",
+                         "nominal_candidate_dims_per_s": cand_dims / (kernel_ms * 1e-3),
+                         "valu_issue_frac": (valu or {}).get("valu_issue_frac"),
+                         "valu_issue_source": "profiles/traffic_%s.json (rocprofv3 --pmc "
+                                              "SQ_INSTS_VALU GRBM_GUI_ACTIVE, the scoring "
+                                              "kernels)" % args.config if valu else None}}
+    cpu = parity = None
+    if not args.no_cpu:
+        cpu, parity = grouped_cpu_baseline(args, lat_np, res[:len(dims)], bits, n_steps)
     line = {"metric": "images coded/s (grouped greedy pipeline)", "value": n_img * args.steps / el,
             "unit": "images/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": el / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
@@ -174,8 +241,85 @@ def grouped_main(args):
                        "mode": ("code_grouped_greedy_sample_batch: every latent set of a step "
                                 "in one call" if batched else
                                 "one code_grouped_greedy_sample call per latent set"),
-                       "batched": batched}}
+                       "batched": batched},
+            "roofline": roofline, "cpu_baseline": cpu, "parity": parity}
     print(json.dumps(line), flush=True)
+
+
+def grouped_cpu_baseline(args, lat_np, res0, bits, n_steps):
+    """The CPU oracle on image 0 of a grouped config (its latent sets lat_np,
+    the GPU's results res0 for them): the whole pipeline
+    (oracle.code_grouped_greedy_sample) where image 0 fits ~cpu_seconds on
+    every usable CPU, else the coder on a prefix of each set's groups (the
+    GPU's partition) with the rate scaled by the prefix's share of the image's
+    candidate-dims.  The sampled groups' indices and sample words are checked
+    against the GPU's."""
+    from oracle import oracle as O
+    from compression_without_quantization_amd.binary_io import bitcode_to_indices
+    from compression_without_quantization_amd.coded_greedy_sampler import group_size_threshold
+    ncpu, quota = affinity_cores()
+    nthr = min(ncpu, int(np.ceil(quota))) if quota else ncpu
+    thr = group_size_threshold(12)
+    sets = []
+    for (ql, qs, pl, ps), (gs, gcode, gst) in zip(lat_np, res0):
+        st = np.asarray(gst, dtype=np.int64)
+        gidx = bitcode_to_indices(gcode, bits, (st.size - 1) * n_steps).reshape(-1, n_steps)
+        sets.append((ql, qs, pl, ps, np.asarray(gs), gidx, st))
+    work = [float(np.diff(st).sum()) * (1 << bits) * n_steps for *_, st in sets]
+
+    def prefix(k_frac, threads):
+        """Code the first k_frac of each set's groups; (seconds, cand-dims, mism)."""
+        t_all = cd = 0.0
+        mi = ms = 0
+        for (ql, qs, pl, ps, gs, gidx, st) in sets:
+            G = st.size - 1
+            k = max(1, int(round(G * k_frac)))
+            e = int(st[k])
+            tl, ts = O.standardise(ql[:e], qs[:e], pl[:e], ps[:e])
+            c0 = time.perf_counter()
+            wi, wsm = O.greedy_encode(tl, ts, np.zeros(e, np.float32), np.ones(e, np.float32),
+                                      st[:k + 1], bits, n_steps, 42, 1.0, 0, threads)
+            t_all += time.perf_counter() - c0
+            smp = O.destandardise(wsm, pl[:e], ps[:e])
+            mi += int((wi != gidx[:k]).sum())
+            ms += int((smp.view(np.uint32) != gs[:e].view(np.uint32)).sum())
+            cd += float(e) * (1 << bits) * n_steps
+        return t_all, cd, mi, ms
+    # calibrate on ~1% of the groups, then size the sample to ~cpu_seconds
+    dt, cd, _, _ = prefix(0.01, nthr)
+    full_s = dt * sum(work) / max(cd, 1.0)
+    if full_s <= args.cpu_seconds:
+        c0 = time.perf_counter()
+        mi = ms = 0
+        for (ql, qs, pl, ps, gs, gidx, st) in sets:
+            wsm, wi, wst = O.code_grouped_greedy_sample(ql, qs, pl, ps, n_steps, bits, 42, thr,
+                                                        1.0, nthr)
+            mi += int(len(wst) != st.size or (np.asarray(wst) != st).any())
+            mi += int((np.asarray(wi).reshape(-1, n_steps) != gidx).sum()) \
+                if len(wst) == st.size else 0
+            ms += int((wsm.view(np.uint32) != gs.view(np.uint32)).sum())
+        dt = time.perf_counter() - c0
+        frac, kind = 1.0, "the whole pipeline (oracle.code_grouped_greedy_sample: standardise, " \
+                          "KL, partition, coder, destandardise)"
+    else:
+        frac = min(1.0, args.cpu_seconds / full_s)
+        dt, cd, mi, ms = prefix(frac, nthr)
+        frac = cd / sum(work)
+        kind = (f"the coder (oracle.greedy_encode) on the first {frac:.2%} of each latent "
+                "set's candidate-dims (the GPU's partition); rate scaled by that share")
+    # 1 core on a short prefix (~3 s)
+    f1 = min(frac, 3.0 / max(full_s * nthr, 1e-9))
+    dt1, cd1, _, _ = prefix(max(f1, 1e-4), 1)
+    one_core = (cd1 / sum(work)) / dt1
+    cpu = {"value": frac / dt, "unit": "images/s", "cores": nthr, "kind": "port",
+           "sample": f"image 0 ({len(sets)} latent set(s), {sum(work):.3g} candidate-dims): "
+                     f"{kind}, {dt:.1f} s, oracle/cwq_oracle.c OpenMP over groups",
+           "affinity_cpus": ncpu, "cgroup_cpu_quota": quota, "one_core_value": one_core,
+           "one_core_sample": f"{cd1 / sum(work):.3%} of image 0's candidate-dims, {dt1:.1f} s"}
+    parity = {"groups_checked": int(round(sum(st.size - 1 for *_, st in sets) * frac)),
+              "index_mismatches": mi, "sample_word_mismatches": ms,
+              "oracle": "oracle/cwq_oracle.c (CPU restatement; TF reference unpinned)"}
+    return cpu, parity
 
 
 def importance_main(args):

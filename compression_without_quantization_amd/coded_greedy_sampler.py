@@ -317,12 +317,15 @@ def _dist_parts(dist, dev, what):
 
 def code_grouped_greedy_sample(sess, target, proposal, n_steps, n_bits_per_step, seed,
                                max_group_size_bits=12, adaptive=True, backfitting_steps=0,
-                               use_log_prob=False, rho=1., *, prune_mode=None):
+                               use_log_prob=False, rho=1., *, prune_mode=None,
+                               eval_events=None):
     """coded_greedy_sampler.py:170-296.
 
     Returns (sample np.float32 [D], bitcode str, group_start_indices list).
     ``prune_mode`` (keyword only, not in the reference): the encoder's
-    cwq_options.prune_mode; results never depend on it.
+    cwq_options.prune_mode; results never depend on it.  ``eval_events``
+    (keyword only): (start, stop) hipEvent_t handles recorded around the
+    candidate-scoring launches (bench.py's kernel timer).
     """
     lib = _lib.load()
     dev = _device_of(target.loc, target.scale, proposal.loc, proposal.scale)
@@ -354,7 +357,7 @@ def code_grouped_greedy_sample(sess, target, proposal, n_steps, n_bits_per_step,
             seed32, float(rho), group_size_threshold(max_group_size_bits), float(n_nats),
             sample_h.ctypes.data, bits_h.ctypes.data, bits_h.size, starts_h.ctypes.data,
             starts_h.size, ctypes.byref(kl_sum) if VERBOSE else None, ws.data_ptr(), ws.numel(),
-            _lib.options(prune_mode), stream),
+            _lib.options(prune_mode, eval_events), stream),
             "cwq_code_grouped_greedy")
     if VERBOSE:
         total_kl_bits = kl_sum.value / np.log(2)
@@ -369,7 +372,8 @@ def code_grouped_greedy_sample(sess, target, proposal, n_steps, n_bits_per_step,
 
 def code_grouped_greedy_sample_batch(sess, targets, proposals, n_steps, n_bits_per_step, seeds,
                                      max_group_size_bits=12, adaptive=True, backfitting_steps=0,
-                                     use_log_prob=False, rho=1., *, prune_mode=None):
+                                     use_log_prob=False, rho=1., *, prune_mode=None,
+                                     eval_events=None):
     """code_grouped_greedy_sample (coded_greedy_sampler.py:170-296) for a batch
     of independent items (the images of a dataset, the ladder levels of several
     images) in one native call (cwq_code_grouped_greedy_batch).
@@ -431,7 +435,7 @@ def code_grouped_greedy_sample_batch(sess, targets, proposals, n_steps, n_bits_p
             group_size_threshold(max_group_size_bits), float(n_nats), sample_h.ctypes.data,
             bits_h.ctypes.data, bits_h.size, bits_off.ctypes.data, starts_h.ctypes.data,
             starts_h.size, n_starts.ctypes.data, ws.data_ptr(), ws.numel(),
-            _lib.options(prune_mode), stream), "cwq_code_grouped_greedy_batch")
+            _lib.options(prune_mode, eval_events), stream), "cwq_code_grouped_greedy_batch")
     out = []
     for i in range(n_items):
         a, b = int(item_off[i]), int(item_off[i + 1])

@@ -1,11 +1,23 @@
 """Turn tools/profile.sh output into the committed evidence under profiles/.
-Usage: python tools/collect_profile.py TAG CONFIG BLOCKS KERNEL_SUBSTR ALG_BYTES"""
+Usage: python tools/collect_profile.py TAG CONFIG KERNEL_SUBSTR [BLOCKS ALG_BYTES]
+KERNEL_SUBSTR selects the priced kernels (every dispatch whose name contains
+it, counters summed: "k_small_" takes prep + screen + survivors).  BLOCKS (the
+blocks or groups of one launch) and ALG_BYTES default to the bench line of the
+trace run (config.blocks_per_gpu / groups_per_step, roofline's algorithmic
+bytes)."""
 import csv, glob, json, os, shutil, sys
 
-tag, config, blocks, ksub, alg = sys.argv[1], sys.argv[2], int(sys.argv[3]), sys.argv[4], int(sys.argv[5])
+tag, config, ksub = sys.argv[1], sys.argv[2], sys.argv[3]
 root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 src = os.path.join(root, "gpurun_out", "prof_" + tag)
 dst = os.path.join(root, "profiles")
+if len(sys.argv) > 5:
+    blocks, alg = int(sys.argv[4]), int(sys.argv[5])
+else:
+    line = [ln for ln in open(os.path.join(src, "trace.log")) if ln.startswith('{"metric"')][-1]
+    bl = json.loads(line)
+    blocks = bl["config"].get("blocks_per_gpu", bl["config"].get("groups_per_step"))
+    alg = bl["roofline"]["algorithmic_bytes_per_launch"]
 
 
 def one(pattern):
