@@ -236,6 +236,12 @@ __global__ void __launch_bounds__(256, CWQ_PRUNE_MIN_WAVES) k_encode_prune(
   __shared__ uint32_t sq_n[CWQ_SURVIVOR_CAP];
   __shared__ float sq_ub[CWQ_SURVIVOR_CAP];
   __shared__ unsigned long long wkey[4];
+#ifdef CWQ_PRUNE_STATS
+  // per-workgroup counters (LDS atomics), added to g_prune_stats once per tile:
+  // one global atomic per finished candidate made C5-sized runs take minutes
+  __shared__ uint32_t s_ps[72];
+  for (int i = threadIdx.x; i < 72; i += blockDim.x) s_ps[i] = 0u;
+#endif
   fill_logtab(logtab);
   const uint32_t wv = wave_id();
   const uint32_t lane = threadIdx.x & 63u;
@@ -493,9 +499,9 @@ __global__ void __launch_bounds__(256, CWQ_PRUNE_MIN_WAVES) k_encode_prune(
         }
         const bool done = complete || prune || !active;
 #ifdef CWQ_PRUNE_STATS
-        if (active && (complete || prune)) atomicAdd(&g_prune_stats[k], 1ull);
-        if (active && complete) atomicAdd(&g_prune_stats[65], 1ull);
-        if (active && complete && upper >= tau) atomicAdd(&g_prune_stats[66], 1ull);
+        if (active && (complete || prune)) atomicAdd(&s_ps[k], 1u);
+        if (active && complete) atomicAdd(&s_ps[65], 1u);
+        if (active && complete && upper >= tau) atomicAdd(&s_ps[66], 1u);
 #endif
         const uint64_t m = __ballot(done);
         const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
@@ -555,6 +561,12 @@ __global__ void __launch_bounds__(256, CWQ_PRUNE_MIN_WAVES) k_encode_prune(
       if (!g_seed_tau && g < kDbgBlocks) g_dbg_best[g] = mk;
 #endif
     }
+#ifdef CWQ_PRUNE_STATS
+    if (tid < 72) {
+      if (s_ps[tid]) atomicAdd(&g_prune_stats[tid], (unsigned long long)s_ps[tid]);
+      s_ps[tid] = 0u;
+    }
+#endif
     __syncthreads();
   }
 }
