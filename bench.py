@@ -513,6 +513,31 @@ def affinity_cores():
     return n, quota
 
 
+def rank_device_map(dist, rank, local_rank, dev):
+    """[{rank, local_rank, host, device, pci_bus}] of every rank (all-gathered);
+    with RCCL (one GPU per rank) two ranks on one GPU are refused."""
+    import socket
+    props = torch.cuda.get_device_properties(dev)
+    me = {"rank": rank, "local_rank": local_rank, "host": socket.gethostname(),
+          "device": dev.index, "pci_bus": getattr(props, "pci_bus_id", None),
+          "visible": os.environ.get("HIP_VISIBLE_DEVICES",
+                                    os.environ.get("CUDA_VISIBLE_DEVICES"))}
+    if dist is None:
+        return [me]
+    allm = [None] * dist.get_world_size()
+    dist.all_gather_object(allm, me)
+    if dist.get_backend() == "nccl":
+        seen = {}
+        for m in allm:
+            key = (m["host"], m["pci_bus"] if m["pci_bus"] is not None else
+                   (m["visible"], m["device"]))
+            if key in seen:
+                raise SystemExit(f"bench.py: ranks {seen[key]} and {m['rank']} share GPU {key} "
+                                 "under RCCL; one GPU per rank is required")
+            seen[key] = m["rank"]
+    return allm
+
+
 def oracle_check(O, host, d, bits, n_steps, seed, block_id_base, idx_h, samp_h, blocks, nthr):
     """Indices and sample words of `blocks` (local block numbers) against the
     CPU oracle: the checker, outside every timed region."""
@@ -564,6 +589,7 @@ def main():
         if dist.get_world_size() != args.gpus:
             raise SystemExit(f"bench.py: process group has {dist.get_world_size()} ranks, "
                              f"--gpus {args.gpus}")
+    rank_devices = rank_device_map(dist, rank, local_rank, dev)
 
     nb_cfg, d, bits, n_steps, desc = CONFIGS[args.config]
     if args.blocks:
@@ -688,6 +714,17 @@ def main():
     bytes_per_launch = nb * (20 * d + 4 * n_steps)
     cand = nb * n_steps * (1 << bits)
     cand_dims = cand * d
+    rank0_kernel = {"blocks": nb, "algorithmic_bytes_per_launch": bytes_per_launch,
+                    "kernel_ms": round(eval_ms, 3)}
+    if dist:
+        # the job's roofline: every rank's launch bytes and candidate-dims
+        # summed, over the slowest rank's kernel time (each rank's GPU runs its
+        # shard concurrently)
+        tot = torch.tensor([bytes_per_launch, cand, cand_dims], dtype=torch.float64,
+                           device=dev if dist.get_backend() == "nccl" else "cpu")
+        dist.all_reduce(tot)
+        bytes_per_launch, cand, cand_dims = (int(v) for v in tot.tolist())
+        eval_ms = eval_ms_max
     achieved = bytes_per_launch / (eval_ms * 1e-3) / 1e9
     traffic = None
     valu = None
@@ -726,6 +763,12 @@ def main():
                            if fast else "k_encode_eval"),
                 "kernel_ms": round(eval_ms, 3),
                 "algorithmic_bytes_per_launch": bytes_per_launch,
+                "scope": ("one GPU" if world == 1 else
+                          f"all {world} GPUs: algorithmic bytes and candidate-dims summed "
+                          "over the ranks' launches, kernel_ms the slowest rank's (HIP "
+                          "events on each rank's launch stream, max-reduced); achieved and "
+                          "nominal rates are whole-job, peak is one GPU's"),
+                "rank0": rank0_kernel if world > 1 else None,
                 "valu": {"unit": "candidate-dims/s",
                          "nominal_candidate_dims_per_s": cand_dims / (eval_ms * 1e-3),
                          "evaluated": evaluated,
@@ -830,7 +873,8 @@ def main():
                        "parallelism": f"block-sharded x{world} ({scaling} scaling), "
                                       "no collective on the data path",
                        "world_size_checked": (dist.get_world_size() if dist else 1),
-                       "backend": (dist.get_backend() if dist else None)},
+                       "backend": (dist.get_backend() if dist else None),
+                       "rank_devices": rank_devices},
             "roofline": roofline,
             "cpu_baseline": cpu,
             "parity": parity,

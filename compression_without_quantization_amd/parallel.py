@@ -34,13 +34,30 @@ def shard_range(nb, world_size, rank, cost=None):
     return int(cuts[rank]), int(cuts[rank + 1])
 
 
-def gather_indices(local_idx, nb_per_rank, group=None):
-    """All-gather each rank's int32 index block (ranks own equal block counts).
+def gather_indices(local_idx, nb_per_rank=None, group=None):
+    """All-gather every rank's index block along dim 0, in rank order.
 
-    Works with any torch.distributed backend (RCCL on GPU, gloo on CPU).
+    Ranks may own different block counts (``shard_range`` cuts are uneven, and
+    cost-balanced cuts for ragged groups more so): the row counts are
+    all-gathered first, each rank's block is padded to the largest, gathered,
+    and the padding dropped.  ``nb_per_rank`` is accepted for compatibility and
+    ignored.  Works with any torch.distributed backend (RCCL on GPU, gloo on
+    CPU); the tensors stay on local_idx's device.  This is the optional
+    collective of SURVEY.md 8(e): the coding itself needs none.
     """
     import torch.distributed as dist
     world = dist.get_world_size(group)
-    parts = [torch.empty_like(local_idx) for _ in range(world)]
-    dist.all_gather(parts, local_idx.contiguous(), group=group)
-    return torch.cat(parts, dim=0)
+    x = local_idx.contiguous()
+    n = torch.tensor([x.shape[0]], dtype=torch.int64, device=x.device)
+    sizes = [torch.empty_like(n) for _ in range(world)]
+    dist.all_gather(sizes, n, group=group)
+    sizes = [int(v.item()) for v in sizes]
+    m = max(sizes) if sizes else 0
+    if m == 0:
+        return x[:0]
+    if x.shape[0] < m:
+        pad = torch.zeros((m - x.shape[0],) + tuple(x.shape[1:]), dtype=x.dtype, device=x.device)
+        x = torch.cat([x, pad], dim=0)
+    parts = [torch.empty_like(x) for _ in range(world)]
+    dist.all_gather(parts, x, group=group)
+    return torch.cat([p[:k] for p, k in zip(parts, sizes)], dim=0)

@@ -248,11 +248,26 @@ static inline float stream_normal(normal_stream* st, uint64_t k) {
 }
 
 /* code_greedy_sample for ONE block of d dims (coded_greedy_sampler.py:29-89).
- * out_idx[n_steps], out_sample[d].  Returns 0 on success. */
+ * out_idx[n_steps], out_sample[d].  Returns 0 on success.  log_scale: NULL
+ * (the declared normaliser, glibc logf of t_scale) or the log(sigma_j) to use
+ * instead (normaliser sensitivity, tools/normaliser_sensitivity.py). */
+static int code_greedy_sample_impl(const float* t_loc, const float* t_scale,
+                                   const float* p_loc, const float* p_scale, int64_t d,
+                                   int n_bits_per_step, int n_steps, int32_t seed, float rho,
+                                   const float* log_scale, int32_t* out_idx, float* out_sample);
+
 CWQO_API int cwqo_code_greedy_sample(const float* t_loc, const float* t_scale,
                                      const float* p_loc, const float* p_scale, int64_t d,
                                      int n_bits_per_step, int n_steps, int32_t seed, float rho,
                                      int32_t* out_idx, float* out_sample) {
+  return code_greedy_sample_impl(t_loc, t_scale, p_loc, p_scale, d, n_bits_per_step, n_steps,
+                                 seed, rho, NULL, out_idx, out_sample);
+}
+
+static int code_greedy_sample_impl(const float* t_loc, const float* t_scale,
+                                   const float* p_loc, const float* p_scale, int64_t d,
+                                   int n_bits_per_step, int n_steps, int32_t seed, float rho,
+                                   const float* log_scale, int32_t* out_idx, float* out_sample) {
   if (n_bits_per_step < 0 || n_bits_per_step > 30 || n_steps < 1 || d < 0) return -1;
   int64_t n_samples = (int64_t)1 << n_bits_per_step;
   size_t db = (size_t)(d > 0 ? d : 1) * sizeof(float);
@@ -265,7 +280,9 @@ CWQO_API int cwqo_code_greedy_sample(const float* t_loc, const float* t_scale,
     return -2;
   }
   shard_params(p_loc, p_scale, d, n_steps, rho, loc_s, scale_s);
-  for (int64_t j = 0; j < d; ++j) lognorm[j] = cwqo_log_normalization(t_scale[j]);
+  for (int64_t j = 0; j < d; ++j)
+    lognorm[j] = log_scale ? half_log_2pi_f32() + log_scale[j]
+                           : cwqo_log_normalization(t_scale[j]);
   for (int64_t j = 0; j < d; ++j) out_sample[j] = 0.0f; /* tf.zeros */
 
   for (int i = 0; i < n_steps; ++i) {
@@ -349,6 +366,78 @@ CWQO_API int cwqo_greedy_encode(const float* t_loc, const float* t_scale, const 
     if (rc) err |= 1;
   }
   return err ? -1 : 0;
+}
+
+/* cwqo_greedy_encode with the per-dim log(sigma) supplied (log_scale [D]):
+ * the normaliser sensitivity experiments. */
+CWQO_API int cwqo_greedy_encode_lsig(const float* t_loc, const float* t_scale,
+                                     const float* p_loc, const float* p_scale,
+                                     const int64_t* block_off, int64_t nb, int n_bits_per_step,
+                                     int n_steps, int32_t seed, float rho, int64_t block_id_base,
+                                     const float* log_scale, int32_t* out_idx, float* out_sample,
+                                     int nthreads) {
+  int err = 0;
+#ifdef _OPENMP
+  if (nthreads > 0) omp_set_num_threads(nthreads);
+#pragma omp parallel for schedule(dynamic, 1) reduction(| : err)
+#endif
+  for (int64_t g = 0; g < nb; ++g) {
+    int64_t o = block_off[g], d = block_off[g + 1] - block_off[g];
+    int32_t sg = (int32_t)((uint32_t)seed + (uint32_t)(block_id_base + g));
+    int rc = code_greedy_sample_impl(t_loc + o, t_scale + o, p_loc + o, p_scale + o, d,
+                                     n_bits_per_step, n_steps, sg, rho, log_scale + o,
+                                     out_idx + g * n_steps, out_sample + o);
+    if (rc) err |= 1;
+  }
+  return err ? -1 : 0;
+}
+
+/* Eigen 3.3 plog<Packet8f> (Eigen/src/Core/arch/AVX/MathFunctions.h, the
+ * Cephes single-precision log) on one lane -- [ext] restated from Eigen's
+ * published source, not from /root/reference: TF's CPU kernel evaluates
+ * log(scale) with it for full 8-wide packets.  fma != 0 uses
+ * fused pmadd (an -mfma build); 0 the mul + add of a plain -mavx build (TF 1.x
+ * pip wheels).  Used only by the normaliser sensitivity experiment. */
+static inline float madd(float a, float b, float c, int fma) {
+  return fma ? fmaf(a, b, c) : a * b + c;
+}
+CWQO_API float cwqo_eigen_plog(float x0, int fma) {
+  if (!(x0 >= 0.0f)) return NAN;      /* invalid_mask (also NaN) */
+  if (x0 == 0.0f) return -INFINITY;   /* iszero_mask */
+  float x = x0 < 1.17549435e-38f ? 1.17549435e-38f : x0;  /* pmax(x, min_norm_pos) */
+  uint32_t u;
+  memcpy(&u, &x, 4);
+  float e = (float)(int32_t)(u >> 23) - 126.0f;
+  u = (u & ~0x7f800000u) | 0x3f000000u;  /* mantissa in [0.5, 1) */
+  memcpy(&x, &u, 4);
+  const int lt = x < 0.707106781186547524f;
+  const float tmp0 = lt ? x : 0.0f;
+  x = x - 1.0f;
+  e = e - (lt ? 1.0f : 0.0f);
+  x = x + tmp0;
+  const float x2 = x * x;
+  const float x3 = x2 * x;
+  float y = madd(7.0376836292E-2f, x, -1.1514610310E-1f, fma);
+  float y1 = madd(-1.2420140846E-1f, x, +1.4249322787E-1f, fma);
+  float y2 = madd(+2.0000714765E-1f, x, -2.4999993993E-1f, fma);
+  y = madd(y, x, 1.1676998740E-1f, fma);
+  y1 = madd(y1, x, -1.6668057665E-1f, fma);
+  y2 = madd(y2, x, +3.3333331174E-1f, fma);
+  y = madd(y, x3, y1, fma);
+  y = madd(y, x3, y2, fma);
+  y = y * x3;
+  y1 = e * -2.12194440e-4f;
+  const float tmp = x2 * 0.5f;
+  y = y + y1;
+  x = x - tmp;
+  y2 = e * 0.693359375f;
+  x = x + y;
+  x = x + y2;
+  return x;
+}
+
+CWQO_API void cwqo_eigen_plog_table(const float* x, int64_t n, int fma, float* out) {
+  for (int64_t i = 0; i < n; ++i) out[i] = cwqo_eigen_plog(x[i], fma);
 }
 
 CWQO_API int cwqo_greedy_decode(const int32_t* idx, const float* p_loc, const float* p_scale,

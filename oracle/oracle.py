@@ -50,6 +50,10 @@ def lib():
             "cwqo_greedy_encode": (ci, [vp, vp, vp, vp, vp, i64, ci, ci, i32, f32, i64, vp, vp,
                                         ci]),
             "cwqo_greedy_decode": (ci, [vp, vp, vp, vp, i64, ci, ci, i32, f32, i64, vp, ci]),
+            "cwqo_greedy_encode_lsig": (ci, [vp, vp, vp, vp, vp, i64, ci, ci, i32, f32, i64, vp,
+                                             vp, vp, ci]),
+            "cwqo_eigen_plog": (f32, [f32, ci]),
+            "cwqo_eigen_plog_table": (None, [vp, i64, ci, vp]),
             "cwqo_standardise": (None, [vp, vp, vp, vp, i64, vp, vp]),
             "cwqo_kl_normal_normal": (None, [vp, vp, vp, vp, i64, vp]),
             "cwqo_group_starts": (i64, [vp, i64, i64, f64, vp, i64]),
@@ -166,6 +170,31 @@ def greedy_encode(t_loc, t_scale, p_loc, p_scale, block_off, n_bits_per_step, n_
                                   int(block_id_base), _p(idx), _p(sample), int(nthreads))
     assert rc == 0, rc
     return idx.reshape(nb, int(n_steps)), sample
+
+
+def greedy_encode_lsig(t_loc, t_scale, p_loc, p_scale, block_off, n_bits_per_step, n_steps,
+                       seed, log_scale, rho=1., block_id_base=0, nthreads=0):
+    """greedy_encode with log(sigma_j) supplied per dim (the per-dim normaliser
+    0.9189385f + log sigma_j of SURVEY.md A.5): normaliser sensitivity only."""
+    tl, ts, pl, ps, ls = map(_f32, (t_loc, t_scale, p_loc, p_scale, log_scale))
+    off = np.ascontiguousarray(np.asarray(block_off, dtype=np.int64))
+    nb = off.size - 1
+    idx = np.zeros(nb * int(n_steps), dtype=np.int32)
+    sample = np.zeros(tl.size, dtype=np.float32)
+    rc = lib().cwqo_greedy_encode_lsig(_p(tl), _p(ts), _p(pl), _p(ps), _p(off), nb,
+                                       int(n_bits_per_step), int(n_steps), int(seed), float(rho),
+                                       int(block_id_base), _p(ls), _p(idx), _p(sample),
+                                       int(nthreads))
+    assert rc == 0, rc
+    return idx.reshape(nb, int(n_steps)), sample
+
+
+def eigen_plog(x, fma=False):
+    """Eigen 3.3 plog<Packet8f> per lane ([ext] restatement, cwq_oracle.c)."""
+    a = _f32(x)
+    out = np.empty_like(a)
+    lib().cwqo_eigen_plog_table(_p(a), a.size, 1 if fma else 0, _p(out))
+    return out
 
 
 def greedy_decode(idx, p_loc, p_scale, block_off, n_bits_per_step, n_steps, seed, rho=1.,

@@ -52,30 +52,26 @@ def _worker(rank, world, port, nb, cost, out):
     h = make_blocks_range(b0, b1, d, bits)
     idx, _ = O.greedy_encode(h["post_loc"], h["post_scale"], h["prior_loc"], h["prior_scale"],
                              np.arange(b1 - b0 + 1, dtype=np.int64) * d, bits, 1, 42, 1.0, b0, 1)
-    local = torch.from_numpy(idx.reshape(-1).astype(np.int32))
-    # ranks may own different block counts (cost-balanced cuts): pad to the max
-    n = torch.tensor([local.numel()])
-    sizes = [torch.zeros_like(n) for _ in range(world)]
-    dist.all_gather(sizes, n)
-    m = int(max(int(v) for v in sizes))
-    padded = torch.full((m,), -1, dtype=torch.int32)
-    padded[:local.numel()] = local
-    full = gather_indices(padded, m)
+    # ranks may own different block counts (cost-balanced cuts): gather_indices
+    # pads and trims internally; [nb, n_steps] rows, an empty shard included
+    local = torch.from_numpy(idx.astype(np.int32))
+    full = gather_indices(local)
     if rank == 0:
-        parts = [full[r * m:r * m + int(sizes[r])] for r in range(world)]
-        out.put(torch.cat(parts).numpy().tolist())
+        out.put(full.reshape(-1).numpy().tolist())
     dist.barrier()
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,balanced", [(2, False), (3, True)])
+@pytest.mark.parametrize("world,balanced", [(2, False), (3, True), (3, "empty")])
 def test_gloo_ranks_gather_oracle_coded_shards(world, balanced):
     from oracle import oracle as O
     from compression_without_quantization_amd.synthetic import make_blocks_range
     O.build()
     nb, d, bits = 40, 8, 6
     cost = None
-    if balanced:
+    if balanced == "empty":  # all the cost in the first block: ranks 1.. own nothing
+        cost = [1e9] + [0.0] * (nb - 1)
+    elif balanced:
         cost = np.random.default_rng(3).integers(1, 50, nb).astype(np.float64).tolist()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -101,3 +97,40 @@ def test_make_blocks_range_is_shard_independent():
         part = make_blocks_range(b0, b1, 4, 8, chunk=1 << 15)
         for k in full:
             assert np.array_equal(part[k], full[k][b0:b1])
+
+
+def test_rank_device_map_refuses_shared_gpu_under_rccl(monkeypatch):
+    """bench.py's rank -> device check: with the nccl (RCCL) backend two ranks
+    on one GPU are refused; distinct GPUs (or gloo, the shared-GPU rehearsal)
+    pass and the map is returned for the bench line."""
+    import sys
+    from conftest import REPO
+    sys.path.insert(0, REPO)
+    monkeypatch.setattr(sys, "argv", ["bench.py"])
+    import bench
+
+    class P:
+        pci_bus_id = None
+
+    monkeypatch.setattr(torch.cuda, "get_device_properties", lambda dev: P())
+
+    class FakeDist:
+        def __init__(self, backend, devices):
+            self.backend, self.devices = backend, devices
+
+        def get_world_size(self):
+            return len(self.devices)
+
+        def get_backend(self):
+            return self.backend
+
+        def all_gather_object(self, out, me):
+            for r, dv in enumerate(self.devices):
+                out[r] = dict(me, rank=r, local_rank=r, device=dv)
+
+    dev = torch.device("cuda", 0)
+    m = bench.rank_device_map(FakeDist("nccl", [0, 1, 2, 3]), 0, 0, dev)
+    assert [x["device"] for x in m] == [0, 1, 2, 3]
+    assert len(bench.rank_device_map(FakeDist("gloo", [0, 0]), 0, 0, dev)) == 2
+    with pytest.raises(SystemExit, match="share GPU"):
+        bench.rank_device_map(FakeDist("nccl", [0, 1, 1]), 0, 0, dev)

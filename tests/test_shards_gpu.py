@@ -256,6 +256,81 @@ def test_bench_launches_two_ranks_itself(cwq):
     assert line["parity"]["blocks_checked"] >= 2 * 16
     assert line["decode_roundtrip_bit_exact"] is True
     assert line["value"] > 0
+    # rank -> device map in the line (both ranks on the box's one GPU: gloo)
+    rd = line["config"]["rank_devices"]
+    assert [m["rank"] for m in rd] == [0, 1] and line["config"]["backend"] == "gloo"
+    # the N > 1 roofline is the job's: both shards' bytes over the slower kernel
+    rf = line["roofline"]
+    assert rf["scope"].startswith("all 2 GPUs")
+    assert rf["algorithmic_bytes_per_launch"] == 8192 * (20 * 32 + 4)
+    assert rf["rank0"]["algorithmic_bytes_per_launch"] == 4096 * (20 * 32 + 4)
+    assert rf["kernel_ms"] == line["eval_kernel_ms_max_over_ranks"]
+
+
+def _ragged_gather_worker(rank, world, port, q):
+    """One rank of test_ragged_shards_gathered: codes its cost-balanced shard of
+    ragged CSR groups on the GPU and all-gathers the indices (gloo, CPU)."""
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import compression_without_quantization_amd as C
+    from compression_without_quantization_amd.parallel import gather_indices, shard_range
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    tl, ts, pl, ps, off, bits, n_steps = _ragged_set()
+    nb = off.size - 1
+    cost = np.diff(off).astype(np.float64) * (1 << bits) * n_steps
+    b0, b1 = shard_range(nb, world, rank, cost)
+    a, b = int(off[b0]), int(off[b1])
+    if b1 > b0:
+        idx, _ = C.encode_blocks(tl[a:b], ts[a:b], pl[a:b], ps[a:b], bits, n_steps, 42,
+                                 block_off=off[b0:b1 + 1] - a, block_id_base=b0)
+        local = idx.cpu()
+    else:
+        local = torch.zeros((0, n_steps), dtype=torch.int32)
+    full = gather_indices(local)
+    if rank == 0:
+        q.put((b1 - b0, full.numpy()))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _ragged_set():
+    rng = np.random.default_rng(5)
+    sizes = np.concatenate([rng.integers(1, 40, 300), [2000, 1], rng.integers(1, 9, 200)])
+    off = np.concatenate([[0], np.cumsum(sizes)]).astype(np.int64)
+    D = int(off[-1])
+    tl = rng.standard_normal(D).astype(np.float32)
+    ts = rng.uniform(0.3, 0.9, D).astype(np.float32)
+    pl = (0.1 * rng.standard_normal(D)).astype(np.float32)
+    ps = rng.uniform(0.8, 1.2, D).astype(np.float32)
+    return tl, ts, pl, ps, off, 10, 2
+
+
+def test_ragged_shards_gathered(cwq):
+    """Three ranks sharing the GPU (gloo) code cost-balanced, unequal shards of
+    ragged groups (1 .. 2000 dims) with block_id_base = their first group, and
+    parallel.gather_indices (which pads and trims internally) returns exactly
+    the indices of one single-process encode of all groups."""
+    import socket
+    import torch.multiprocessing as mp
+    tl, ts, pl, ps, off, bits, n_steps = _ragged_set()
+    want, _ = cwq.encode_blocks(tl, ts, pl, ps, bits, n_steps, 42, block_off=off)
+    want = want.cpu().numpy()
+    sk = socket.socket()
+    sk.bind(("127.0.0.1", 0))
+    port = sk.getsockname()[1]
+    sk.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_ragged_gather_worker, args=(r, 3, port, q)) for r in range(3)]
+    for p in procs:
+        p.start()
+    n0, got = q.get(timeout=240)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    assert 0 < n0 < off.size - 1  # rank 0's shard is a strict part: shards are unequal
+    assert np.array_equal(got, want)
 
 
 def test_bench_weak_scaling_two_ranks(cwq):
