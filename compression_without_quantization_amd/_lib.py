@@ -25,20 +25,25 @@ c_str = ctypes.c_char_p
 class Options(ctypes.Structure):
     """cwq_options (include/cwq.h): per-call encoder options."""
     _fields_ = [("prune_mode", ctypes.c_int32), ("reserved", ctypes.c_int32),
-                ("eval_start_event", c_vp), ("eval_stop_event", c_vp)]
+                ("eval_start_event", c_vp), ("eval_stop_event", c_vp),
+                ("eval_ms_out", ctypes.POINTER(ctypes.c_float))]
 
 
 c_opts = ctypes.POINTER(Options)
 
 
-def options(prune_mode=None, eval_events=None):
+def options(prune_mode=None, eval_events=None, eval_ms_out=None):
     """A cwq_options pointer for one call, or None (the library defaults:
-    prune_mode 2, no events).  eval_events: (start, stop) hipEvent_t handles."""
-    if prune_mode is None and eval_events is None:
+    prune_mode 2, no events).  eval_events: (start, stop) hipEvent_t handles;
+    eval_ms_out: a ctypes.c_float the fused grouped calls write their scoring
+    launches' milliseconds to."""
+    if prune_mode is None and eval_events is None and eval_ms_out is None:
         return None
-    o = Options(2 if prune_mode is None else int(prune_mode), 0, None, None)
+    o = Options(2 if prune_mode is None else int(prune_mode), 0, None, None, None)
     if eval_events is not None:
         o.eval_start_event, o.eval_stop_event = eval_events
+    if eval_ms_out is not None:
+        o.eval_ms_out = ctypes.pointer(eval_ms_out)
     return ctypes.pointer(o)
 
 
@@ -68,9 +73,11 @@ SIGNATURES = {
                                         c_i64, c_f64, c_vp, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp,
                                         c_size, c_opts, c_vp]),
     "cwq_code_grouped_greedy_batch_workspace_size": (c_size, [c_i64, c_i64, c_int]),
+    "cwq_code_grouped_greedy_batch_host_workspace_size": (c_size, [c_i64, c_i64, c_int]),
     "cwq_code_grouped_greedy_batch": (c_i64, [c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int,
                                               c_vp, c_f32, c_i64, c_f64, c_vp, c_vp, c_i64, c_vp,
-                                              c_vp, c_i64, c_vp, c_vp, c_size, c_opts, c_vp]),
+                                              c_vp, c_i64, c_vp, c_vp, c_size, c_vp, c_size,
+                                              c_opts, c_vp]),
     "cwq_importance_workspace_size": (c_size, [c_i64, c_i64]),
     "cwq_importance_encode": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i32,
                                       c_i64, c_vp, c_vp, c_vp, c_size, c_opts, c_vp]),

@@ -25,6 +25,7 @@ Differences from the TF1 reference (deliberate, documented in DESIGN.md):
 All arithmetic runs in libcwq.so; nothing here computes samples on the CPU.
 """
 import ctypes
+import threading
 
 import numpy as np
 import torch
@@ -318,7 +319,7 @@ def _dist_parts(dist, dev, what):
 def code_grouped_greedy_sample(sess, target, proposal, n_steps, n_bits_per_step, seed,
                                max_group_size_bits=12, adaptive=True, backfitting_steps=0,
                                use_log_prob=False, rho=1., *, prune_mode=None,
-                               eval_events=None):
+                               eval_events=None, eval_ms_out=None):
     """coded_greedy_sampler.py:170-296.
 
     Returns (sample np.float32 [D], bitcode str, group_start_indices list).
@@ -357,7 +358,7 @@ def code_grouped_greedy_sample(sess, target, proposal, n_steps, n_bits_per_step,
             seed32, float(rho), group_size_threshold(max_group_size_bits), float(n_nats),
             sample_h.ctypes.data, bits_h.ctypes.data, bits_h.size, starts_h.ctypes.data,
             starts_h.size, ctypes.byref(kl_sum) if VERBOSE else None, ws.data_ptr(), ws.numel(),
-            _lib.options(prune_mode, eval_events), stream),
+            _lib.options(prune_mode, eval_events, eval_ms_out), stream),
             "cwq_code_grouped_greedy")
     if VERBOSE:
         total_kl_bits = kl_sum.value / np.log(2)
@@ -373,7 +374,7 @@ def code_grouped_greedy_sample(sess, target, proposal, n_steps, n_bits_per_step,
 def code_grouped_greedy_sample_batch(sess, targets, proposals, n_steps, n_bits_per_step, seeds,
                                      max_group_size_bits=12, adaptive=True, backfitting_steps=0,
                                      use_log_prob=False, rho=1., *, prune_mode=None,
-                                     eval_events=None):
+                                     eval_events=None, eval_ms_out=None):
     """code_grouped_greedy_sample (coded_greedy_sampler.py:170-296) for a batch
     of independent items (the images of a dataset, the ladder levels of several
     images) in one native call (cwq_code_grouped_greedy_batch).
@@ -420,10 +421,16 @@ def code_grouped_greedy_sample_batch(sess, targets, proposals, n_steps, n_bits_p
     seeds32 = np.array([np.int32(np.uint32(x & 0xFFFFFFFF)) for x in seeds], dtype=np.int32)
     need = int(lib.cwq_code_grouped_greedy_batch_workspace_size(D, n_items, n_steps))
     ws = torch.empty(max(need, 1), dtype=torch.uint8, device=dev)
-    sample_h = np.empty(max(D, 1), dtype=np.float32)
+    # page-locked host memory from torch's caching host allocator: the staging
+    # the library copies through and the sample / starts this call returns
+    # (asynchronous DMA copies; cached blocks are reused without page faults)
+    hneed = int(lib.cwq_code_grouped_greedy_batch_host_workspace_size(D, n_items, n_steps))
+    hws = torch.empty(max(hneed, 1), dtype=torch.uint8, pin_memory=True)
+    sample_t = torch.empty(max(D, 1), dtype=torch.float32, pin_memory=True)
+    starts_t = torch.empty(D + 2 * n_items, dtype=torch.int64, pin_memory=True)
+    sample_h, starts_h = sample_t.numpy(), starts_t.numpy()
     bits_cap = (D + n_items) * n_bits_per_group
-    bits_h = np.empty(max(bits_cap, 1), dtype=np.uint8)
-    starts_h = np.empty(D + 2 * n_items, dtype=np.int64)
+    bits_h = _scratch_bytes(bits_cap)  # consumed into str below: reusable
     bits_off = np.empty(n_items + 1, dtype=np.int64)
     n_starts = np.empty(n_items, dtype=np.int64)
     n_nats = n_bits_per_group * np.log(2) - 1
@@ -433,16 +440,31 @@ def code_grouped_greedy_sample_batch(sess, targets, proposals, n_steps, n_bits_p
             n_items, item_off.ctypes.data, _ptr(cat[0]), _ptr(cat[1]), _ptr(cat[2]),
             _ptr(cat[3]), n_steps, n_bits_per_step, seeds32.ctypes.data, float(rho),
             group_size_threshold(max_group_size_bits), float(n_nats), sample_h.ctypes.data,
-            bits_h.ctypes.data, bits_h.size, bits_off.ctypes.data, starts_h.ctypes.data,
-            starts_h.size, n_starts.ctypes.data, ws.data_ptr(), ws.numel(),
-            _lib.options(prune_mode, eval_events), stream), "cwq_code_grouped_greedy_batch")
+            bits_h.ctypes.data, bits_cap, bits_off.ctypes.data, starts_h.ctypes.data,
+            starts_h.size, n_starts.ctypes.data, ws.data_ptr(), ws.numel(), hws.data_ptr(),
+            hws.numel(), _lib.options(prune_mode, eval_events, eval_ms_out), stream),
+            "cwq_code_grouped_greedy_batch")
     out = []
+    mv = memoryview(bits_h)
     for i in range(n_items):
         a, b = int(item_off[i]), int(item_off[i + 1])
-        bitcode = bits_h[bits_off[i]:bits_off[i + 1]].tobytes().decode('ascii')
+        bitcode = str(mv[bits_off[i]:bits_off[i + 1]], 'ascii')
         s0 = a + 2 * i  # item i's starts region (cwq_code_grouped_greedy_batch)
         out.append((sample_h[a:b], bitcode, starts_h[s0:s0 + n_starts[i]]))
     return out
+
+
+_scratch = threading.local()
+
+
+def _scratch_bytes(n):
+    """A per-thread reusable uint8 buffer of at least n bytes (its pages stay
+    mapped between calls)."""
+    buf = getattr(_scratch, "buf", None)
+    if buf is None or buf.size < n:
+        buf = np.empty(max(int(n), 1), dtype=np.uint8)
+        _scratch.buf = buf
+    return buf
 
 
 def decode_grouped_greedy_sample(sess, bitcode, group_start_indices, proposal, n_bits_per_step,

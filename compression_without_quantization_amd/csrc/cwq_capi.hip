@@ -13,6 +13,8 @@
 #include <immintrin.h>
 
 #include <atomic>
+#include <condition_variable>
+#include <mutex>
 #include <sched.h>
 #include <stdlib.h>
 #include <thread>
@@ -551,6 +553,29 @@ GroupedWs grouped_ws(int64_t D, int n_steps, int64_t max_groups) {
   l.total = o;
   return l;
 }
+// Events of one call, created on the stream's device and destroyed with it.
+struct CallEvents {
+  std::vector<hipEvent_t> ev;
+  int dev_prev = -1;
+  bool made(int n, hipStream_t s, unsigned flags) {
+    int dev = 0;
+    if (hipStreamGetDevice(s, &dev) != hipSuccess) return false;
+    int cur = 0;
+    if (hipGetDevice(&cur) != hipSuccess) return false;
+    if (cur != dev && hipSetDevice(dev) != hipSuccess) return false;
+    bool ok = true;
+    for (int i = 0; i < n && ok; ++i) {
+      hipEvent_t e = nullptr;
+      ok = hipEventCreateWithFlags(&e, flags) == hipSuccess;
+      if (ok) ev.push_back(e);
+    }
+    if (cur != dev) (void)hipSetDevice(cur);
+    return ok;
+  }
+  ~CallEvents() {
+    for (hipEvent_t e : ev) (void)hipEventDestroy(e);
+  }
+};
 thread_local std::vector<float> g_kl_host;
 thread_local std::vector<int32_t> g_idx_host;
 // :81-87, :288 (and binary_io.py:41-53) each of n indices as n_bits LSB-first
@@ -594,8 +619,8 @@ int64_t cwq_code_grouped_greedy(const float* q_loc, const float* q_scale, const 
                                 char* bits_host, int64_t bits_cap, int64_t* starts_host,
                                 int64_t starts_cap, double* kl_sum_out, void* workspace,
                                 size_t workspace_bytes, const cwq_options* opts, void* stream) {
+  cwq_options o;
   {
-    cwq_options o;
     const int rc0 = read_options(opts, &o);
     if (rc0) return rc0;
   }
@@ -680,10 +705,18 @@ int64_t cwq_code_grouped_greedy(const float* q_loc, const float* q_scale, const 
       hipSuccess)
     return hip_fail(e, "offsets to device");
   // :273-284 one greedy coder per group, seed + g
+  CallEvents tev;
+  if (o.eval_ms_out && (!tev.made(2, s, hipEventDefault) ||
+                        hipEventRecord(tev.ev[0], s) != hipSuccess))
+    return fail(CWQ_ERR_HIP, "cwq_code_grouped_greedy: timing events failed");
   if ((rc = cwq_greedy_encode(t_loc, t_scale, zeros, ones, offs, G, D, maxd, n_bits_per_step,
                               n_steps, seed, rho, 0, idx, sample, w + l.enc,
                               workspace_bytes - l.enc, opts, stream)) < 0)
     return rc;
+  if (o.eval_ms_out && (e = hipEventRecord(tev.ev[1], s)) != hipSuccess) {
+    (void)hipStreamSynchronize(s);
+    return hip_fail(e, "event");
+  }
   // :292 destandardise
   if ((rc = cwq_destandardise(sample, p_loc, p_scale, D, out, stream)) < 0) return rc;
   g_idx_host.resize((size_t)(G * n_steps));
@@ -695,6 +728,9 @@ int64_t cwq_code_grouped_greedy(const float* q_loc, const float* q_scale, const 
     return hip_fail(e, "sample to host");
   if ((e = hipStreamSynchronize(s)) != hipSuccess) return hip_fail(e, "sync");
   lap("encode");
+  if (o.eval_ms_out && (e = hipEventElapsedTime(o.eval_ms_out, tev.ev[0], tev.ev[1])) !=
+                           hipSuccess)
+    return hip_fail(e, "event time");
   // :81-87, :288 each index as n_bits_per_step LSB-first chars, steps then groups
   {
     const int64_t nw = write_bitcode(g_idx_host.data(), G * n_steps, n_bits_per_step, bits_host);
@@ -718,19 +754,45 @@ int64_t cwq_code_grouped_greedy(const float* q_loc, const float* q_scale, const 
 // each.
 // ---------------------------------------------------------------------------
 namespace {
+// Device workspace of the batch: the grouped layout for D dims, with the
+// per-chunk regions of the group-indexed arrays (chunk c of a call owns
+// [a_c + i0_c, ...) of them, a_c its first dim and i0_c its first item, so
+// chunks never share a slot however their group counts come out): offsets
+// D + 2 n + 1 entries, indices / seeds D + n.
 struct BatchWs {
   GroupedWs g;
   size_t seeds, total;
 };
 BatchWs batch_ws(int64_t D, int64_t n_items, int n_steps) {
   BatchWs l;
-  const int64_t G = D + (n_items > 0 ? n_items : 0);  // at most D_i + 1 groups per item
-  l.g = grouped_ws(D, n_steps, G);
+  const int64_t n = n_items > 0 ? n_items : 0;
+  l.g = grouped_ws(D, n_steps, D + 2 * n + 1);
   l.seeds = l.g.total;
-  l.total = align_up(l.seeds + (size_t)(G > 0 ? G : 1) * 4, 256);
+  l.total = align_up(l.seeds + (size_t)(D + n + 1) * 4, 256);
   return l;
 }
-// Host threads for the per-item phases: CWQ_HOST_THREADS if set, else the
+// Host staging of the batch (the caller's pinned memory, or thread-local
+// vectors): per-dim KL, then the offsets / seeds / indices regions as above.
+struct BatchHostWs {
+  size_t kl, offs, seeds, idx, total;
+};
+BatchHostWs batch_host_ws(int64_t D, int64_t n_items, int n_steps) {
+  BatchHostWs h;
+  const int64_t n = n_items > 0 ? n_items : 0;
+  size_t o = 0;
+  auto take = [&](size_t bytes) {
+    const size_t at = o;
+    o = align_up(o + bytes, 256);
+    return at;
+  };
+  h.kl = take((size_t)D * 4);
+  h.offs = take((size_t)(D + 2 * n + 1) * 8);
+  h.seeds = take((size_t)(D + n + 1) * 4);
+  h.idx = take((size_t)(D + n + 1) * (size_t)(n_steps > 0 ? n_steps : 1) * 4);
+  h.total = o;
+  return h;
+}
+// Host threads for the per-chunk host phases: CWQ_HOST_THREADS if set, else the
 // CPUs this process may run on, at most 8.  (On the GPU boxes, whose cgroup
 // quota is 16 CPUs, 12 or 16 threads sporadically ran C3 2.5x slower: the
 // quota's throttling; 4 and 8 were steady at 9-10 ms per 24 images.)
@@ -748,13 +810,34 @@ int64_t host_threads() {
   }();
   return n;
 }
-thread_local std::vector<int32_t> g_seed_host;
-thread_local std::vector<int64_t> g_offs_host;
+// Chunks a batch is pipelined in (CWQ_BATCH_CHUNKS, default below): the host
+// phases of one chunk run while the device codes another.
+#ifndef CWQ_BATCH_CHUNKS
+#define CWQ_BATCH_CHUNKS 6
+#endif
+int64_t batch_chunks() {
+  static const int64_t n = [] {
+    if (const char* e = getenv("CWQ_BATCH_CHUNKS")) {
+      const long v = strtol(e, nullptr, 10);
+      if (v >= 1) return (int64_t)v;
+    }
+    return (int64_t)CWQ_BATCH_CHUNKS;
+  }();
+  return n;
+}
+thread_local std::vector<char> g_batch_host;
+
 }  // namespace
 
 size_t cwq_code_grouped_greedy_batch_workspace_size(int64_t D, int64_t n_items, int n_steps) {
   if (D < 0 || n_items < 0 || n_steps < 0) return 0;
   return batch_ws(D, n_items, n_steps).total;
+}
+
+size_t cwq_code_grouped_greedy_batch_host_workspace_size(int64_t D, int64_t n_items,
+                                                         int n_steps) {
+  if (D < 0 || n_items < 0 || n_steps < 0) return 0;
+  return batch_host_ws(D, n_items, n_steps).total;
 }
 
 int64_t cwq_code_grouped_greedy_batch(
@@ -763,9 +846,9 @@ int64_t cwq_code_grouped_greedy_batch(
     const int32_t* seeds, float rho, int64_t size_threshold, double n_nats, float* sample_host,
     char* bits_host, int64_t bits_cap, int64_t* bits_off, int64_t* starts_host,
     int64_t starts_cap, int64_t* n_starts, void* workspace, size_t workspace_bytes,
-    const cwq_options* opts, void* stream) {
+    void* host_workspace, size_t host_workspace_bytes, const cwq_options* opts, void* stream) {
+  cwq_options o;
   {
-    cwq_options o;
     const int rc0 = read_options(opts, &o);
     if (rc0) return rc0;
   }
@@ -788,43 +871,36 @@ int64_t cwq_code_grouped_greedy_batch(
   if (workspace_bytes < bl.total || !workspace)
     return fail(CWQ_ERR_WORKSPACE, "workspace %zu bytes < required %zu", workspace_bytes,
                 bl.total);
+  const BatchHostWs hl = batch_host_ws(D, n_items, n_steps);
+  if (host_workspace && host_workspace_bytes < hl.total)
+    return fail(CWQ_ERR_WORKSPACE, "host workspace %zu bytes < required %zu",
+                host_workspace_bytes, hl.total);
+  if (bits_cap > 0 && !bits_host)
+    return fail(CWQ_ERR_INVALID, "cwq_code_grouped_greedy_batch: null bits_host");
+  bits_off[0] = 0;
+  if (n_items == 0) return ok();
   hipStream_t s = (hipStream_t)stream;
 #ifdef CWQ_PHASE_TIMES  // tuning builds: per-phase host wall times to stderr
-  struct timespec ts0, ts1;
-  clock_gettime(CLOCK_MONOTONIC, &ts0);
-  auto lap = [&](const char* what) {
-    clock_gettime(CLOCK_MONOTONIC, &ts1);
-    fprintf(stderr, "[cwq batch] %-10s %8.1f us\n", what,
-            (ts1.tv_sec - ts0.tv_sec) * 1e6 + (ts1.tv_nsec - ts0.tv_nsec) * 1e-3);
-    ts0 = ts1;
+  struct timespec ts_start;
+  clock_gettime(CLOCK_MONOTONIC, &ts_start);
+  auto lap = [&](const char* what, int64_t c) {
+    struct timespec t;
+    clock_gettime(CLOCK_MONOTONIC, &t);
+    fprintf(stderr, "[cwq batch] %-12s chunk %2lld at %8.1f us\n", what, (long long)c,
+            (t.tv_sec - ts_start.tv_sec) * 1e6 + (t.tv_nsec - ts_start.tv_nsec) * 1e-3);
   };
 #else
-  auto lap = [](const char*) {};
+  auto lap = [](const char*, int64_t) {};
 #endif
-  // fn(i) for every item, on up to host_threads() threads when the batch is large
-  const int64_t nthr = std::min<int64_t>(n_items, host_threads());
-  auto for_items = [&](auto fn) {
-    if (nthr <= 1 || item_off[n_items] < (1 << 16)) {
-      for (int64_t i = 0; i < n_items; ++i) fn(i);
-      return;
-    }
-    // items handed out one at a time (sizes differ by orders of magnitude:
-    // both ladder levels of an image alternate in a batch)
-    std::atomic<int64_t> next{0};
-    auto work = [&]() {
-      for (int64_t i = next++; i < n_items; i = next++) fn(i);
-    };
-    // thread creation may fail (pids cgroup, RLIMIT_NPROC): the exception must
-    // not cross the C ABI, so the threads that did start and this one share
-    // the items, down to the calling thread alone
-    std::vector<std::thread> pool;
-    try {
-      for (int64_t t = 1; t < nthr; ++t) pool.emplace_back(work);
-    } catch (...) {
-    }
-    work();
-    for (auto& th : pool) th.join();
-  };
+  char* hw = (char*)host_workspace;
+  if (!hw) {  // no pinned staging from the caller: pageable, thread-local
+    g_batch_host.resize(hl.total);
+    hw = g_batch_host.data();
+  }
+  float* kl_h = (float*)(hw + hl.kl);
+  int64_t* offs_h = (int64_t*)(hw + hl.offs);
+  int32_t* seed_h = (int32_t*)(hw + hl.seeds);
+  int32_t* idx_h = (int32_t*)(hw + hl.idx);
   char* w = (char*)workspace;
   float* t_loc = (float*)(w + l.t_loc);
   float* t_scale = (float*)(w + l.t_scale);
@@ -836,125 +912,271 @@ int64_t cwq_code_grouped_greedy_batch(
   int64_t* offs = (int64_t*)(w + l.offs);
   int32_t* idx = (int32_t*)(w + l.idx);
   int32_t* bseed = (int32_t*)(w + bl.seeds);
+
+  // chunks of consecutive items, about D / K dims each (at least one item)
+  std::vector<int64_t> ci;  // chunk c = items [ci[c], ci[c + 1])
+  {
+    const int64_t K = D < (1 << 16) ? 1 : std::min<int64_t>(batch_chunks(), n_items);
+    ci.push_back(0);
+    for (int64_t i = 1; i < n_items; ++i)
+      if ((int64_t)ci.size() < K &&
+          item_off[i] * K >= D * (int64_t)ci.size() && item_off[i] > item_off[ci.back()])
+        ci.push_back(i);
+    ci.push_back(n_items);
+  }
+  const int64_t K = (int64_t)ci.size() - 1;
+  auto a_of = [&](int64_t c) { return item_off[ci[(size_t)c]]; };
+  auto gbase = [&](int64_t c) { return a_of(c) + ci[(size_t)c]; };  // group-array region
+
+  // events: K KL copies, K chunk results; + 2 K timing events for eval_ms_out
+  CallEvents evs;
+  if (!evs.made((int)(2 * K), s, hipEventDisableTiming))
+    return fail(CWQ_ERR_HIP, "cwq_code_grouped_greedy_batch: event creation failed");
+  CallEvents tev;
+  if (o.eval_ms_out && !tev.made((int)(2 * K), s, hipEventDefault))
+    return fail(CWQ_ERR_HIP, "cwq_code_grouped_greedy_batch: event creation failed");
+  hipEvent_t* kl_ev = evs.ev.data();
+  hipEvent_t* done_ev = evs.ev.data() + K;
+
   hipError_t e = hipSuccess;
   int rc;
-  if (D > 0) {  // :193-210 for every item at once (elementwise)
-    if ((rc = cwq_standardise(q_loc, q_scale, p_loc, p_scale, D, t_loc, t_scale, stream)) < 0)
-      return rc;
-    if ((rc = cwq_kl_normal_normal(q_loc, q_scale, p_loc, p_scale, D, kl, stream)) < 0) return rc;
-    if ((e = hipMemsetAsync(zeros, 0, (size_t)D * 4, s)) != hipSuccess) return hip_fail(e, "memset");
-    if ((e = hipMemsetD32Async((hipDeviceptr_t)ones, 0x3f800000u, (size_t)D, s)) != hipSuccess)
-      return hip_fail(e, "memset");
-    g_kl_host.resize((size_t)D);
-    if ((e = hipMemcpyAsync(g_kl_host.data(), kl, (size_t)D * 4, hipMemcpyDeviceToHost, s)) !=
-        hipSuccess)
-      return hip_fail(e, "KL to host");
-    if ((e = hipStreamSynchronize(s)) != hipSuccess) return hip_fail(e, "sync");
+  // :193-210 for every item at once (elementwise), then the KL to the host chunk
+  // by chunk, so the first chunk's partitions start before the rest arrives
+  if ((rc = cwq_standardise(q_loc, q_scale, p_loc, p_scale, D, t_loc, t_scale, stream)) < 0)
+    return rc;
+  if ((rc = cwq_kl_normal_normal(q_loc, q_scale, p_loc, p_scale, D, kl, stream)) < 0) return rc;
+  if (D > 0 && (e = hipMemsetAsync(zeros, 0, (size_t)D * 4, s)) != hipSuccess)
+    return hip_fail(e, "memset");
+  if (D > 0 && (e = hipMemsetD32Async((hipDeviceptr_t)ones, 0x3f800000u, (size_t)D, s)) !=
+                   hipSuccess)
+    return hip_fail(e, "memset");
+  for (int64_t c = 0; c < K; ++c) {
+    const int64_t a = a_of(c), n = a_of(c + 1) - a;
+    if (n > 0 && (e = hipMemcpyAsync(kl_h + a, kl + a, (size_t)n * 4, hipMemcpyDeviceToHost, s)) !=
+                     hipSuccess)
+      break;
+    if ((e = hipEventRecord(kl_ev[c], s)) != hipSuccess) break;
   }
-  lap("kl");
-  // :207-252 each item's own partition, item i's starts at item_off[i] + 2 i
-  // (room for its D_i + 2 entries); the items are independent, so several
-  // host threads partition them side by side
-  {
-    std::vector<int64_t> rcs((size_t)n_items, 0);
-    const float* klh = g_kl_host.data();  // thread_local: resolve here, not in the workers
-    for_items([&](int64_t i) {
-      const int64_t a = item_off[i], Di = item_off[i + 1] - a;
-      const int64_t n = group_starts_impl(Di > 0 ? klh + a : nullptr, Di, size_threshold, n_nats,
-                                          starts_host + a + 2 * i, Di + 2, false);
-      rcs[(size_t)i] = n;
-      n_starts[i] = n < 0 ? 0 : n;
-    });
-    for (int64_t i = 0; i < n_items; ++i)
-      if (rcs[(size_t)i] < 0)
-        return fail((int)rcs[(size_t)i], "cwq_code_grouped_greedy_batch: partition of item %lld",
-                    (long long)i);
+  if (e != hipSuccess) {
+    (void)hipStreamSynchronize(s);
+    return hip_fail(e, "KL to host");
   }
-  lap("group");
-  // the items' groups concatenated into one CSR layout, seeds seeds[i] + g
-  // (item i's groups start at global group gfirst[i]), filled per item on the
-  // same host threads
-  std::vector<int64_t> gfirst((size_t)n_items + 1, 0);
-  std::vector<int64_t> imaxd((size_t)n_items, 0);
-  bits_off[0] = 0;
-  for (int64_t i = 0; i < n_items; ++i) {
-    const int64_t Gi = n_starts[i] - 1 > 0 ? n_starts[i] - 1 : 0;
-    gfirst[(size_t)i + 1] = gfirst[(size_t)i] + Gi;
-    bits_off[i + 1] = bits_off[i] + Gi * (int64_t)n_steps * n_bits_per_step;
-  }
-  const int64_t G = gfirst[(size_t)n_items], nbits = bits_off[n_items];
-  g_offs_host.resize((size_t)G + 1);
-  g_seed_host.resize((size_t)(G > 0 ? G : 1));
-  {
-    int64_t* go = g_offs_host.data();  // thread_local: resolve here, not in the workers
-    int32_t* gs = g_seed_host.data();
-    for_items([&](int64_t i) {
-      const int64_t a = item_off[i], g0 = gfirst[(size_t)i];
-      const int64_t* st = starts_host + a + 2 * i;
-      const int64_t Gi = gfirst[(size_t)i + 1] - g0;
-      int64_t md = 0;
+  lap("kl queued", 0);
+
+  // Host tasks, on worker threads (the calling thread sequences the device):
+  //   prep(c): the items' partitions (:207-252; item i's starts at
+  //            item_off[i] + 2 i) and the chunk's CSR layout, local group
+  //            numbers, seeds seeds[i] + g (:282);
+  //   bits(c): after chunk c's indices are on the host, the items' LSB-first
+  //            bitcodes at bits_off[i] (:81-87, :288).
+  // The calling thread runs any task no worker has taken when it needs it
+  // (also when no worker thread could be started).
+  struct ChunkState {
+    std::atomic<int> prep_claimed{0}, bits_claimed{0};
+    std::atomic<int> prepared{0};  // 1 done, -1 failed
+    std::atomic<int> enqueued{0};  // 1 results on their way (bits_off known), -1 abandoned
+    int64_t G = 0, maxd = 0;
+  };
+  std::vector<ChunkState> cs((size_t)K);
+  std::vector<int64_t> gloc((size_t)n_items + 1, 0);  // item's first group within its chunk
+  std::atomic<int> err_rc{0};
+  std::mutex mu;
+  std::condition_variable cv;
+  const float* klh = kl_h;
+  auto prep = [&](int64_t c) -> int {
+    if (hipEventSynchronize(kl_ev[c]) != hipSuccess)
+      return fail(CWQ_ERR_HIP, "KL copy failed");
+    const int64_t i0 = ci[(size_t)c], i1 = ci[(size_t)c + 1], a = a_of(c), gb = gbase(c);
+    int64_t gl = 0, md = 0;
+    for (int64_t i = i0; i < i1; ++i) {
+      const int64_t ai = item_off[i], Di = item_off[i + 1] - ai;
+      int64_t* st = starts_host + ai + 2 * i;
+      const int64_t ns = group_starts_impl(Di > 0 ? klh + ai : nullptr, Di, size_threshold,
+                                           n_nats, st, Di + 2, false);
+      if (ns < 0) return (int)ns;
+      n_starts[i] = ns;
+      const int64_t Gi = ns - 1 > 0 ? ns - 1 : 0;
+      gloc[(size_t)i] = gl;
+      int64_t* go = offs_h + gb + c + gl;  // offsets relative to the chunk's first dim
+      int32_t* gs = seed_h + gb + gl;
+      const int64_t rel = ai - a;
       for (int64_t g = 0; g < Gi; ++g) {
-        go[g0 + g] = a + st[g];
-        gs[g0 + g] = (int32_t)((uint32_t)seeds[i] + (uint32_t)g);  // :282, int32 wrap
+        go[g] = rel + st[g];
+        gs[g] = (int32_t)((uint32_t)seeds[i] + (uint32_t)g);  // :282, int32 wrap
         const int64_t dg = st[g + 1] - st[g];
         md = dg > md ? dg : md;
       }
-      imaxd[(size_t)i] = md;
-    });
-  }
-  g_offs_host[(size_t)G] = D;
-  if (bits_cap < nbits || (nbits > 0 && !bits_host))
-    return fail(CWQ_ERR_CAPACITY, "cwq_code_grouped_greedy_batch: bits_cap %lld < %lld",
-                (long long)bits_cap, (long long)nbits);
-  if (G <= 0) {
-    if (D > 0 && (e = hipMemcpyAsync(sample_host, zeros, (size_t)D * 4, hipMemcpyDeviceToHost,
-                                     s)) != hipSuccess)
-      return hip_fail(e, "sample to host");
-    if ((e = hipStreamSynchronize(s)) != hipSuccess) return hip_fail(e, "sync");
-    cwq::set_error(CWQ_OK, "");
-    return 0;
-  }
-  int64_t maxd = 0;
-  for (int64_t i = 0; i < n_items; ++i) maxd = imaxd[(size_t)i] > maxd ? imaxd[(size_t)i] : maxd;
-  if ((e = hipMemcpyAsync(offs, g_offs_host.data(), (size_t)(G + 1) * 8, hipMemcpyHostToDevice,
-                          s)) != hipSuccess)
-    return hip_fail(e, "offsets to device");
-  if ((e = hipMemcpyAsync(bseed, g_seed_host.data(), (size_t)G * 4, hipMemcpyHostToDevice, s)) !=
-      hipSuccess)
-    return hip_fail(e, "seeds to device");
-  lap("layout");
-  // :273-284 every item's groups in one launch
-  if ((rc = encode_impl(t_loc, t_scale, zeros, ones, offs, 0, G, D, maxd, n_bits_per_step,
-                        n_steps, 0, rho, 0, idx, sample, w + l.enc, workspace_bytes - l.enc, opts,
-                        stream, bseed)) < 0)
-    return rc;
-  if ((rc = cwq_destandardise(sample, p_loc, p_scale, D, out, stream)) < 0) return rc;  // :292
-  g_idx_host.resize((size_t)(G * n_steps));
-  if ((e = hipMemcpyAsync(g_idx_host.data(), idx, (size_t)(G * n_steps) * 4,
-                          hipMemcpyDeviceToHost, s)) != hipSuccess)
-    return hip_fail(e, "indices to host");
-  if ((e = hipMemcpyAsync(sample_host, out, (size_t)D * 4, hipMemcpyDeviceToHost, s)) !=
-      hipSuccess)
-    return hip_fail(e, "sample to host");
-  if ((e = hipStreamSynchronize(s)) != hipSuccess) return hip_fail(e, "sync");
-  lap("encode");
-  // :81-87, :288 the items' bitcodes at bits_off[i] (items are consecutive in
-  // the group order), items side by side on host threads as the partitions
+      gl += Gi;
+    }
+    offs_h[gb + c + gl] = a_of(c + 1) - a;
+    cs[(size_t)c].G = gl;
+    cs[(size_t)c].maxd = md;
+    return CWQ_OK;
+  };
+  auto bits = [&](int64_t c) -> int {
+    if (hipEventSynchronize(done_ev[c]) != hipSuccess)
+      return fail(CWQ_ERR_HIP, "results copy failed");
+    const int64_t gb = gbase(c);
+    for (int64_t i = ci[(size_t)c]; i < ci[(size_t)c + 1]; ++i) {
+      const int64_t Gi = n_starts[i] - 1 > 0 ? n_starts[i] - 1 : 0;
+      const int64_t nw = write_bitcode(idx_h + (gb + gloc[(size_t)i]) * n_steps, Gi * n_steps,
+                                       n_bits_per_step, bits_host + bits_off[i]);
+      if (nw < 0) return (int)nw;
+    }
+    return CWQ_OK;
+  };
+  auto set_flag = [&](std::atomic<int>& f, int v) {
+    {
+      std::lock_guard<std::mutex> lk(mu);
+      f.store(v);
+    }
+    cv.notify_all();
+  };
+  auto run_prep = [&](int64_t c) {
+    const int r = prep(c);
+    if (r < 0) {
+      int z = 0;
+      err_rc.compare_exchange_strong(z, r);
+    }
+    set_flag(cs[(size_t)c].prepared, r < 0 ? -1 : 1);
+  };
+  auto run_bits = [&](int64_t c) {
+    {  // bits_off of the chunk's items is known once the chunk is enqueued
+      std::unique_lock<std::mutex> lk(mu);
+      cv.wait(lk, [&] { return cs[(size_t)c].enqueued.load() != 0; });
+    }
+    if (cs[(size_t)c].enqueued.load() < 0) return;
+    const int r = bits(c);
+    if (r < 0) {
+      int z = 0;
+      err_rc.compare_exchange_strong(z, r);
+    }
+  };
+  auto worker = [&]() {
+    for (int64_t c = 0; c < K; ++c)
+      if (!cs[(size_t)c].prep_claimed.exchange(1)) run_prep(c);
+    for (int64_t c = 0; c < K; ++c)
+      if (!cs[(size_t)c].bits_claimed.exchange(1)) run_bits(c);
+  };
+  std::vector<std::thread> pool;
   {
-    std::vector<int64_t> rcs((size_t)n_items, 0);
-    const int32_t* idh = g_idx_host.data();  // thread_local: resolve here, not in the workers
-    for_items([&](int64_t i) {
-      rcs[(size_t)i] = write_bitcode(idh + gfirst[(size_t)i] * n_steps,
-                                     (gfirst[(size_t)i + 1] - gfirst[(size_t)i]) * n_steps,
-                                     n_bits_per_step, bits_host + bits_off[i]);
-    });
-    for (int64_t i = 0; i < n_items; ++i)
-      if (rcs[(size_t)i] < 0) return fail((int)rcs[(size_t)i], "index does not fit %d bits",
-                                          n_bits_per_step);
+    // thread creation may fail (pids cgroup, RLIMIT_NPROC): the exception must
+    // not cross the C ABI; the calling thread then runs the remaining tasks
+    const int64_t nw = K > 1 ? std::min<int64_t>(host_threads() - 1, 2 * K) : 0;
+    try {
+      for (int64_t t = 0; t < nw; ++t) pool.emplace_back(worker);
+    } catch (...) {
+    }
   }
-  lap("bits");
+  // the calling thread: chunk by chunk, in order, enqueue the device work
+  int64_t Gtot = 0;
+  int64_t c_done = 0;  // chunks whose device work was enqueued
+  for (int64_t c = 0; c < K && err_rc.load() == 0; ++c) {
+    if (!cs[(size_t)c].prep_claimed.exchange(1)) run_prep(c);
+    {
+      std::unique_lock<std::mutex> lk(mu);
+      cv.wait(lk, [&] { return cs[(size_t)c].prepared.load() != 0; });
+    }
+    if (cs[(size_t)c].prepared.load() < 0) break;
+    lap("prepared", c);
+    const int64_t i0 = ci[(size_t)c], i1 = ci[(size_t)c + 1];
+    for (int64_t i = i0; i < i1; ++i) {
+      const int64_t Gi = n_starts[i] - 1 > 0 ? n_starts[i] - 1 : 0;
+      bits_off[i + 1] = bits_off[i] + Gi * (int64_t)n_steps * n_bits_per_step;
+    }
+    if (bits_off[i1] > bits_cap) {
+      int z = 0;
+      err_rc.compare_exchange_strong(
+          z, fail(CWQ_ERR_CAPACITY, "cwq_code_grouped_greedy_batch: bits_cap %lld < %lld",
+                  (long long)bits_cap, (long long)bits_off[i1]));
+      break;
+    }
+    const ChunkState& ch = cs[(size_t)c];
+    const int64_t a = a_of(c), Dc = a_of(c + 1) - a, gb = gbase(c);
+    Gtot += ch.G;
+    rc = CWQ_OK;
+    // the caller's eval events span the chunks' encodes (device gaps between
+    // chunks included); eval_ms_out sums the chunks' own spans
+    if (o.eval_start_event && c == 0 &&
+        (e = hipEventRecord((hipEvent_t)o.eval_start_event, s)) != hipSuccess)
+      rc = hip_fail(e, "event");
+    if (rc == CWQ_OK && ch.G > 0) {
+      if ((e = hipMemcpyAsync(offs + gb + c, offs_h + gb + c, (size_t)(ch.G + 1) * 8,
+                              hipMemcpyHostToDevice, s)) != hipSuccess ||
+          (e = hipMemcpyAsync(bseed + gb, seed_h + gb, (size_t)ch.G * 4, hipMemcpyHostToDevice,
+                              s)) != hipSuccess)
+        rc = hip_fail(e, "layout to device");
+      if (rc == CWQ_OK && o.eval_ms_out)
+        if ((e = hipEventRecord(tev.ev[(size_t)(2 * c)], s)) != hipSuccess)
+          rc = hip_fail(e, "event");
+      // :273-284 the chunk's groups in one launch sequence (events: none here)
+      cwq_options oc = o;
+      oc.eval_start_event = oc.eval_stop_event = nullptr;
+      oc.eval_ms_out = nullptr;
+      if (rc == CWQ_OK)
+        rc = encode_impl(t_loc + a, t_scale + a, zeros + a, ones + a, offs + gb + c, 0, ch.G, Dc,
+                         ch.maxd, n_bits_per_step, n_steps, 0, rho, 0, idx + gb * n_steps,
+                         sample + a, w + l.enc, workspace_bytes - l.enc, &oc, stream, bseed + gb);
+      if (rc == CWQ_OK && o.eval_ms_out)
+        if ((e = hipEventRecord(tev.ev[(size_t)(2 * c + 1)], s)) != hipSuccess)
+          rc = hip_fail(e, "event");
+      if (rc == CWQ_OK)  // :292 destandardise
+        rc = cwq_destandardise(sample + a, p_loc + a, p_scale + a, Dc, out + a, stream);
+      if (rc == CWQ_OK &&
+          (e = hipMemcpyAsync(idx_h + gb * n_steps, idx + gb * n_steps,
+                              (size_t)(ch.G * n_steps) * 4, hipMemcpyDeviceToHost, s)) !=
+              hipSuccess)
+        rc = hip_fail(e, "indices to host");
+    } else if (rc == CWQ_OK && Dc > 0) {  // no groups (empty items only): the sample is zeros
+      if ((e = hipMemsetAsync(out + a, 0, (size_t)Dc * 4, s)) != hipSuccess)
+        rc = hip_fail(e, "memset");
+    }
+    if (rc == CWQ_OK && o.eval_stop_event && c == K - 1 &&
+        (e = hipEventRecord((hipEvent_t)o.eval_stop_event, s)) != hipSuccess)
+      rc = hip_fail(e, "event");
+    if (rc == CWQ_OK && Dc > 0 &&
+        (e = hipMemcpyAsync(sample_host + a, out + a, (size_t)Dc * 4, hipMemcpyDeviceToHost,
+                            s)) != hipSuccess)
+      rc = hip_fail(e, "sample to host");
+    if (rc == CWQ_OK && (e = hipEventRecord(done_ev[c], s)) != hipSuccess)
+      rc = hip_fail(e, "event");
+    if (rc < 0) {
+      int z = 0;
+      err_rc.compare_exchange_strong(z, rc);
+      break;
+    }
+    set_flag(cs[(size_t)c].enqueued, 1);
+    c_done = c + 1;
+    lap("enqueued", c);
+  }
+  // chunks never enqueued release the workers waiting for them; then the
+  // calling thread takes the bitcode tasks no worker took
+  for (int64_t c = c_done; c < K; ++c) {
+    cs[(size_t)c].prep_claimed.store(1);  // not started from now on
+    set_flag(cs[(size_t)c].enqueued, -1);
+  }
+  for (int64_t c = 0; c < K; ++c)
+    if (!cs[(size_t)c].bits_claimed.exchange(1)) run_bits(c);
+  for (auto& th : pool) th.join();
+  // no device work of this call may outlive it (also after an error)
+  if ((e = hipStreamSynchronize(s)) != hipSuccess && err_rc.load() == 0)
+    return hip_fail(e, "sync");
+  if (err_rc.load() < 0) return err_rc.load();
+  lap("bits done", K);
+  if (o.eval_ms_out) {
+    float tot = 0.0f;
+    for (int64_t c = 0; c < K; ++c) {
+      if (cs[(size_t)c].G <= 0) continue;
+      float ms = 0.0f;
+      if ((e = hipEventElapsedTime(&ms, tev.ev[(size_t)(2 * c)], tev.ev[(size_t)(2 * c + 1)])) !=
+          hipSuccess)
+        return hip_fail(e, "event time");
+      tot += ms;
+    }
+    *o.eval_ms_out = tot;
+  }
   cwq::set_error(CWQ_OK, "");
-  return G;
+  return Gtot;
 }
 
 // ---------------------------------------------------------------------------

@@ -91,14 +91,21 @@ int cwq_stateless_normal_sample(const float* loc, const float* scale, int64_t d,
  *   eval_start_event / eval_stop_event: hipEvent_t handles (both or neither)
  *               recorded on the call's stream right before the first
  *               candidate-scoring launch and right after the last one, so a
- *               caller can time the dominant kernel alone (bench.py). */
+ *               caller can time the dominant kernel alone (bench.py).
+ *   eval_ms_out: HOST float, or NULL.  The fused grouped greedy calls
+ *               (cwq_code_grouped_greedy[_batch]), which synchronise, write
+ *               the summed milliseconds of their candidate-scoring launches
+ *               (a pipelined batch codes in chunks: device gaps between them
+ *               are excluded, unlike the event span).  Asynchronous entry
+ *               points ignore it. */
 typedef struct cwq_options {
   int32_t prune_mode;
   int32_t reserved; /* must be 0 */
   void* eval_start_event;
   void* eval_stop_event;
+  float* eval_ms_out;
 } cwq_options;
-#define CWQ_OPTIONS_INIT {2, 0, NULL, NULL}
+#define CWQ_OPTIONS_INIT {2, 0, NULL, NULL, NULL}
 
 /* Workspace bytes needed by cwq_greedy_encode (CSR blocks) for nb blocks
  * holding total_dims dims in all, none longer than max_block_dim: the argmax
@@ -203,25 +210,35 @@ int64_t cwq_code_grouped_greedy(const float* q_loc, const float* q_scale, const 
  * concatenated DEVICE q_* / p_* (item_off: HOST int64 [n_items + 1], item_off[0]
  * == 0) and is coded exactly as cwq_code_grouped_greedy on that slice with seed
  * seeds[i] (HOST int32 [n_items]): its own partition (:207-252), its groups
- * numbered from 0 and coded with seeds[i] + g (:273-284).  One standardisation,
- * one KL copy, ONE encode launch over every item's groups (per-block seeds) and
- * one destandardisation serve all items; the host partitions and bitcodes of
- * the items run on up to 8 host threads.  HOST outputs: sample_host
- * [D_total]; item i's bitcode at bits_host[bits_off[i], bits_off[i+1])
- * (bits_off: HOST int64 [n_items + 1], written); item i's group_start_indices
- * (local, incl. its trailing D_i): n_starts[i] entries (HOST int64 [n_items],
- * written) at starts_host + item_off[i] + 2 i (starts_cap >= D_total + 2
- * n_items).  Returns the total number of groups, or a negative error code.
- * Synchronises twice. */
+ * numbered from 0 and coded with seeds[i] + g (:273-284).  One standardisation
+ * and KL launch serve all items; the items are then pipelined in chunks of
+ * consecutive items (CWQ_BATCH_CHUNKS, about D_total / 6 dims each): chunk
+ * c's KL arrives on the host, host threads partition it and lay out its groups
+ * while the device codes chunk c - 1 (one encode launch sequence per chunk,
+ * per-block seeds), and chunk c - 1's bitcodes are written while chunk c codes.
+ * HOST outputs: sample_host [D_total]; item i's bitcode at
+ * bits_host[bits_off[i], bits_off[i+1]) (bits_off: HOST int64 [n_items + 1],
+ * written); item i's group_start_indices (local, incl. its trailing D_i):
+ * n_starts[i] entries (HOST int64 [n_items], written) at starts_host +
+ * item_off[i] + 2 i (starts_cap >= D_total + 2 n_items).  host_workspace:
+ * HOST staging of host_workspace_bytes >=
+ * cwq_code_grouped_greedy_batch_host_workspace_size (per-dim KL, group
+ * offsets, seeds, indices), page-locked for asynchronous copies (hipHostMalloc,
+ * or torch's pinned memory); NULL = library-owned pageable staging (slower
+ * copies).  sample_host is best page-locked as well.  Returns the total number
+ * of groups, or a negative error code.  Returns only after all of its device
+ * work has finished (also on error). */
 size_t cwq_code_grouped_greedy_batch_workspace_size(int64_t D_total, int64_t n_items,
                                                     int n_steps);
+size_t cwq_code_grouped_greedy_batch_host_workspace_size(int64_t D_total, int64_t n_items,
+                                                         int n_steps);
 int64_t cwq_code_grouped_greedy_batch(
     int64_t n_items, const int64_t* item_off, const float* q_loc, const float* q_scale,
     const float* p_loc, const float* p_scale, int n_steps, int n_bits_per_step,
     const int32_t* seeds, float rho, int64_t size_threshold, double n_nats, float* sample_host,
     char* bits_host, int64_t bits_cap, int64_t* bits_off, int64_t* starts_host,
     int64_t starts_cap, int64_t* n_starts, void* workspace, size_t workspace_bytes,
-    const cwq_options* opts, void* stream);
+    void* host_workspace, size_t host_workspace_bytes, const cwq_options* opts, void* stream);
 
 /* ---- Importance sampler (code/coded_importance_sampler.py) ------------- */
 /* Workspace bytes for cwq_importance_encode. */
