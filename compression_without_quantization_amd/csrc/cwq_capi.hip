@@ -913,30 +913,47 @@ int64_t cwq_code_grouped_greedy_batch(
   int32_t* idx = (int32_t*)(w + l.idx);
   int32_t* bseed = (int32_t*)(w + bl.seeds);
 
-  // chunks of consecutive items, about D / K dims each (at least one item)
+  // chunks of consecutive items (at least one each): the first about half the
+  // size of the others, so the device starts after a short first host phase
   std::vector<int64_t> ci;  // chunk c = items [ci[c], ci[c + 1])
   {
     const int64_t K = D < (1 << 16) ? 1 : std::min<int64_t>(batch_chunks(), n_items);
     ci.push_back(0);
-    for (int64_t i = 1; i < n_items; ++i)
-      if ((int64_t)ci.size() < K &&
-          item_off[i] * K >= D * (int64_t)ci.size() && item_off[i] > item_off[ci.back()])
+    for (int64_t i = 1; i < n_items; ++i) {
+      const int64_t c = (int64_t)ci.size();  // boundary c at D (c - 1/2) / (K - 1/2)
+      if (c < K && item_off[i] * (2 * K - 1) >= D * (2 * c - 1) &&
+          item_off[i] > item_off[ci.back()])
         ci.push_back(i);
+    }
     ci.push_back(n_items);
   }
   const int64_t K = (int64_t)ci.size() - 1;
   auto a_of = [&](int64_t c) { return item_off[ci[(size_t)c]]; };
   auto gbase = [&](int64_t c) { return a_of(c) + ci[(size_t)c]; };  // group-array region
 
-  // events: K KL copies, K chunk results; + 2 K timing events for eval_ms_out
+  // Streams: the coding on the caller's stream s; device-to-host copies (the
+  // KL chunks, then each chunk's results) on d2h and the chunks' layouts on
+  // h2d, library copy streams of s's device, so the copies overlap the coding.
+  // Events: KL ready; per chunk its KL on the host, its layout on the device,
+  // its results computed, its results on the host (+ 2 K timing events).
+  hipStream_t d2h = cwq::copy_stream(s, 0), h2d = cwq::copy_stream(s, 1);
+  if (!d2h || !h2d) d2h = h2d = s;
   CallEvents evs;
-  if (!evs.made((int)(2 * K), s, hipEventDisableTiming))
+  if (!evs.made((int)(4 * K + 1), s, hipEventDisableTiming))
     return fail(CWQ_ERR_HIP, "cwq_code_grouped_greedy_batch: event creation failed");
   CallEvents tev;
   if (o.eval_ms_out && !tev.made((int)(2 * K), s, hipEventDefault))
     return fail(CWQ_ERR_HIP, "cwq_code_grouped_greedy_batch: event creation failed");
   hipEvent_t* kl_ev = evs.ev.data();
   hipEvent_t* done_ev = evs.ev.data() + K;
+  hipEvent_t* h2d_ev = evs.ev.data() + 2 * K;
+  hipEvent_t* res_ev = evs.ev.data() + 3 * K;
+  hipEvent_t kl_ready = evs.ev[(size_t)(4 * K)];
+  auto drain = [&]() {  // nothing this call queued may outlive it
+    (void)hipStreamSynchronize(h2d);
+    (void)hipStreamSynchronize(s);
+    (void)hipStreamSynchronize(d2h);
+  };
 
   hipError_t e = hipSuccess;
   int rc;
@@ -950,15 +967,17 @@ int64_t cwq_code_grouped_greedy_batch(
   if (D > 0 && (e = hipMemsetD32Async((hipDeviceptr_t)ones, 0x3f800000u, (size_t)D, s)) !=
                    hipSuccess)
     return hip_fail(e, "memset");
-  for (int64_t c = 0; c < K; ++c) {
+  if ((e = hipEventRecord(kl_ready, s)) == hipSuccess) e = hipStreamWaitEvent(d2h, kl_ready, 0);
+  for (int64_t c = 0; c < K && e == hipSuccess; ++c) {
     const int64_t a = a_of(c), n = a_of(c + 1) - a;
-    if (n > 0 && (e = hipMemcpyAsync(kl_h + a, kl + a, (size_t)n * 4, hipMemcpyDeviceToHost, s)) !=
-                     hipSuccess)
+    if (n > 0 &&
+        (e = hipMemcpyAsync(kl_h + a, kl + a, (size_t)n * 4, hipMemcpyDeviceToHost, d2h)) !=
+            hipSuccess)
       break;
-    if ((e = hipEventRecord(kl_ev[c], s)) != hipSuccess) break;
+    e = hipEventRecord(kl_ev[c], d2h);
   }
   if (e != hipSuccess) {
-    (void)hipStreamSynchronize(s);
+    drain();
     return hip_fail(e, "KL to host");
   }
   lap("kl queued", 0);
@@ -1102,9 +1121,11 @@ int64_t cwq_code_grouped_greedy_batch(
       rc = hip_fail(e, "event");
     if (rc == CWQ_OK && ch.G > 0) {
       if ((e = hipMemcpyAsync(offs + gb + c, offs_h + gb + c, (size_t)(ch.G + 1) * 8,
-                              hipMemcpyHostToDevice, s)) != hipSuccess ||
+                              hipMemcpyHostToDevice, h2d)) != hipSuccess ||
           (e = hipMemcpyAsync(bseed + gb, seed_h + gb, (size_t)ch.G * 4, hipMemcpyHostToDevice,
-                              s)) != hipSuccess)
+                              h2d)) != hipSuccess ||
+          (e = hipEventRecord(h2d_ev[c], h2d)) != hipSuccess ||
+          (e = hipStreamWaitEvent(s, h2d_ev[c], 0)) != hipSuccess)
         rc = hip_fail(e, "layout to device");
       if (rc == CWQ_OK && o.eval_ms_out)
         if ((e = hipEventRecord(tev.ev[(size_t)(2 * c)], s)) != hipSuccess)
@@ -1122,11 +1143,6 @@ int64_t cwq_code_grouped_greedy_batch(
           rc = hip_fail(e, "event");
       if (rc == CWQ_OK)  // :292 destandardise
         rc = cwq_destandardise(sample + a, p_loc + a, p_scale + a, Dc, out + a, stream);
-      if (rc == CWQ_OK &&
-          (e = hipMemcpyAsync(idx_h + gb * n_steps, idx + gb * n_steps,
-                              (size_t)(ch.G * n_steps) * 4, hipMemcpyDeviceToHost, s)) !=
-              hipSuccess)
-        rc = hip_fail(e, "indices to host");
     } else if (rc == CWQ_OK && Dc > 0) {  // no groups (empty items only): the sample is zeros
       if ((e = hipMemsetAsync(out + a, 0, (size_t)Dc * 4, s)) != hipSuccess)
         rc = hip_fail(e, "memset");
@@ -1134,11 +1150,20 @@ int64_t cwq_code_grouped_greedy_batch(
     if (rc == CWQ_OK && o.eval_stop_event && c == K - 1 &&
         (e = hipEventRecord((hipEvent_t)o.eval_stop_event, s)) != hipSuccess)
       rc = hip_fail(e, "event");
+    // the chunk's results to the host on d2h, behind the coding of the next chunk
+    if (rc == CWQ_OK && ((e = hipEventRecord(res_ev[c], s)) != hipSuccess ||
+                         (e = hipStreamWaitEvent(d2h, res_ev[c], 0)) != hipSuccess))
+      rc = hip_fail(e, "event");
+    if (rc == CWQ_OK && ch.G > 0 &&
+        (e = hipMemcpyAsync(idx_h + gb * n_steps, idx + gb * n_steps,
+                            (size_t)(ch.G * n_steps) * 4, hipMemcpyDeviceToHost, d2h)) !=
+            hipSuccess)
+      rc = hip_fail(e, "indices to host");
     if (rc == CWQ_OK && Dc > 0 &&
         (e = hipMemcpyAsync(sample_host + a, out + a, (size_t)Dc * 4, hipMemcpyDeviceToHost,
-                            s)) != hipSuccess)
+                            d2h)) != hipSuccess)
       rc = hip_fail(e, "sample to host");
-    if (rc == CWQ_OK && (e = hipEventRecord(done_ev[c], s)) != hipSuccess)
+    if (rc == CWQ_OK && (e = hipEventRecord(done_ev[c], d2h)) != hipSuccess)
       rc = hip_fail(e, "event");
     if (rc < 0) {
       int z = 0;
@@ -1158,7 +1183,14 @@ int64_t cwq_code_grouped_greedy_batch(
   for (int64_t c = 0; c < K; ++c)
     if (!cs[(size_t)c].bits_claimed.exchange(1)) run_bits(c);
   for (auto& th : pool) th.join();
-  // no device work of this call may outlive it (also after an error)
+  // no device work of this call may outlive it (also after an error); the
+  // caller's stream is ordered after the copies
+  if (c_done > 0 && (e = hipStreamWaitEvent(s, done_ev[c_done - 1], 0)) != hipSuccess &&
+      err_rc.load() == 0) {
+    drain();
+    return hip_fail(e, "join");
+  }
+  drain();
   if ((e = hipStreamSynchronize(s)) != hipSuccess && err_rc.load() == 0)
     return hip_fail(e, "sync");
   if (err_rc.load() < 0) return err_rc.load();

@@ -74,6 +74,11 @@ struct EncodeArgs {
 
 #define CWQ_SLIST_PER_BLOCK 8
 
+// Library copy streams (which = 0: device to host, 1: host to device) on the
+// device of the caller's stream, created once per host thread; nullptr if they
+// cannot be made.  Used by the pipelined batch coder to overlap its copies with
+// the coding on the caller's stream.
+hipStream_t copy_stream(hipStream_t stream, int which);
 hipError_t launch_encode(const EncodeArgs& a, hipStream_t stream);
 hipError_t launch_decode(const int32_t* idx, const float* p_loc, const float* p_scale,
                          const int64_t* block_off, int64_t ud, int64_t nb, int64_t total_dims,

@@ -2310,6 +2310,7 @@ constexpr int kMaxDevices = 16;
 struct ForkStreams {
   bool ok = false;
   hipStream_t s[kMaxSplit] = {};
+  hipStream_t cp[2] = {};  // copy streams of the pipelined batch coder (D2H, H2D)
   hipEvent_t fork = nullptr, join[kMaxSplit] = {};
   ~ForkStreams() {  // thread exit (the process's main thread: exit(), before HIP's teardown)
     if (!ok) return;
@@ -2317,6 +2318,7 @@ struct ForkStreams {
       (void)hipStreamDestroy(s[i]);
       (void)hipEventDestroy(join[i]);
     }
+    for (int i = 0; i < 2; ++i) (void)hipStreamDestroy(cp[i]);
     (void)hipEventDestroy(fork);
   }
 };
@@ -2333,17 +2335,22 @@ ForkStreams* fork_streams(hipStream_t stream) {
     if (hipGetDevice(&cur) != hipSuccess) return nullptr;
     if (cur != dev && hipSetDevice(dev) != hipSuccess) return nullptr;
     bool good = true;
-    int made_s = 0, made_e = 0;
+    int made_s = 0, made_e = 0, made_c = 0;
     for (int i = 0; i < kMaxSplit && good; ++i) {
       good = hipStreamCreateWithFlags(&f.s[i], hipStreamNonBlocking) == hipSuccess;
       made_s += good;
       good = good && hipEventCreateWithFlags(&f.join[i], hipEventDisableTiming) == hipSuccess;
       made_e += good;
     }
+    for (int i = 0; i < 2 && good; ++i) {
+      good = hipStreamCreateWithFlags(&f.cp[i], hipStreamNonBlocking) == hipSuccess;
+      made_c += good;
+    }
     good = good && hipEventCreateWithFlags(&f.fork, hipEventDisableTiming) == hipSuccess;
     if (!good) {  // nothing half-made stays behind; the caller runs unsplit
       for (int i = 0; i < made_s; ++i) (void)hipStreamDestroy(f.s[i]);
       for (int i = 0; i < made_e; ++i) (void)hipEventDestroy(f.join[i]);
+      for (int i = 0; i < made_c; ++i) (void)hipStreamDestroy(f.cp[i]);
     }
     if (cur != dev) (void)hipSetDevice(cur);
     if (!good) return nullptr;
@@ -2352,6 +2359,11 @@ ForkStreams* fork_streams(hipStream_t stream) {
   return &f;
 }
 }  // namespace
+
+hipStream_t copy_stream(hipStream_t stream, int which) {
+  ForkStreams* f = fork_streams(stream);
+  return f && which >= 0 && which < 2 ? f->cp[which] : nullptr;
+}
 
 hipError_t launch_encode(const EncodeArgs& a, hipStream_t stream) {
   hipError_t e;
