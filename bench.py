@@ -318,7 +318,8 @@ def grouped_cpu_baseline(args, lat_np, res0, bits, n_steps):
            "one_core_sample": f"{cd1 / sum(work):.3%} of image 0's candidate-dims, {dt1:.2f} s"}
     parity = {"groups_checked": int(round(sum(st.size - 1 for *_, st in sets) * frac)),
               "index_mismatches": mi, "sample_word_mismatches": ms,
-              "oracle": "oracle/cwq_oracle.c (CPU restatement; TF reference unpinned)"}
+              "oracle": "oracle/cwq_oracle.c (CPU restatement; TF reference unpinned)",
+              "normaliser_sensitivity": normaliser_sensitivity("c2") if bits == 8 else None}
     return cpu, parity
 
 
@@ -508,6 +509,30 @@ def affinity_cores():
     except (OSError, ValueError):
         pass
     return n, quota
+
+
+def normaliser_sensitivity(section):
+    """profiles/normaliser_sensitivity.json's record for one workload (the
+    oracle re-encoded with log sigma from Eigen plog, +-1 ulp, random +-1 ulp:
+    tools/normaliser_sensitivity.py) as the parity field's bound on how many
+    indices hang on the undeclarable normaliser choice."""
+    f = os.path.join(REPO, "profiles", "normaliser_sensitivity.json")
+    if not os.path.exists(f):
+        return None
+    with open(f) as fh:
+        r = json.load(fh).get(section)
+    if not r:
+        return None
+    var = ("plog", "plog_fma", "up", "down", "random")
+    flips = {v: r[v]["index_flips"] for v in var if v in r}
+    n = r["indices"]
+    return {"normaliser_ulp_flip_rate": max(flips.values()) / n if flips else None,
+            "indices_per_variant": n, "flips": flips,
+            "flip_rate_95pct_upper": (3.0 / n if flips and max(flips.values()) == 0 else None),
+            "best_second_gap_min": r.get("best_second_gap", {}).get("min"),
+            "source": "profiles/normaliser_sensitivity.json (tools/normaliser_sensitivity.py, "
+                      "CPU oracle; log sigma from Eigen plog / plog+FMA / logf +1 ulp / -1 ulp / "
+                      "random +-1 ulp)"}
 
 
 def rank_device_map(dist, rank, local_rank, dev):
@@ -853,7 +878,9 @@ def main():
             checked, mism_idx, mism_smp = (int(v) for v in m.tolist())
         parity = {"blocks_checked": checked, "index_mismatches": mism_idx,
                   "sample_word_mismatches": mism_smp,
-                  "oracle": "oracle/cwq_oracle.c (CPU restatement; TF reference unpinned)"}
+                  "oracle": "oracle/cwq_oracle.c (CPU restatement; TF reference unpinned)",
+                  "normaliser_sensitivity": (normaliser_sensitivity("c4")
+                                             if (d, bits, n_steps) == (32, 16, 1) else None)}
 
     if rank == 0:
         line = {

@@ -12,7 +12,9 @@
 #include <time.h>
 #include <immintrin.h>
 
+#include <algorithm>
 #include <atomic>
+#include <memory>
 #include <condition_variable>
 #include <mutex>
 #include <sched.h>
@@ -982,67 +984,43 @@ int64_t cwq_code_grouped_greedy_batch(
   }
   lap("kl queued", 0);
 
-  // Host tasks, on worker threads (the calling thread sequences the device):
-  //   prep(c): the items' partitions (:207-252; item i's starts at
-  //            item_off[i] + 2 i) and the chunk's CSR layout, local group
-  //            numbers, seeds seeds[i] + g (:282);
-  //   bits(c): after chunk c's indices are on the host, the items' LSB-first
-  //            bitcodes at bits_off[i] (:81-87, :288).
+  // Host tasks, on worker threads (the calling thread sequences the device),
+  // claimed in item order:
+  //   part(i): item i's partition (:207-252; its starts at item_off[i] + 2 i)
+  //            once its chunk's KL is on the host; the thread that finishes a
+  //            chunk's last partition lays out the chunk's CSR offsets (local
+  //            group numbers) and seeds seeds[i] + g (:282);
+  //   bits(i): once item i's chunk is on the host, its LSB-first bitcode at
+  //            bits_off[i] (:81-87, :288).
   // The calling thread runs any task no worker has taken when it needs it
   // (also when no worker thread could be started).
   struct ChunkState {
-    std::atomic<int> prep_claimed{0}, bits_claimed{0};
-    std::atomic<int> prepared{0};  // 1 done, -1 failed
+    std::atomic<int64_t> parts_left{0};
+    std::atomic<int> failed{0};
+    std::atomic<int> prepared{0};  // 1 laid out, -1 failed
     std::atomic<int> enqueued{0};  // 1 results on their way (bits_off known), -1 abandoned
     int64_t G = 0, maxd = 0;
   };
   std::vector<ChunkState> cs((size_t)K);
+  std::vector<int64_t> chunk_of((size_t)n_items), imaxd((size_t)n_items, 0);
+  for (int64_t c = 0; c < K; ++c) {
+    cs[(size_t)c].parts_left.store(ci[(size_t)c + 1] - ci[(size_t)c]);
+    for (int64_t i = ci[(size_t)c]; i < ci[(size_t)c + 1]; ++i) chunk_of[(size_t)i] = c;
+  }
+  std::unique_ptr<std::atomic<int>[]> part_claimed(new std::atomic<int>[(size_t)n_items]);
+  std::unique_ptr<std::atomic<int>[]> bits_claimed(new std::atomic<int>[(size_t)n_items]);
+  for (int64_t i = 0; i < n_items; ++i) {
+    part_claimed[(size_t)i].store(0);
+    bits_claimed[(size_t)i].store(0);
+  }
   std::vector<int64_t> gloc((size_t)n_items + 1, 0);  // item's first group within its chunk
   std::atomic<int> err_rc{0};
   std::mutex mu;
   std::condition_variable cv;
   const float* klh = kl_h;
-  auto prep = [&](int64_t c) -> int {
-    if (hipEventSynchronize(kl_ev[c]) != hipSuccess)
-      return fail(CWQ_ERR_HIP, "KL copy failed");
-    const int64_t i0 = ci[(size_t)c], i1 = ci[(size_t)c + 1], a = a_of(c), gb = gbase(c);
-    int64_t gl = 0, md = 0;
-    for (int64_t i = i0; i < i1; ++i) {
-      const int64_t ai = item_off[i], Di = item_off[i + 1] - ai;
-      int64_t* st = starts_host + ai + 2 * i;
-      const int64_t ns = group_starts_impl(Di > 0 ? klh + ai : nullptr, Di, size_threshold,
-                                           n_nats, st, Di + 2, false);
-      if (ns < 0) return (int)ns;
-      n_starts[i] = ns;
-      const int64_t Gi = ns - 1 > 0 ? ns - 1 : 0;
-      gloc[(size_t)i] = gl;
-      int64_t* go = offs_h + gb + c + gl;  // offsets relative to the chunk's first dim
-      int32_t* gs = seed_h + gb + gl;
-      const int64_t rel = ai - a;
-      for (int64_t g = 0; g < Gi; ++g) {
-        go[g] = rel + st[g];
-        gs[g] = (int32_t)((uint32_t)seeds[i] + (uint32_t)g);  // :282, int32 wrap
-        const int64_t dg = st[g + 1] - st[g];
-        md = dg > md ? dg : md;
-      }
-      gl += Gi;
-    }
-    offs_h[gb + c + gl] = a_of(c + 1) - a;
-    cs[(size_t)c].G = gl;
-    cs[(size_t)c].maxd = md;
-    return CWQ_OK;
-  };
-  auto bits = [&](int64_t c) -> int {
-    if (hipEventSynchronize(done_ev[c]) != hipSuccess)
-      return fail(CWQ_ERR_HIP, "results copy failed");
-    const int64_t gb = gbase(c);
-    for (int64_t i = ci[(size_t)c]; i < ci[(size_t)c + 1]; ++i) {
-      const int64_t Gi = n_starts[i] - 1 > 0 ? n_starts[i] - 1 : 0;
-      const int64_t nw = write_bitcode(idx_h + (gb + gloc[(size_t)i]) * n_steps, Gi * n_steps,
-                                       n_bits_per_step, bits_host + bits_off[i]);
-      if (nw < 0) return (int)nw;
-    }
-    return CWQ_OK;
+  auto record_err = [&](int r) {
+    int z = 0;
+    err_rc.compare_exchange_strong(z, r);
   };
   auto set_flag = [&](std::atomic<int>& f, int v) {
     {
@@ -1051,37 +1029,82 @@ int64_t cwq_code_grouped_greedy_batch(
     }
     cv.notify_all();
   };
-  auto run_prep = [&](int64_t c) {
-    const int r = prep(c);
-    if (r < 0) {
-      int z = 0;
-      err_rc.compare_exchange_strong(z, r);
-    }
-    set_flag(cs[(size_t)c].prepared, r < 0 ? -1 : 1);
+  auto partition = [&](int64_t i) -> int {
+    const int64_t c = chunk_of[(size_t)i];
+    if (hipEventSynchronize(kl_ev[c]) != hipSuccess) return fail(CWQ_ERR_HIP, "KL copy failed");
+    const int64_t ai = item_off[i], Di = item_off[i + 1] - ai;
+    int64_t* st = starts_host + ai + 2 * i;
+    const int64_t ns = group_starts_impl(Di > 0 ? klh + ai : nullptr, Di, size_threshold, n_nats,
+                                         st, Di + 2, false);
+    if (ns < 0) return (int)ns;
+    n_starts[i] = ns;
+    int64_t md = 0;
+    for (int64_t g = 0; g + 1 < ns; ++g) md = std::max(md, st[g + 1] - st[g]);
+    imaxd[(size_t)i] = md;
+    return CWQ_OK;
   };
-  auto run_bits = [&](int64_t c) {
+  auto layout = [&](int64_t c) {  // every item of chunk c is partitioned
+    const int64_t a = a_of(c), gb = gbase(c);
+    int64_t gl = 0, md = 0;
+    for (int64_t i = ci[(size_t)c]; i < ci[(size_t)c + 1]; ++i) {
+      const int64_t* st = starts_host + item_off[i] + 2 * i;
+      const int64_t Gi = n_starts[i] - 1 > 0 ? n_starts[i] - 1 : 0;
+      gloc[(size_t)i] = gl;
+      int64_t* go = offs_h + gb + c + gl;  // offsets relative to the chunk's first dim
+      int32_t* gs = seed_h + gb + gl;
+      const int64_t rel = item_off[i] - a;
+      for (int64_t g = 0; g < Gi; ++g) {
+        go[g] = rel + st[g];
+        gs[g] = (int32_t)((uint32_t)seeds[i] + (uint32_t)g);  // :282, int32 wrap
+      }
+      md = std::max(md, imaxd[(size_t)i]);
+      gl += Gi;
+    }
+    offs_h[gb + c + gl] = a_of(c + 1) - a;
+    cs[(size_t)c].G = gl;
+    cs[(size_t)c].maxd = md;
+  };
+  auto run_part = [&](int64_t i) {
+    const int64_t c = chunk_of[(size_t)i];
+    const int r = err_rc.load() ? CWQ_OK : partition(i);
+    if (r < 0) {
+      record_err(r);
+      cs[(size_t)c].failed.store(1);
+    }
+    if (cs[(size_t)c].parts_left.fetch_sub(1) == 1) {  // the chunk's last partition
+      const bool bad = cs[(size_t)c].failed.load() || err_rc.load();
+      if (!bad) layout(c);
+      lap("prepared", c);
+      set_flag(cs[(size_t)c].prepared, bad ? -1 : 1);
+    }
+  };
+  auto run_bits = [&](int64_t i) {
+    const int64_t c = chunk_of[(size_t)i];
     {  // bits_off of the chunk's items is known once the chunk is enqueued
       std::unique_lock<std::mutex> lk(mu);
       cv.wait(lk, [&] { return cs[(size_t)c].enqueued.load() != 0; });
     }
     if (cs[(size_t)c].enqueued.load() < 0) return;
-    const int r = bits(c);
-    if (r < 0) {
-      int z = 0;
-      err_rc.compare_exchange_strong(z, r);
+    if (hipEventSynchronize(done_ev[c]) != hipSuccess) {
+      record_err(fail(CWQ_ERR_HIP, "results copy failed"));
+      return;
     }
+    const int64_t Gi = n_starts[i] - 1 > 0 ? n_starts[i] - 1 : 0;
+    const int64_t nw = write_bitcode(idx_h + (gbase(c) + gloc[(size_t)i]) * n_steps, Gi * n_steps,
+                                     n_bits_per_step, bits_host + bits_off[i]);
+    if (nw < 0) record_err((int)nw);
   };
   auto worker = [&]() {
-    for (int64_t c = 0; c < K; ++c)
-      if (!cs[(size_t)c].prep_claimed.exchange(1)) run_prep(c);
-    for (int64_t c = 0; c < K; ++c)
-      if (!cs[(size_t)c].bits_claimed.exchange(1)) run_bits(c);
+    for (int64_t i = 0; i < n_items; ++i)
+      if (!part_claimed[(size_t)i].exchange(1)) run_part(i);
+    for (int64_t i = 0; i < n_items; ++i)
+      if (!bits_claimed[(size_t)i].exchange(1)) run_bits(i);
   };
   std::vector<std::thread> pool;
   {
     // thread creation may fail (pids cgroup, RLIMIT_NPROC): the exception must
     // not cross the C ABI; the calling thread then runs the remaining tasks
-    const int64_t nw = K > 1 ? std::min<int64_t>(host_threads() - 1, 2 * K) : 0;
+    const int64_t nw = K > 1 ? std::min<int64_t>(host_threads() - 1, n_items) : 0;
     try {
       for (int64_t t = 0; t < nw; ++t) pool.emplace_back(worker);
     } catch (...) {
@@ -1091,23 +1114,21 @@ int64_t cwq_code_grouped_greedy_batch(
   int64_t Gtot = 0;
   int64_t c_done = 0;  // chunks whose device work was enqueued
   for (int64_t c = 0; c < K && err_rc.load() == 0; ++c) {
-    if (!cs[(size_t)c].prep_claimed.exchange(1)) run_prep(c);
+    for (int64_t i = ci[(size_t)c]; i < ci[(size_t)c + 1]; ++i)
+      if (!part_claimed[(size_t)i].exchange(1)) run_part(i);
     {
       std::unique_lock<std::mutex> lk(mu);
       cv.wait(lk, [&] { return cs[(size_t)c].prepared.load() != 0; });
     }
     if (cs[(size_t)c].prepared.load() < 0) break;
-    lap("prepared", c);
     const int64_t i0 = ci[(size_t)c], i1 = ci[(size_t)c + 1];
     for (int64_t i = i0; i < i1; ++i) {
       const int64_t Gi = n_starts[i] - 1 > 0 ? n_starts[i] - 1 : 0;
       bits_off[i + 1] = bits_off[i] + Gi * (int64_t)n_steps * n_bits_per_step;
     }
     if (bits_off[i1] > bits_cap) {
-      int z = 0;
-      err_rc.compare_exchange_strong(
-          z, fail(CWQ_ERR_CAPACITY, "cwq_code_grouped_greedy_batch: bits_cap %lld < %lld",
-                  (long long)bits_cap, (long long)bits_off[i1]));
+      record_err(fail(CWQ_ERR_CAPACITY, "cwq_code_grouped_greedy_batch: bits_cap %lld < %lld",
+                      (long long)bits_cap, (long long)bits_off[i1]));
       break;
     }
     const ChunkState& ch = cs[(size_t)c];
@@ -1166,8 +1187,7 @@ int64_t cwq_code_grouped_greedy_batch(
     if (rc == CWQ_OK && (e = hipEventRecord(done_ev[c], d2h)) != hipSuccess)
       rc = hip_fail(e, "event");
     if (rc < 0) {
-      int z = 0;
-      err_rc.compare_exchange_strong(z, rc);
+      record_err(rc);
       break;
     }
     set_flag(cs[(size_t)c].enqueued, 1);
@@ -1176,12 +1196,11 @@ int64_t cwq_code_grouped_greedy_batch(
   }
   // chunks never enqueued release the workers waiting for them; then the
   // calling thread takes the bitcode tasks no worker took
-  for (int64_t c = c_done; c < K; ++c) {
-    cs[(size_t)c].prep_claimed.store(1);  // not started from now on
-    set_flag(cs[(size_t)c].enqueued, -1);
-  }
-  for (int64_t c = 0; c < K; ++c)
-    if (!cs[(size_t)c].bits_claimed.exchange(1)) run_bits(c);
+  for (int64_t i = 0; i < n_items; ++i)
+    if (chunk_of[(size_t)i] >= c_done) part_claimed[(size_t)i].store(1);  // not started from now on
+  for (int64_t c = c_done; c < K; ++c) set_flag(cs[(size_t)c].enqueued, -1);
+  for (int64_t i = 0; i < n_items; ++i)
+    if (!bits_claimed[(size_t)i].exchange(1)) run_bits(i);
   for (auto& th : pool) th.join();
   // no device work of this call may outlive it (also after an error); the
   // caller's stream is ordered after the copies

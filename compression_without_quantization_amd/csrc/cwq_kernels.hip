@@ -1663,33 +1663,72 @@ __global__ void __launch_bounds__(256) k_small_survivors(
     const int64_t* __restrict__ block_off, int64_t ud, int64_t nb, int64_t n_cand, SeedSpec sd,
     int32_t step, const float4* __restrict__ grp, const uint32_t* __restrict__ gtau,
     const uint32_t* __restrict__ scnt, const uint2* __restrict__ slist,
-    unsigned long long* __restrict__ keys) {
+    const float* __restrict__ bpre, unsigned long long* __restrict__ keys) {
   __shared__ double logtab[32];
+  // per wave: the listed rows still reaching their block's final threshold,
+  // queued until 64 of them can be scored at once, one per lane (a lane per
+  // slot left ~6% of the lanes busy: ~1 survivor per block, 8 slots)
+  constexpr int kQueue = 64 + 64 * CWQ_SLIST_PER_BLOCK;
+  __shared__ int64_t q_g[4][kQueue];
+  __shared__ uint32_t q_n[4][kQueue];
   fill_logtab(logtab);
   const uint32_t lane = threadIdx.x & 63u;
-  const int64_t nthr = (int64_t)gridDim.x * blockDim.x;
-  // listed rows, one slot per thread (blocks and alignments differ from lane
-  // to lane)
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-       i < CWQ_SLIST_PER_BLOCK * nb; i += nthr) {
-    const int64_t g = i / CWQ_SLIST_PER_BLOCK;
-    const uint32_t slot = (uint32_t)(i - g * CWQ_SLIST_PER_BLOCK);
-    if (grp[g].x == 0.0f) continue;  // scored exactly below
-    const BlockSpan sp = block_span(block_off, ud, g);
-    if (slot >= scnt[sp.off + 12 * g]) continue;
-    const uint2 e = slist[i];
-    const int64_t n = (int64_t)e.x;
-    if (u2f(e.y) < unord_f32(gtau[g * CWQ_CSR_GTAU_STRIDE])) continue;
-    const PhiloxStream st = generate_key(step_seed(sd.of(g), step), 42);
-    const float v = eval_row<0, STEP0>(st, (uint64_t)n * (uint64_t)sp.d, sp.d,
-                                       (int)(((uint64_t)n * (uint64_t)sp.d) & 3u),
-                                       loc_s + sp.off, scale_s + sp.off, t_loc + sp.off,
-                                       t_scale + sp.off, lognorm + sp.off,
-                                       STEP0 ? nullptr : best + sp.off, logtab);
-    atomicMax(&keys[g], (unsigned long long)argmax_key(v, (uint32_t)n));
-  }
-  // blocks whose constants failed the gate, or whose survivors overflowed
+  const uint32_t wv = wave_id();
   const int64_t nwaves = (int64_t)gridDim.x * 4;
+  auto score = [&](int64_t g, uint32_t n) {
+    const BlockSpan sp = block_span(block_off, ud, g);
+    const float* bg = bpre + sp.off + 12 * g;  // k_small_prep: the step's stream key
+    const PhiloxStream st{f2u(bg[1]), f2u(bg[2]), f2u(bg[3]), f2u(bg[4])};
+    const uint64_t k0 = (uint64_t)n * (uint64_t)sp.d;
+    const float v = eval_row<0, STEP0>(st, k0, sp.d, (int)(k0 & 3u), loc_s + sp.off,
+                                       scale_s + sp.off, t_loc + sp.off, t_scale + sp.off,
+                                       lognorm + sp.off, STEP0 ? nullptr : best + sp.off, logtab);
+    atomicMax(&keys[g], (unsigned long long)argmax_key(v, n));
+  };
+  int q = 0;  // wave-uniform queue length
+  for (int64_t gb = ((int64_t)blockIdx.x * 4 + wv) * 64; gb < nb; gb += nwaves * 64) {
+    const int64_t g = gb + lane;
+    uint32_t cnt = 0, keep = 0;  // listed slots; bit s: slot s survives
+    if (g < nb && grp[g].x != 0.0f) {  // exact blocks are scored below
+      const BlockSpan sp = block_span(block_off, ud, g);
+      const uint32_t c = scnt[sp.off + 12 * g];
+      const uint32_t ns = c < CWQ_SLIST_PER_BLOCK ? c : CWQ_SLIST_PER_BLOCK;
+      const float tau = unord_f32(gtau[g * CWQ_CSR_GTAU_STRIDE]);
+      for (uint32_t sl = 0; sl < ns; ++sl)
+        if (u2f(slist[CWQ_SLIST_PER_BLOCK * g + sl].y) >= tau) {
+          keep |= 1u << sl;
+          ++cnt;
+        }
+    }
+    // exclusive scan of the counts: this lane's first queue position
+    uint32_t inc = cnt;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t t = (uint32_t)__shfl_up((int)inc, (unsigned)o, 64);
+      if (lane >= (uint32_t)o) inc += t;
+    }
+    const uint32_t total = (uint32_t)__shfl((int)inc, 63, 64);
+    uint32_t pos = (uint32_t)q + inc - cnt;
+    for (uint32_t m = keep; m != 0u; m &= m - 1u) {
+      const uint32_t sl = (uint32_t)__builtin_ctz(m);
+      q_g[wv][pos] = g;
+      q_n[wv][pos] = slist[CWQ_SLIST_PER_BLOCK * g + sl].x;
+      ++pos;
+    }
+    q += (int)total;
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    while (q >= 64) {  // a full batch: the queue's last 64 entries
+      q -= 64;
+      const int64_t qg = q_g[wv][q + (int)lane];
+      const uint32_t qn = q_n[wv][q + (int)lane];
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      score(qg, qn);
+    }
+  }
+  if ((int)lane < q) score(q_g[wv][lane], q_n[wv][lane]);
+  // blocks whose constants failed the gate, or whose survivors overflowed
   for (int64_t g = (int64_t)blockIdx.x * 4 + wave_id(); g < nb; g += nwaves) {
     if (grp[g].x != 0.0f) continue;
     const BlockSpan sp = block_span(block_off, ud, g);
@@ -2208,12 +2247,11 @@ static void launch_small(const EncodeArgs& a, int step, hipStream_t stream) {
                      dim3(256), 0, stream, a.block_off, a.ud, ntiles, a.tiles_per_block,
                      a.cand_per_tile, a.n_cand, seeds_of(a), step, (const float2*)a.sab,
                      (const float*)a.bpre, a.grp, a.gtau, a.ordu, a.slist);
-  hipLaunchKernelGGL((k_small_survivors<STEP0>), dim3(grid_for(CWQ_SLIST_PER_BLOCK * a.nb, 256,
-                                                               4096)),
+  hipLaunchKernelGGL((k_small_survivors<STEP0>), dim3(grid_for(a.nb, 4 * 64, 4096)),
                      dim3(256), 0, stream, a.t_loc, a.t_scale, a.loc_s, a.scale_s, a.lognorm,
                      a.out_sample, a.block_off, a.ud, a.nb, a.n_cand, seeds_of(a), step,
                      (const float4*)a.grp, (const uint32_t*)a.gtau, (const uint32_t*)a.ordu,
-                     (const uint2*)a.slist, a.keys);
+                     (const uint2*)a.slist, (const float*)a.bpre, a.keys);
 }
 
 template <bool STEP0>

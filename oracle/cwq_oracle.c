@@ -254,20 +254,22 @@ static inline float stream_normal(normal_stream* st, uint64_t k) {
 static int code_greedy_sample_impl(const float* t_loc, const float* t_scale,
                                    const float* p_loc, const float* p_scale, int64_t d,
                                    int n_bits_per_step, int n_steps, int32_t seed, float rho,
-                                   const float* log_scale, int32_t* out_idx, float* out_sample);
+                                   const float* log_scale, int32_t* out_idx, float* out_sample,
+                                   double* out_gap);
 
 CWQO_API int cwqo_code_greedy_sample(const float* t_loc, const float* t_scale,
                                      const float* p_loc, const float* p_scale, int64_t d,
                                      int n_bits_per_step, int n_steps, int32_t seed, float rho,
                                      int32_t* out_idx, float* out_sample) {
   return code_greedy_sample_impl(t_loc, t_scale, p_loc, p_scale, d, n_bits_per_step, n_steps,
-                                 seed, rho, NULL, out_idx, out_sample);
+                                 seed, rho, NULL, out_idx, out_sample, NULL);
 }
 
 static int code_greedy_sample_impl(const float* t_loc, const float* t_scale,
                                    const float* p_loc, const float* p_scale, int64_t d,
                                    int n_bits_per_step, int n_steps, int32_t seed, float rho,
-                                   const float* log_scale, int32_t* out_idx, float* out_sample) {
+                                   const float* log_scale, int32_t* out_idx, float* out_sample,
+                                   double* out_gap) {
   if (n_bits_per_step < 0 || n_bits_per_step > 30 || n_steps < 1 || d < 0) return -1;
   int64_t n_samples = (int64_t)1 << n_bits_per_step;
   size_t db = (size_t)(d > 0 ? d : 1) * sizeof(float);
@@ -291,6 +293,7 @@ static int code_greedy_sample_impl(const float* t_loc, const float* t_scale,
     cwqo_generate_key(step_seed(seed, i), 42, st.key, st.ctr);
     int64_t best_idx = 0;
     float best_val = -FLT_MAX; /* ArgMaxTupleReducer initial accumulator */
+    float second_val = -FLT_MAX; /* diagnostics only (out_gap) */
     for (int64_t n = 0; n < n_samples; ++n) {
       for (int64_t j = 0; j < d; ++j) {
         float z = stream_normal(&st, (uint64_t)(n * d + j));
@@ -300,8 +303,10 @@ static int code_greedy_sample_impl(const float* t_loc, const float* t_scale,
         row[j] = log_prob_c(tv, t_loc[j], t_scale[j], lognorm[j]); /* :59 */
       }
       float v = cwqo_eigen_rowsum(row, d); /* :59 reduce_sum axis=1 */
-      if (v > best_val) { best_val = v; best_idx = n; } /* :61 argmax */
+      if (v > best_val) { second_val = best_val; best_val = v; best_idx = n; } /* :61 argmax */
+      else if (v > second_val) second_val = v;
     }
+    if (out_gap) out_gap[i] = (double)best_val - (double)second_val;
     /* :63 best_sample = test_samples[index, :] */
     for (int64_t j = 0; j < d; ++j) {
       float z = stream_normal(&st, (uint64_t)(best_idx * d + j));
@@ -368,14 +373,16 @@ CWQO_API int cwqo_greedy_encode(const float* t_loc, const float* t_scale, const 
   return err ? -1 : 0;
 }
 
-/* cwqo_greedy_encode with the per-dim log(sigma) supplied (log_scale [D]):
- * the normaliser sensitivity experiments. */
+/* cwqo_greedy_encode with the per-dim log(sigma) supplied (log_scale [D], or
+ * NULL for logf) and, if out_gap is non-NULL, the gap between the best and the
+ * second-best row value of every step: the normaliser sensitivity experiments
+ * (DESIGN.md 2). */
 CWQO_API int cwqo_greedy_encode_lsig(const float* t_loc, const float* t_scale,
                                      const float* p_loc, const float* p_scale,
                                      const int64_t* block_off, int64_t nb, int n_bits_per_step,
                                      int n_steps, int32_t seed, float rho, int64_t block_id_base,
                                      const float* log_scale, int32_t* out_idx, float* out_sample,
-                                     int nthreads) {
+                                     double* out_gap, int nthreads) {
   int err = 0;
 #ifdef _OPENMP
   if (nthreads > 0) omp_set_num_threads(nthreads);
@@ -385,8 +392,9 @@ CWQO_API int cwqo_greedy_encode_lsig(const float* t_loc, const float* t_scale,
     int64_t o = block_off[g], d = block_off[g + 1] - block_off[g];
     int32_t sg = (int32_t)((uint32_t)seed + (uint32_t)(block_id_base + g));
     int rc = code_greedy_sample_impl(t_loc + o, t_scale + o, p_loc + o, p_scale + o, d,
-                                     n_bits_per_step, n_steps, sg, rho, log_scale + o,
-                                     out_idx + g * n_steps, out_sample + o);
+                                     n_bits_per_step, n_steps, sg, rho,
+                                     log_scale ? log_scale + o : NULL, out_idx + g * n_steps,
+                                     out_sample + o, out_gap ? out_gap + g * n_steps : NULL);
     if (rc) err |= 1;
   }
   return err ? -1 : 0;

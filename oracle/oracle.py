@@ -51,7 +51,7 @@ def lib():
                                         ci]),
             "cwqo_greedy_decode": (ci, [vp, vp, vp, vp, i64, ci, ci, i32, f32, i64, vp, ci]),
             "cwqo_greedy_encode_lsig": (ci, [vp, vp, vp, vp, vp, i64, ci, ci, i32, f32, i64, vp,
-                                             vp, vp, ci]),
+                                             vp, vp, vp, ci]),
             "cwqo_eigen_plog": (f32, [f32, ci]),
             "cwqo_eigen_plog_table": (None, [vp, i64, ci, vp]),
             "cwqo_standardise": (None, [vp, vp, vp, vp, i64, vp, vp]),
@@ -173,19 +173,25 @@ def greedy_encode(t_loc, t_scale, p_loc, p_scale, block_off, n_bits_per_step, n_
 
 
 def greedy_encode_lsig(t_loc, t_scale, p_loc, p_scale, block_off, n_bits_per_step, n_steps,
-                       seed, log_scale, rho=1., block_id_base=0, nthreads=0):
+                       seed, log_scale, rho=1., block_id_base=0, nthreads=0, gaps=False):
     """greedy_encode with log(sigma_j) supplied per dim (the per-dim normaliser
-    0.9189385f + log sigma_j of SURVEY.md A.5): normaliser sensitivity only."""
-    tl, ts, pl, ps, ls = map(_f32, (t_loc, t_scale, p_loc, p_scale, log_scale))
+    0.9189385f + log sigma_j of SURVEY.md A.5; None = logf): normaliser
+    sensitivity only.  gaps=True also returns the best - second-best row value
+    of every step (float64 [nb, n_steps])."""
+    tl, ts, pl, ps = map(_f32, (t_loc, t_scale, p_loc, p_scale))
+    ls = None if log_scale is None else _f32(log_scale)
     off = np.ascontiguousarray(np.asarray(block_off, dtype=np.int64))
     nb = off.size - 1
     idx = np.zeros(nb * int(n_steps), dtype=np.int32)
     sample = np.zeros(tl.size, dtype=np.float32)
+    gap = np.zeros(nb * int(n_steps), dtype=np.float64) if gaps else None
     rc = lib().cwqo_greedy_encode_lsig(_p(tl), _p(ts), _p(pl), _p(ps), _p(off), nb,
                                        int(n_bits_per_step), int(n_steps), int(seed), float(rho),
-                                       int(block_id_base), _p(ls), _p(idx), _p(sample),
+                                       int(block_id_base), _p(ls), _p(idx), _p(sample), _p(gap),
                                        int(nthreads))
     assert rc == 0, rc
+    if gaps:
+        return idx.reshape(nb, int(n_steps)), sample, gap.reshape(nb, int(n_steps))
     return idx.reshape(nb, int(n_steps)), sample
 
 

@@ -61,10 +61,20 @@ def variants(ts, block_off, rng):
 def run(name, tl, ts, pl, ps, off, bits, n_steps, thr):
     base_idx, base_s = O.greedy_encode(tl, ts, pl, ps, off, bits, n_steps, 42, 1.0, 0, thr)
     lf = O.logf_table(ts)
-    same_idx, same_s = O.greedy_encode_lsig(tl, ts, pl, ps, off, bits, n_steps, 42, lf, 1.0, 0, thr)
+    same_idx, same_s, gap = O.greedy_encode_lsig(tl, ts, pl, ps, off, bits, n_steps, 42, lf, 1.0,
+                                                 0, thr, gaps=True)
     assert np.array_equal(same_idx, base_idx) and np.array_equal(same_s.view(np.uint32),
                                                                    base_s.view(np.uint32))
     out = {"indices": int(base_idx.size), "blocks": int(off.size - 1), "n_bits": bits}
+    # a changed normaliser moves every row by nearly the same amount: only rows
+    # within the summation's rounding noise (~1e-5 nats for these rows) of the
+    # winner can trade places, so the best - second-best gaps bound the rate
+    g = gap.reshape(-1)
+    out["best_second_gap"] = {
+        "min": float(g.min()), "median": float(np.median(g)),
+        "frac_below_1e-4": float((g < 1e-4).mean()), "frac_below_1e-5": float((g < 1e-5).mean()),
+        "frac_below_1e-6": float((g < 1e-6).mean()),
+        "frac_below_1e-2_per_nat": float((g < 1e-2).mean() / 1e-2)}
     half = np.float32(0.5 * np.log(2.0 * np.pi))
     c_base = half + lf
     for vname, ls in variants(ts, off, np.random.default_rng(7)).items():
