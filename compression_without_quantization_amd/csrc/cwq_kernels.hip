@@ -1726,28 +1726,30 @@ __global__ void __launch_bounds__(256) k_small_survivors(
       __builtin_amdgcn_wave_barrier();
       score(qg, qn);
     }
+    // blocks k_small_screen did not screen (constants failed the gate, or
+    // their survivor slots overflowed): every candidate exactly, the wave per block
+    for (uint64_t m = __ballot(g < nb && grp[g].x == 0.0f); m != 0ull; m &= m - 1ull) {
+      const int64_t ge = gb + (int64_t)__builtin_ctzll(m);
+      const BlockSpan sp = block_span(block_off, ud, ge);
+      const float* bg = bpre + sp.off + 12 * ge;
+      const PhiloxStream st{f2u(bg[1]), f2u(bg[2]), f2u(bg[3]), f2u(bg[4])};
+      uint64_t bestk = 0;
+      for (int r = 0; r < 4; ++r) {  // rows n = r (mod 4): one alignment class per pass
+        const int align = (int)(((uint64_t)r * (uint64_t)sp.d) & 3u);
+        for (int64_t n = r + 4 * (int64_t)lane; n < n_cand; n += 256) {
+          const float v = eval_row<0, STEP0>(st, (uint64_t)n * (uint64_t)sp.d, sp.d, align,
+                                             loc_s + sp.off, scale_s + sp.off, t_loc + sp.off,
+                                             t_scale + sp.off, lognorm + sp.off,
+                                             STEP0 ? nullptr : best + sp.off, logtab);
+          const uint64_t k = argmax_key(v, (uint32_t)n);
+          bestk = k > bestk ? k : bestk;
+        }
+      }
+      bestk = wave_max_u64(bestk);
+      if (lane == 0 && bestk) atomicMax(&keys[ge], (unsigned long long)bestk);
+    }
   }
   if ((int)lane < q) score(q_g[wv][lane], q_n[wv][lane]);
-  // blocks whose constants failed the gate, or whose survivors overflowed
-  for (int64_t g = (int64_t)blockIdx.x * 4 + wave_id(); g < nb; g += nwaves) {
-    if (grp[g].x != 0.0f) continue;
-    const BlockSpan sp = block_span(block_off, ud, g);
-    const PhiloxStream st = generate_key(step_seed(sd.of(g), step), 42);
-    uint64_t bestk = 0;
-    for (int r = 0; r < 4; ++r) {  // rows n = r (mod 4): one alignment class per pass
-      const int align = (int)(((uint64_t)r * (uint64_t)sp.d) & 3u);
-      for (int64_t n = r + 4 * (int64_t)lane; n < n_cand; n += 256) {
-        const float v = eval_row<0, STEP0>(st, (uint64_t)n * (uint64_t)sp.d, sp.d, align,
-                                           loc_s + sp.off, scale_s + sp.off, t_loc + sp.off,
-                                           t_scale + sp.off, lognorm + sp.off,
-                                           STEP0 ? nullptr : best + sp.off, logtab);
-        const uint64_t k = argmax_key(v, (uint32_t)n);
-        bestk = k > bestk ? k : bestk;
-      }
-    }
-    bestk = wave_max_u64(bestk);
-    if (lane == 0 && bestk) atomicMax(&keys[g], (unsigned long long)bestk);
-  }
 }
 
 // ---------------------------------------------------------------------------

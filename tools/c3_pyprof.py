@@ -26,6 +26,20 @@ def step():
     return C.code_grouped_greedy_sample_batch(None, T, P, 1, 8, 42)
 
 
+native_s = []
+if os.environ.get("C3_SPLIT"):  # time the native call inside the wrapper
+    from compression_without_quantization_amd import _lib
+    lib = _lib.load()
+    fn = lib.cwq_code_grouped_greedy_batch
+
+    def timed_native(*a):
+        t = time.perf_counter()
+        r = fn(*a)
+        native_s.append(time.perf_counter() - t)
+        return r
+    lib.cwq_code_grouped_greedy_batch = timed_native
+
+
 for _ in range(3):
     step()
 torch.cuda.synchronize()
@@ -34,6 +48,8 @@ t0 = time.perf_counter()
 for _ in range(n):
     step()
 print("ms per call", (time.perf_counter() - t0) / n * 1e3)
+if native_s:
+    print("native ms per call", sum(native_s[-n:]) / n * 1e3)
 if os.environ.get("C3_NO_CPROFILE"):
     sys.exit(0)
 pr = cProfile.Profile()
