@@ -1917,6 +1917,9 @@ __global__ void __launch_bounds__(256) k_decode(
 #ifndef CWQ_DECODE_MIN_WAVES
 #define CWQ_DECODE_MIN_WAVES 1  // waves/SIMD the decoder's registers must allow (tuning)
 #endif
+#ifndef CWQ_DECODE_NT
+#define CWQ_DECODE_NT 0
+#endif
 __global__ void __launch_bounds__(256, CWQ_DECODE_MIN_WAVES) k_decode_q4(
     const int32_t* __restrict__ idx, const float4* __restrict__ p_loc,
     const float4* __restrict__ p_scale, uint32_t qpb, uint32_t bpw, int64_t nb, int n_steps,
@@ -1942,8 +1945,16 @@ __global__ void __launch_bounds__(256, CWQ_DECODE_MIN_WAVES) k_decode_q4(
       const int64_t g = gb0 + (int64_t)(j * bpw + L.lb);
       if (L.active && g < nb) {
         const int64_t t = g * qpb + L.q;
+#if CWQ_DECODE_NT  // streamed once: non-temporal loads (tuning builds)
+        typedef float nt4 __attribute__((ext_vector_type(4)));
+        const nt4 va = __builtin_nontemporal_load(reinterpret_cast<const nt4*>(p_loc) + t);
+        const nt4 vb = __builtin_nontemporal_load(reinterpret_cast<const nt4*>(p_scale) + t);
+        a = float4{va.x, va.y, va.z, va.w};
+        b = float4{vb.x, vb.y, vb.z, vb.w};
+#else
         a = p_loc[t];
         b = p_scale[t];
+#endif
         if (unit) n = idx[g];
       }
     };
@@ -1986,7 +1997,13 @@ __global__ void __launch_bounds__(256, CWQ_DECODE_MIN_WAVES) k_decode_q4(
           v[w] = v[w] + sv;  // :153 tile(sample) + samples, row indices[i]
         }
       }
+#if CWQ_DECODE_NT
+      typedef float nt4 __attribute__((ext_vector_type(4)));
+      const nt4 vo = {v[0], v[1], v[2], v[3]};
+      __builtin_nontemporal_store(vo, reinterpret_cast<nt4*>(out_sample) + g * qpb + L.q);
+#else
       out_sample[g * qpb + L.q] = make_float4(v[0], v[1], v[2], v[3]);
+#endif
     }
   }
 }
