@@ -57,6 +57,8 @@ def _is_float32(x):
 
 def _f32(x, device, what):
     if isinstance(x, torch.Tensor):
+        if x.device == device and x.dtype == torch.float32 and x.is_contiguous():
+            return x.view(-1)  # the common case, without three no-op torch calls
         t = x
     else:
         t = torch.from_numpy(np.ascontiguousarray(np.asarray(x)))
@@ -421,14 +423,17 @@ def code_grouped_greedy_sample_batch(sess, targets, proposals, n_steps, n_bits_p
     seeds32 = np.array([np.int32(np.uint32(x & 0xFFFFFFFF)) for x in seeds], dtype=np.int32)
     need = int(lib.cwq_code_grouped_greedy_batch_workspace_size(D, n_items, n_steps))
     ws = torch.empty(max(need, 1), dtype=torch.uint8, device=dev)
-    # page-locked host memory from torch's caching host allocator: the staging
-    # the library copies through and the sample / starts this call returns
-    # (asynchronous DMA copies; cached blocks are reused without page faults)
+    # page-locked host memory (asynchronous DMA copies, no page faults): the
+    # staging the library copies through is this thread's cached buffer; the
+    # sample and starts this call returns share one block of torch's caching
+    # host allocator (the arrays keep it alive)
     hneed = int(lib.cwq_code_grouped_greedy_batch_host_workspace_size(D, n_items, n_steps))
-    hws = torch.empty(max(hneed, 1), dtype=torch.uint8, pin_memory=True)
-    sample_t = torch.empty(max(D, 1), dtype=torch.float32, pin_memory=True)
-    starts_t = torch.empty(D + 2 * n_items, dtype=torch.int64, pin_memory=True)
-    sample_h, starts_h = sample_t.numpy(), starts_t.numpy()
+    hws = _pinned_scratch(hneed)
+    n_out = D + 2 * n_items
+    out_t = torch.empty(max(D, 1) * 4 + n_out * 8, dtype=torch.uint8, pin_memory=True)
+    out_np = out_t.numpy()
+    starts_h = out_np[:n_out * 8].view(np.int64)
+    sample_h = out_np[n_out * 8:].view(np.float32)
     bits_cap = (D + n_items) * n_bits_per_group
     bits_h = _scratch_bytes(bits_cap)  # consumed into str below: reusable
     bits_off = np.empty(n_items + 1, dtype=np.int64)
@@ -442,7 +447,7 @@ def code_grouped_greedy_sample_batch(sess, targets, proposals, n_steps, n_bits_p
             group_size_threshold(max_group_size_bits), float(n_nats), sample_h.ctypes.data,
             bits_h.ctypes.data, bits_cap, bits_off.ctypes.data, starts_h.ctypes.data,
             starts_h.size, n_starts.ctypes.data, ws.data_ptr(), ws.numel(), hws.data_ptr(),
-            hws.numel(), _lib.options(prune_mode, eval_events, eval_ms_out), stream),
+            hneed, _lib.options(prune_mode, eval_events, eval_ms_out), stream),
             "cwq_code_grouped_greedy_batch")
     out = []
     mv = memoryview(bits_h)
@@ -455,6 +460,16 @@ def code_grouped_greedy_sample_batch(sess, targets, proposals, n_steps, n_bits_p
 
 
 _scratch = threading.local()
+
+
+def _pinned_scratch(n):
+    """This thread's reusable page-locked host buffer of at least n bytes (a
+    torch pinned tensor; the library's staging, never returned to callers)."""
+    buf = getattr(_scratch, "pinned", None)
+    if buf is None or buf.numel() < n:
+        buf = torch.empty(max(int(n), 1), dtype=torch.uint8, pin_memory=True)
+        _scratch.pinned = buf
+    return buf
 
 
 def _scratch_bytes(n):
