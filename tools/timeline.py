@@ -21,7 +21,20 @@ ev.sort()
 end = max(e[1] for e in ev)
 sel = [e for e in ev if e[0] >= end - win * 1e6]
 t0 = sel[0][0]
-busy = 0
-last = t0
 for s, e, n in sel:
     print(f"{(s - t0) / 1e3:9.1f} {(e - t0) / 1e3:9.1f} {(e - s) / 1e3:8.1f}  {n}")
+# device-busy fraction of the window: the union of the dispatch intervals
+busy, cur_s, cur_e = 0, None, None
+for s, e, n in sel:
+    if not n.startswith("K"):
+        continue
+    if cur_e is None or s > cur_e:
+        if cur_e is not None:
+            busy += cur_e - cur_s
+        cur_s, cur_e = s, e
+    else:
+        cur_e = max(cur_e, e)
+if cur_e is not None:
+    busy += cur_e - cur_s
+span = sel[-1][1] - t0
+print(f"# window {span / 1e3:.1f} us, kernels busy {busy / 1e3:.1f} us = {busy / span:.1%}")
