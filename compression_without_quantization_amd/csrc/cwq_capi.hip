@@ -935,15 +935,15 @@ int64_t cwq_code_grouped_greedy_batch(
   int32_t* idx = (int32_t*)(w + l.idx);
   int32_t* bseed = (int32_t*)(w + bl.seeds);
 
-  // chunks of consecutive items (at least one each): the first about half the
-  // size of the others, so the device starts after a short first host phase
+  // chunks of consecutive items (at least one each): the first about a quarter
+  // the size of the others, so the device starts after a short first host phase
   std::vector<int64_t> ci;  // chunk c = items [ci[c], ci[c + 1])
   {
     const int64_t K = D < (1 << 16) ? 1 : std::min<int64_t>(batch_chunks(), n_items);
     ci.push_back(0);
     for (int64_t i = 1; i < n_items; ++i) {
-      const int64_t c = (int64_t)ci.size();  // boundary c at D (c - 1/2) / (K - 1/2)
-      if (c < K && item_off[i] * (2 * K - 1) >= D * (2 * c - 1) &&
+      const int64_t c = (int64_t)ci.size();  // boundary c at D (c - 3/4) / (K - 3/4)
+      if (c < K && item_off[i] * (4 * K - 3) >= D * (4 * c - 3) &&
           item_off[i] > item_off[ci.back()])
         ci.push_back(i);
     }
