@@ -598,6 +598,17 @@ struct CallEvents {
       for (hipEvent_t e : ev) tl_events.free_ev[dev][timing].push_back(e);
   }
 };
+// Waits for an event by polling (the batch coder's host threads wait on
+// copies of a few hundred microseconds: a blocking wait's wake-up latency is
+// of the same order), falling back to the blocking wait after ~2 ms.
+hipError_t wait_event(hipEvent_t e) {
+  for (int i = 0; i < 20000; ++i) {
+    const hipError_t q = hipEventQuery(e);
+    if (q != hipErrorNotReady) return q;
+    _mm_pause();
+  }
+  return hipEventSynchronize(e);
+}
 thread_local std::vector<float> g_kl_host;
 thread_local std::vector<int32_t> g_idx_host;
 // :81-87, :288 (and binary_io.py:41-53) each of n indices as n_bits LSB-first
@@ -1051,7 +1062,8 @@ int64_t cwq_code_grouped_greedy_batch(
   };
   auto partition = [&](int64_t i) -> int {
     const int64_t c = chunk_of[(size_t)i];
-    if (hipEventSynchronize(kl_ev[c]) != hipSuccess) return fail(CWQ_ERR_HIP, "KL copy failed");
+    if (wait_event(kl_ev[c]) != hipSuccess) return fail(CWQ_ERR_HIP, "KL copy failed");
+    lap("kl in", i);
     const int64_t ai = item_off[i], Di = item_off[i + 1] - ai;
     int64_t* st = starts_host + ai + 2 * i;
     const int64_t ns = group_starts_impl(Di > 0 ? klh + ai : nullptr, Di, size_threshold, n_nats,
@@ -1061,6 +1073,7 @@ int64_t cwq_code_grouped_greedy_batch(
     int64_t md = 0;
     for (int64_t g = 0; g + 1 < ns; ++g) md = std::max(md, st[g + 1] - st[g]);
     imaxd[(size_t)i] = md;
+    lap("parted", i);
     return CWQ_OK;
   };
   auto layout = [&](int64_t c) {  // every item of chunk c is partitioned
@@ -1105,7 +1118,7 @@ int64_t cwq_code_grouped_greedy_batch(
       cv.wait(lk, [&] { return cs[(size_t)c].enqueued.load() != 0; });
     }
     if (cs[(size_t)c].enqueued.load() < 0) return;
-    if (hipEventSynchronize(done_ev[c]) != hipSuccess) {
+    if (wait_event(done_ev[c]) != hipSuccess) {
       record_err(fail(CWQ_ERR_HIP, "results copy failed"));
       return;
     }

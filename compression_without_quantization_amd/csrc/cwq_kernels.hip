@@ -33,7 +33,11 @@ __global__ void __launch_bounds__(256) k_prep_dims(
     const float* __restrict__ t_scale, const float* __restrict__ p_loc,
     const float* __restrict__ p_scale, int64_t n, float nst, float sdiv, float rho,
     float* __restrict__ loc_s, float* __restrict__ scale_s, float* __restrict__ lognorm,
-    float* __restrict__ out_sample) {
+    float* __restrict__ out_sample, unsigned long long* __restrict__ keys, int64_t nb) {
+  // step 0's argmax keys start at 0 (one launch less than a memset)
+  for (int64_t g = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; g < nb;
+       g += (int64_t)gridDim.x * blockDim.x)
+    keys[g] = 0ull;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x) {
     loc_s[i] = p_loc[i] / nst;                // p_loc / n_steps
@@ -2158,12 +2162,14 @@ static bool aligned16(const void* a, const void* b, const void* c) {
 
 hipError_t launch_prep_dims(const float* t_scale, const float* p_loc, const float* p_scale,
                             int64_t n, int n_steps, float rho, float* loc_s, float* scale_s,
-                            float* lognorm, float* out_sample, hipStream_t stream) {
-  if (n <= 0) return hipSuccess;
+                            float* lognorm, float* out_sample, unsigned long long* keys,
+                            int64_t nb, hipStream_t stream) {
+  if (n <= 0 && nb <= 0) return hipSuccess;
   const float nst = (float)n_steps;
   const float sdiv = (float)__builtin_sqrt((double)n_steps);
-  hipLaunchKernelGGL(k_prep_dims, dim3(grid_for(n, 256, 65536)), dim3(256), 0, stream, t_scale,
-                     p_loc, p_scale, n, nst, sdiv, rho, loc_s, scale_s, lognorm, out_sample);
+  hipLaunchKernelGGL(k_prep_dims, dim3(grid_for(n > nb ? n : nb, 256, 65536)), dim3(256), 0,
+                     stream, t_scale, p_loc, p_scale, n, nst, sdiv, rho, loc_s, scale_s, lognorm,
+                     out_sample, keys, nb);
   return hipGetLastError();
 }
 
@@ -2319,8 +2325,10 @@ static hipError_t encode_steps(const EncodeArgs& a, hipStream_t stream, bool eve
   const unsigned fgrid_dims =
       grid_for(a.total_dims > a.nb ? a.total_dims : a.nb, 256, CWQ_FIN_MAX_WGS);
   for (int s = 0; s < a.n_steps; ++s) {
-    e = hipMemsetAsync(a.keys, 0, (size_t)a.nb * sizeof(unsigned long long), stream);
-    if (e != hipSuccess) return e;
+    // step 0's keys were zeroed by k_prep_dims (launch_encode)
+    if (s > 0 && (e = hipMemsetAsync(a.keys, 0, (size_t)a.nb * sizeof(unsigned long long),
+                                     stream)) != hipSuccess)
+      return e;
     if (events && s == 0 && a.ev_start) {
       e = hipEventRecord((hipEvent_t)a.ev_start, stream);
       if (e != hipSuccess) return e;
@@ -2425,7 +2433,7 @@ hipStream_t copy_stream(hipStream_t stream, int which) {
 hipError_t launch_encode(const EncodeArgs& a, hipStream_t stream) {
   hipError_t e;
   e = launch_prep_dims(a.t_scale, a.p_loc, a.p_scale, a.total_dims, a.n_steps, a.rho, a.loc_s,
-                       a.scale_s, a.lognorm, a.out_sample, stream);
+                       a.scale_s, a.lognorm, a.out_sample, a.keys, a.nb, stream);
   if (e != hipSuccess) return e;
   if (a.nb == 0) return hipSuccess;
   ForkStreams* f = (CWQ_ENCODE_SPLIT > 1 && a.block_off != nullptr && a.n_steps > 1 &&
