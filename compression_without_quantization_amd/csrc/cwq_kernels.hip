@@ -1921,6 +1921,9 @@ __global__ void __launch_bounds__(256) k_decode(
 #ifndef CWQ_DECODE_MIN_WAVES
 #define CWQ_DECODE_MIN_WAVES 1  // waves/SIMD the decoder's registers must allow (tuning)
 #endif
+#ifndef CWQ_DECODE_PROBE
+#define CWQ_DECODE_PROBE 0  // tuning builds: 1 = loads/stores only, 2 = arithmetic only
+#endif
 #ifndef CWQ_DECODE_NT
 #define CWQ_DECODE_NT 1  // non-temporal float4 streams: 3-4% faster on C4 (tools/decode_variants.sh)
 #endif
@@ -1947,6 +1950,12 @@ __global__ void __launch_bounds__(256, CWQ_DECODE_MIN_WAVES) k_decode_q4(
     int32_t n1 = 0;  // single-step index
     auto load = [&](uint32_t j, float4& a, float4& b, int32_t& n) {
       const int64_t g = gb0 + (int64_t)(j * bpw + L.lb);
+      if (CWQ_DECODE_PROBE == 2) {  // timing probe only: arithmetic without the loads
+        a = float4{0.1f, 0.2f, 0.3f, (float)g};
+        b = float4{1.0f, 1.1f, 1.2f, 1.3f};
+        n = (int32_t)(g * 7919u) & 0xffff;
+        return;
+      }
       if (L.active && g < nb) {
         const int64_t t = g * qpb + L.q;
 #if CWQ_DECODE_NT  // streamed once: non-temporal loads (tuning builds)
@@ -1992,7 +2001,11 @@ __global__ void __launch_bounds__(256, CWQ_DECODE_MIN_WAVES) k_decode_q4(
           continue;
         }
         const PhiloxStream st = unit ? ku : generate_key(step_seed(sg, i), 42);
+#if CWQ_DECODE_PROBE == 1  // timing probe only: memory traffic without the arithmetic
+        const F4 z{__builtin_bit_cast(float, st.k0 ^ (uint32_t)n), 1.0f, 1.0f, 1.0f};
+#else
         const F4 z = normal4_dev(st, (uint64_t)n * qpb + L.q, logtab);
+#endif
         const float zz[4] = {z.a, z.b, z.c, z.d};
 #pragma unroll
         for (int w = 0; w < 4; ++w) {

@@ -204,6 +204,10 @@ def test_c3_batch_equals_per_image_calls(cwq):
     ([5000, 300, 6000], [1, 2, 3], 14, 3),   # multi-step: the forked stream parts
     ([2, 1, 3], 9, 6, 2),                    # tiny items, one seed for all
     ([0, 5, 0, 0, 700], [3, 4, 5, 6, 7], 8, 1),  # empty items (one empty group each)
+    # >= 65,536 dims: the pipelined path (several chunks, empty and 1-dim items
+    # inside chunks, a chunk boundary next to an empty item)
+    ([70000, 0, 1, 30000, 0, 50000, 2, 40000, 3, 0], list(range(10)), 8, 1),
+    ([40000, 30000, 20000, 5, 25000], [11, -12, 13, 14, 15], 12, 3),  # chunked multi-step
 ])
 def test_grouped_batch_equals_single_calls(cwq, sizes, seeds, bits, n_steps):
     """Per-item seeds (int32 wrap-around included), items of 1 dim, and
@@ -365,3 +369,56 @@ def test_encode_blocks_host_streamed_equals_one_call(cwq, nb, d, chunk, n_steps,
     assert hi.shape == (nb, n_steps) and hs.shape == (nb * d,)
     assert np.array_equal(hi, gi.cpu().numpy())
     assert np.array_equal(hs.view(np.uint32), gs.cpu().numpy().view(np.uint32))
+
+
+def test_grouped_batch_errors_and_pageable_staging(cwq):
+    """cwq_code_grouped_greedy_batch through ctypes: a short host workspace or
+    bits buffer is refused (CWQ_ERR_WORKSPACE / CWQ_ERR_CAPACITY) and the call
+    returns with no device work outstanding; with no host workspace (library
+    pageable staging) the results equal the pinned path's."""
+    import ctypes
+    from compression_without_quantization_amd import _lib
+    from compression_without_quantization_amd.coded_greedy_sampler import group_size_threshold
+    lib = _lib.load()
+    rng = np.random.default_rng(9)
+    sizes = [50000, 3, 30000, 0, 20000]
+    D, n = sum(sizes), len(sizes)
+    cat = []
+    pl = (0.1 * rng.standard_normal(D)).astype(np.float32)
+    ps = rng.uniform(0.8, 1.2, D).astype(np.float32)
+    ql = (pl + ps * rng.standard_normal(D) * 0.7).astype(np.float32)
+    qs = (ps * rng.uniform(0.3, 1.0, D)).astype(np.float32)
+    cat = [torch.from_numpy(x).cuda() for x in (ql, qs, pl, ps)]
+    item_off = np.concatenate([[0], np.cumsum(sizes)]).astype(np.int64)
+    seeds = np.arange(n, dtype=np.int32)
+    ws = torch.empty(lib.cwq_code_grouped_greedy_batch_workspace_size(D, n, 1), dtype=torch.uint8,
+                     device="cuda")
+    hneed = lib.cwq_code_grouped_greedy_batch_host_workspace_size(D, n, 1)
+    hws = torch.empty(hneed, dtype=torch.uint8, pin_memory=True)
+
+    def call(bits_cap, host_ws, host_bytes):
+        sample = np.empty(D, np.float32)
+        bits = np.empty(max(bits_cap, 1), np.uint8)
+        starts = np.empty(D + 2 * n, np.int64)
+        bits_off = np.empty(n + 1, np.int64)
+        n_starts = np.empty(n, np.int64)
+        rc = lib.cwq_code_grouped_greedy_batch(
+            n, item_off.ctypes.data, cat[0].data_ptr(), cat[1].data_ptr(), cat[2].data_ptr(),
+            cat[3].data_ptr(), 1, 8, seeds.ctypes.data, 1.0, group_size_threshold(12),
+            8 * np.log(2) - 1, sample.ctypes.data, bits.ctypes.data, bits_cap,
+            bits_off.ctypes.data, starts.ctypes.data, starts.size, n_starts.ctypes.data,
+            ws.data_ptr(), ws.numel(), host_ws, host_bytes, None,
+            torch.cuda.current_stream().cuda_stream)
+        return rc, sample, bits[:bits_off[-1]].tobytes() if rc >= 0 else b"", starts, n_starts
+    rc, s1, b1, st1, n1 = call((D + n) * 8, hws.data_ptr(), hneed)
+    assert rc > 0
+    rc2, s2, b2, st2, n2 = call((D + n) * 8, None, 0)  # pageable library staging
+    assert rc2 == rc and b2 == b1 and np.array_equal(s2.view(np.uint32), s1.view(np.uint32))
+    assert np.array_equal(n2, n1)
+    rc3 = call((D + n) * 8, hws.data_ptr(), hneed - 1)[0]
+    assert rc3 == -3 and b"host workspace" in lib.cwq_last_error()
+    rc4 = call(100, hws.data_ptr(), hneed)[0]  # bits buffer far too small
+    assert rc4 == -4 and b"bits_cap" in lib.cwq_last_error()
+    torch.cuda.synchronize()
+    rc5, s5, b5, _, _ = call((D + n) * 8, hws.data_ptr(), hneed)  # the library still works
+    assert rc5 == rc and b5 == b1

@@ -66,6 +66,9 @@ declare -A V=(
   [upl2w5m7]="-DCWQ_COOP_UPL=2 -DCWQ_CSR_COOP_MIN_WAVES=5 -DCWQ_TAU_SHARE_MASK=7u"
   [u6w4]="-DCWQ_COOP_UPL=6 -DCWQ_CSR_COOP_MIN_WAVES=4"
   [dnt]="-DCWQ_DECODE_NT=1"
+  [dtm]="-DCWQ_DECODE_PROBE=1"
+  [dcomp]="-DCWQ_DECODE_PROBE=2"
+  [dw4]="-DCWQ_DECODE_MIN_WAVES=4"
   [u4w3]="-DCWQ_COOP_UPL=4 -DCWQ_CSR_COOP_MIN_WAVES=3"
   [u4w5]="-DCWQ_COOP_UPL=4 -DCWQ_CSR_COOP_MIN_WAVES=5"
   [u8w3]="-DCWQ_COOP_UPL=8 -DCWQ_CSR_COOP_MIN_WAVES=3"
