@@ -84,7 +84,7 @@ WsLayout ws_layout(int64_t nb, int64_t total_dims, bool csr, bool recs) {
     l.slist = o;  // the screened small-candidate path's survivor slots (8 B each)
     o = align_up(o + (size_t)nb * CWQ_SLIST_PER_BLOCK * 8, 256);
     l.sab = o;
-    o = align_up(o + (size_t)(total_dims + 8 * nb) * 8, 256);
+    o = align_up(o + (size_t)(total_dims + 8 * nb + 4) * 8, 256);  // + 4 zeros (pad unit)
     l.cdim = o;
     o = align_up(o + (size_t)total_dims * 4, 256);
     l.bpre = o;

@@ -685,9 +685,9 @@ __global__ void __launch_bounds__(256) k_csr_prep(
     int ok = 1;
     float2* sabg = sab + off + 8 * g + 4;  // 4 zero pads either side (partial units)
     float* cg = cdim + off;
-    if (lead && tid < 4) {
-      sabg[tid - 4] = float2{0.f, 0.f};
-      sabg[d + tid] = float2{0.f, 0.f};
+    if (lead && tid < 8) {  // 8 trailing zeros: the last 4 are the next block's
+      if (tid < 4) sabg[tid - 4] = float2{0.f, 0.f};  // leading pads (or the slack
+      sabg[d + tid] = float2{0.f, 0.f};               // past the last block)
     }
     for (int64_t j = tid; j < d; j += 256) {
       const CsrDim o =
@@ -829,12 +829,12 @@ __global__ void __launch_bounds__(256) k_csr_prep(
           else
             unit(u, cu, gu);
         }
-        if (recs && k < U) {  // the unit's four (sa, sb), zero for absent words
-          float e[8];
+        if (recs && k <= U) {  // the unit's four (sa, sb), zero for absent words
+          float e[8];          // (position U: the zero record of the pad unit)
           for (int t = 0; t < 4; ++t) {
             const int64_t j = 4 * u - c + t;
             float2 ab = float2{0.f, 0.f};
-            if (j >= 0 && j < d) ab = sab_at(j);
+            if (k < U && j >= 0 && j < d) ab = sab_at(j);
             e[2 * t] = ab.x;
             e[2 * t + 1] = ab.y;
           }
@@ -856,7 +856,10 @@ __global__ void __launch_bounds__(256) k_csr_prep(
         const double excl = carry + (pre + v) - cu;
         if (k <= U) {
           bpre[reg + c * cs + k] = round_up_f32(SM + excl * (1.0 + 0x1p-20) + sl);
-          ordu[reg + c * cs + k] = (uint32_t)(k < U ? u : 0);
+          // position U: the pad unit U, whose words all fall on zero constants
+          // (sab's and the scoring kernel's LDS pads), so a unit read past a
+          // row's end scores exactly 0 without a mask
+          ordu[reg + c * cs + k] = (uint32_t)(k < U ? u : U);
         }
         carry += total;
         __syncthreads();
@@ -1001,7 +1004,7 @@ __global__ void __launch_bounds__(256, COOP ? CWQ_CSR_COOP_MIN_WAVES : CWQ_CSR_R
   __shared__ uint32_t sq_n[CWQ_CSR_SURVIVOR_CAP];
   __shared__ float sq_ub[CWQ_CSR_SURVIVOR_CAP];
   __shared__ unsigned long long wkey[4];
-  __shared__ float2 l_ab[CWQ_CSR_LDS_DIMS + 8];
+  __shared__ float2 l_ab[CWQ_CSR_LDS_DIMS + 12];
   __shared__ float l_bp[CWQ_CSR_LDS_DIMS + 12];
   __shared__ uint32_t l_ord[CWQ_CSR_LDS_DIMS + 12];
   __shared__ float rowbuf[4][kRowChunk];
@@ -1029,7 +1032,9 @@ __global__ void __launch_bounds__(256, COOP ? CWQ_CSR_COOP_MIN_WAVES : CWQ_CSR_R
     const bool in_lds = d <= CWQ_CSR_LDS_DIMS;
     const int64_t reg = off + 12 * g, cs = csr_cls_stride(d);
     if (gc.x != 0.0f && in_lds) {
-      for (int64_t j = tid; j < d + 8; j += blockDim.x) l_ab[j] = sab[off + 8 * g + j];
+      // 4 zero pads before, 8 after (the pad unit U's words reach d + 7 + 4)
+      for (int64_t j = tid; j < d + 12; j += blockDim.x)
+        l_ab[j] = j < d + 8 ? sab[off + 8 * g + j] : float2{0.f, 0.f};
       for (int64_t j = tid; j < 4 * cs; j += blockDim.x) {
         l_bp[j] = bpre[reg + j];
         l_ord[j] = ordu[reg + j];
@@ -1057,8 +1062,13 @@ __global__ void __launch_bounds__(256, COOP ? CWQ_CSR_COOP_MIN_WAVES : CWQ_CSR_R
       const int d32 = (int)d;
       // ab: natural-order (sa, sb) (LDS or global); rec (REC true): the
       // visit-order records of k_csr_prep's abp, read at the lane's position
+      // Past-the-end positions read the pad unit's zero constants (LDS, sab or
+      // records: k_csr_prep), so their units add exactly 0 without a mask.
+      // HI0: every Philox block index of the launch is below 2^32 (counter
+      // word 1 is 0, which makes round 2's first product lane-invariant).
       auto run = [&](const float2* ab, const float* bp, const uint32_t* od, const float4* rec,
-                     auto REC) __attribute__((always_inline)) {
+                     auto REC, auto HI0T) __attribute__((always_inline)) {
+        constexpr bool HI0 = decltype(HI0T)::value;
         uint32_t wnext = r0 + 64u;
         uint32_t r = r0 + lane;
         bool active = r < r1;
@@ -1113,7 +1123,8 @@ __global__ void __launch_bounds__(256, COOP ? CWQ_CSR_COOP_MIN_WAVES : CWQ_CSR_R
               e[i][2] = float2{rb2.x, rb2.y};
               e[i][3] = float2{rb2.z, rb2.w};
             } else {
-              const uint32_t jp = (uint32_t)(4 * (int)(pp < U ? u[i] : 0u) - c + 4);
+              const uint32_t jp =
+                  (uint32_t)(4 * (int)u[i] - c + 4);
               e[i][0] = ld_u32off(ab, jp);  // padded index of word 0
               e[i][1] = ld_u32off(ab, jp + 1u);
               e[i][2] = ld_u32off(ab, jp + 2u);
@@ -1129,22 +1140,21 @@ __global__ void __launch_bounds__(256, COOP ? CWQ_CSR_COOP_MIN_WAVES : CWQ_CSR_R
 #pragma unroll
           for (int i = 0; i < RUPL; ++i) {
             const uint64_t blk = rb + u[i];
-            const U4 x =
-                philox10_dev((uint32_t)blk, (uint32_t)(blk >> 32), st.c2, st.c3, kk0, kk1);
+            const U4 x = philox10_dev((uint32_t)blk, HI0 ? 0u : (uint32_t)(blk >> 32), st.c2,
+                                      st.c3, kk0, kk1);
             F4 z;
             box_muller_screen(x.x, x.y, z.a, z.b);
             box_muller_screen(x.z, x.w, z.c, z.d);
-            const bool in = i == 0 || k + i < U;
-            const float a0 = in ? __builtin_fmaf(e[i][0].x, z.a, e[i][0].y) : 0.0f;
-            const float a1 = in ? __builtin_fmaf(e[i][1].x, z.b, e[i][1].y) : 0.0f;
-            const float a2 = in ? __builtin_fmaf(e[i][2].x, z.c, e[i][2].y) : 0.0f;
-            const float a3 = in ? __builtin_fmaf(e[i][3].x, z.d, e[i][3].y) : 0.0f;
+            const float a0 = __builtin_fmaf(e[i][0].x, z.a, e[i][0].y);
+            const float a1 = __builtin_fmaf(e[i][1].x, z.b, e[i][1].y);
+            const float a2 = __builtin_fmaf(e[i][2].x, z.c, e[i][2].y);
+            const float a3 = __builtin_fmaf(e[i][3].x, z.d, e[i][3].y);
             s = __builtin_fmaf(-a0, a0, s);
             s = __builtin_fmaf(-a1, a1, s);
             s = __builtin_fmaf(-a2, a2, s);
             s = __builtin_fmaf(-a3, a3, s);
 #ifdef CWQ_PRUNE_STATS
-            if (active && in) atomicAdd(&g_prune_stats[43], 1ull);
+            if (active && (i == 0 || k + i < U)) atomicAdd(&g_prune_stats[43], 1ull);
 #endif
           }
           k = kn;
@@ -1209,7 +1219,8 @@ __global__ void __launch_bounds__(256, COOP ? CWQ_CSR_COOP_MIN_WAVES : CWQ_CSR_R
       // The bound's float-summation factor is taken at this tree's depth
       // (k_csr_prep: 4 in-lane + 4 butterfly + one per chunk).
       auto run_coop = [&](const float2* ab, const float* bp, const uint32_t* od,
-                          const float4* rec, auto REC) __attribute__((always_inline)) {
+                          const float4* rec, auto REC, auto HI0T) __attribute__((always_inline)) {
+        constexpr bool HI0 = decltype(HI0T)::value;
         const uint32_t t = lane & 15u, slot = lane >> 4;
         const uint64_t below = (1ull << (slot * 16u)) - 1ull;  // lanes of lower slots
 #if CWQ_CSR_COOP_CLASS_WAVES
@@ -1280,7 +1291,8 @@ __global__ void __launch_bounds__(256, COOP ? CWQ_CSR_COOP_MIN_WAVES : CWQ_CSR_R
               e[i][2] = float2{rb2.x, rb2.y};
               e[i][3] = float2{rb2.z, rb2.w};
             } else {
-              const uint32_t jp = (uint32_t)(4 * (int)(pp < U ? u[i] : 0u) - c + 4);
+              const uint32_t jp =
+                  (uint32_t)(4 * (int)u[i] - c + 4);
               e[i][0] = ld_u32off(ab, jp);
               e[i][1] = ld_u32off(ab, jp + 1u);
               e[i][2] = ld_u32off(ab, jp + 2u);
@@ -1295,8 +1307,8 @@ __global__ void __launch_bounds__(256, COOP ? CWQ_CSR_COOP_MIN_WAVES : CWQ_CSR_R
 #pragma unroll
             for (int i = 0; i < UPL; ++i) {
               const uint64_t blk = rb + u[i];
-              const U4 x =
-                  philox10_dev((uint32_t)blk, (uint32_t)(blk >> 32), st.c2, st.c3, kk0, kk1);
+              const U4 x = philox10_dev((uint32_t)blk, HI0 ? 0u : (uint32_t)(blk >> 32), st.c2,
+                                        st.c3, kk0, kk1);
               F4 z;
               box_muller_screen(x.x, x.y, z.a, z.b);
               box_muller_screen(x.z, x.w, z.c, z.d);
@@ -1311,7 +1323,7 @@ __global__ void __launch_bounds__(256, COOP ? CWQ_CSR_COOP_MIN_WAVES : CWQ_CSR_R
               if (i == 0)
                 part = pu;
               else
-                part = part + (p + 16 * i < U ? pu : 0.0f);
+                part = part + pu;
             }
           }
 #ifdef CWQ_PRUNE_STATS
@@ -1364,30 +1376,40 @@ __global__ void __launch_bounds__(256, COOP ? CWQ_CSR_COOP_MIN_WAVES : CWQ_CSR_R
         if (lane == 0) atomicMax(&tau_ord, ord_f32(tm));
       };
       const bool coop = d >= coop_min_d;
+      // the block's largest Philox block index, ((n_cand - 1) d + d - 1) / 4
+      const bool lo32 = (uint64_t)n_cand * (uint64_t)d <= (1ull << 34);
       // survivor list overflow (near-ties everywhere, or a weak early tau):
       // redo the pass starting from the final tau, then score exactly
       for (int pass = 0;; ++pass) {
         using NoRec = std::integral_constant<bool, false>;
         using Rec = std::integral_constant<bool, true>;
+        using Lo32 = std::integral_constant<bool, true>;   // block indices < 2^32
+        using Hi32 = std::integral_constant<bool, false>;
         // each launch mode instantiates only its own loops (register
         // allocation is per kernel: the largest loop sets every loop's budget)
-        if constexpr (COOP) {
-          if (coop) {
-            if (in_lds)
-              run_coop(l_ab, l_bp, l_ord, nullptr, NoRec{});
-            else if (abp)
-              run_coop(nullptr, bpre + reg, ordu + reg, abp + 2 * csr_rec_base(off), Rec{});
-            else
-              run_coop(sab + off + 8 * g, bpre + reg, ordu + reg, nullptr, NoRec{});
-          } else {  // d < coop_min_d <= CWQ_CSR_LDS_DIMS: the constants are in LDS
-            run(l_ab, l_bp, l_ord, nullptr, NoRec{});
-          }
-        } else if (in_lds)
-          run(l_ab, l_bp, l_ord, nullptr, NoRec{});
-        else if (abp)
-          run(nullptr, bpre + reg, ordu + reg, abp + 2 * csr_rec_base(off), Rec{});
+        auto any_run = [&](auto HI0T) __attribute__((always_inline)) {
+          if constexpr (COOP) {
+            if (coop) {
+              if (in_lds)
+                run_coop(l_ab, l_bp, l_ord, nullptr, NoRec{}, HI0T);
+              else if (abp)
+                run_coop(nullptr, bpre + reg, ordu + reg, abp + 2 * csr_rec_base(off), Rec{}, HI0T);
+              else
+                run_coop(sab + off + 8 * g, bpre + reg, ordu + reg, nullptr, NoRec{}, HI0T);
+            } else {  // d < coop_min_d <= CWQ_CSR_LDS_DIMS: the constants are in LDS
+              run(l_ab, l_bp, l_ord, nullptr, NoRec{}, HI0T);
+            }
+          } else if (in_lds)
+            run(l_ab, l_bp, l_ord, nullptr, NoRec{}, HI0T);
+          else if (abp)
+            run(nullptr, bpre + reg, ordu + reg, abp + 2 * csr_rec_base(off), Rec{}, HI0T);
+          else
+            run(sab + off + 8 * g, bpre + reg, ordu + reg, nullptr, NoRec{}, HI0T);
+        };
+        if (lo32)
+          any_run(Lo32{});
         else
-          run(sab + off + 8 * g, bpre + reg, ordu + reg, nullptr, NoRec{});
+          any_run(Hi32{});
         __syncthreads();
         if (tid == 0) {
           const uint32_t mine = tau_ord;

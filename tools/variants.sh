@@ -72,6 +72,7 @@ declare -A V=(
   [u4w3]="-DCWQ_COOP_UPL=4 -DCWQ_CSR_COOP_MIN_WAVES=3"
   [u4w5]="-DCWQ_COOP_UPL=4 -DCWQ_CSR_COOP_MIN_WAVES=5"
   [u8w3]="-DCWQ_COOP_UPL=8 -DCWQ_CSR_COOP_MIN_WAVES=3"
+  [prepad]=prebuilt
 )
 if [ "$1" = build ]; then
   mkdir -p $OUT
