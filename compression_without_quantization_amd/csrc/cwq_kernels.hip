@@ -975,6 +975,9 @@ __device__ __forceinline__ float exact_row_wave(
 #ifndef CWQ_COOP_UPL
 #define CWQ_COOP_UPL 4                // units per lane per iteration of a cooperative row
 #endif
+#ifndef CWQ_COOP_LOAD_ORDER
+#define CWQ_COOP_LOAD_ORDER 0         // 1: a cooperative iteration's loads issued in unit order
+#endif
 
 // element idx of base through an unsigned 32-bit byte offset (base + voffset)
 template <class T>
@@ -1123,8 +1126,7 @@ __global__ void __launch_bounds__(256, COOP ? CWQ_CSR_COOP_MIN_WAVES : CWQ_CSR_R
               e[i][2] = float2{rb2.x, rb2.y};
               e[i][3] = float2{rb2.z, rb2.w};
             } else {
-              const uint32_t jp =
-                  (uint32_t)(4 * (int)u[i] - c + 4);
+              const uint32_t jp = (uint32_t)(4 * (int)u[i] - c + 4);
               e[i][0] = ld_u32off(ab, jp);  // padded index of word 0
               e[i][1] = ld_u32off(ab, jp + 1u);
               e[i][2] = ld_u32off(ab, jp + 2u);
@@ -1276,7 +1278,7 @@ __global__ void __launch_bounds__(256, COOP ? CWQ_CSR_COOP_MIN_WAVES : CWQ_CSR_R
           for (int i = 0; i < UPL; ++i) u[i] = u_nx[i];
           load_units(p + CH);
           // constants and the slot's next drop bound ahead of the Philox
-          // rounds, as in run (positions past U clamp to U: in the region)
+          // rounds, as in run (positions past U clamp to U, the pad unit)
           const int kn = (k + CH < U) ? k + CH : U;
           const float bnext = ld_u32off(bp, (uint32_t)(cb + kn));
           float2 e[UPL][4];
@@ -1291,19 +1293,24 @@ __global__ void __launch_bounds__(256, COOP ? CWQ_CSR_COOP_MIN_WAVES : CWQ_CSR_R
               e[i][2] = float2{rb2.x, rb2.y};
               e[i][3] = float2{rb2.z, rb2.w};
             } else {
-              const uint32_t jp =
-                  (uint32_t)(4 * (int)u[i] - c + 4);
+              const uint32_t jp = (uint32_t)(4 * (int)u[i] - c + 4);
               e[i][0] = ld_u32off(ab, jp);
               e[i][1] = ld_u32off(ab, jp + 1u);
               e[i][2] = ld_u32off(ab, jp + 2u);
               e[i][3] = ld_u32off(ab, jp + 3u);
             }
+#if CWQ_COOP_LOAD_ORDER
+            // issue unit i's loads before unit i + 1's: the first unit's
+            // constants then arrive first (loads complete in order), so its
+            // wait does not also cover the later units' loads
+            asm volatile("" ::: "memory");
+#endif
           }
           if (active && p < U) {
             uint32_t kk0 = st.k0, kk1 = st.k1;
             asm volatile("" : "+s"(kk0), "+s"(kk1));
             // the UPL units are independent chains (ILP); a unit past the row
-            // end (its clamped constants may be anything) adds 0
+            // end reads the pad unit's zero constants and adds exactly 0
 #pragma unroll
             for (int i = 0; i < UPL; ++i) {
               const uint64_t blk = rb + u[i];

@@ -349,6 +349,86 @@ CWQO_API int cwqo_decode_greedy_sample(const int32_t* idx, const float* p_loc,
   return 0;
 }
 
+/* code_greedy_sample for ONE block and ONE step with the candidate rows split
+ * over OpenMP threads (the per-block coder above is serial over rows): each
+ * thread scans a contiguous row range with the reference's argmax rule
+ * (strictly greater replaces, from -FLT_MAX), and the ranges are merged in
+ * row order with the same rule, so the first maximal row wins as in the serial
+ * scan (coded_greedy_sampler.py:59-63).  For blocks too large for one core:
+ * the tests of launches whose Philox block indices pass 2^32. */
+CWQO_API int cwqo_code_greedy_sample_rows(const float* t_loc, const float* t_scale,
+                                          const float* p_loc, const float* p_scale, int64_t d,
+                                          int n_bits_per_step, int32_t seed, float rho,
+                                          int32_t* out_idx, float* out_sample, int nthreads) {
+  if (n_bits_per_step < 0 || n_bits_per_step > 30 || d < 1) return -1;
+  const int64_t n_samples = (int64_t)1 << n_bits_per_step;
+  const size_t db = (size_t)d * sizeof(float);
+  float* loc_s = (float*)malloc(db);
+  float* scale_s = (float*)malloc(db);
+  float* lognorm = (float*)malloc(db);
+  if (!loc_s || !scale_s || !lognorm) {
+    free(loc_s); free(scale_s); free(lognorm);
+    return -2;
+  }
+  shard_params(p_loc, p_scale, d, 1, rho, loc_s, scale_s);
+  for (int64_t j = 0; j < d; ++j) lognorm[j] = cwqo_log_normalization(t_scale[j]);
+  uint32_t key[2], ctr[4];
+  cwqo_generate_key(step_seed(seed, 0), 42, key, ctr);
+  const int64_t nchunk = 1024;
+  float* cval = (float*)malloc(sizeof(float) * nchunk);
+  int64_t* cidx = (int64_t*)malloc(sizeof(int64_t) * nchunk);
+  int err = 0;
+  if (!cval || !cidx) err = 1;
+#ifdef _OPENMP
+  if (nthreads > 0) omp_set_num_threads(nthreads);
+#pragma omp parallel for schedule(dynamic, 1) reduction(| : err)
+#endif
+  for (int64_t ch = 0; ch < nchunk; ++ch) {
+    if (!cval || !cidx) continue;
+    float* row = (float*)malloc(db);
+    if (!row) { err |= 1; continue; }
+    normal_stream st;
+    memset(&st, 0, sizeof(st));
+    memcpy(st.key, key, sizeof(key));
+    memcpy(st.ctr, ctr, sizeof(ctr));
+    const int64_t n0 = n_samples * ch / nchunk, n1 = n_samples * (ch + 1) / nchunk;
+    float bv = -FLT_MAX;
+    int64_t bi = n0;
+    for (int64_t n = n0; n < n1; ++n) {
+      for (int64_t j = 0; j < d; ++j) {
+        float z = stream_normal(&st, (uint64_t)(n * d + j));
+        float s = scale_s[j] * z;
+        s = loc_s[j] + s;
+        float tv = 0.0f + s; /* step 0: best_sample is tf.zeros */
+        row[j] = log_prob_c(tv, t_loc[j], t_scale[j], lognorm[j]);
+      }
+      float v = cwqo_eigen_rowsum(row, d);
+      if (v > bv) { bv = v; bi = n; }
+    }
+    cval[ch] = bv;
+    cidx[ch] = n1 > n0 ? bi : -1;
+    free(row);
+  }
+  if (!err) {
+    float best_val = -FLT_MAX;
+    int64_t best_idx = 0;
+    for (int64_t ch = 0; ch < nchunk; ++ch)
+      if (cidx[ch] >= 0 && cval[ch] > best_val) { best_val = cval[ch]; best_idx = cidx[ch]; }
+    normal_stream st;
+    memset(&st, 0, sizeof(st));
+    memcpy(st.key, key, sizeof(key));
+    memcpy(st.ctr, ctr, sizeof(ctr));
+    for (int64_t j = 0; j < d; ++j) {
+      float z = stream_normal(&st, (uint64_t)(best_idx * d + j));
+      float s = scale_s[j] * z;
+      out_sample[j] = 0.0f + (loc_s[j] + s);
+    }
+    out_idx[0] = (int32_t)best_idx;
+  }
+  free(cval); free(cidx); free(loc_s); free(scale_s); free(lognorm);
+  return err ? -2 : 0;
+}
+
 /* Batched (CSR) encoder: block g = dims [off[g], off[g+1]), seed + block_id_base + g
  * (coded_greedy_sampler.py:282 `seed_feed: seed + i`).  OpenMP over blocks.
  * nthreads <= 0 -> OpenMP default. */

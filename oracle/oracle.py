@@ -47,6 +47,7 @@ def lib():
             "cwqo_eigen_rowsum": (f32, [vp, i64]),
             "cwqo_code_greedy_sample": (ci, [vp, vp, vp, vp, i64, ci, ci, i32, f32, vp, vp]),
             "cwqo_decode_greedy_sample": (ci, [vp, vp, vp, i64, ci, ci, i32, f32, vp]),
+            "cwqo_code_greedy_sample_rows": (ci, [vp, vp, vp, vp, i64, ci, i32, f32, vp, vp, ci]),
             "cwqo_greedy_encode": (ci, [vp, vp, vp, vp, vp, i64, ci, ci, i32, f32, i64, vp, vp,
                                         ci]),
             "cwqo_greedy_decode": (ci, [vp, vp, vp, vp, i64, ci, ci, i32, f32, i64, vp, ci]),
@@ -144,6 +145,20 @@ def code_greedy_sample(t_loc, t_scale, p_loc, p_scale, n_bits_per_step, n_steps,
     rc = lib().cwqo_code_greedy_sample(_p(tl), _p(ts), _p(pl), _p(ps), tl.size,
                                        int(n_bits_per_step), int(n_steps), int(seed),
                                        float(rho), _p(idx), _p(sample))
+    assert rc == 0, rc
+    return idx, sample
+
+
+def code_greedy_sample_rows(t_loc, t_scale, p_loc, p_scale, n_bits, seed, rho=1., nthreads=0):
+    """code_greedy_sample for one block and one step with the candidate rows
+    split over OpenMP threads (same argmax as the serial scan): blocks too large
+    for one core."""
+    tl, ts, pl, ps = map(_f32, (t_loc, t_scale, p_loc, p_scale))
+    idx = np.zeros(1, dtype=np.int32)
+    sample = np.zeros(tl.size, dtype=np.float32)
+    rc = lib().cwqo_code_greedy_sample_rows(_p(tl), _p(ts), _p(pl), _p(ps), tl.size, int(n_bits),
+                                            int(seed), float(rho), _p(idx), _p(sample),
+                                            int(nthreads))
     assert rc == 0, rc
     return idx, sample
 

@@ -800,6 +800,28 @@ def test_csr_cooperative_rows_vs_oracle(cwq, cwqlib, oracle, sizes, bits, n_step
         _assert_bits_equal(gs, ws, f"coop {kind} mode {mode}")
 
 
+@pytest.mark.parametrize("d,bits", [
+    (1100, 24),   # per-lane rows, visit-order records: n_cand d = 1.06 * 2^34
+    (1024, 24),   # constants in LDS, n_cand d = 2^34 exactly: the last 32-bit launch
+    (8200, 21),   # cooperative rows, natural order: n_cand d = 1.0009 * 2^34
+])
+def test_csr_wide_counters_vs_oracle(cwq, cwqlib, oracle, d, bits):
+    """The general pruned kernel drops counter word 1 from its Philox rounds
+    (HI0) only when every block index (n d + j) / 4 of the launch is below
+    2^32, i.e. n_cand d <= 2^34.  One block on either side of that limit,
+    against the oracle's full scan (its rows split over threads)."""
+    rng = np.random.default_rng(d * bits)
+    tl = rng.standard_normal(d).astype(np.float32)
+    ts = rng.uniform(0.2, 1.0, d).astype(np.float32)
+    pl = (0.1 * rng.standard_normal(d)).astype(np.float32)
+    ps = rng.uniform(0.8, 1.2, d).astype(np.float32)
+    off = np.array([0, d], np.int64)
+    wi, ws = oracle.code_greedy_sample_rows(tl, ts, pl, ps, bits, 42)
+    gi, gs = _csr_encode(cwq, cwqlib, tl, ts, pl, ps, off, bits, 1, 42, 1.0, 2)
+    assert int(gi.reshape(-1)[0]) == int(wi[0]), (d, bits, gi.reshape(-1), wi)
+    _assert_bits_equal(gs, ws, f"wide counters d={d} bits={bits}")
+
+
 @pytest.mark.parametrize("sizes,bits,n_steps", [
     ([300, 40] * 7, 16, 1),    # 14 groups: 439 tiles/group asked, 437 hold candidates
     ([260] * 3 + [20] * 36, 16, 2),  # three stream parts of 13 groups: 473 asked, 472 used

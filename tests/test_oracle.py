@@ -197,6 +197,27 @@ def test_oracle_single_block_equals_batched(oracle, golden):
         assert np.array_equal(sample.view(np.uint32), g["sample"][s].view(np.uint32))
 
 
+@pytest.mark.parametrize("d,bits,kind", [(40, 6, "normal"), (9, 12, "normal"),
+                                         (33, 11, "flat"), (5, 10, "ties")])
+def test_oracle_rows_split_equals_serial(oracle, d, bits, kind):
+    """cwqo_code_greedy_sample_rows (rows over threads, the wide-counter GPU
+    tests' checker) returns the serial scan's first maximal row and sample."""
+    rng = np.random.default_rng(d * bits)
+    tl = rng.standard_normal(d).astype(np.float32)
+    ts = rng.uniform(0.2, 1, d).astype(np.float32)
+    pl = (0.1 * rng.standard_normal(d)).astype(np.float32)
+    ps = rng.uniform(0.8, 1.2, d).astype(np.float32)
+    if kind == "flat":     # near-ties everywhere
+        tl, ts = np.zeros(d, np.float32), np.full(d, 1e3, np.float32)
+    if kind == "ties":     # every row has the same value: row 0 must win
+        tl, ts = np.zeros(d, np.float32), np.full(d, np.inf, np.float32)
+    for nthreads in (1, 3, 0):
+        want = oracle.code_greedy_sample(tl, ts, pl, ps, bits, 1, 77)
+        got = oracle.code_greedy_sample_rows(tl, ts, pl, ps, bits, 77, nthreads=nthreads)
+        assert int(got[0][0]) == int(want[0][0]), (kind, nthreads, got[0], want[0])
+        assert np.array_equal(got[1].view(np.uint32), want[1].view(np.uint32))
+
+
 def test_oracle_argmax_is_best(oracle):
     # brute force: argmax of the row sums over the materialised candidates
     rng = np.random.default_rng(5)
