@@ -149,8 +149,12 @@ constexpr double kScreenEz =
     (1.0 + kScreenEs) * kScreenEr + kScreenRmax * kScreenEs + 0x1p-23 * (kScreenRmax + kScreenEr);
 constexpr double kScreenZm = 5.7;     // bound on |z| and |z~|
 
+// HI0: the caller guarantees grp < 2^32 (counter word 1 is 0: round 2's
+// first product is then lane-invariant, one v_mad_u64_u32 less per block)
+template <bool HI0 = false>
 __device__ __forceinline__ F4 normal4_screen(const PhiloxStream& s, uint64_t grp) {
-  const U4 x = philox_block_dev(s, grp);
+  const U4 x = philox10_dev((uint32_t)grp, HI0 ? 0u : (uint32_t)(grp >> 32), s.c2, s.c3, s.k0,
+                            s.k1);
   F4 z;
   box_muller_screen(x.x, x.y, z.a, z.b);
   box_muller_screen(x.z, x.w, z.c, z.d);

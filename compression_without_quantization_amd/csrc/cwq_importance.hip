@@ -77,13 +77,14 @@ __global__ void __launch_bounds__(1024) k_imp_tiles(const int64_t* __restrict__ 
 // Screening row value: sum_j (A_j z_j + B_j) z_j + C_j over the candidate's
 // dims, z from the hardware-transcendental Box-Muller ("screening
 // the importance sampler").  `align` = (kbase mod 4) must be wave-uniform.
+template <bool HI0>
 __device__ __forceinline__ float screen_row_imp(const PhiloxStream& st, uint64_t kbase, int64_t d,
                                                 int align, const float4* __restrict__ coef) {
   float s = 0.0f;
   F4 z = {0.f, 0.f, 0.f, 0.f};
   for (int64_t e = 0; e < d; ++e) {
     const int w = (align + (int)(e & 3)) & 3;  // wave-uniform
-    if (w == 0 || e == 0) z = normal4_screen(st, (kbase + (uint64_t)e) >> 2);
+    if (w == 0 || e == 0) z = normal4_screen<HI0>(st, (kbase + (uint64_t)e) >> 2);
     const float zz = w == 0 ? z.a : (w == 1 ? z.b : (w == 2 ? z.c : z.d));
     const float4 c = coef[e];
     s = s + __builtin_fmaf(__builtin_fmaf(c.x, zz, c.y), zz, c.z);
@@ -298,74 +299,84 @@ __global__ void __launch_bounds__(256, CWQ_IMP_MIN_WAVES) k_imp_eval(
           bestk = k > bestk ? k : bestk;
         }
       };
-      if (d >= kImpPruneMinD) {
-        // pruned screening: one Philox block of the lane's row per iteration;
-        // a row stops once s + E + sum of the unvisited dims' maxima < tau.
-        // Lanes refill from the wave's contiguous candidate range.
-        const int64_t per_wave = (n1 - n0 + 3) / 4;
-        const int64_t w0 = n0 + (int64_t)wv * per_wave;
-        const int64_t w1 = (w0 + per_wave < n1) ? w0 + per_wave : n1;
-        int64_t wnext = w0 + 64;
-        int64_t n = w0 + lane;
-        bool active = n < w1;
-        int j = 0;
-        float s = 0.0f;
-        uint32_t iter = 0;
-        while (__ballot(active) != 0ull) {
-          const uint64_t k = (uint64_t)n * (uint64_t)d + (uint64_t)j;
-          const F4 z = normal4_screen(st, k >> 2);
-          const int wa = (int)(k & 3u);
-          const int cnt = (4 - wa) < (int)(d - j) ? (4 - wa) : (int)(d - j);
-#pragma unroll
-          for (int t = 0; t < 4; ++t) {
-            if (t < cnt) {
-              const int w = wa + t;
-              const float zz = w == 0 ? z.a : (w == 1 ? z.b : (w == 2 ? z.c : z.d));
-              const float4 c = coef[j + t];
-              s = s + __builtin_fmaf(__builtin_fmaf(c.x, zz, c.y), zz, c.z);
+      // every Philox block index (n d + j) / 4 of the group below 2^32:
+      // counter word 1 is 0 (normal4_screen<true>: one multiply less per block)
+      const bool lo32 = (uint64_t)N * (uint64_t)d <= (1ull << 34);
+      auto scan = [&](auto HI0T) __attribute__((always_inline)) {
+        constexpr bool HI0 = decltype(HI0T)::value;
+        if (d >= kImpPruneMinD) {
+          // pruned screening: one Philox block of the lane's row per iteration;
+          // a row stops once s + E + sum of the unvisited dims' maxima < tau.
+          // Lanes refill from the wave's contiguous candidate range.
+          const int64_t per_wave = (n1 - n0 + 3) / 4;
+          const int64_t w0 = n0 + (int64_t)wv * per_wave;
+          const int64_t w1 = (w0 + per_wave < n1) ? w0 + per_wave : n1;
+          int64_t wnext = w0 + 64;
+          int64_t n = w0 + lane;
+          bool active = n < w1;
+          int j = 0;
+          float s = 0.0f;
+          uint32_t iter = 0;
+          while (__ballot(active) != 0ull) {
+            const uint64_t k = (uint64_t)n * (uint64_t)d + (uint64_t)j;
+            const F4 z = normal4_screen<HI0>(st, k >> 2);
+            const int wa = (int)(k & 3u);
+            const int cnt = (4 - wa) < (int)(d - j) ? (4 - wa) : (int)(d - j);
+  #pragma unroll
+            for (int t = 0; t < 4; ++t) {
+              if (t < cnt) {
+                const int w = wa + t;
+                const float zz = w == 0 ? z.a : (w == 1 ? z.b : (w == 2 ? z.c : z.d));
+                const float4 c = coef[j + t];
+                s = s + __builtin_fmaf(__builtin_fmaf(c.x, zz, c.y), zz, c.z);
+              }
+            }
+            j += cnt;
+            const bool complete = (j == (int)d);
+            const float slack = E + __builtin_fabsf(s) * 0x1p-22f;
+            const float upper = (s + slack) + dsuf[j];
+            const bool prune = !complete && (upper < tau);
+            if (complete && active && upper >= tau) keep(n, s, slack);
+            const bool done = complete || prune || !active;
+            const uint64_t m = __ballot(done);
+            const uint32_t rank = __builtin_amdgcn_mbcnt_hi(
+                (uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+            if (done) {
+              n = wnext + rank;
+              j = 0;
+              s = 0.0f;
+            }
+            wnext += (int64_t)__builtin_popcountll(m);
+            active = n < w1;
+            if (((++iter) & 15u) == 0u) {  // share tau with the workgroup
+              const float tm = wave_max_f32(tau);
+              if (lane == 0) atomicMax(&tau_ord, ord_f32(tm));
+              uint32_t o = __atomic_load_n(&tau_ord, __ATOMIC_RELAXED);
+  #if CWQ_IMP_GTAU_MASK
+              // and every 64 units with the group's other tiles (publishing only
+              // an improvement; I1 -2.5% on top of the permuted hand-out)
+              if ((iter & CWQ_IMP_GTAU_MASK) == 0u) {
+                const uint32_t o2 = __hip_atomic_load(&gtau[g], __ATOMIC_RELAXED,
+                                                      __HIP_MEMORY_SCOPE_AGENT);
+                if (lane == 0 && ord_f32(tm) > o2) atomicMax(&gtau[g], ord_f32(tm));
+                o = o > o2 ? o : o2;
+              }
+  #endif
+              tau = fmaxf(tau, unord_f32(o));
             }
           }
-          j += cnt;
-          const bool complete = (j == (int)d);
-          const float slack = E + __builtin_fabsf(s) * 0x1p-22f;
-          const float upper = (s + slack) + dsuf[j];
-          const bool prune = !complete && (upper < tau);
-          if (complete && active && upper >= tau) keep(n, s, slack);
-          const bool done = complete || prune || !active;
-          const uint64_t m = __ballot(done);
-          const uint32_t rank = __builtin_amdgcn_mbcnt_hi(
-              (uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-          if (done) {
-            n = wnext + rank;
-            j = 0;
-            s = 0.0f;
-          }
-          wnext += (int64_t)__builtin_popcountll(m);
-          active = n < w1;
-          if (((++iter) & 15u) == 0u) {  // share tau with the workgroup
-            const float tm = wave_max_f32(tau);
-            if (lane == 0) atomicMax(&tau_ord, ord_f32(tm));
-            uint32_t o = __atomic_load_n(&tau_ord, __ATOMIC_RELAXED);
-#if CWQ_IMP_GTAU_MASK
-            // and every 64 units with the group's other tiles (publishing only
-            // an improvement; I1 -2.5% on top of the permuted hand-out)
-            if ((iter & CWQ_IMP_GTAU_MASK) == 0u) {
-              const uint32_t o2 = __hip_atomic_load(&gtau[g], __ATOMIC_RELAXED,
-                                                    __HIP_MEMORY_SCOPE_AGENT);
-              if (lane == 0 && ord_f32(tm) > o2) atomicMax(&gtau[g], ord_f32(tm));
-              o = o > o2 ? o : o2;
-            }
-#endif
-            tau = fmaxf(tau, unord_f32(o));
+        } else {
+          for (int64_t n = n0 + 4 * (int64_t)lane + wv; n < n1; n += 256) {
+            const float sh = screen_row_imp<HI0>(st, (uint64_t)n * (uint64_t)d, d, align, coef);
+            const float slack = E + __builtin_fabsf(sh) * 0x1p-22f;
+            if (sh + slack >= tau) keep(n, sh, slack);
           }
         }
-      } else {
-        for (int64_t n = n0 + 4 * (int64_t)lane + wv; n < n1; n += 256) {
-          const float sh = screen_row_imp(st, (uint64_t)n * (uint64_t)d, d, align, coef);
-          const float slack = E + __builtin_fabsf(sh) * 0x1p-22f;
-          if (sh + slack >= tau) keep(n, sh, slack);
-        }
-      }
+      };
+      if (lo32)
+        scan(std::integral_constant<bool, true>{});
+      else
+        scan(std::integral_constant<bool, false>{});
       {
         const float tm = wave_max_f32(tau);
         if (lane == 0) atomicMax(&tau_ord, ord_f32(tm));

@@ -102,6 +102,49 @@ __global__ void k_sin_mix(float* out, float a) {
   float s = 0; for (int i = 0; i < CH; ++i) s += x[i] + y[i]; out[blockIdx.x * blockDim.x + threadIdx.x] = s;
 }
 
+// one v_mad_u64_u32 (+ the xor that keeps the chain) per 4 independent f32
+// FMAs: do plain ops issue in the multiply's shadow?
+__global__ void k_mad_mix(uint32_t* out, uint32_t m) {
+  uint32_t x[CH]; float y[CH];
+  for (int i = 0; i < CH; ++i) { x[i] = threadIdx.x * 7 + i; y[i] = (float)x[i]; }
+  const float a = __uint_as_float(0x3f7ff000u);
+  for (int it = 0; it < ITERS; ++it)
+#pragma unroll
+    for (int i = 0; i < CH; ++i) {
+      uint64_t p = (uint64_t)x[i] * m; x[i] = (uint32_t)(p >> 32) ^ (uint32_t)p;
+      y[i] = __builtin_fmaf(y[i], a, 0.5f);
+      y[i] = __builtin_fmaf(y[i], a, 0.25f);
+      y[i] = __builtin_fmaf(y[i], a, 0.125f);
+      y[i] = __builtin_fmaf(y[i], a, 0.0625f);
+    }
+  uint32_t s = 0; for (int i = 0; i < CH; ++i) s ^= x[i] ^ __float_as_uint(y[i]);
+  out[blockIdx.x * blockDim.x + threadIdx.x] = s;
+}
+// the screening unit's quarter-rate mix alone: 9 v_mad_u64_u32 (+ xor) and 4
+// transcendentals per chain-iteration, then the same with 25 plain f32 ops
+template <int PLAIN>
+__global__ void k_unit_mix(uint32_t* out, uint32_t m) {
+  uint32_t x[CH]; float y[CH], t[CH];
+  for (int i = 0; i < CH; ++i) { x[i] = threadIdx.x * 7 + i; y[i] = (float)x[i]; t[i] = 0.5f; }
+  const float a = __uint_as_float(0x3f7ff000u);
+  for (int it = 0; it < ITERS; ++it)
+#pragma unroll
+    for (int i = 0; i < CH; ++i) {
+#pragma unroll
+      for (int r = 0; r < 9; ++r) {
+        uint64_t p = (uint64_t)x[i] * m; x[i] = (uint32_t)(p >> 32) ^ (uint32_t)p;
+      }
+      const float u = __uint_as_float((x[i] & 0x7fffffu) | 0x3f800000u);
+      t[i] += __builtin_amdgcn_sinf(u) + __builtin_amdgcn_cosf(u) + __builtin_amdgcn_logf(u) +
+              __builtin_amdgcn_sqrtf(u);
+#pragma unroll
+      for (int r = 0; r < PLAIN; ++r) y[i] = __builtin_fmaf(y[i], a, 0.5f);
+    }
+  uint32_t s = 0;
+  for (int i = 0; i < CH; ++i) s ^= x[i] ^ __float_as_uint(y[i]) ^ __float_as_uint(t[i]);
+  out[blockIdx.x * blockDim.x + threadIdx.x] = s;
+}
+
 template <typename K, typename T>
 void run(const char* name, K k, T arg, int ops_per_iter_per_chain) {
   void* out; hipMalloc(&out, 256 * 8192 * 8);
@@ -134,5 +177,11 @@ int main() {
   run("rsq+add", k_rsq_f32, 1.0f, 2);
   run("exp2+add", k_exp_f32, -1.0f, 2);
   run("sin+4fma", k_sin_mix, 0.999f, 5);
+  run("mad+xor+4fma", k_mad_mix, 0xD2511F53u, 6);
+  // unit mix: counted as "instructions" (9 mad + 9 xor + 4 trans + 3 add + 2 and/or + PLAIN)
+  run("unit_mix+0", k_unit_mix<0>, 0xD2511F53u, 27);
+  run("unit_mix+12", k_unit_mix<12>, 0xD2511F53u, 39);
+  run("unit_mix+25", k_unit_mix<25>, 0xD2511F53u, 52);
+  run("unit_mix+50", k_unit_mix<50>, 0xD2511F53u, 77);
   return 0;
 }
