@@ -74,6 +74,64 @@ __device__ __forceinline__ U4 philox10_dev(uint32_t c0, uint32_t c1, uint32_t c2
   return U4{c0, c1, c2, c3};
 }
 
+// Philox-10 of the counter (c0, 0, c2, c3) with c2, c3 and the key
+// wave-uniform (a stream's blocks below 2^32).  Rounds 0-2 then carry
+// wave-uniform terms: round 0's n0 and round 1's products of it, round 1's c3.
+// Their XORs with the round keys are folded per stream into four scalars
+// (philox_lo_key), so each of those rounds needs one two-operand v_xor_b32
+// with a scalar instead of a three-input v_bitop3_b32 with two scalars (the
+// constant bus takes one: a v_mov per round) or a uniform value held in a VGPR.
+// Same results as philox10_dev(c0, 0, c2, c3, k0, k1) (tests/test_gpu.py).
+struct PhiloxLo {
+  uint32_t A, B, C, D;
+};
+__device__ __forceinline__ PhiloxLo philox_lo_key(const PhiloxStream& s) {
+  const uint64_t p1 = (uint64_t)kPhiloxM1 * s.c2;
+  const uint32_t n0 = (uint32_t)(p1 >> 32) ^ s.k0;       // round 0's n0
+  const uint64_t q0 = (uint64_t)kPhiloxM0 * n0;           // round 1's first product
+  PhiloxLo o;
+  o.A = s.c3 ^ s.k1;                                      // round 0: n2 = hi(M0 c0) ^ A
+  o.B = (uint32_t)p1 ^ (s.k0 + kPhiloxW0);                // round 1: n0 = hi(M1 n2) ^ B
+  o.C = (uint32_t)(q0 >> 32) ^ (s.k1 + kPhiloxW1);        // round 1: n2 = lo(M0 c0) ^ C
+  o.D = (uint32_t)q0 ^ (s.k1 + 2u * kPhiloxW1);           // round 2: n2 = hi(M0 c0') ^ D
+  // opaque scalars: the compiler must not re-associate the XORs into
+  // three-input bitop3 forms with two scalar operands
+  asm volatile("" : "+s"(o.A), "+s"(o.B), "+s"(o.C), "+s"(o.D));
+  return o;
+}
+// k0, k1: the stream's key (callers may pass it through an opaque move)
+__device__ __forceinline__ U4 philox10_lo(uint32_t c0, const PhiloxLo& K, uint32_t k0,
+                                          uint32_t k1) {
+  const uint64_t p0 = (uint64_t)kPhiloxM0 * c0;                 // round 0
+  const uint32_t r0n2 = (uint32_t)(p0 >> 32) ^ K.A;
+  const uint64_t q1 = (uint64_t)kPhiloxM1 * r0n2;               // round 1
+  uint32_t x0 = (uint32_t)(q1 >> 32) ^ K.B;
+  uint32_t x1 = (uint32_t)q1;
+  uint32_t x2 = (uint32_t)p0 ^ K.C;
+  const uint64_t s0 = (uint64_t)kPhiloxM0 * x0;                 // round 2
+  const uint64_t s1 = (uint64_t)kPhiloxM1 * x2;
+  x0 = __builtin_amdgcn_bitop3_b32((uint32_t)(s1 >> 32), x1, k0 + 2u * kPhiloxW0, 0x96);
+  x2 = (uint32_t)(s0 >> 32) ^ K.D;
+  x1 = (uint32_t)s1;
+  uint32_t x3 = (uint32_t)s0;
+  k0 += 3u * kPhiloxW0;
+  k1 += 3u * kPhiloxW1;
+#pragma unroll
+  for (int r = 3; r < 10; ++r) {
+    const uint64_t a0 = (uint64_t)kPhiloxM0 * x0;
+    const uint64_t a1 = (uint64_t)kPhiloxM1 * x2;
+    const uint32_t n0 = __builtin_amdgcn_bitop3_b32((uint32_t)(a1 >> 32), x1, k0, 0x96);
+    const uint32_t n2 = __builtin_amdgcn_bitop3_b32((uint32_t)(a0 >> 32), x3, k1, 0x96);
+    x1 = (uint32_t)a1;
+    x3 = (uint32_t)a0;
+    x0 = n0;
+    x2 = n2;
+    k0 += kPhiloxW0;
+    k1 += kPhiloxW1;
+  }
+  return U4{x0, x1, x2, x3};
+}
+
 __device__ __forceinline__ U4 philox_block_dev(const PhiloxStream& s, uint64_t grp) {
   return philox10_dev((uint32_t)grp, (uint32_t)(grp >> 32), s.c2, s.c3, s.k0, s.k1);
 }
@@ -149,12 +207,18 @@ constexpr double kScreenEz =
     (1.0 + kScreenEs) * kScreenEr + kScreenRmax * kScreenEs + 0x1p-23 * (kScreenRmax + kScreenEr);
 constexpr double kScreenZm = 5.7;     // bound on |z| and |z~|
 
-// HI0: the caller guarantees grp < 2^32 (counter word 1 is 0: round 2's
-// first product is then lane-invariant, one v_mad_u64_u32 less per block)
-template <bool HI0 = false>
 __device__ __forceinline__ F4 normal4_screen(const PhiloxStream& s, uint64_t grp) {
-  const U4 x = philox10_dev((uint32_t)grp, HI0 ? 0u : (uint32_t)(grp >> 32), s.c2, s.c3, s.k0,
-                            s.k1);
+  const U4 x = philox_block_dev(s, grp);
+  F4 z;
+  box_muller_screen(x.x, x.y, z.a, z.b);
+  box_muller_screen(x.z, x.w, z.c, z.d);
+  return z;
+}
+
+// normal4_screen of a block below 2^32, K = philox_lo_key(s)
+__device__ __forceinline__ F4 normal4_screen_lo(const PhiloxStream& s, const PhiloxLo& K,
+                                                uint32_t grp) {
+  const U4 x = philox10_lo(grp, K, s.k0, s.k1);
   F4 z;
   box_muller_screen(x.x, x.y, z.a, z.b);
   box_muller_screen(x.z, x.w, z.c, z.d);

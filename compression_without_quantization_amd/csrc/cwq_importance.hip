@@ -77,14 +77,19 @@ __global__ void __launch_bounds__(1024) k_imp_tiles(const int64_t* __restrict__ 
 // Screening row value: sum_j (A_j z_j + B_j) z_j + C_j over the candidate's
 // dims, z from the hardware-transcendental Box-Muller ("screening
 // the importance sampler").  `align` = (kbase mod 4) must be wave-uniform.
+// HI0: every block index of the row is below 2^32 (lok = philox_lo_key(st))
 template <bool HI0>
-__device__ __forceinline__ float screen_row_imp(const PhiloxStream& st, uint64_t kbase, int64_t d,
-                                                int align, const float4* __restrict__ coef) {
+__device__ __forceinline__ float screen_row_imp(const PhiloxStream& st, const PhiloxLo& lok,
+                                                uint64_t kbase, int64_t d, int align,
+                                                const float4* __restrict__ coef) {
   float s = 0.0f;
   F4 z = {0.f, 0.f, 0.f, 0.f};
   for (int64_t e = 0; e < d; ++e) {
     const int w = (align + (int)(e & 3)) & 3;  // wave-uniform
-    if (w == 0 || e == 0) z = normal4_screen<HI0>(st, (kbase + (uint64_t)e) >> 2);
+    if (w == 0 || e == 0) {
+      const uint64_t grp = (kbase + (uint64_t)e) >> 2;
+      z = HI0 ? normal4_screen_lo(st, lok, (uint32_t)grp) : normal4_screen(st, grp);
+    }
     const float zz = w == 0 ? z.a : (w == 1 ? z.b : (w == 2 ? z.c : z.d));
     const float4 c = coef[e];
     s = s + __builtin_fmaf(__builtin_fmaf(c.x, zz, c.y), zz, c.z);
@@ -300,10 +305,11 @@ __global__ void __launch_bounds__(256, CWQ_IMP_MIN_WAVES) k_imp_eval(
         }
       };
       // every Philox block index (n d + j) / 4 of the group below 2^32:
-      // counter word 1 is 0 (normal4_screen<true>: one multiply less per block)
+      // counter word 1 is 0 (normal4_screen_lo: one multiply less per block)
       const bool lo32 = (uint64_t)N * (uint64_t)d <= (1ull << 34);
       auto scan = [&](auto HI0T) __attribute__((always_inline)) {
         constexpr bool HI0 = decltype(HI0T)::value;
+        [[maybe_unused]] const PhiloxLo lok = HI0 ? philox_lo_key(st) : PhiloxLo{};
         if (d >= kImpPruneMinD) {
           // pruned screening: one Philox block of the lane's row per iteration;
           // a row stops once s + E + sum of the unvisited dims' maxima < tau.
@@ -319,7 +325,8 @@ __global__ void __launch_bounds__(256, CWQ_IMP_MIN_WAVES) k_imp_eval(
           uint32_t iter = 0;
           while (__ballot(active) != 0ull) {
             const uint64_t k = (uint64_t)n * (uint64_t)d + (uint64_t)j;
-            const F4 z = normal4_screen<HI0>(st, k >> 2);
+            const F4 z = HI0 ? normal4_screen_lo(st, lok, (uint32_t)(k >> 2))
+                             : normal4_screen(st, k >> 2);
             const int wa = (int)(k & 3u);
             const int cnt = (4 - wa) < (int)(d - j) ? (4 - wa) : (int)(d - j);
   #pragma unroll
@@ -367,7 +374,7 @@ __global__ void __launch_bounds__(256, CWQ_IMP_MIN_WAVES) k_imp_eval(
           }
         } else {
           for (int64_t n = n0 + 4 * (int64_t)lane + wv; n < n1; n += 256) {
-            const float sh = screen_row_imp<HI0>(st, (uint64_t)n * (uint64_t)d, d, align, coef);
+            const float sh = screen_row_imp<HI0>(st, lok, (uint64_t)n * (uint64_t)d, d, align, coef);
             const float slack = E + __builtin_fabsf(sh) * 0x1p-22f;
             if (sh + slack >= tau) keep(n, sh, slack);
           }

@@ -422,12 +422,13 @@ __global__ void __launch_bounds__(256, CWQ_PRUNE_MIN_WAVES) k_encode_prune(
     uint64_t bestk = 0;
     uint32_t iter = 0;
 
+    const PhiloxLo lok = philox_lo_key(st);  // block indices < 2^32 (launch_prune_t)
     auto pass = [&](auto screen_tag) {
       constexpr bool SCREEN = decltype(screen_tag)::value;
       while (__ballot(active) != 0ull) {
         const int2 mt = meta[k];
         const uint32_t grp = (uint32_t)n * (uint32_t)G + (uint32_t)mt.x;
-        const U4 x = philox10_dev(grp, 0u, st.c2, st.c3, st.k0, st.k1);
+        const U4 x = philox10_lo(grp, lok, st.k0, st.k1);
         float z0, z1, z2, z3;
         float upper;
         if constexpr (SCREEN) {
@@ -1072,6 +1073,7 @@ __global__ void __launch_bounds__(256, COOP ? CWQ_CSR_COOP_MIN_WAVES : CWQ_CSR_R
       auto run = [&](const float2* ab, const float* bp, const uint32_t* od, const float4* rec,
                      auto REC, auto HI0T) __attribute__((always_inline)) {
         constexpr bool HI0 = decltype(HI0T)::value;
+        [[maybe_unused]] const PhiloxLo lok = HI0 ? philox_lo_key(st) : PhiloxLo{};
         uint32_t wnext = r0 + 64u;
         uint32_t r = r0 + lane;
         bool active = r < r1;
@@ -1142,8 +1144,9 @@ __global__ void __launch_bounds__(256, COOP ? CWQ_CSR_COOP_MIN_WAVES : CWQ_CSR_R
 #pragma unroll
           for (int i = 0; i < RUPL; ++i) {
             const uint64_t blk = rb + u[i];
-            const U4 x = philox10_dev((uint32_t)blk, HI0 ? 0u : (uint32_t)(blk >> 32), st.c2,
-                                      st.c3, kk0, kk1);
+            const U4 x = HI0 ? philox10_lo((uint32_t)blk, lok, kk0, kk1)
+                             : philox10_dev((uint32_t)blk, (uint32_t)(blk >> 32), st.c2, st.c3,
+                                            kk0, kk1);
             F4 z;
             box_muller_screen(x.x, x.y, z.a, z.b);
             box_muller_screen(x.z, x.w, z.c, z.d);
@@ -1223,6 +1226,7 @@ __global__ void __launch_bounds__(256, COOP ? CWQ_CSR_COOP_MIN_WAVES : CWQ_CSR_R
       auto run_coop = [&](const float2* ab, const float* bp, const uint32_t* od,
                           const float4* rec, auto REC, auto HI0T) __attribute__((always_inline)) {
         constexpr bool HI0 = decltype(HI0T)::value;
+        [[maybe_unused]] const PhiloxLo lok = HI0 ? philox_lo_key(st) : PhiloxLo{};
         const uint32_t t = lane & 15u, slot = lane >> 4;
         const uint64_t below = (1ull << (slot * 16u)) - 1ull;  // lanes of lower slots
 #if CWQ_CSR_COOP_CLASS_WAVES
@@ -1314,8 +1318,9 @@ __global__ void __launch_bounds__(256, COOP ? CWQ_CSR_COOP_MIN_WAVES : CWQ_CSR_R
 #pragma unroll
             for (int i = 0; i < UPL; ++i) {
               const uint64_t blk = rb + u[i];
-              const U4 x = philox10_dev((uint32_t)blk, HI0 ? 0u : (uint32_t)(blk >> 32), st.c2,
-                                        st.c3, kk0, kk1);
+              const U4 x = HI0 ? philox10_lo((uint32_t)blk, lok, kk0, kk1)
+                               : philox10_dev((uint32_t)blk, (uint32_t)(blk >> 32), st.c2,
+                                              st.c3, kk0, kk1);
               F4 z;
               box_muller_screen(x.x, x.y, z.a, z.b);
               box_muller_screen(x.z, x.w, z.c, z.d);
