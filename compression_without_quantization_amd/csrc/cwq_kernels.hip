@@ -976,9 +976,6 @@ __device__ __forceinline__ float exact_row_wave(
 #ifndef CWQ_COOP_UPL
 #define CWQ_COOP_UPL 4                // units per lane per iteration of a cooperative row
 #endif
-#ifndef CWQ_CSR_XCD_MAP
-#define CWQ_CSR_XCD_MAP 0             // 1: cooperative tiles mapped to XCDs by block-major eighths (2: every launch)
-#endif
 #ifndef CWQ_COOP_LOAD_ORDER
 #define CWQ_COOP_LOAD_ORDER 0         // 1: a cooperative iteration's loads issued in unit order
 #endif
@@ -1026,23 +1023,8 @@ __global__ void __launch_bounds__(256, COOP ? CWQ_CSR_COOP_MIN_WAVES : CWQ_CSR_R
     // published their threshold in gtau (the loop shares tau inside the
     // workgroup only: per-iteration global atomics cost more than they prune)
     const int64_t nbk = ntiles / tiles_per_block;
-    int64_t tt, g;
-#if CWQ_CSR_XCD_MAP
-    if (gridDim.x == ntiles && (COOP || CWQ_CSR_XCD_MAP == 2)) {
-      // XCD-aware (workgroup i runs on XCD i mod 8, a placement the hardware
-      // does not guarantee: speed only): XCD x takes the x-th eighth of the
-      // block-major tile list, so its L2 holds the constants and visit-order
-      // records of ~nb/8 + 1 blocks instead of every block's
-      const int64_t x = tile & 7, j = tile >> 3, q = ntiles >> 3, rm = ntiles & 7;
-      const int64_t tb = x * q + (x < rm ? x : rm) + j;
-      g = tb / tiles_per_block;
-      tt = tb - g * tiles_per_block;
-    } else
-#endif
-    {
-      tt = tile / nbk;
-      g = tile - tt * nbk;
-    }
+    const int64_t tt = tile / nbk;
+    const int64_t g = tile - tt * nbk;
     const BlockSpan sp = block_span(block_off, ud, g);
     const int64_t off = sp.off, d = sp.d;
     const int64_t n0 = tt * cand_per_tile;

@@ -75,8 +75,6 @@ declare -A V=(
   [prepad]=prebuilt
   [head2]=prebuilt
   [lord]="-DCWQ_COOP_LOAD_ORDER=1"
-  [xcd]="-DCWQ_CSR_XCD_MAP=1"
-  [xcd2]="-DCWQ_CSR_XCD_MAP=2"
 )
 if [ "$1" = build ]; then
   mkdir -p $OUT
