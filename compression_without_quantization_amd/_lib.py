@@ -72,6 +72,10 @@ SIGNATURES = {
     "cwq_code_grouped_greedy": (c_i64, [c_vp, c_vp, c_vp, c_vp, c_i64, c_int, c_int, c_i32, c_f32,
                                         c_i64, c_f64, c_vp, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp,
                                         c_size, c_opts, c_vp]),
+    "cwq_code_grouped_greedy_begin": (c_i64, [c_vp, c_vp, c_vp, c_vp, c_i64, c_int, c_int, c_i32,
+                                              c_f32, c_i64, c_f64, c_vp, c_vp, c_i64, c_vp, c_i64,
+                                              c_vp, c_vp, c_size, c_opts, c_vp]),
+    "cwq_code_grouped_greedy_end": (c_i64, [c_vp, c_i64, c_int, c_int, c_vp, c_i64, c_vp]),
     "cwq_code_grouped_greedy_batch_workspace_size": (c_size, [c_i64, c_i64, c_int]),
     "cwq_code_grouped_greedy_batch_host_workspace_size": (c_size, [c_i64, c_i64, c_int]),
     "cwq_code_grouped_greedy_batch": (c_i64, [c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int,
@@ -110,7 +114,7 @@ TOOL_SIGNATURES = {
 
 # CWQ_ABI_VERSION of the include/cwq.h these signatures mirror: a library
 # reporting another version has other argument lists and is refused.
-ABI_VERSION = (0 << 16) | 2
+ABI_VERSION = (0 << 16) | 3
 
 _lib = None
 

@@ -348,20 +348,38 @@ def code_grouped_greedy_sample(sess, target, proposal, n_steps, n_bits_per_step,
     # the LSB-first bitcode (:81-87, :288)
     need = int(lib.cwq_code_grouped_greedy_workspace_size(D, n_steps))
     ws = torch.empty(max(need, 1), dtype=torch.uint8, device=dev)
-    sample_h = np.empty(D, dtype=np.float32)
-    bits_h = np.empty(max((D + 1) * n_bits_per_group, 1), dtype=np.uint8)  # <= D + 1 groups
+    bits_h = _scratch_bytes(max((D + 1) * n_bits_per_group, 1))  # <= D + 1 groups
     starts_h = np.empty(D + 2, dtype=np.int64)
     kl_sum = ctypes.c_double(0.0)
     n_nats = n_bits_per_group * np.log(2) - 1
     seed32 = int(np.int32(np.uint32(int(seed) & 0xFFFFFFFF)))
+    args = (_ptr(q_loc), _ptr(q_scale), _ptr(p_loc), _ptr(p_scale), D, n_steps, n_bits_per_step,
+            seed32, float(rho), group_size_threshold(max_group_size_bits), float(n_nats))
+    opts = _lib.options(prune_mode, eval_events, eval_ms_out)
+    kls = ctypes.byref(kl_sum) if VERBOSE else None
     with torch.cuda.device(dev):
-        G = _lib.check(lib.cwq_code_grouped_greedy(
-            _ptr(q_loc), _ptr(q_scale), _ptr(p_loc), _ptr(p_scale), D, n_steps, n_bits_per_step,
-            seed32, float(rho), group_size_threshold(max_group_size_bits), float(n_nats),
-            sample_h.ctypes.data, bits_h.ctypes.data, bits_h.size, starts_h.ctypes.data,
-            starts_h.size, ctypes.byref(kl_sum) if VERBOSE else None, ws.data_ptr(), ws.numel(),
-            _lib.options(prune_mode, eval_events, eval_ms_out), stream),
-            "cwq_code_grouped_greedy")
+        if eval_ms_out is not None:  # the library times the encode: the one-shot call
+            sample_h = np.empty(D, dtype=np.float32)
+            G = _lib.check(lib.cwq_code_grouped_greedy(
+                *args, sample_h.ctypes.data, bits_h.ctypes.data, bits_h.size,
+                starts_h.ctypes.data, starts_h.size, kls, ws.data_ptr(), ws.numel(), opts, stream),
+                "cwq_code_grouped_greedy")
+            starts = starts_h[:G + 1].tolist()
+        else:
+            # two halves: the ~D/5-element Python list of group starts (~0.3 ms
+            # for a Kodak image's 41k groups) is built while the device codes;
+            # the sample comes back into page-locked memory it keeps alive
+            sample_h = torch.empty(max(D, 1), dtype=torch.float32, pin_memory=True).numpy()[:D]
+            idx_h = _pinned_scratch((D + 1) * n_steps * 4)
+            G = _lib.check(lib.cwq_code_grouped_greedy_begin(
+                *args, sample_h.ctypes.data, idx_h.data_ptr(), (D + 1) * n_steps,
+                starts_h.ctypes.data, starts_h.size, kls, ws.data_ptr(), ws.numel(), opts, stream),
+                "cwq_code_grouped_greedy_begin")
+            starts = starts_h[:G + 1].tolist()
+            _lib.check(lib.cwq_code_grouped_greedy_end(idx_h.data_ptr(), G, n_steps,
+                                                       n_bits_per_step, bits_h.ctypes.data,
+                                                       bits_h.size, stream),
+                       "cwq_code_grouped_greedy_end")
     if VERBOSE:
         total_kl_bits = kl_sum.value / np.log(2)
         print("Total KL to split up: {:.2f} bits, "
@@ -369,8 +387,8 @@ def code_grouped_greedy_sample(sess, target, proposal, n_steps, n_bits_per_step,
               "estimated number of groups: {},"
               "coding {} dimensions".format(total_kl_bits, n_bits_per_group,
                                             total_kl_bits // n_bits_per_group + 1, D))
-    bitcode = bits_h[:G * n_bits_per_group].tobytes().decode('ascii')
-    return sample_h, bitcode, starts_h[:G + 1].tolist()
+    bitcode = str(memoryview(bits_h)[:G * n_bits_per_group], 'ascii')
+    return sample_h, bitcode, starts
 
 
 def code_grouped_greedy_sample_batch(sess, targets, proposals, n_steps, n_bits_per_step, seeds,

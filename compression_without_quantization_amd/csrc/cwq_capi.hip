@@ -645,24 +645,27 @@ size_t cwq_code_grouped_greedy_workspace_size(int64_t D, int n_steps) {
   return grouped_ws(D, n_steps, D + 1).total;
 }
 
-int64_t cwq_code_grouped_greedy(const float* q_loc, const float* q_scale, const float* p_loc,
-                                const float* p_scale, int64_t D, int n_steps,
-                                int n_bits_per_step, int32_t seed, float rho,
-                                int64_t size_threshold, double n_nats, float* sample_host,
-                                char* bits_host, int64_t bits_cap, int64_t* starts_host,
-                                int64_t starts_cap, double* kl_sum_out, void* workspace,
-                                size_t workspace_bytes, const cwq_options* opts, void* stream) {
-  cwq_options o;
-  {
-    const int rc0 = read_options(opts, &o);
-    if (rc0) return rc0;
-  }
+namespace {
+// cwq_code_grouped_greedy up to its last copies: standardise, KL, host
+// partition (starts_host), the encode, destandardisation, and the copies of
+// the G * n_steps indices to idx_host and the sample to sample_host, all
+// enqueued on the stream.  Returns G.  tev (eval_ms_out only): its two
+// timing events, recorded around the encode.  bits_cap >= 0: the bitcode
+// capacity, checked once G is known, before the encode.
+int64_t grouped_begin(const float* q_loc, const float* q_scale, const float* p_loc,
+                      const float* p_scale, int64_t D, int n_steps, int n_bits_per_step,
+                      int32_t seed, float rho, int64_t size_threshold, double n_nats,
+                      float* sample_host, int32_t* idx_host, int64_t idx_cap,
+                      int64_t* starts_host, int64_t starts_cap, double* kl_sum_out,
+                      void* workspace, size_t workspace_bytes, const cwq_options* opts,
+                      const cwq_options& o, CallEvents* tev, int n_bits_cap_check,
+                      int64_t bits_cap, void* stream, const char* who) {
   if (D < 0 || n_steps < 1 || n_bits_per_step < 0 || n_bits_per_step > CWQ_MAX_BITS_PER_STEP)
-    return fail(CWQ_ERR_INVALID, "cwq_code_grouped_greedy: bad sizes");
+    return fail(CWQ_ERR_INVALID, "%s: bad sizes", who);
   if (D > 0 && (!q_loc || !q_scale || !p_loc || !p_scale || !sample_host))
-    return fail(CWQ_ERR_INVALID, "cwq_code_grouped_greedy: null pointer");
+    return fail(CWQ_ERR_INVALID, "%s: null pointer", who);
   if (!starts_host || starts_cap < D + 2)
-    return fail(CWQ_ERR_CAPACITY, "cwq_code_grouped_greedy: starts_cap must be >= D + 2");
+    return fail(CWQ_ERR_CAPACITY, "%s: starts_cap must be >= D + 2", who);
   const GroupedWs l = grouped_ws(D, n_steps, D + 1);
   if (workspace_bytes < l.total || !workspace)
     return fail(CWQ_ERR_WORKSPACE, "workspace %zu bytes < required %zu", workspace_bytes,
@@ -721,14 +724,13 @@ int64_t cwq_code_grouped_greedy(const float* q_loc, const float* q_scale, const 
   if (n < 0) return n;
   const int64_t G = n - 1;
   lap("group");
-  const int64_t nbits = G * (int64_t)n_steps * n_bits_per_step;
-  if (bits_cap < nbits || (nbits > 0 && !bits_host))
-    return fail(CWQ_ERR_CAPACITY, "cwq_code_grouped_greedy: bits_cap %lld < %lld",
-                (long long)bits_cap, (long long)nbits);
-  if (G <= 0) {
-    cwq::set_error(CWQ_OK, "");
-    return G < 0 ? 0 : G;
-  }
+  if (n_bits_cap_check && bits_cap < G * (int64_t)n_steps * n_bits_per_step)
+    return fail(CWQ_ERR_CAPACITY, "%s: bits_cap %lld < %lld", who, (long long)bits_cap,
+                (long long)(G * (int64_t)n_steps * n_bits_per_step));
+  if (G <= 0) return G < 0 ? 0 : G;
+  if (idx_cap < G * (int64_t)n_steps || !idx_host)
+    return fail(CWQ_ERR_CAPACITY, "%s: index buffer %lld < %lld", who, (long long)idx_cap,
+                (long long)(G * n_steps));
   int64_t maxd = 0;
   for (int64_t g = 0; g < G; ++g) {
     const int64_t dg = starts_host[g + 1] - starts_host[g];
@@ -738,40 +740,118 @@ int64_t cwq_code_grouped_greedy(const float* q_loc, const float* q_scale, const 
       hipSuccess)
     return hip_fail(e, "offsets to device");
   // :273-284 one greedy coder per group, seed + g
-  CallEvents tev;
-  if (o.eval_ms_out && (!tev.made(2, s, hipEventDefault) ||
-                        hipEventRecord(tev.ev[0], s) != hipSuccess))
-    return fail(CWQ_ERR_HIP, "cwq_code_grouped_greedy: timing events failed");
+  if (o.eval_ms_out && (!tev->made(2, s, hipEventDefault) ||
+                        hipEventRecord(tev->ev[0], s) != hipSuccess))
+    return fail(CWQ_ERR_HIP, "%s: timing events failed", who);
   if ((rc = cwq_greedy_encode(t_loc, t_scale, zeros, ones, offs, G, D, maxd, n_bits_per_step,
                               n_steps, seed, rho, 0, idx, sample, w + l.enc,
                               workspace_bytes - l.enc, opts, stream)) < 0)
     return rc;
-  if (o.eval_ms_out && (e = hipEventRecord(tev.ev[1], s)) != hipSuccess) {
+  if (o.eval_ms_out && (e = hipEventRecord(tev->ev[1], s)) != hipSuccess) {
     (void)hipStreamSynchronize(s);
     return hip_fail(e, "event");
   }
   // :292 destandardise
   if ((rc = cwq_destandardise(sample, p_loc, p_scale, D, out, stream)) < 0) return rc;
-  g_idx_host.resize((size_t)(G * n_steps));
-  if ((e = hipMemcpyAsync(g_idx_host.data(), idx, (size_t)(G * n_steps) * 4,
-                          hipMemcpyDeviceToHost, s)) != hipSuccess)
+  if ((e = hipMemcpyAsync(idx_host, idx, (size_t)(G * n_steps) * 4, hipMemcpyDeviceToHost, s)) !=
+      hipSuccess)
     return hip_fail(e, "indices to host");
   if ((e = hipMemcpyAsync(sample_host, out, (size_t)D * 4, hipMemcpyDeviceToHost, s)) !=
       hipSuccess)
     return hip_fail(e, "sample to host");
-  if ((e = hipStreamSynchronize(s)) != hipSuccess) return hip_fail(e, "sync");
-  lap("encode");
-  if (o.eval_ms_out && (e = hipEventElapsedTime(o.eval_ms_out, tev.ev[0], tev.ev[1])) !=
-                           hipSuccess)
-    return hip_fail(e, "event time");
-  // :81-87, :288 each index as n_bits_per_step LSB-first chars, steps then groups
+  lap("enqueued");
+  return G;
+}
+
+// :81-87, :288 each of the G * n_steps indices as n_bits_per_step LSB-first
+// chars, steps then groups
+int64_t grouped_bits(const int32_t* idx_host, int64_t G, int n_steps, int n_bits_per_step,
+                     char* bits_host, int64_t bits_cap, const char* who) {
+  const int64_t nbits = G * (int64_t)n_steps * n_bits_per_step;
+  if (bits_cap < nbits || (nbits > 0 && !bits_host))
+    return fail(CWQ_ERR_CAPACITY, "%s: bits_cap %lld < %lld", who, (long long)bits_cap,
+                (long long)nbits);
+  if (G <= 0) return 0;
+  return write_bitcode(idx_host, G * n_steps, n_bits_per_step, bits_host);
+}
+}  // namespace
+
+int64_t cwq_code_grouped_greedy(const float* q_loc, const float* q_scale, const float* p_loc,
+                                const float* p_scale, int64_t D, int n_steps,
+                                int n_bits_per_step, int32_t seed, float rho,
+                                int64_t size_threshold, double n_nats, float* sample_host,
+                                char* bits_host, int64_t bits_cap, int64_t* starts_host,
+                                int64_t starts_cap, double* kl_sum_out, void* workspace,
+                                size_t workspace_bytes, const cwq_options* opts, void* stream) {
+  static const char* const who = "cwq_code_grouped_greedy";
+  cwq_options o;
   {
-    const int64_t nw = write_bitcode(g_idx_host.data(), G * n_steps, n_bits_per_step, bits_host);
-    if (nw < 0) return nw;
+    const int rc0 = read_options(opts, &o);
+    if (rc0) return rc0;
   }
-  lap("bits");
+  CallEvents tev;
+  g_idx_host.resize((size_t)((D + 1) * (n_steps > 0 ? n_steps : 1)));
+  const int64_t G = grouped_begin(q_loc, q_scale, p_loc, p_scale, D, n_steps, n_bits_per_step,
+                                  seed, rho, size_threshold, n_nats, sample_host,
+                                  g_idx_host.data(), (int64_t)g_idx_host.size(), starts_host,
+                                  starts_cap, kl_sum_out, workspace, workspace_bytes, opts, o,
+                                  &tev, 1, bits_cap, stream, who);
+  if (G < 0) return G;
+  hipError_t e;
+  if (G > 0 && (e = hipStreamSynchronize((hipStream_t)stream)) != hipSuccess)
+    return hip_fail(e, "sync");
+  if (G > 0 && o.eval_ms_out &&
+      (e = hipEventElapsedTime(o.eval_ms_out, tev.ev[0], tev.ev[1])) != hipSuccess)
+    return hip_fail(e, "event time");
+  const int64_t nw = grouped_bits(g_idx_host.data(), G, n_steps, n_bits_per_step, bits_host,
+                                  bits_cap, who);
+  if (nw < 0) return nw;
   cwq::set_error(CWQ_OK, "");
   return G;
+}
+
+int64_t cwq_code_grouped_greedy_begin(const float* q_loc, const float* q_scale,
+                                      const float* p_loc, const float* p_scale, int64_t D,
+                                      int n_steps, int n_bits_per_step, int32_t seed, float rho,
+                                      int64_t size_threshold, double n_nats, float* sample_host,
+                                      int32_t* idx_host, int64_t idx_cap, int64_t* starts_host,
+                                      int64_t starts_cap, double* kl_sum_out, void* workspace,
+                                      size_t workspace_bytes, const cwq_options* opts,
+                                      void* stream) {
+  static const char* const who = "cwq_code_grouped_greedy_begin";
+  cwq_options o;
+  {
+    const int rc0 = read_options(opts, &o);
+    if (rc0) return rc0;
+  }
+  if (o.eval_ms_out)
+    return fail(CWQ_ERR_INVALID, "%s: eval_ms_out needs the synchronous call (use the events)",
+                who);
+  const int64_t G = grouped_begin(q_loc, q_scale, p_loc, p_scale, D, n_steps, n_bits_per_step,
+                                  seed, rho, size_threshold, n_nats, sample_host, idx_host,
+                                  idx_cap, starts_host, starts_cap, kl_sum_out, workspace,
+                                  workspace_bytes, opts, o, nullptr, 0, 0, stream, who);
+  if (G < 0) {
+    (void)hipStreamSynchronize((hipStream_t)stream);  // nothing queued may outlive an error
+    return G;
+  }
+  cwq::set_error(CWQ_OK, "");
+  return G;
+}
+
+int64_t cwq_code_grouped_greedy_end(const int32_t* idx_host, int64_t G, int n_steps,
+                                    int n_bits_per_step, char* bits_host, int64_t bits_cap,
+                                    void* stream) {
+  static const char* const who = "cwq_code_grouped_greedy_end";
+  if (G < 0 || n_steps < 1 || n_bits_per_step < 0 || n_bits_per_step > CWQ_MAX_BITS_PER_STEP)
+    return fail(CWQ_ERR_INVALID, "%s: bad sizes", who);
+  hipError_t e;
+  if ((e = hipStreamSynchronize((hipStream_t)stream)) != hipSuccess) return hip_fail(e, "sync");
+  if (G > 0 && !idx_host) return fail(CWQ_ERR_INVALID, "%s: null pointer", who);
+  const int64_t nw = grouped_bits(idx_host, G, n_steps, n_bits_per_step, bits_host, bits_cap, who);
+  if (nw < 0) return nw;
+  cwq::set_error(CWQ_OK, "");
+  return nw;
 }
 
 // ---------------------------------------------------------------------------

@@ -68,7 +68,7 @@ extern "C" {
  * cwq_greedy_encode_workspace_size, no process-wide tuning setters.  Bindings
  * must refuse a library whose cwq_version() differs from the header they were
  * written against. */
-#define CWQ_ABI_VERSION ((0 << 16) | 2)
+#define CWQ_ABI_VERSION ((0 << 16) | 3)
 int cwq_version(void);
 
 /* Thread-local description of the last error ("" if none). */
@@ -203,6 +203,29 @@ int64_t cwq_code_grouped_greedy(const float* q_loc, const float* q_scale, const 
                                 char* bits_host, int64_t bits_cap, int64_t* starts_host,
                                 int64_t starts_cap, double* kl_sum_out, void* workspace,
                                 size_t workspace_bytes, const cwq_options* opts, void* stream);
+
+/* cwq_code_grouped_greedy in two halves, so the caller can work while the
+ * device codes (the Python wrapper builds the reference's group_start_indices
+ * list meanwhile).  _begin: the same inputs; synchronises once (after the KL),
+ * writes starts_host[0..G] and returns G (or a negative error code), with the
+ * encode, the destandardisation and the copies of the G * n_steps indices to
+ * idx_host (idx_cap >= G * n_steps; D + 1 groups at most) and of the sample to
+ * sample_host still in flight on the stream: both must stay valid until _end,
+ * and page-locked host memory keeps the copies asynchronous.
+ * opts->eval_ms_out must be NULL (the caller's eval events work).  _end:
+ * synchronises the stream and writes the bitcode of those indices; returns
+ * the number of chars (G * n_steps * n_bits_per_step) or a negative code. */
+int64_t cwq_code_grouped_greedy_begin(const float* q_loc, const float* q_scale,
+                                      const float* p_loc, const float* p_scale, int64_t D,
+                                      int n_steps, int n_bits_per_step, int32_t seed, float rho,
+                                      int64_t size_threshold, double n_nats, float* sample_host,
+                                      int32_t* idx_host, int64_t idx_cap, int64_t* starts_host,
+                                      int64_t starts_cap, double* kl_sum_out, void* workspace,
+                                      size_t workspace_bytes, const cwq_options* opts,
+                                      void* stream);
+int64_t cwq_code_grouped_greedy_end(const int32_t* idx_host, int64_t G, int n_steps,
+                                    int n_bits_per_step, char* bits_host, int64_t bits_cap,
+                                    void* stream);
 
 /* A batch of independent code_grouped_greedy_sample calls (coded_greedy_sampler.py:170-296
  * once per item: the images of a dataset, or the ladder levels of several

@@ -235,6 +235,49 @@ def test_grouped_batch_equals_single_calls(cwq, sizes, seeds, bits, n_steps):
         assert np.array_equal(_u32(bs), _u32(sample)), k
 
 
+@pytest.mark.parametrize("D,bits,n_steps", [(0, 8, 1), (1, 8, 1), (3000, 8, 1), (20000, 10, 2),
+                                             (9000, 14, 3)])
+def test_grouped_two_halves_equal_one_shot(cwq, cwqlib, D, bits, n_steps):
+    """code_grouped_greedy_sample takes cwq_code_grouped_greedy_begin / _end
+    (the group-start list is built while the device codes) unless the caller
+    asks the library to time the encode (eval_ms_out: the one-shot call); both
+    give the same sample, bitcode and starts, also for D = 0 and 1 and
+    multi-step groups on the forked streams.  _begin refuses eval_ms_out."""
+    import ctypes
+    cwq.coded_greedy_sampler.VERBOSE = False
+    rng = np.random.default_rng(D + bits)
+    pl = (0.1 * rng.standard_normal(D)).astype(np.float32)
+    ps = rng.uniform(0.8, 1.2, D).astype(np.float32)
+    ql = (pl + ps * rng.standard_normal(D) * 0.7).astype(np.float32)
+    qs = (ps * rng.uniform(0.3, 1.0, D)).astype(np.float32)
+    tg = cwq.Normal(torch.from_numpy(ql).cuda(), torch.from_numpy(qs).cuda())
+    pr = cwq.Normal(torch.from_numpy(pl).cuda(), torch.from_numpy(ps).cuda())
+    a = cwq.code_grouped_greedy_sample(None, tg, pr, n_steps, bits, 42)
+    ms = ctypes.c_float(-1.0)
+    b = cwq.code_grouped_greedy_sample(None, tg, pr, n_steps, bits, 42, eval_ms_out=ms)
+    assert a[2] == b[2] and isinstance(a[2], list)
+    assert a[1] == b[1]
+    assert np.array_equal(_u32(a[0]), _u32(b[0]))
+    assert len(a[1]) == (len(a[2]) - 1) * n_steps * bits
+    if D > 0:
+        assert ms.value >= 0.0
+    # the C ABI: eval_ms_out is refused by _begin (it returns before the encode ends)
+    from compression_without_quantization_amd import _lib
+    ws = torch.empty(max(1, int(cwqlib.cwq_code_grouped_greedy_workspace_size(16, 1))),
+                     dtype=torch.uint8, device="cuda")
+    x = torch.ones(16, device="cuda")
+    sample = np.empty(16, np.float32)
+    idx = np.empty(17, np.int32)
+    starts = np.empty(18, np.int64)
+    rc = cwqlib.cwq_code_grouped_greedy_begin(
+        x.data_ptr(), x.data_ptr(), x.data_ptr(), x.data_ptr(), 16, 1, 8, 42, 1.0, 4095, 4.5,
+        sample.ctypes.data, idx.ctypes.data, 17, starts.ctypes.data, 18, None, ws.data_ptr(),
+        ws.numel(), _lib.options(None, None, ctypes.c_float(0.0)),
+        torch.cuda.current_stream().cuda_stream)
+    assert rc < 0
+    assert b"eval_ms_out" in cwqlib.cwq_last_error()
+
+
 def _bench(args, timeout=300):
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
     r = subprocess.run([sys.executable, "-u", os.path.join(REPO, "bench.py")] + args,
