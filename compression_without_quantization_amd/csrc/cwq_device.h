@@ -300,6 +300,9 @@ __device__ __forceinline__ uint32_t ord_f32(float v) {
 __device__ __forceinline__ float unord_f32(uint32_t o) {
   return u2f((o & 0x80000000u) ? (o & 0x7fffffffu) : ~o);
 }
+#ifndef CWQ_WAVE_MAX_ASM
+#define CWQ_WAVE_MAX_ASM 1  // 1: one v_max_f32_dpp per step (inline asm)
+#endif
 // Wave-wide max with GFX9 DPP (quad perms, row mirrors, row_bcast:15/31):
 // six v_max_f32_dpp and one readlane.  Requires a full exec mask.
 template <int CTRL, int ROW_MASK>
@@ -309,6 +312,29 @@ __device__ __forceinline__ float dpp_max_step(float v) {
                                             false);
   return fmaxf(v, __builtin_bit_cast(float, o));
 }
+#if CWQ_WAVE_MAX_ASM
+// The same six steps as one v_max_f32_dpp each: v = max(v[dpp], v), and lanes a
+// step's row mask leaves unwritten keep v.  Through the builtins each step is a
+// v_mov_b32_dpp from a -inf "old" value plus two v_max_f32 (fmaxf's IEEE
+// canonicalisation of the moved value): 25 VALU instructions against 6 (the
+// tau sharing of the pruned loops, every 16 units).  Each step starts with the
+// two wait states a DPP read of a VGPR written by the previous VALU needs, and
+// the last ends with them before the readlane.  tau is never a signalling NaN,
+// for which the two forms would differ.
+#define CWQ_DPP_MAX_STEP(v, ctl, rmask) \
+  asm volatile("s_nop 1\n\tv_max_f32_dpp %0, %0, %0 " ctl " row_mask:" rmask " bank_mask:0xf" \
+               : "+v"(v))
+__device__ __forceinline__ float wave_max_f32(float v) {
+  CWQ_DPP_MAX_STEP(v, "quad_perm:[1,0,3,2]", "0xf");
+  CWQ_DPP_MAX_STEP(v, "quad_perm:[2,3,0,1]", "0xf");
+  CWQ_DPP_MAX_STEP(v, "row_half_mirror", "0xf");
+  CWQ_DPP_MAX_STEP(v, "row_mirror", "0xf");
+  CWQ_DPP_MAX_STEP(v, "row_bcast:15", "0xa");
+  CWQ_DPP_MAX_STEP(v, "row_bcast:31", "0xc");
+  asm volatile("s_nop 1" : "+v"(v));
+  return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 63));
+}
+#else
 __device__ __forceinline__ float wave_max_f32(float v) {
   v = dpp_max_step<0xb1, 0xf>(v);   // quad_perm [1,0,3,2]
   v = dpp_max_step<0x4e, 0xf>(v);   // quad_perm [2,3,0,1]
@@ -318,6 +344,7 @@ __device__ __forceinline__ float wave_max_f32(float v) {
   v = dpp_max_step<0x143, 0xc>(v);  // row_bcast:31 into rows 2, 3: lane 63 holds the max
   return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 63));
 }
+#endif
 // Sum over each 16-lane DPP row, the same value in all 16 lanes: butterflies
 // (quad xor 1, quad xor 2, half-row mirror, row mirror) pair lanes
 // symmetrically and float addition commutes, so every lane forms the

@@ -75,6 +75,7 @@ declare -A V=(
   [prepad]=prebuilt
   [head2]=prebuilt
   [lord]="-DCWQ_COOP_LOAD_ORDER=1"
+  [nowma]="-DCWQ_WAVE_MAX_ASM=0"
 )
 if [ "$1" = build ]; then
   mkdir -p $OUT
