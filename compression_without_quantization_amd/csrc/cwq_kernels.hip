@@ -409,10 +409,11 @@ __global__ void __launch_bounds__(256, CWQ_PRUNE_MIN_WAVES) k_encode_prune(
     // this wave's contiguous share of the tile's candidates
     const int64_t per_wave = (n1 - n0 + 3) / 4;
     const int64_t w0 = n0 + (int64_t)wv * per_wave;
-    const int64_t w1 = (w0 + per_wave < n1) ? w0 + per_wave : n1;
-    int64_t wnext = w0 + 64;
-    int64_t n = w0 + lane;
-    bool active = n < w1;
+    // candidate indices stay below 2^32 in this kernel (launch_prune_t):
+    // 32-bit counters (a 64-bit add and compare cost two VALU slots each)
+    const uint32_t w1 = (uint32_t)((w0 + per_wave < n1) ? w0 + per_wave : n1);
+    uint32_t wnext = (uint32_t)w0 + 64u;
+    uint32_t n = (uint32_t)w0 + lane;
     int k = 0;
     float s = 0.0f;
     float tau = -__builtin_inff();
@@ -425,7 +426,11 @@ __global__ void __launch_bounds__(256, CWQ_PRUNE_MIN_WAVES) k_encode_prune(
     const PhiloxLo lok = philox_lo_key(st);  // block indices < 2^32 (launch_prune_t)
     auto pass = [&](auto screen_tag) {
       constexpr bool SCREEN = decltype(screen_tag)::value;
-      while (__ballot(active) != 0ull) {
+      for (;;) {
+        // a lane is active while its row index is in the wave's range (a
+        // compare each iteration, not a flag carried in a VGPR)
+        const bool active = n < w1;
+        if (__ballot(active) == 0ull) break;
         const int2 mt = meta[k];
         const uint32_t grp = (uint32_t)n * (uint32_t)G + (uint32_t)mt.x;
         const U4 x = philox10_lo(grp, lok, st.k0, st.k1);
@@ -479,7 +484,13 @@ __global__ void __launch_bounds__(256, CWQ_PRUNE_MIN_WAVES) k_encode_prune(
         }
         k += 1;
         const bool complete = (k == G);
-        const bool prune = !complete && (upper < tau);
+        const bool below = upper < tau;
+        const bool prune = !complete && below;
+        const bool done = complete || below || !active;
+        // the finished lanes' mask from the compares' own masks (SALU): a
+        // ballot of the combined flag costs a v_cndmask + v_cmp to rebuild it
+        const uint64_t m = __ballot(complete) | __ballot(below) |
+                           (__builtin_amdgcn_read_exec() & ~__ballot(active));
         if (complete && active && upper >= tau) {  // may be the best: keep it
           float lower;
           if constexpr (SCREEN)
@@ -502,13 +513,11 @@ __global__ void __launch_bounds__(256, CWQ_PRUNE_MIN_WAVES) k_encode_prune(
             bestk = kv > bestk ? kv : bestk;
           }
         }
-        const bool done = complete || prune || !active;
 #ifdef CWQ_PRUNE_STATS
         if (active && (complete || prune)) atomicAdd(&s_ps[k], 1u);
         if (active && complete) atomicAdd(&s_ps[65], 1u);
         if (active && complete && upper >= tau) atomicAdd(&s_ps[66], 1u);
 #endif
-        const uint64_t m = __ballot(done);
         const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
                                                         __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
         if (done) {
@@ -516,8 +525,7 @@ __global__ void __launch_bounds__(256, CWQ_PRUNE_MIN_WAVES) k_encode_prune(
           k = 0;
           s = 0.0f;
         }
-        wnext += (int64_t)__builtin_popcountll(m);
-        active = n < w1;
+        wnext += (uint32_t)__builtin_popcountll(m);
         if (((++iter) & CWQ_TAU_SHARE_MASK) == 0u) {  // share tau across the workgroup's waves
           const float tm = wave_max_f32(tau);
           if (lane == 0) atomicMax(&tau_ord, ord_f32(tm));
