@@ -984,6 +984,9 @@ __device__ __forceinline__ float exact_row_wave(
 #ifndef CWQ_COOP_UPL
 #define CWQ_COOP_UPL 4                // units per lane per iteration of a cooperative row
 #endif
+#ifndef CWQ_COOP_CLASS_TILES
+#define CWQ_COOP_CLASS_TILES 1        // 1: cooperative tiles hold one alignment class (rows n = R mod 4)
+#endif
 #ifndef CWQ_COOP_LOAD_ORDER
 #define CWQ_COOP_LOAD_ORDER 0         // 1: a cooperative iteration's loads issued in unit order
 #endif
@@ -1035,9 +1038,27 @@ __global__ void __launch_bounds__(256, COOP ? CWQ_CSR_COOP_MIN_WAVES : CWQ_CSR_R
     const int64_t g = tile - tt * nbk;
     const BlockSpan sp = block_span(block_off, ud, g);
     const int64_t off = sp.off, d = sp.d;
-    const int64_t n0 = tt * cand_per_tile;
-    const int64_t n1 = (n0 + cand_per_tile < n_cand) ? n0 + cand_per_tile : n_cand;
-    if (n1 <= n0) continue;  // empty tile (the launcher sizes tiles so there are none)
+    // the tile's rows: n0 + rstep m, m < nrt
+    int64_t n0, nrt;
+    uint32_t rlog = 0;  // log2 rstep
+#if CWQ_COOP_CLASS_TILES && CWQ_CSR_COOP_CLASS_WAVES
+    if (COOP && d >= coop_min_d && (tiles_per_block & 3) == 0) {
+      // one alignment class per workgroup: tile tt takes the rows n = R (mod 4)
+      // of chunk J (4 tiles' worth of candidates), R = tt mod 4, J = tt / 4, so
+      // its four waves read one class's visit-order records, not four
+      const int64_t J = tt >> 2, C4 = 4 * cand_per_tile;
+      const int64_t lim = (J + 1) * C4 < n_cand ? (J + 1) * C4 : n_cand;
+      n0 = J * C4 + (tt & 3);
+      nrt = lim > n0 ? (lim - n0 + 3) / 4 : 0;
+      rlog = 2;
+    } else
+#endif
+    {
+      n0 = tt * cand_per_tile;
+      nrt = ((n0 + cand_per_tile < n_cand) ? n0 + cand_per_tile : n_cand) - n0;
+    }
+    if (nrt <= 0) continue;  // empty tile
+    const int64_t n1 = n0 + nrt;  // contiguous tiles (rlog == 0): the rows' end
     const PhiloxStream st =
         generate_key(step_seed(sd.of(g), step), 42);
     const float4 gc = grp[g];
@@ -1240,9 +1261,9 @@ __global__ void __launch_bounds__(256, COOP ? CWQ_CSR_COOP_MIN_WAVES : CWQ_CSR_R
 #if CWQ_CSR_COOP_CLASS_WAVES
         // wave wv walks rows wv, wv + 4, wv + 8, ... of the tile: one alignment
         // class per wave, so its slots share one class's visit order
-        const uint32_t nrows = (uint32_t)(n1 - n0);
+        const uint32_t nrows = (uint32_t)nrt;
         const uint32_t q0 = 0u, q1 = nrows > wv ? (nrows - wv + 3u) / 4u : 0u;
-        auto row_of = [&](uint32_t q) { return wv + 4u * q; };
+        auto row_of = [&](uint32_t q) { return (wv + 4u * q) << rlog; };
 #else
         const uint32_t q0 = r0, q1 = r1;
         auto row_of = [&](uint32_t q) { return q; };
@@ -1468,8 +1489,9 @@ __global__ void __launch_bounds__(256, COOP ? CWQ_CSR_COOP_MIN_WAVES : CWQ_CSR_R
         }
       }
     } else {
-      const int align = (int)(((uint64_t)(n0 + wv) * (uint64_t)d) & 3u);
-      for (int64_t n = n0 + 4 * (int64_t)lane + wv; n < n1; n += 256) {
+      const int align = (int)(((uint64_t)(n0 + ((int64_t)wv << rlog)) * (uint64_t)d) & 3u);
+      for (int64_t m = 4 * (int64_t)lane + wv; m < nrt; m += 256) {
+        const int64_t n = n0 + (m << rlog);
         const float v = eval_row<0, STEP0>(st, (uint64_t)n * (uint64_t)d, d, align, loc_s + off,
                                            scale_s + off, t_loc + off, t_scale + off,
                                            lognorm + off, STEP0 ? nullptr : best + off, logtab);
@@ -2287,6 +2309,11 @@ static void launch_prune_csr(const EncodeArgs& a, int step, hipStream_t stream) 
   tpb = tpb < max_tpb ? tpb : max_tpb;
   const int64_t cpt = (a.n_cand + tpb - 1) / tpb;
   tpb = (a.n_cand + cpt - 1) / cpt;  // no tile may start at or past n_cand
+#if CWQ_COOP_CLASS_TILES
+  // one-class tiles come in fours (the kernel skips a residue tile that gets
+  // no row of a short last chunk)
+  if (coop && tpb >= 4) tpb = (tpb + 3) & ~(int64_t)3;
+#endif
   const int64_t ntiles = a.nb * tpb;
   const int64_t coop_min_d = coop ? (int64_t)CWQ_CSR_COOP_MIN_D : INT64_MAX;
 #ifndef CWQ_PREP_SPLIT_MAX_NB

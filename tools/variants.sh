@@ -76,6 +76,7 @@ declare -A V=(
   [head3]=prebuilt
   [lord]="-DCWQ_COOP_LOAD_ORDER=1"
   [nowma]="-DCWQ_WAVE_MAX_ASM=0"
+  [noctile]="-DCWQ_COOP_CLASS_TILES=0"
 )
 if [ "$1" = build ]; then
   mkdir -p $OUT
