@@ -1019,10 +1019,19 @@ __global__ void __launch_bounds__(256, COOP ? CWQ_CSR_COOP_MIN_WAVES : CWQ_CSR_R
   __shared__ uint32_t sq_n[CWQ_CSR_SURVIVOR_CAP];
   __shared__ float sq_ub[CWQ_CSR_SURVIVOR_CAP];
   __shared__ unsigned long long wkey[4];
-  __shared__ float2 l_ab[CWQ_CSR_LDS_DIMS + 12];
-  __shared__ float l_bp[CWQ_CSR_LDS_DIMS + 12];
-  __shared__ uint32_t l_ord[CWQ_CSR_LDS_DIMS + 12];
-  __shared__ float rowbuf[4][kRowChunk];
+  // One LDS region, two uses that never overlap in time: a short block's
+  // natural-order constants, drop bounds and visit order (l_ab, l_bp, l_ord),
+  // and the survivors' exact-row buffers (rowbuf, after the loops).
+  constexpr int kNatF4 = (CWQ_CSR_LDS_DIMS + 12) * 2 / 4;   // l_ab in float4s
+  constexpr int kIdxF4 = (CWQ_CSR_LDS_DIMS + 12) / 4;       // l_bp, l_ord
+  static_assert((CWQ_CSR_LDS_DIMS + 12) % 4 == 0, "LDS sub-arrays in whole float4s");
+  constexpr int kUnionF4 = kNatF4 + 2 * kIdxF4;
+  static_assert(kUnionF4 * 4 >= 4 * kRowChunk, "rowbuf fits the region");
+  __shared__ float4 l_u[kUnionF4];
+  float2* const l_ab = reinterpret_cast<float2*>(l_u);
+  float* const l_bp = reinterpret_cast<float*>(l_u + kNatF4);
+  uint32_t* const l_ord = reinterpret_cast<uint32_t*>(l_u + kNatF4 + kIdxF4);
+  float(*const rowbuf)[kRowChunk] = reinterpret_cast<float(*)[kRowChunk]>(l_u);
   fill_logtab(logtab);
   const uint32_t wv = wave_id();
   const uint32_t lane = threadIdx.x & 63u;
@@ -1422,8 +1431,8 @@ __global__ void __launch_bounds__(256, COOP ? CWQ_CSR_COOP_MIN_WAVES : CWQ_CSR_R
       // survivor list overflow (near-ties everywhere, or a weak early tau):
       // redo the pass starting from the final tau, then score exactly
       for (int pass = 0;; ++pass) {
-        using NoRec = std::integral_constant<bool, false>;
-        using Rec = std::integral_constant<bool, true>;
+        using NoRec = std::integral_constant<int, 0>;
+        using Rec = std::integral_constant<int, 1>;
         using Lo32 = std::integral_constant<bool, true>;   // block indices < 2^32
         using Hi32 = std::integral_constant<bool, false>;
         // each launch mode instantiates only its own loops (register

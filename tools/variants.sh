@@ -73,7 +73,6 @@ declare -A V=(
   [u4w5]="-DCWQ_COOP_UPL=4 -DCWQ_CSR_COOP_MIN_WAVES=5"
   [u8w3]="-DCWQ_COOP_UPL=8 -DCWQ_CSR_COOP_MIN_WAVES=3"
   [prepad]=prebuilt
-  [head3]=prebuilt
   [lord]="-DCWQ_COOP_LOAD_ORDER=1"
   [nowma]="-DCWQ_WAVE_MAX_ASM=0"
   [noctile]="-DCWQ_COOP_CLASS_TILES=0"
