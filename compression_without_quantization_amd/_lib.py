@@ -26,20 +26,22 @@ class Options(ctypes.Structure):
     """cwq_options (include/cwq.h): per-call encoder options."""
     _fields_ = [("prune_mode", ctypes.c_int32), ("reserved", ctypes.c_int32),
                 ("eval_start_event", c_vp), ("eval_stop_event", c_vp),
-                ("eval_ms_out", ctypes.POINTER(ctypes.c_float))]
+                ("eval_ms_out", ctypes.POINTER(ctypes.c_float)),
+                ("item_ready", c_vp)]
 
 
 c_opts = ctypes.POINTER(Options)
 
 
-def options(prune_mode=None, eval_events=None, eval_ms_out=None):
+def options(prune_mode=None, eval_events=None, eval_ms_out=None, item_ready=None):
     """A cwq_options pointer for one call, or None (the library defaults:
     prune_mode 2, no events).  eval_events: (start, stop) hipEvent_t handles;
     eval_ms_out: a ctypes.c_float the fused grouped calls write their scoring
-    launches' milliseconds to."""
-    if prune_mode is None and eval_events is None and eval_ms_out is None:
+    launches' milliseconds to; item_ready: the address of the batch call's
+    per-item int32 flags (zeroed)."""
+    if prune_mode is None and eval_events is None and eval_ms_out is None and item_ready is None:
         return None
-    o = Options(2 if prune_mode is None else int(prune_mode), 0, None, None, None)
+    o = Options(2 if prune_mode is None else int(prune_mode), 0, None, None, None, item_ready)
     if eval_events is not None:
         o.eval_start_event, o.eval_stop_event = eval_events
     if eval_ms_out is not None:
@@ -114,7 +116,7 @@ TOOL_SIGNATURES = {
 
 # CWQ_ABI_VERSION of the include/cwq.h these signatures mirror: a library
 # reporting another version has other argument lists and is refused.
-ABI_VERSION = (0 << 16) | 3
+ABI_VERSION = (0 << 16) | 4
 
 _lib = None
 

@@ -24,8 +24,10 @@ Differences from the TF1 reference (deliberate, documented in DESIGN.md):
 
 All arithmetic runs in libcwq.so; nothing here computes samples on the CPU.
 """
+import concurrent.futures
 import ctypes
 import threading
+import time
 
 import numpy as np
 import torch
@@ -457,24 +459,61 @@ def code_grouped_greedy_sample_batch(sess, targets, proposals, n_steps, n_bits_p
     bits_off = np.empty(n_items + 1, dtype=np.int64)
     n_starts = np.empty(n_items, dtype=np.int64)
     n_nats = n_bits_per_group * np.log(2) - 1
-    with torch.cuda.device(dev):
-        stream = torch.cuda.current_stream(dev).cuda_stream
-        _lib.check(lib.cwq_code_grouped_greedy_batch(
-            n_items, item_off.ctypes.data, _ptr(cat[0]), _ptr(cat[1]), _ptr(cat[2]),
-            _ptr(cat[3]), n_steps, n_bits_per_step, seeds32.ctypes.data, float(rho),
-            group_size_threshold(max_group_size_bits), float(n_nats), sample_h.ctypes.data,
-            bits_h.ctypes.data, bits_cap, bits_off.ctypes.data, starts_h.ctypes.data,
-            starts_h.size, n_starts.ctypes.data, ws.data_ptr(), ws.numel(), hws.data_ptr(),
-            hneed, _lib.options(prune_mode, eval_events, eval_ms_out), stream),
-            "cwq_code_grouped_greedy_batch")
-    out = []
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    # With several items the call runs on a helper thread (ctypes releases the
+    # GIL) and raises item i's flag once its outputs are final: this thread
+    # turns the finished items' bitcodes into str while later chunks code.
+    ready = np.zeros(n_items, dtype=np.int32) if n_items > 1 else None
+
+    def call():
+        with torch.cuda.device(dev):
+            opts = _lib.options(prune_mode, eval_events, eval_ms_out,
+                                None if ready is None else ready.ctypes.data)
+            _lib.check(lib.cwq_code_grouped_greedy_batch(
+                n_items, item_off.ctypes.data, _ptr(cat[0]), _ptr(cat[1]), _ptr(cat[2]),
+                _ptr(cat[3]), n_steps, n_bits_per_step, seeds32.ctypes.data, float(rho),
+                group_size_threshold(max_group_size_bits), float(n_nats), sample_h.ctypes.data,
+                bits_h.ctypes.data, bits_cap, bits_off.ctypes.data, starts_h.ctypes.data,
+                starts_h.size, n_starts.ctypes.data, ws.data_ptr(), ws.numel(), hws.data_ptr(),
+                hneed, opts, stream), "cwq_code_grouped_greedy_batch")
+
     mv = memoryview(bits_h)
-    for i in range(n_items):
+
+    def item(i):
         a, b = int(item_off[i]), int(item_off[i + 1])
         bitcode = str(mv[bits_off[i]:bits_off[i + 1]], 'ascii')
         s0 = a + 2 * i  # item i's starts region (cwq_code_grouped_greedy_batch)
-        out.append((sample_h[a:b], bitcode, starts_h[s0:s0 + n_starts[i]]))
+        return sample_h[a:b], bitcode, starts_h[s0:s0 + n_starts[i]]
+
+    out = []
+    if ready is None:
+        call()
+    else:
+        fut = _batch_thread().submit(call)
+        for i in range(n_items):
+            while not ready[i] and not fut.done():
+                time.sleep(0)  # yields the GIL; the call needs it only to return
+            if not ready[i]:
+                break  # the call ended early: its error is raised below
+            out.append(item(i))
+        fut.result()
+    out.extend(item(i) for i in range(len(out), n_items))
     return out
+
+
+_batch_pool = None
+_batch_pool_lock = threading.Lock()
+
+
+def _batch_thread():
+    """The helper thread code_grouped_greedy_sample_batch runs the native call
+    on (one, created on first use; calls from several threads queue on it)."""
+    global _batch_pool
+    with _batch_pool_lock:
+        if _batch_pool is None:
+            _batch_pool = concurrent.futures.ThreadPoolExecutor(
+                max_workers=1, thread_name_prefix="cwq-batch")
+        return _batch_pool
 
 
 _scratch = threading.local()

@@ -1205,7 +1205,11 @@ int64_t cwq_code_grouped_greedy_batch(
     const int64_t Gi = n_starts[i] - 1 > 0 ? n_starts[i] - 1 : 0;
     const int64_t nw = write_bitcode(idx_h + (gbase(c) + gloc[(size_t)i]) * n_steps, Gi * n_steps,
                                      n_bits_per_step, bits_host + bits_off[i]);
-    if (nw < 0) record_err((int)nw);
+    if (nw < 0) {
+      record_err((int)nw);
+      return;
+    }
+    if (o.item_ready) __atomic_store_n(o.item_ready + i, 1, __ATOMIC_RELEASE);
   };
   auto worker = [&]() {
     for (int64_t i = 0; i < n_items; ++i)

@@ -68,7 +68,7 @@ extern "C" {
  * cwq_greedy_encode_workspace_size, no process-wide tuning setters.  Bindings
  * must refuse a library whose cwq_version() differs from the header they were
  * written against. */
-#define CWQ_ABI_VERSION ((0 << 16) | 3)
+#define CWQ_ABI_VERSION ((0 << 16) | 4)
 int cwq_version(void);
 
 /* Thread-local description of the last error ("" if none). */
@@ -97,15 +97,25 @@ int cwq_stateless_normal_sample(const float* loc, const float* scale, int64_t d,
  *               the summed milliseconds of their candidate-scoring launches
  *               (a pipelined batch codes in chunks: device gaps between them
  *               are excluded, unlike the event span).  Asynchronous entry
- *               points ignore it. */
+ *               points ignore it.
+ *   item_ready: HOST int32 array of n_items flags, zeroed by the caller, or
+ *               NULL.  cwq_code_grouped_greedy_batch sets flag i to 1 (a
+ *               release store) as soon as item i's sample, bitcode, bits_off
+ *               and starts are final in the host arrays, while later chunks
+ *               still code; a caller running the call on another thread can
+ *               consume the items as they complete (coded_greedy_sampler.py
+ *               builds the bitcode strings this way).  The call itself still
+ *               returns only when everything is done; on an error some flags
+ *               stay 0.  Other entry points ignore it. */
 typedef struct cwq_options {
   int32_t prune_mode;
   int32_t reserved; /* must be 0 */
   void* eval_start_event;
   void* eval_stop_event;
   float* eval_ms_out;
+  int32_t* item_ready;
 } cwq_options;
-#define CWQ_OPTIONS_INIT {2, 0, NULL, NULL, NULL}
+#define CWQ_OPTIONS_INIT {2, 0, NULL, NULL, NULL, NULL}
 
 /* Workspace bytes needed by cwq_greedy_encode (CSR blocks) for nb blocks
  * holding total_dims dims in all, none longer than max_block_dim: the argmax

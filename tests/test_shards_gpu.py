@@ -439,7 +439,7 @@ def test_grouped_batch_errors_and_pageable_staging(cwq):
     hneed = lib.cwq_code_grouped_greedy_batch_host_workspace_size(D, n, 1)
     hws = torch.empty(hneed, dtype=torch.uint8, pin_memory=True)
 
-    def call(bits_cap, host_ws, host_bytes):
+    def call(bits_cap, host_ws, host_bytes, opts=None):
         sample = np.empty(D, np.float32)
         bits = np.empty(max(bits_cap, 1), np.uint8)
         starts = np.empty(D + 2 * n, np.int64)
@@ -450,7 +450,7 @@ def test_grouped_batch_errors_and_pageable_staging(cwq):
             cat[3].data_ptr(), 1, 8, seeds.ctypes.data, 1.0, group_size_threshold(12),
             8 * np.log(2) - 1, sample.ctypes.data, bits.ctypes.data, bits_cap,
             bits_off.ctypes.data, starts.ctypes.data, starts.size, n_starts.ctypes.data,
-            ws.data_ptr(), ws.numel(), host_ws, host_bytes, None,
+            ws.data_ptr(), ws.numel(), host_ws, host_bytes, opts,
             torch.cuda.current_stream().cuda_stream)
         return rc, sample, bits[:bits_off[-1]].tobytes() if rc >= 0 else b"", starts, n_starts
     rc, s1, b1, st1, n1 = call((D + n) * 8, hws.data_ptr(), hneed)
@@ -462,6 +462,39 @@ def test_grouped_batch_errors_and_pageable_staging(cwq):
     assert rc3 == -3 and b"host workspace" in lib.cwq_last_error()
     rc4 = call(100, hws.data_ptr(), hneed)[0]  # bits buffer far too small
     assert rc4 == -4 and b"bits_cap" in lib.cwq_last_error()
+    # item_ready: every flag raised on success (results unchanged), not all on an error
+    ready = np.zeros(n, np.int32)
+    rc5, s5, b5, _, _ = call((D + n) * 8, hws.data_ptr(), hneed,
+                             _lib.options(item_ready=ready.ctypes.data))
+    assert rc5 == rc and b5 == b1 and np.array_equal(s5.view(np.uint32), s1.view(np.uint32))
+    assert ready.tolist() == [1] * n
+    ready[:] = 0
+    assert call(100, hws.data_ptr(), hneed, _lib.options(item_ready=ready.ctypes.data))[0] == -4
+    assert ready.sum() < n
     torch.cuda.synchronize()
-    rc5, s5, b5, _, _ = call((D + n) * 8, hws.data_ptr(), hneed)  # the library still works
-    assert rc5 == rc and b5 == b1
+    rc6, s6, b6, _, _ = call((D + n) * 8, hws.data_ptr(), hneed)  # the library still works
+    assert rc6 == rc and b6 == b1
+
+
+def test_grouped_batch_wrapper_raises_from_helper_thread(cwq):
+    """code_grouped_greedy_sample_batch runs the native call on a helper thread
+    for several items: a failing call still raises CwqError with the library's
+    message (read on the thread that made the call), and the next call works."""
+    from compression_without_quantization_amd import _lib
+    rng = np.random.default_rng(3)
+    items = []
+    for D in (3000, 2000):
+        pl = (0.1 * rng.standard_normal(D)).astype(np.float32)
+        ps = rng.uniform(0.8, 1.2, D).astype(np.float32)
+        ql = (pl + 0.5 * ps * rng.standard_normal(D)).astype(np.float32)
+        qs = (ps * rng.uniform(0.3, 1.0, D)).astype(np.float32)
+        items.append((cwq.Normal(torch.from_numpy(ql).cuda(), torch.from_numpy(qs).cuda()),
+                      cwq.Normal(torch.from_numpy(pl).cuda(), torch.from_numpy(ps).cuda())))
+    tg, pr = [t for t, _ in items], [p for _, p in items]
+    with pytest.raises(_lib.CwqError, match="prune_mode"):
+        cwq.code_grouped_greedy_sample_batch(None, tg, pr, 1, 8, 5, prune_mode=7)
+    out = cwq.code_grouped_greedy_sample_batch(None, tg, pr, 1, 8, 5)
+    for (t, p), (sample, bitcode, starts) in zip(items, out):
+        s1, b1, st1 = cwq.code_grouped_greedy_sample(None, t, p, 1, 8, 5)
+        assert bitcode == b1 and list(starts) == list(st1)
+        assert np.array_equal(sample.view(np.uint32), np.asarray(s1).view(np.uint32))

@@ -43,3 +43,6 @@ dstr, _ = tm(lambda: [str(mv[off[i]:off[i + 1]], 'ascii') for i in range(48)])
 dstr2, _ = tm(lambda: [buf[off[i]:off[i + 1]].tobytes().decode('ascii') for i in range(48)])
 print(f"dist_parts {dparts:.3f} ms, cat {dcat:.3f} ms, pinned allocs {dpin:.3f} ms, "
       f"str(memoryview) {dstr:.3f} ms, tobytes+decode {dstr2:.3f} ms")
+dcall, _ = tm(lambda: S.code_grouped_greedy_sample_batch(None, [t for t, _ in lat], [p for _, p in lat],
+                                                         1, 8, 1, max_group_size_bits=4), n=30)
+print(f"whole call {dcall:.3f} ms")
