@@ -99,6 +99,7 @@ SIGNATURES = {
     "cwq_ac_decode": (c_i64, [c_vp, c_i64, c_int, c_vp, c_i64, c_vp, c_i64]),
     "cwq_elias_delta_encode": (c_i64, [c_vp, c_i64, c_vp, c_i64]),
     "cwq_elias_delta_decode": (c_i64, [c_vp, c_i64, c_i64, c_vp]),
+    "cwq_bitcode_to_indices": (c_i64, [c_vp, c_i64, c_int, c_i64, c_vp]),
     "cwq_selftest_bm_tables": (c_int, [ctypes.c_uint32, c_i64, c_vp, c_vp, c_vp, c_vp]),
     "cwq_selftest_screen_tables": (c_int, [ctypes.c_uint32, c_i64, c_vp, c_vp, c_vp, c_vp]),
     "cwq_selftest_logf": (c_int, [c_vp, c_i64, c_vp, c_vp]),

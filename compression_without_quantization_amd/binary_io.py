@@ -51,16 +51,23 @@ def indices_to_bitcode(indices, num_bits):
     return bits.tobytes().decode('ascii')
 
 
-def bitcode_to_indices(bitcode, num_bits, count):
-    """Inverse of indices_to_bitcode for ``count`` indices.
+def bitcode_to_indices(bitcode, num_bits, count, dtype=np.int64):
+    """Inverse of indices_to_bitcode for ``count`` indices (as ``dtype``).
 
     Missing trailing characters read as '0' (``from_bit_string`` of a short
-    substring, as tf.strings.substr yields at the end of the string).
+    substring, as tf.strings.substr yields at the end of the string).  Widths
+    up to 30 bits (CWQ_MAX_BITS_PER_STEP) are parsed by one native pass
+    (cwq_bitcode_to_indices).
     """
-    if isinstance(bitcode, bytes):
-        raw = np.frombuffer(bitcode, dtype=np.uint8)
-    else:
-        raw = np.frombuffer(bitcode.encode('ascii'), dtype=np.uint8)
+    raw_b = bitcode if isinstance(bitcode, bytes) else bitcode.encode('ascii')
+    count, num_bits = int(count), int(num_bits)
+    if 0 <= num_bits <= 30 and count >= 0:
+        from . import _lib
+        out = np.empty(count, dtype=np.int32)
+        _lib.check(_lib.load().cwq_bitcode_to_indices(raw_b, len(raw_b), num_bits, count,
+                                                      out.ctypes.data), "bitcode parse")
+        return out if dtype == np.int32 else out.astype(dtype)
+    raw = np.frombuffer(raw_b, dtype=np.uint8)
     need = count * num_bits
     bits = np.zeros(need, dtype=np.int64)
     m = min(need, raw.size)
@@ -69,7 +76,7 @@ def bitcode_to_indices(bitcode, num_bits, count):
         return np.zeros(count, dtype=np.int64)
     bits = bits.reshape(count, num_bits)
     weights = (np.int64(1) << np.arange(num_bits, dtype=np.int64))
-    return (bits * weights[None, :]).sum(axis=1)
+    return (bits * weights[None, :]).sum(axis=1).astype(dtype)
 
 
 def elias_delta_code(x):

@@ -24,6 +24,7 @@ Differences from the TF1 reference (deliberate, documented in DESIGN.md):
 
 All arithmetic runs in libcwq.so; nothing here computes samples on the CPU.
 """
+import array
 import concurrent.futures
 import ctypes
 import threading
@@ -539,6 +540,17 @@ def _scratch_bytes(n):
     return buf
 
 
+def _int64_array(x):
+    """A flat np.int64 copy of ``x``; a Python list of ints (the encoder's
+    group_start_indices) goes through array.array, ~2x faster than np.asarray."""
+    if isinstance(x, list):
+        try:
+            return np.frombuffer(array.array('q', x), dtype=np.int64)
+        except (TypeError, OverflowError):
+            pass
+    return np.asarray(x, dtype=np.int64).reshape(-1)
+
+
 def decode_grouped_greedy_sample(sess, bitcode, group_start_indices, proposal, n_bits_per_step,
                                  n_steps, seed, adaptive=True, rho=1.):
     """coded_greedy_sampler.py:299-364.  Returns np.float32 [D]."""
@@ -549,18 +561,18 @@ def decode_grouped_greedy_sample(sess, bitcode, group_start_indices, proposal, n
     p_loc, p_scale = _dist_parts(proposal, dev, "Proposal")
     D = p_loc.numel()
     n_bits_per_group = n_bits_per_step * n_steps
-    starts = np.append(np.asarray(group_start_indices, dtype=np.int64).reshape(-1), D)  # :323
+    starts = np.append(_int64_array(group_start_indices), D)  # :323
     n_listed = len(starts) - 1
     # :345-347 decode group i while its bit slice is non-empty
     n_avail = -(-len(bitcode) // n_bits_per_group) if n_bits_per_group else n_listed
     G = min(n_listed, n_avail)
-    idx = bitcode_to_indices(bitcode, int(n_bits_per_step), G * int(n_steps))
+    idx = bitcode_to_indices(bitcode, int(n_bits_per_step), G * int(n_steps), dtype=np.int32)
     offs = np.asarray(starts[:G + 1], dtype=np.int64)
     if G == 0 or offs[-1] != D:
         raise ValueError(f"decoded groups cover {int(offs[-1]) if G else 0} of {D} dims")
     zeros = torch.zeros(D, dtype=torch.float32, device=dev)
     ones = torch.ones(D, dtype=torch.float32, device=dev)
-    sample = decode_blocks(idx.astype(np.int32), zeros, ones, n_bits_per_step, n_steps, seed,
+    sample = decode_blocks(idx, zeros, ones, n_bits_per_step, n_steps, seed,
                            rho=rho, block_off=offs)
     out = torch.empty(D, dtype=torch.float32, device=dev)
     with torch.cuda.device(dev):

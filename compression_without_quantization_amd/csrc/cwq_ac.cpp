@@ -16,8 +16,11 @@
 // (width*C[j]) // R <= z - low, which is what the linear decoder (:162-181)
 // finds as well.  Products are formed in 128-bit integers, so no count
 // total can overflow (the reference's int64 arithmetic would for R > 2^31).
+// The bit-string codecs of binary_io.py (Elias-delta, the greedy coder's
+// fixed-width index parse) sit here too: host-side, serial byte work.
 #include <stdint.h>
 #include <stddef.h>
+#include <string.h>
 
 #include <vector>
 
@@ -229,6 +232,42 @@ int64_t cwq_elias_delta_decode(const char* bits, int64_t nbits, int64_t count, i
   }
   cwq::set_error(CWQ_OK, "");
   return pos;
+}
+
+int64_t cwq_bitcode_to_indices(const char* bits, int64_t nbits, int num_bits, int64_t count,
+                               int32_t* out) {
+  if (nbits < 0 || count < 0 || num_bits < 0 || num_bits > CWQ_MAX_BITS_PER_STEP ||
+      (nbits > 0 && !bits) || (count > 0 && !out) || count > (INT64_MAX >> 5))
+    return cwq::set_error(CWQ_ERR_INVALID, "cwq_bitcode_to_indices: bad arguments");
+  const int64_t need = count * num_bits;
+  const int64_t m = nbits < need ? nbits : need;  // chars past the string read as '0'
+  // the chars as a packed LSB-first bit stream (8 spare zero bytes for the
+  // 64-bit field reads below), 8 chars per step: a byte of x ^ "11111111" is
+  // zero iff its char is '1'; folding each byte's complement onto its bit 0
+  // and gathering those bits with one multiply gives the 8 flags in order
+  thread_local std::vector<uint8_t> packed;
+  packed.assign((size_t)((need + 7) >> 3) + 8, 0);
+  int64_t k = 0;
+  for (; k + 8 <= m; k += 8) {
+    uint64_t x;
+    memcpy(&x, bits + k, 8);
+    uint64_t y = ~(x ^ 0x3131313131313131ull);
+    y &= y >> 4;
+    y &= y >> 2;
+    y &= y >> 1;
+    packed[(size_t)(k >> 3)] = (uint8_t)(((y & 0x0101010101010101ull) * 0x0102040810204080ull) >> 56);
+  }
+  for (; k < m; ++k)
+    if (bits[k] == '1') packed[(size_t)(k >> 3)] |= (uint8_t)(1u << (k & 7));
+  const uint64_t mask = (1ull << num_bits) - 1;
+  for (int64_t i = 0; i < count; ++i) {
+    const int64_t off = i * num_bits;
+    uint64_t w;
+    memcpy(&w, packed.data() + (off >> 3), 8);
+    out[i] = (int32_t)((w >> (off & 7)) & mask);
+  }
+  cwq::set_error(CWQ_OK, "");
+  return count;
 }
 
 }  // extern "C"

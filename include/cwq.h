@@ -359,6 +359,16 @@ int64_t cwq_ac_decode(const int64_t* counts, int64_t K, int precision, const cha
 int64_t cwq_elias_delta_encode(const int64_t* x, int64_t n, char* out, int64_t cap);
 int64_t cwq_elias_delta_decode(const char* bits, int64_t nbits, int64_t count, int64_t* out);
 
+/* The greedy coder's bit parse (code/coded_greedy_sampler.py:107-126 and
+ * :330-342, binary_io.py:55-67 from_bit_string of each num_bits substring):
+ * count indices of num_bits LSB-first chars each from bits[0..nbits) into
+ * out.  Chars past nbits read as '0' (the short substring tf.strings.substr
+ * yields at the end of the string); any char other than '1' reads as 0.  Host
+ * memory.  Returns count, or CWQ_ERR_INVALID (num_bits outside
+ * [0, CWQ_MAX_BITS_PER_STEP], negative sizes, null pointers). */
+int64_t cwq_bitcode_to_indices(const char* bits, int64_t nbits, int num_bits, int64_t count,
+                               int32_t* out);
+
 /* Diagnostics (used by the parity tests): evaluate the device restatement of
  * the Box-Muller transcendentals for the 23-bit mantissas m0 .. m0+count-1:
  *   radius[i] = sqrtf(-2 logf(max(m*2^-23, 1e-7f)))    (BoxMullerFloat u2)

@@ -134,6 +134,26 @@ def test_bitcode_vectorised_matches_scalar():
     assert list(B.bitcode_to_indices("1011", 3, 2)) == [5, 1]
 
 
+def test_bitcode_parse_native_matches_scalar():
+    """cwq_bitcode_to_indices (the native parse behind bitcode_to_indices for
+    widths <= 30) against from_bit_string of each LSB-first slice, on every
+    width, truncated strings (missing chars read '0') and chars other than '1'."""
+    rng = np.random.default_rng(1)
+    for nbits in range(0, 31):
+        for count in (0, 1, 7, 64, 129):
+            idx = rng.integers(0, 1 << nbits, size=count) if nbits else np.zeros(count, np.int64)
+            code = B.indices_to_bitcode(idx, nbits)
+            for cut in sorted({len(code), max(len(code) - 5, 0), len(code) // 3}):
+                s = code[:cut]
+                want = [B.from_bit_string(s[i * nbits:(i + 1) * nbits]) for i in range(count)]
+                got = B.bitcode_to_indices(s, nbits, count)
+                assert got.dtype == np.int64 and list(got) == want, (nbits, count, cut)
+                assert list(B.bitcode_to_indices(s.encode(), nbits, count, dtype=np.int32)) == want
+    assert list(B.bitcode_to_indices("1x21" * 3, 2, 6)) == [1, 2, 1, 2, 1, 2]
+    with pytest.raises(Exception):
+        B.bitcode_to_indices("0101", 3, -1)
+
+
 def _eigen_sum_py(x):
     x = np.asarray(x, np.float32)
     d = x.size
