@@ -9,6 +9,7 @@ import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import compression_without_quantization_amd as C  # noqa: E402
+import compression_without_quantization_amd.coded_greedy_sampler as S  # noqa: E402
 from compression_without_quantization_amd.binary_io import bitcode_to_indices  # noqa: E402
 from compression_without_quantization_amd.synthetic import make_latents  # noqa: E402
 
@@ -33,6 +34,6 @@ def tm(f, n=50):
 d_all, dec = tm(lambda: C.decode_grouped_greedy_sample(None, bitcode, starts, p, 8, 1, 42))
 assert np.array_equal(dec.view(np.uint32), np.asarray(sample).view(np.uint32))
 d_bits, _ = tm(lambda: bitcode_to_indices(bitcode, 8, len(starts)))
-d_arr, _ = tm(lambda: np.asarray(starts, dtype=np.int64))
+d_arr, _ = tm(lambda: S._int64_array(starts))
 print(f"groups {len(starts)}: decode_grouped_greedy_sample {d_all:.3f} ms "
       f"(bitcode_to_indices {d_bits:.3f} ms, starts list -> array {d_arr:.3f} ms)")
