@@ -1660,75 +1660,117 @@ __global__ void __launch_bounds__(256) k_small_screen(
     const float bf = bg[0];
     const PhiloxStream st{f2u(bg[1]), f2u(bg[2]), f2u(bg[3]), f2u(bg[4])};
     const float2* ab = sab + off + 8 * g + 4;
-    float tau = unord_f32(__hip_atomic_load(&gtau[g * CWQ_CSR_GTAU_STRIDE], __ATOMIC_RELAXED,
-                                            __HIP_MEMORY_SCOPE_AGENT));
+    // A block that is one tile (C2/C3's 256 candidates) belongs to this wave
+    // alone: its threshold starts at k_small_prep's -inf and its slot count
+    // lives in a scalar, both stored once at the end -- no global atomics.
+    const bool own = tiles_per_block == 1;
+    float tau = own ? -__builtin_inff()
+                    : unord_f32(__hip_atomic_load(&gtau[g * CWQ_CSR_GTAU_STRIDE],
+                                                  __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    uint32_t used = 0;  // own block: slots taken so far (wave-uniform)
     // lane span m: rows n0 + 4 (lane + 64 m) + q, q = 0..3.  n0 is a multiple
     // of 4 (tiles are multiples of 256 candidates), so a span's 4d words are
     // exactly Philox blocks [n d / 4, n d / 4 + d): every block is computed
     // once (a row alone would start and end inside blocks its neighbours also
     // compute), and the dim index of each word is the same in every lane, so
     // the per-dim constants are wave-uniform loads.
-    for (int64_t m0 = 0; n0 + 256 * m0 < n1; ++m0) {
-      const int64_t ns = n0 + 4 * ((int64_t)lane + 64 * m0);
-      const uint64_t b0 = (uint64_t)ns * (uint64_t)d / 4u;
-      float rs0 = 0.0f, rs1 = 0.0f, rs2 = 0.0f, rs3 = 0.0f;  // the span's four row sums
-      float cur = 0.0f;  // natural order, sequential sum (h = d), as k_small_prep's bound
-      int j = 0, q = 0;
-      for (int b = 0; b < d; ++b) {
-        const uint64_t blk = b0 + (uint64_t)b;
-        const U4 x = philox10_dev((uint32_t)blk, (uint32_t)(blk >> 32), st.c2, st.c3, st.k0,
-                                  st.k1);
-        float z[4];
-        box_muller_screen(x.x, x.y, z[0], z[1]);
-        box_muller_screen(x.z, x.w, z[2], z[3]);
+    auto spans = [&](auto lo_tag) {
+      constexpr bool LO = decltype(lo_tag)::value;  // every Philox block index < 2^32
+      const PhiloxLo K = philox_lo_key(st);
+      for (int64_t m0 = 0; n0 + 256 * m0 < n1; ++m0) {
+        const int64_t ns = n0 + 4 * ((int64_t)lane + 64 * m0);
+        const uint64_t b0 = (uint64_t)ns * (uint64_t)d / 4u;
+        float rs[4] = {0.0f, 0.0f, 0.0f, 0.0f};  // the span's four row sums
+        float cur = 0.0f;  // natural order, sequential sum (h = d), as k_small_prep's bound
+        int j = 0, q = 0;
+        for (int b = 0; b < d; ++b) {
+          const uint64_t blk = b0 + (uint64_t)b;
+          const U4 x = LO ? philox10_lo((uint32_t)blk, K, st.k0, st.k1)
+                          : philox10_dev((uint32_t)blk, (uint32_t)(blk >> 32), st.c2, st.c3,
+                                         st.k0, st.k1);
+          float z[4];
+          box_muller_screen(x.x, x.y, z[0], z[1]);
+          box_muller_screen(x.z, x.w, z[2], z[3]);
 #pragma unroll
-        for (int t = 0; t < 4; ++t) {
-          const float2 e = ab[j];
-          const float a = __builtin_fmaf(e.x, z[t], e.y);
-          cur = __builtin_fmaf(-a, a, cur);
-          if (++j == d) {  // wave-uniform: a row of the span is complete
-            if (q == 0) rs0 = cur;
-            else if (q == 1) rs1 = cur;
-            else if (q == 2) rs2 = cur;
-            else rs3 = cur;
-            cur = 0.0f;
-            j = 0;
-            ++q;
+          for (int t = 0; t < 4; ++t) {
+            const float2 e = ab[j];
+            const float a = __builtin_fmaf(e.x, z[t], e.y);
+            cur = __builtin_fmaf(-a, a, cur);
+            if (++j == d) {  // wave-uniform: a row of the span is complete
+              if (q == 0) rs[0] = cur;
+              else if (q == 1) rs[1] = cur;
+              else if (q == 2) rs[2] = cur;
+              else rs[3] = cur;
+              cur = 0.0f;
+              j = 0;
+              ++q;
+            }
           }
         }
-      }
+        // tau from the lane's best valid row: the lower bound is monotone in
+        // the screened value, and any row's lower bound is a valid threshold,
+        // so one wave max per span replaces one per row
+        float smax = -__builtin_inff();
+        bool any = false;
 #pragma unroll
-      for (int qq = 0; qq < 4; ++qq) {
-        const float sv = qq == 0 ? rs0 : (qq == 1 ? rs1 : (qq == 2 ? rs2 : rs3));
-        const int64_t n = ns + qq;
-        const bool valid = n < n1;
-        const float upper = __builtin_fmaf(sv, gc.x, bf);
-        const float lower = valid ? __builtin_fmaf(sv, gc.y, gc.z) -
-                                        gc.w * __builtin_amdgcn_sqrtf(-sv)
-                                  : -__builtin_inff();
+        for (int qq = 0; qq < 4; ++qq)
+          if (ns + qq < n1) {
+            smax = fmaxf(smax, rs[qq]);
+            any = true;
+          }
+        const float lower = any ? __builtin_fmaf(smax, gc.y, gc.z) -
+                                      gc.w * __builtin_amdgcn_sqrtf(-smax)
+                                : -__builtin_inff();
         tau = fmaxf(tau, wave_max_f32(lower));
-        const bool push = valid && upper >= tau;
-        const uint64_t m = __ballot(push);
-        if (m) {
-          const uint32_t cnt = (uint32_t)__builtin_popcountll(m);
-          // the block's own slots (a global counter serialised every wave)
-          uint32_t base = 0;
-          if (lane == 0) base = atomicAdd(&scnt[off + 12 * g], cnt);
-          base = (uint32_t)__shfl((int)base, 0, 64);
-          const uint32_t rank = __builtin_amdgcn_mbcnt_hi(
-              (uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-          if (push) {
-            const uint32_t slot = base + rank;
-            if (slot < CWQ_SLIST_PER_BLOCK)
-              slist[CWQ_SLIST_PER_BLOCK * g + slot] = uint2{(uint32_t)n, f2u(upper)};
+        uint64_t m[4];
+        uint32_t cnt = 0;
+#pragma unroll
+        for (int qq = 0; qq < 4; ++qq) {
+          m[qq] = __ballot(ns + qq < n1 && __builtin_fmaf(rs[qq], gc.x, bf) >= tau);
+          cnt += (uint32_t)__builtin_popcountll(m[qq]);
+        }
+        if (cnt) {
+          // the block's slots: this wave's scalar count, or a global counter
+          // shared with the block's other tiles
+          uint32_t base = used;
+          if (own) {
+            used += cnt;
+          } else {
+            if (lane == 0) base = atomicAdd(&scnt[off + 12 * g], cnt);
+            base = (uint32_t)__shfl((int)base, 0, 64);
+          }
+          uint32_t pre = base;
+#pragma unroll
+          for (int qq = 0; qq < 4; ++qq) {
+            const uint64_t mq = m[qq];
+            if ((mq >> lane) & 1ull) {
+              const uint32_t slot = pre + __builtin_amdgcn_mbcnt_hi(
+                                              (uint32_t)(mq >> 32),
+                                              __builtin_amdgcn_mbcnt_lo((uint32_t)mq, 0u));
+              if (slot < CWQ_SLIST_PER_BLOCK)
+                slist[CWQ_SLIST_PER_BLOCK * g + slot] =
+                    uint2{(uint32_t)(ns + qq), f2u(__builtin_fmaf(rs[qq], gc.x, bf))};
+            }
+            pre += (uint32_t)__builtin_popcountll(mq);
           }
           if (base + cnt > CWQ_SLIST_PER_BLOCK && lane == 0)  // slots full: score the block exactly
             __hip_atomic_store(reinterpret_cast<uint32_t*>(&grp[g].x), 0u, __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_AGENT);
         }
       }
+    };
+    if ((uint64_t)(n1 + 4) * (uint64_t)d / 4u + (uint64_t)d <= 0xffffffffull)
+      spans(std::true_type{});
+    else
+      spans(std::false_type{});
+    if (lane == 0) {
+      if (own) {
+        scnt[off + 12 * g] = used;
+        gtau[g * CWQ_CSR_GTAU_STRIDE] = ord_f32(tau);
+      } else {
+        atomicMax(&gtau[g * CWQ_CSR_GTAU_STRIDE], ord_f32(tau));
+      }
     }
-    if (lane == 0) atomicMax(&gtau[g * CWQ_CSR_GTAU_STRIDE], ord_f32(tau));
   }
 }
 
