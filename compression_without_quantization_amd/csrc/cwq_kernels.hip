@@ -1543,6 +1543,9 @@ __global__ void __launch_bounds__(256, COOP ? CWQ_CSR_COOP_MIN_WAVES : CWQ_CSR_R
 // hardware transcendentals); survivors are ~1 per block, so the step costs
 // about a third of scoring every candidate exactly.
 // ---------------------------------------------------------------------------
+#ifndef CWQ_SMALL_SCREEN_WAVES
+#define CWQ_SMALL_SCREEN_WAVES 8  // waves/SIMD k_small_screen's registers must allow
+#endif
 #ifndef CWQ_SMALL_MIN_CAND
 #define CWQ_SMALL_MIN_CAND 64  // fewer candidates: the exact kernel (screening would not pay)
 #endif
@@ -1552,6 +1555,28 @@ __global__ void __launch_bounds__(256, COOP ? CWQ_CSR_COOP_MIN_WAVES : CWQ_CSR_R
 // with the whole wave, lanes over dims.  The block's stream key for this step
 // (a Philox-10 call) is stored too, so the screening rows do not repeat it.
 constexpr int64_t kSmallLaneD = 32;
+// Per-block header of the small path, 12 words at bpre + 12 g (bpre holds
+// total_dims + 12 nb words; a forked part's bpre moves by 12 g0): [0] the
+// full-row bound B, [1..4] the step's stream key, [5..8] grp's (c1, c2, As, Pq),
+// [9..10] the block's dim offset, [11] its dims.  The slot count is at
+// scnt[12 g].
+constexpr int64_t kSmallHdr = 12;
+struct SmallHdr {
+  float bf;
+  PhiloxStream st;
+  float4 gc;
+  int64_t off;
+  int d;
+};
+__device__ __forceinline__ SmallHdr small_hdr(const float4 h0, const float4 h1, const float4 h2) {
+  SmallHdr h;
+  h.bf = h0.x;
+  h.st = PhiloxStream{f2u(h0.y), f2u(h0.z), f2u(h0.w), f2u(h1.x)};
+  h.gc = float4{h1.y, h1.z, h1.w, h2.x};
+  h.off = (int64_t)(((uint64_t)f2u(h2.z) << 32) | (uint64_t)f2u(h2.y));
+  h.d = (int)f2u(h2.w);
+  return h;
+}
 
 template <bool STEP0>
 __global__ void __launch_bounds__(256) k_small_prep(
@@ -1594,15 +1619,16 @@ __global__ void __launch_bounds__(256) k_small_prep(
     const float pq = round_up_f32(2.01 * u.mx * __builtin_sqrt((double)(d > 0 ? d : 1)) *
                                   (1.0 + 0x1p-11));
     const bool fin = as - as == 0.0f && pq - pq == 0.0f && bf - bf == 0.0f;
-    grp[g] = (u.ok && fin && d > 0) ? float4{c1, c2, as, pq} : float4{0.f, 0.f, 0.f, 0.f};
-    float* bg = bpre + off + 12 * g;  // [0] the full-row bound, [1..4] the stream key
-    bg[0] = bf;
+    const float4 gc = (u.ok && fin && d > 0) ? float4{c1, c2, as, pq} : float4{0.f, 0.f, 0.f, 0.f};
+    grp[g] = gc;
+    // the block's header (kSmallHdr), indexed by g alone: the screen reads it
+    // with one load level and prefetches the next tile's
     const PhiloxStream st = generate_key(step_seed(sd.of(g), step), 42);
-    bg[1] = u2f(st.k0);
-    bg[2] = u2f(st.k1);
-    bg[3] = u2f(st.c2);
-    bg[4] = u2f(st.c3);
-    scnt[off + 12 * g] = 0u;
+    float4* hg = reinterpret_cast<float4*>(bpre + kSmallHdr * g);
+    hg[0] = float4{bf, u2f(st.k0), u2f(st.k1), u2f(st.c2)};
+    hg[1] = float4{u2f(st.c3), gc.x, gc.y, gc.z};
+    hg[2] = float4{gc.w, u2f((uint32_t)off), u2f((uint32_t)((uint64_t)off >> 32)), u2f((uint32_t)d)};
+    scnt[kSmallHdr * g] = 0u;
     gtau[g * CWQ_CSR_GTAU_STRIDE] = ord_f32(-__builtin_inff());
   };
   for (int64_t gb = ((int64_t)blockIdx.x * 4 + wave_id()) * 64; gb < nb; gb += nwaves * 64) {
@@ -1637,28 +1663,33 @@ __global__ void __launch_bounds__(256) k_small_prep(
 }
 
 template <bool STEP0>
-__global__ void __launch_bounds__(256) k_small_screen(
+__global__ void __launch_bounds__(256, CWQ_SMALL_SCREEN_WAVES) k_small_screen(
     const int64_t* __restrict__ block_off, int64_t ud, int64_t ntiles, int64_t tiles_per_block,
     int64_t cand_per_tile, int64_t n_cand, SeedSpec sd, int32_t step,
     const float2* __restrict__ sab, const float* __restrict__ bpre, float4* __restrict__ grp,
     uint32_t* __restrict__ gtau, uint32_t* __restrict__ scnt, uint2* __restrict__ slist) {
-  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t lane0 = threadIdx.x & 63u;
   const int64_t nwaves = (int64_t)gridDim.x * 4;
-  // a wave takes a whole tile (the block's loads, key and threshold once per
-  // tile), 256 rows per round
+  // a wave takes a whole tile (the block's header, key and threshold once per
+  // tile), 256 rows per round.  The header (k_small_prep) is one load level.
   for (int64_t tile = (int64_t)blockIdx.x * 4 + wave_id(); tile < ntiles; tile += nwaves) {
+    // the lane index behind an opaque move: the many span variants' lane-derived
+    // values are then computed per tile instead of hoisted out of the tile loop
+    // (and spilled)
+    uint32_t lane = lane0;
+    asm volatile("" : "+v"(lane));
     const int64_t g = tiles_per_block == 1 ? tile : tile / tiles_per_block;
     const int64_t tt = tile - g * tiles_per_block;
-    const float4 gc = grp[g];
+    const float4* hp = reinterpret_cast<const float4*>(bpre + kSmallHdr * g);
+    const SmallHdr h = small_hdr(hp[0], hp[1], hp[2]);
+    const float4 gc = h.gc;
     if (gc.x == 0.0f) continue;  // scored exactly by k_small_survivors
-    const BlockSpan sp = block_span(block_off, ud, g);
-    const int64_t off = sp.off;
-    const int d = (int)sp.d;
+    const int64_t off = h.off;
+    const int d = h.d;
     const int64_t n0 = tt * cand_per_tile;
     const int64_t n1 = (n0 + cand_per_tile < n_cand) ? n0 + cand_per_tile : n_cand;
-    const float* bg = bpre + off + 12 * g;  // k_small_prep: bound, then the stream key
-    const float bf = bg[0];
-    const PhiloxStream st{f2u(bg[1]), f2u(bg[2]), f2u(bg[3]), f2u(bg[4])};
+    const float bf = h.bf;
+    const PhiloxStream st = h.st;
     const float2* ab = sab + off + 8 * g + 4;
     // A block that is one tile (C2/C3's 256 candidates) belongs to this wave
     // alone: its threshold starts at k_small_prep's -inf and its slot count
@@ -1674,9 +1705,68 @@ __global__ void __launch_bounds__(256) k_small_screen(
     // once (a row alone would start and end inside blocks its neighbours also
     // compute), and the dim index of each word is the same in every lane, so
     // the per-dim constants are wave-uniform loads.
-    auto spans = [&](auto lo_tag) {
+    const PhiloxLo K = philox_lo_key(st);
+    // tau, survivor slots of one span's four rows (rs: their screened values)
+    auto span_tail = [&](int64_t ns, const float (&rs)[4]) __attribute__((always_inline)) {
+      // tau from the lane's best valid row: the lower bound is monotone in
+      // the screened value, and any row's lower bound is a valid threshold,
+      // so one wave max per span replaces one per row
+      float smax = -__builtin_inff();
+      bool any = false;
+#pragma unroll
+      for (int qq = 0; qq < 4; ++qq)
+        if (ns + qq < n1) {
+          smax = fmaxf(smax, rs[qq]);
+          any = true;
+        }
+      const float lower = any ? __builtin_fmaf(smax, gc.y, gc.z) -
+                                    gc.w * __builtin_amdgcn_sqrtf(-smax)
+                              : -__builtin_inff();
+      tau = fmaxf(tau, wave_max_f32(lower));
+      uint64_t m[4];
+      uint32_t cnt = 0;
+#pragma unroll
+      for (int qq = 0; qq < 4; ++qq) {
+        m[qq] = __ballot(ns + qq < n1 && __builtin_fmaf(rs[qq], gc.x, bf) >= tau);
+        cnt += (uint32_t)__builtin_popcountll(m[qq]);
+      }
+      if (cnt) {
+        // the block's slots: this wave's scalar count, or a global counter
+        // shared with the block's other tiles
+        uint32_t base = used;
+        if (own) {
+          used += cnt;
+        } else {
+          if (lane == 0) base = atomicAdd(&scnt[kSmallHdr * g], cnt);
+          base = (uint32_t)__shfl((int)base, 0, 64);
+        }
+        uint32_t pre = base;
+#pragma unroll
+        for (int qq = 0; qq < 4; ++qq) {
+          const uint64_t mq = m[qq];
+          if ((mq >> lane) & 1ull) {
+            const uint32_t slot = pre + __builtin_amdgcn_mbcnt_hi(
+                                            (uint32_t)(mq >> 32),
+                                            __builtin_amdgcn_mbcnt_lo((uint32_t)mq, 0u));
+            if (slot < CWQ_SLIST_PER_BLOCK)
+              slist[CWQ_SLIST_PER_BLOCK * g + slot] =
+                  uint2{(uint32_t)(ns + qq), f2u(__builtin_fmaf(rs[qq], gc.x, bf))};
+          }
+          pre += (uint32_t)__builtin_popcountll(mq);
+        }
+        if (base + cnt > CWQ_SLIST_PER_BLOCK && lane == 0)  // slots full: score the block exactly
+          __hip_atomic_store(reinterpret_cast<uint32_t*>(&grp[g].x), 0u, __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+      }
+    };
+    // lane span m: rows n0 + 4 (lane + 64 m) + q, q = 0..3.  n0 is a multiple
+    // of 4 (tiles are multiples of 256 candidates), so a span's 4d words are
+    // exactly Philox blocks [n d / 4, n d / 4 + d): every block is computed
+    // once (a row alone would start and end inside blocks its neighbours also
+    // compute), and the dim index of each word is the same in every lane, so
+    // the per-dim constants are wave-uniform loads.
+    auto spans = [&](auto lo_tag) __attribute__((always_inline)) {
       constexpr bool LO = decltype(lo_tag)::value;  // every Philox block index < 2^32
-      const PhiloxLo K = philox_lo_key(st);
       for (int64_t m0 = 0; n0 + 256 * m0 < n1; ++m0) {
         const int64_t ns = n0 + 4 * ((int64_t)lane + 64 * m0);
         const uint64_t b0 = (uint64_t)ns * (uint64_t)d / 4u;
@@ -1707,65 +1797,18 @@ __global__ void __launch_bounds__(256) k_small_screen(
             }
           }
         }
-        // tau from the lane's best valid row: the lower bound is monotone in
-        // the screened value, and any row's lower bound is a valid threshold,
-        // so one wave max per span replaces one per row
-        float smax = -__builtin_inff();
-        bool any = false;
-#pragma unroll
-        for (int qq = 0; qq < 4; ++qq)
-          if (ns + qq < n1) {
-            smax = fmaxf(smax, rs[qq]);
-            any = true;
-          }
-        const float lower = any ? __builtin_fmaf(smax, gc.y, gc.z) -
-                                      gc.w * __builtin_amdgcn_sqrtf(-smax)
-                                : -__builtin_inff();
-        tau = fmaxf(tau, wave_max_f32(lower));
-        uint64_t m[4];
-        uint32_t cnt = 0;
-#pragma unroll
-        for (int qq = 0; qq < 4; ++qq) {
-          m[qq] = __ballot(ns + qq < n1 && __builtin_fmaf(rs[qq], gc.x, bf) >= tau);
-          cnt += (uint32_t)__builtin_popcountll(m[qq]);
-        }
-        if (cnt) {
-          // the block's slots: this wave's scalar count, or a global counter
-          // shared with the block's other tiles
-          uint32_t base = used;
-          if (own) {
-            used += cnt;
-          } else {
-            if (lane == 0) base = atomicAdd(&scnt[off + 12 * g], cnt);
-            base = (uint32_t)__shfl((int)base, 0, 64);
-          }
-          uint32_t pre = base;
-#pragma unroll
-          for (int qq = 0; qq < 4; ++qq) {
-            const uint64_t mq = m[qq];
-            if ((mq >> lane) & 1ull) {
-              const uint32_t slot = pre + __builtin_amdgcn_mbcnt_hi(
-                                              (uint32_t)(mq >> 32),
-                                              __builtin_amdgcn_mbcnt_lo((uint32_t)mq, 0u));
-              if (slot < CWQ_SLIST_PER_BLOCK)
-                slist[CWQ_SLIST_PER_BLOCK * g + slot] =
-                    uint2{(uint32_t)(ns + qq), f2u(__builtin_fmaf(rs[qq], gc.x, bf))};
-            }
-            pre += (uint32_t)__builtin_popcountll(mq);
-          }
-          if (base + cnt > CWQ_SLIST_PER_BLOCK && lane == 0)  // slots full: score the block exactly
-            __hip_atomic_store(reinterpret_cast<uint32_t*>(&grp[g].x), 0u, __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
-        }
+        span_tail(ns, rs);
       }
     };
-    if ((uint64_t)(n1 + 4) * (uint64_t)d / 4u + (uint64_t)d <= 0xffffffffull)
+    const bool lo = (uint64_t)(n1 + 4) * (uint64_t)d / 4u + (uint64_t)d <= 0xffffffffull;
+    if (lo) {
       spans(std::true_type{});
-    else
+    } else {
       spans(std::false_type{});
+    }
     if (lane == 0) {
       if (own) {
-        scnt[off + 12 * g] = used;
+        scnt[kSmallHdr * g] = used;
         gtau[g * CWQ_CSR_GTAU_STRIDE] = ord_f32(tau);
       } else {
         atomicMax(&gtau[g * CWQ_CSR_GTAU_STRIDE], ord_f32(tau));
@@ -1796,7 +1839,7 @@ __global__ void __launch_bounds__(256) k_small_survivors(
   const int64_t nwaves = (int64_t)gridDim.x * 4;
   auto score = [&](int64_t g, uint32_t n) {
     const BlockSpan sp = block_span(block_off, ud, g);
-    const float* bg = bpre + sp.off + 12 * g;  // k_small_prep: the step's stream key
+    const float* bg = bpre + kSmallHdr * g;  // k_small_prep's header: the step's stream key
     const PhiloxStream st{f2u(bg[1]), f2u(bg[2]), f2u(bg[3]), f2u(bg[4])};
     const uint64_t k0 = (uint64_t)n * (uint64_t)sp.d;
     const float v = eval_row<0, STEP0>(st, k0, sp.d, (int)(k0 & 3u), loc_s + sp.off,
@@ -1809,8 +1852,7 @@ __global__ void __launch_bounds__(256) k_small_survivors(
     const int64_t g = gb + lane;
     uint32_t cnt = 0, keep = 0;  // listed slots; bit s: slot s survives
     if (g < nb && grp[g].x != 0.0f) {  // exact blocks are scored below
-      const BlockSpan sp = block_span(block_off, ud, g);
-      const uint32_t c = scnt[sp.off + 12 * g];
+      const uint32_t c = scnt[kSmallHdr * g];
       const uint32_t ns = c < CWQ_SLIST_PER_BLOCK ? c : CWQ_SLIST_PER_BLOCK;
       const float tau = unord_f32(gtau[g * CWQ_CSR_GTAU_STRIDE]);
       for (uint32_t sl = 0; sl < ns; ++sl)
@@ -1850,7 +1892,7 @@ __global__ void __launch_bounds__(256) k_small_survivors(
     for (uint64_t m = __ballot(g < nb && grp[g].x == 0.0f); m != 0ull; m &= m - 1ull) {
       const int64_t ge = gb + (int64_t)__builtin_ctzll(m);
       const BlockSpan sp = block_span(block_off, ud, ge);
-      const float* bg = bpre + sp.off + 12 * ge;
+      const float* bg = bpre + kSmallHdr * ge;
       const PhiloxStream st{f2u(bg[1]), f2u(bg[2]), f2u(bg[3]), f2u(bg[4])};
       uint64_t bestk = 0;
       for (int r = 0; r < 4; ++r) {  // rows n = r (mod 4): one alignment class per pass
