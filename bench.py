@@ -344,7 +344,10 @@ def grouped_cpu_baseline(args, lat_np, res0, bits, n_steps):
     parity = {"groups_checked": int(round(sum(st.size - 1 for *_, st in sets) * frac)),
               "index_mismatches": mi, "sample_word_mismatches": ms,
               "oracle": "oracle/cwq_oracle.c (CPU restatement; TF reference unpinned)",
-              "normaliser_sensitivity": normaliser_sensitivity("c2") if bits == 8 else None}
+              "normaliser_sensitivity": normaliser_sensitivity("c2") if bits == 8 else None,
+              # C3's level-1 sets are C2-shaped and its level-2 groups the same 8-bit coder
+              "semantics_sensitivity": semantics_sensitivity(
+                  {"c3": "c2"}.get(args.config, args.config))}
     return cpu, parity
 
 
@@ -558,6 +561,30 @@ def normaliser_sensitivity(section):
             "source": "profiles/normaliser_sensitivity.json (tools/normaliser_sensitivity.py, "
                       "CPU oracle; log sigma from Eigen plog / plog+FMA / logf +1 ulp / -1 ulp / "
                       "random +-1 ulp)"}
+
+
+def semantics_sensitivity(section):
+    """profiles/semantics_sensitivity.json's record for one workload: the
+    oracle scoring every candidate also under TFP >= 0.8's log-prob form and
+    five other Eigen sum orders (tools/semantics_sensitivity.py), i.e. how many
+    indices hang on the per-candidate declared semantics."""
+    f = os.path.join(REPO, "profiles", "semantics_sensitivity.json")
+    if not os.path.exists(f):
+        return None
+    with open(f) as fh:
+        r = json.load(fh).get(section)
+    if not r:
+        return None
+    flips = {v: x["index_flips"] for v, x in r["variants"].items()}
+    n = r["indices"]
+    return {"variants": len(flips), "indices_per_variant": n, "sample": r["sample"],
+            "max_flips": max(flips.values()), "flips": flips,
+            "flip_rate_95pct_upper": (3.0 / n if max(flips.values()) == 0 else None),
+            "model_flip_rate_max": r.get("max_model_flip_rate_over_variants"),
+            "best_second_gap_min": r["best_second_gap"]["min"],
+            "source": "profiles/semantics_sensitivity.json (tools/semantics_sensitivity.py, CPU "
+                      "oracle; TFP>=0.8 squared_difference log_prob x {Eigen AVX, SSE, AVX x2, "
+                      "AVX-512, sequential, tree} row sums)"}
 
 
 def rank_device_map(dist, rank, local_rank, dev):
@@ -905,7 +932,9 @@ def main():
                   "sample_word_mismatches": mism_smp,
                   "oracle": "oracle/cwq_oracle.c (CPU restatement; TF reference unpinned)",
                   "normaliser_sensitivity": (normaliser_sensitivity("c4")
-                                             if (d, bits, n_steps) == (32, 16, 1) else None)}
+                                             if (d, bits, n_steps) == (32, 16, 1) else None),
+                  "semantics_sensitivity": semantics_sensitivity(
+                      {(32, 16, 1): "c4", (16, 24, 1): "c5"}.get((d, bits, n_steps), ""))}
 
     if rank == 0:
         line = {

@@ -117,7 +117,7 @@ TOOL_SIGNATURES = {
 
 # CWQ_ABI_VERSION of the include/cwq.h these signatures mirror: a library
 # reporting another version has other argument lists and is refused.
-ABI_VERSION = (0 << 16) | 4
+ABI_VERSION = (0 << 16) | 5
 
 _lib = None
 
@@ -144,6 +144,8 @@ def load():
                           f"bindings need {ABI_VERSION >> 16}.{ABI_VERSION & 0xffff}: rebuild it")
     for name, (res, args) in list(SIGNATURES.items()) + list(TOOL_SIGNATURES.items()):
         if not hasattr(lib, name):
+            if name in TOOL_SIGNATURES:  # tools only: a product build need not export them
+                continue
             raise ImportError(f"{LIB_PATH} does not export {name}: rebuild it")
         fn = getattr(lib, name)
         fn.restype = res

@@ -492,8 +492,13 @@ def code_grouped_greedy_sample_batch(sess, targets, proposals, n_steps, n_bits_p
     else:
         fut = _batch_thread().submit(call)
         for i in range(n_items):
+            spins = 0
             while not ready[i] and not fut.done():
-                time.sleep(0)  # yields the GIL; the call needs it only to return
+                # yield the GIL (the call needs it only to return); after a
+                # short spin back off, so this thread does not hold a whole
+                # CPU of the quota the native host threads partition on
+                spins += 1
+                time.sleep(0 if spins < 32 else 5e-5)
             if not ready[i]:
                 break  # the call ended early: its error is raised below
             out.append(item(i))

@@ -789,14 +789,26 @@ int64_t cwq_code_grouped_greedy(const float* q_loc, const float* q_scale, const 
     const int rc0 = read_options(opts, &o);
     if (rc0) return rc0;
   }
+  if (D < 0 || n_steps < 1 || D > (INT64_MAX / 8) / n_steps)
+    return fail(CWQ_ERR_INVALID, "%s: D %lld, n_steps %d", who, (long long)D, n_steps);
   CallEvents tev;
-  g_idx_host.resize((size_t)((D + 1) * (n_steps > 0 ? n_steps : 1)));
+  try {
+    g_idx_host.resize((size_t)((D + 1) * n_steps));
+  } catch (...) {
+    return fail(CWQ_ERR_ALLOC, "%s: host index buffer of %lld entries", who,
+                (long long)((D + 1) * n_steps));
+  }
   const int64_t G = grouped_begin(q_loc, q_scale, p_loc, p_scale, D, n_steps, n_bits_per_step,
                                   seed, rho, size_threshold, n_nats, sample_host,
                                   g_idx_host.data(), (int64_t)g_idx_host.size(), starts_host,
                                   starts_cap, kl_sum_out, workspace, workspace_bytes, opts, o,
                                   &tev, 1, bits_cap, stream, who);
-  if (G < 0) return G;
+  if (G < 0) {
+    // work grouped_begin queued (the encode, the copies into g_idx_host) may
+    // still be in flight: drain it before g_idx_host or the events are reused
+    (void)hipStreamSynchronize((hipStream_t)stream);
+    return G;
+  }
   hipError_t e;
   if (G > 0 && (e = hipStreamSynchronize((hipStream_t)stream)) != hipSuccess)
     return hip_fail(e, "sync");

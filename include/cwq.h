@@ -60,15 +60,21 @@ extern "C" {
 #define CWQ_ERR_HIP (-2)       /* HIP runtime error (launch, memset) */
 #define CWQ_ERR_WORKSPACE (-3) /* workspace too small */
 #define CWQ_ERR_CAPACITY (-4)  /* output buffer too small (retry with a larger one) */
+#define CWQ_ERR_ALLOC (-5)     /* host allocation failed */
 
 #define CWQ_MAX_BITS_PER_STEP 30
 
-/* ABI version, (major << 16) | minor.  0.2: per-call cwq_options before the
- * stream in the encoders, a max_block_dim argument to
- * cwq_greedy_encode_workspace_size, no process-wide tuning setters.  Bindings
- * must refuse a library whose cwq_version() differs from the header they were
- * written against. */
-#define CWQ_ABI_VERSION ((0 << 16) | 4)
+/* ABI version, (major << 16) | minor.  Bindings must refuse a library whose
+ * cwq_version() differs from the header they were written against.
+ *   0.2  per-call cwq_options before the stream in the encoders, a
+ *        max_block_dim argument to cwq_greedy_encode_workspace_size, no
+ *        process-wide tuning setters;
+ *   0.3  cwq_code_grouped_greedy_begin / _end;
+ *   0.4  per-item ready flags of the batched grouped coder
+ *        (cwq_options.item_ready);
+ *   0.5  CWQ_ERR_ALLOC (host allocation failures are returned, never thrown);
+ *        starts_host of the grouped _begin calls is read asynchronously. */
+#define CWQ_ABI_VERSION ((0 << 16) | 5)
 int cwq_version(void);
 
 /* Thread-local description of the last error ("" if none). */
@@ -221,7 +227,9 @@ int64_t cwq_code_grouped_greedy(const float* q_loc, const float* q_scale, const 
  * encode, the destandardisation and the copies of the G * n_steps indices to
  * idx_host (idx_cap >= G * n_steps; D + 1 groups at most) and of the sample to
  * sample_host still in flight on the stream: both must stay valid until _end,
- * and page-locked host memory keeps the copies asynchronous.
+ * and page-locked host memory keeps the copies asynchronous.  starts_host is
+ * also the source of an asynchronous copy of the group offsets to the device:
+ * it must stay valid and unchanged until _end too.
  * opts->eval_ms_out must be NULL (the caller's eval events work).  _end:
  * synchronises the stream and writes the bitcode of those indices; returns
  * the number of chars (G * n_steps * n_bits_per_step) or a negative code. */

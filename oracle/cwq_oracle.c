@@ -480,6 +480,178 @@ CWQO_API int cwqo_greedy_encode_lsig(const float* t_loc, const float* t_scale,
   return err ? -1 : 0;
 }
 
+/* ------------------------------------------------------------------------ */
+/* Per-candidate semantics sensitivity (tools/semantics_        */
+/* sensitivity.py).  The declared row value (A.5 TFP<=0.7 log_prob, A.6 Eigen */
+/* 3.3 AVX order) is one of several a TF build could have computed; these    */
+/* variants change every candidate's value by a different rounding, so they  */
+/* are the choices that could move an argmax.  [ext] all recalled from the   */
+/* libraries' public sources, unverifiable offline.                          */
+/* ------------------------------------------------------------------------ */
+#define SEM_NFORM 2 /* 0: TFP<=0.7 (declared), 1: TFP>=0.8 squared_difference */
+#define SEM_NSUM 6  /* row-sum orders, see sem_rowsum */
+#define SEM_NV (SEM_NFORM * SEM_NSUM)
+
+/* TFP >= 0.8 Normal._log_prob:
+ *   -0.5 * squared_difference(x / scale, loc / scale) - (0.5 log 2pi + log scale)
+ * squared_difference(a, b) = (a - b) * (a - b). */
+static inline float log_prob_tfp08(float x, float loc, float scale, float lognorm) {
+  float a = x / scale, b = loc / scale;
+  float dd = a - b;
+  float u = -0.5f * (dd * dd);
+  return u - lognorm;
+}
+
+/* Eigen InnerMostDimReducer<SumReducer> packet orders:
+ *  0 avx8   Packet8f (declared, cwqo_eigen_rowsum)
+ *  1 sse4   Packet4f: 4 lane partials, predux (p0+p2)+(p1+p3), tail t, t + r
+ *  2 avx8x2 Eigen 3.4 style: two Packet8f accumulators over packet pairs,
+ *           leftover packet into the first, then p + p2, predux as avx8
+ *  3 avx512 Packet16f (AVX512DQ predux): fold the 16 partials to 8 as
+ *           l + (l + 8), then the avx8 predux
+ *  4 seq    a scalar (non-vectorised) build: ((x0 + x1) + x2) + ...
+ *  5 tree   pairwise halving: sum(x[0:h]) + sum(x[h:n]), h = n / 2 (a GPU-style
+ *           tree, representative only) */
+static float packet_sum(const float* x, int64_t d, int w, int npacc) {
+  float p[2][16];
+  memset(p, 0, sizeof(p));
+  int64_t vec = (d / w) * w;
+  int64_t np = vec / w, pairs = npacc == 2 ? (np / 2) * 2 : 0;
+  int64_t k = 0;
+  for (; k < pairs; k += 2)
+    for (int a = 0; a < 2; ++a)
+      for (int l = 0; l < w; ++l) p[a][l] = p[a][l] + x[(k + a) * w + l];
+  for (; k < np; ++k)
+    for (int l = 0; l < w; ++l) p[0][l] = p[0][l] + x[k * w + l];
+  if (npacc == 2)
+    for (int l = 0; l < w; ++l) p[0][l] = p[0][l] + p[1][l];
+  float t = 0.0f;
+  for (int64_t j = vec; j < d; ++j) t = t + x[j];
+  float* q = p[0];
+  if (w == 16) for (int l = 0; l < 8; ++l) q[l] = q[l] + q[l + 8];
+  if (w >= 8) for (int l = 0; l < 4; ++l) q[l] = q[l] + q[l + 4];
+  float r = (q[0] + q[2]) + (q[1] + q[3]);
+  return t + r;
+}
+
+static float tree_sum(const float* x, int64_t n) {
+  if (n <= 0) return 0.0f;
+  if (n == 1) return x[0];
+  int64_t h = n / 2;
+  return tree_sum(x, h) + tree_sum(x + h, n - h);
+}
+
+static float sem_rowsum(const float* x, int64_t d, int order) {
+  switch (order) {
+    case 0: return cwqo_eigen_rowsum(x, d);
+    case 1: return packet_sum(x, d, 4, 1);
+    case 2: return packet_sum(x, d, 8, 2);
+    case 3: return packet_sum(x, d, 16, 1);
+    case 4: {
+      float s = 0.0f;
+      for (int64_t j = 0; j < d; ++j) s = s + x[j];
+      return s;
+    }
+    default: return tree_sum(x, d);
+  }
+}
+
+CWQO_API int cwqo_sem_num_variants(void) { return SEM_NV; }
+CWQO_API float cwqo_sem_rowsum(const float* x, int64_t d, int order) {
+  return sem_rowsum(x, d, order);
+}
+
+/* The encoder of code_greedy_sample_impl with every candidate row also scored
+ * under the SEM_NV variants v = form * SEM_NSUM + order (v = 0 is the declared
+ * semantics).  The chain of best samples follows the declared argmax, so
+ * out_vidx[(g * n_steps + i) * SEM_NV + v] is the index variant v would emit
+ * at step i given the same history: a conditional per-index flip test.
+ * out_gap[g * n_steps + i]: declared best minus second-best row value;
+ * out_dev[(g * n_steps + i) * SEM_NV + v] (optional): variant v's value of the
+ * declared best row minus the declared value (how far each choice moves a row). */
+CWQO_API int cwqo_greedy_encode_semvar(const float* t_loc, const float* t_scale,
+                                       const float* p_loc, const float* p_scale,
+                                       const int64_t* block_off, int64_t nb,
+                                       int n_bits_per_step, int n_steps, int32_t seed,
+                                       float rho, int64_t block_id_base, int32_t* out_vidx,
+                                       float* out_sample, double* out_gap, float* out_dev,
+                                       int nthreads) {
+  if (n_bits_per_step < 0 || n_bits_per_step > 30 || n_steps < 1) return -1;
+  int err = 0;
+#ifdef _OPENMP
+  if (nthreads > 0) omp_set_num_threads(nthreads);
+#pragma omp parallel for schedule(dynamic, 1) reduction(| : err)
+#endif
+  for (int64_t g = 0; g < nb; ++g) {
+    const int64_t o = block_off[g], d = block_off[g + 1] - block_off[g];
+    const int32_t sg = (int32_t)((uint32_t)seed + (uint32_t)(block_id_base + g));
+    const float *tl = t_loc + o, *ts = t_scale + o;
+    float* best = out_sample + o;
+    const size_t db = (size_t)(d > 0 ? d : 1) * sizeof(float);
+    float* loc_s = (float*)malloc(db);
+    float* scale_s = (float*)malloc(db);
+    float* lognorm = (float*)malloc(db);
+    float* row = (float*)malloc(2 * db);
+    if (!loc_s || !scale_s || !lognorm || !row) {
+      free(loc_s); free(scale_s); free(lognorm); free(row);
+      err |= 1;
+      continue;
+    }
+    float* row8 = row + (d > 0 ? d : 1);
+    shard_params(p_loc + o, p_scale + o, d, n_steps, rho, loc_s, scale_s);
+    for (int64_t j = 0; j < d; ++j) lognorm[j] = cwqo_log_normalization(ts[j]);
+    for (int64_t j = 0; j < d; ++j) best[j] = 0.0f;
+    const int64_t n_samples = (int64_t)1 << n_bits_per_step;
+    for (int i = 0; i < n_steps; ++i) {
+      normal_stream st;
+      memset(&st, 0, sizeof(st));
+      cwqo_generate_key(step_seed(sg, i), 42, st.key, st.ctr);
+      float bv[SEM_NV], bdev[SEM_NV];
+      int64_t bi[SEM_NV];
+      for (int v = 0; v < SEM_NV; ++v) { bv[v] = -FLT_MAX; bi[v] = 0; }
+      float second = -FLT_MAX;
+      for (int v = 0; v < SEM_NV; ++v) bdev[v] = 0.0f;
+      for (int64_t n = 0; n < n_samples; ++n) {
+        for (int64_t j = 0; j < d; ++j) {
+          float z = stream_normal(&st, (uint64_t)(n * d + j));
+          float s = scale_s[j] * z;
+          s = loc_s[j] + s;
+          float tv = best[j] + s;
+          row[j] = log_prob_c(tv, tl[j], ts[j], lognorm[j]);
+          row8[j] = log_prob_tfp08(tv, tl[j], ts[j], lognorm[j]);
+        }
+        float vals[SEM_NV];
+        for (int f = 0; f < SEM_NFORM; ++f)
+          for (int ord = 0; ord < SEM_NSUM; ++ord) {
+            const int v = f * SEM_NSUM + ord;
+            const float val = sem_rowsum(f ? row8 : row, d, ord);
+            vals[v] = val;
+            if (v == 0) {
+              if (val > bv[0]) second = bv[0];
+              else if (val > second) second = val;
+            }
+            if (val > bv[v]) { bv[v] = val; bi[v] = n; }
+          }
+        if (bi[0] == n) /* the declared best row so far: each variant's deviation on it */
+          for (int v = 0; v < SEM_NV; ++v) bdev[v] = vals[v] - vals[0];
+      }
+      if (out_gap) out_gap[g * n_steps + i] = (double)bv[0] - (double)second;
+      for (int v = 0; v < SEM_NV; ++v) {
+        out_vidx[(g * n_steps + i) * SEM_NV + v] = (int32_t)bi[v];
+        if (out_dev) out_dev[(g * n_steps + i) * SEM_NV + v] = bdev[v];
+      }
+      for (int64_t j = 0; j < d; ++j) {
+        float z = stream_normal(&st, (uint64_t)(bi[0] * d + j));
+        float s = scale_s[j] * z;
+        s = loc_s[j] + s;
+        best[j] = best[j] + s;
+      }
+    }
+    free(loc_s); free(scale_s); free(lognorm); free(row);
+  }
+  return err ? -1 : 0;
+}
+
 /* Eigen 3.3 plog<Packet8f> (Eigen/src/Core/arch/AVX/MathFunctions.h, the
  * Cephes single-precision log) on one lane -- [ext] restated from Eigen's
  * published source, not from /root/reference: TF's CPU kernel evaluates

@@ -53,6 +53,10 @@ def lib():
             "cwqo_greedy_decode": (ci, [vp, vp, vp, vp, i64, ci, ci, i32, f32, i64, vp, ci]),
             "cwqo_greedy_encode_lsig": (ci, [vp, vp, vp, vp, vp, i64, ci, ci, i32, f32, i64, vp,
                                              vp, vp, vp, ci]),
+            "cwqo_greedy_encode_semvar": (ci, [vp, vp, vp, vp, vp, i64, ci, ci, i32, f32, i64,
+                                               vp, vp, vp, vp, ci]),
+            "cwqo_sem_num_variants": (ci, []),
+            "cwqo_sem_rowsum": (f32, [vp, i64, ci]),
             "cwqo_eigen_plog": (f32, [f32, ci]),
             "cwqo_eigen_plog_table": (None, [vp, i64, ci, vp]),
             "cwqo_standardise": (None, [vp, vp, vp, vp, i64, vp, vp]),
@@ -208,6 +212,46 @@ def greedy_encode_lsig(t_loc, t_scale, p_loc, p_scale, block_off, n_bits_per_ste
     if gaps:
         return idx.reshape(nb, int(n_steps)), sample, gap.reshape(nb, int(n_steps))
     return idx.reshape(nb, int(n_steps)), sample
+
+
+SEM_FORMS = ("tfp07", "tfp08")
+SEM_ORDERS = ("avx8", "sse4", "avx8x2", "avx512", "seq", "tree")
+
+
+def sem_variant_names():
+    """Names of the per-candidate semantics variants, in the oracle's order
+    v = form * len(SEM_ORDERS) + order; v = 0 ('tfp07/avx8') is declared."""
+    return [f + "/" + o for f in SEM_FORMS for o in SEM_ORDERS]
+
+
+def sem_rowsum(x, order):
+    a = _f32(x)
+    return float(lib().cwqo_sem_rowsum(_p(a), a.size, int(order)))
+
+
+def greedy_encode_semvar(t_loc, t_scale, p_loc, p_scale, block_off, n_bits_per_step, n_steps,
+                         seed, rho=1., block_id_base=0, nthreads=0):
+    """The declared encoder with every candidate row also scored under each
+    per-candidate semantics variant (sem_variant_names()).  Returns
+    (vidx int32 [nb, n_steps, V], sample [D] of the declared chain, gap float64
+    [nb, n_steps] = declared best - second-best, dev float32 [nb, n_steps, V] =
+    variant v's value of the declared best row minus the declared value).
+    vidx[..., v] is the index variant v would emit at that step given the
+    declared history."""
+    tl, ts, pl, ps = map(_f32, (t_loc, t_scale, p_loc, p_scale))
+    off = np.ascontiguousarray(np.asarray(block_off, dtype=np.int64))
+    nb, ns = off.size - 1, int(n_steps)
+    nv = lib().cwqo_sem_num_variants()
+    vidx = np.zeros(nb * ns * nv, dtype=np.int32)
+    sample = np.zeros(tl.size, dtype=np.float32)
+    gap = np.zeros(nb * ns, dtype=np.float64)
+    dev = np.zeros(nb * ns * nv, dtype=np.float32)
+    rc = lib().cwqo_greedy_encode_semvar(_p(tl), _p(ts), _p(pl), _p(ps), _p(off), nb,
+                                         int(n_bits_per_step), ns, int(seed), float(rho),
+                                         int(block_id_base), _p(vidx), _p(sample), _p(gap),
+                                         _p(dev), int(nthreads))
+    assert rc == 0, rc
+    return vidx.reshape(nb, ns, nv), sample, gap.reshape(nb, ns), dev.reshape(nb, ns, nv)
 
 
 def eigen_plog(x, fma=False):

@@ -1,0 +1,65 @@
+#!/bin/bash
+# One parametrised entry point for ad-hoc GPU-box work (replaces the round-3
+# one-off gpu_r03*.sh scripts).  Every GPU step runs under its own timeout and
+# the first failure ends the script.
+#   tools/gpu_task.sh tests                      full -m gpu suite + smoke()
+#   tools/gpu_task.sh bench CONFIG [bench args]  one bench line -> gpurun_out/b_CONFIG.log
+#   tools/gpu_task.sh trace TAG [bench args]     rocprofv3 kernel trace + stats
+#   tools/gpu_task.sh pmc TAG SET [bench args]   one PMC set (mem | valu | wait | lds),
+#                                                one rocprofv3 pass per counter group
+#   tools/gpu_task.sh stress [N]                 CSR + small-path stress sweeps
+# Several tasks can be chained: tools/gpu_task.sh tests -- pmc c2 wait --config c2
+set -o pipefail
+cd "$(dirname "$0")/.."
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+prof() {  # prof DIR ARGS... -- python3 bench args
+  local d=$1; shift
+  timeout -s KILL 180 rocprofv3 "$@" -d gpurun_out/$d -o run --output-format csv -- \
+    python3 bench.py --no-cpu --no-e2e $BARGS > gpurun_out/$d.log 2>&1
+}
+run_one() {
+  local task=$1; shift
+  case $task in
+    tests)
+      timeout -k 10 900 python -u -m pytest tests -x -q -m gpu --timeout 300 \
+        --timeout-method thread > gpurun_out/t_all.log 2>&1 && tail -1 gpurun_out/t_all.log && \
+      timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" \
+        > gpurun_out/smoke.log 2>&1 && echo smoke ok ;;
+    bench)
+      local c=$1; shift
+      timeout -k 10 600 python -u bench.py --config $c "$@" > gpurun_out/b_$c.log 2>&1 && \
+        tail -1 gpurun_out/b_$c.log | cut -c1-200 ;;
+    trace)
+      local tag=$1; shift
+      BARGS="$* --steps 3 --warmup 1" prof prof_${tag}_trace --kernel-trace --stats && \
+        echo trace $tag ok ;;
+    pmc)
+      local tag=$1 set=$2; shift 2
+      BARGS="$* --steps 1 --warmup 0"
+      case $set in
+        mem)  prof prof_${tag}_fetch --pmc FETCH_SIZE && prof prof_${tag}_write --pmc WRITE_SIZE ;;
+        valu) prof prof_${tag}_valu --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE ;;
+        wait) prof prof_${tag}_wait --pmc SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_BUSY_CYCLES SQ_WAVES ;;
+        lds)  prof prof_${tag}_lds --pmc SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_SMEM SQ_WAVES ;;
+        *) echo "unknown PMC set $set"; return 2 ;;
+      esac && echo pmc $tag $set ok ;;
+    stress)
+      local n=${1:-400}
+      timeout -k 10 300 python -u tools/stress_csr.py $n ${STRESS_SEED:-20000} 200 \
+        > gpurun_out/stress_csr.log 2>&1 && tail -1 gpurun_out/stress_csr.log && \
+      STRESS_BITS=6,11 timeout -k 10 300 python -u tools/stress_csr.py $n ${STRESS_SEED:-20000} 200 \
+        > gpurun_out/stress_small.log 2>&1 && tail -1 gpurun_out/stress_small.log ;;
+    *) echo "unknown task $task"; return 2 ;;
+  esac
+}
+args=()
+for a in "$@" --; do
+  if [ "$a" = "--" ]; then
+    [ ${#args[@]} -gt 0 ] && { run_one "${args[@]}" || exit 1; }
+    args=()
+  else
+    args+=("$a")
+  fi
+done
+echo gpu_task done
