@@ -2369,7 +2369,35 @@ static void launch_prune_t(const EncodeArgs& a, int step, hipStream_t stream) {
 #ifndef CWQ_TILE_INTERLEAVE
 #define CWQ_TILE_INTERLEAVE 1
 #endif
-  if (CWQ_TILE_INTERLEAVE && a.tiles_per_block > 1)
+  // tau seeding: when a block spans several tiles, most of them
+  // run at once and each would warm its threshold up from -inf.  A first launch
+  // scores the block's first 2^CWQ_SEED_LOG2 candidates in small tiles; their
+  // exact best keys land in keys[g], and every tile of the main launch starts
+  // from that value (an actual row's exact value, so never above the block's
+  // best).  The sample's rows are scored again by the main launch: its keys
+  // are exact, so the final argmax is unchanged.
+#ifndef CWQ_SEED_LOG2
+#define CWQ_SEED_LOG2 16
+#endif
+#ifndef CWQ_SEED_TILE
+#define CWQ_SEED_TILE 4096
+#endif
+#ifndef CWQ_SEED_MIN_TPB
+#define CWQ_SEED_MIN_TPB 2
+#endif
+  const int64_t seed_n = CWQ_SEED_LOG2 > 0 ? ((int64_t)1 << CWQ_SEED_LOG2) : 0;
+  const bool seeded = CWQ_TILE_INTERLEAVE && seed_n > 0 && a.tiles_per_block >= CWQ_SEED_MIN_TPB &&
+                      a.n_cand >= 4 * seed_n;
+  if (seeded) {
+    const int64_t cpt_s = seed_n < CWQ_SEED_TILE ? seed_n : CWQ_SEED_TILE;
+    const int64_t nt_s = a.nb * (seed_n / cpt_s);
+    hipLaunchKernelGGL((k_encode_prune<D, STEP0, true>),
+                       dim3((unsigned)(nt_s < kPruneGrid ? nt_s : kPruneGrid)), dim3(256), 0,
+                       stream, a.t_loc, a.t_scale, a.loc_s, a.scale_s, a.lognorm, a.out_sample,
+                       nt_s, seed_n / cpt_s, cpt_s, seed_n, seeds_of(a), step,
+                       a.prune >= 2 ? 1 : 0, a.keys);
+  }
+  if (CWQ_TILE_INTERLEAVE && (a.tiles_per_block > 1 || seeded))
     hipLaunchKernelGGL((k_encode_prune<D, STEP0, true>), dim3(grid), dim3(256), 0, stream,
                        a.t_loc, a.t_scale, a.loc_s, a.scale_s, a.lognorm, a.out_sample, ntiles,
                        a.tiles_per_block, a.cand_per_tile, a.n_cand, seeds_of(a), step,

@@ -3,7 +3,7 @@
 # one-off gpu_r03*.sh scripts).  Every GPU step runs under its own timeout and
 # the first failure ends the script.
 #   tools/gpu_task.sh tests                      full -m gpu suite + smoke()
-#   tools/gpu_task.sh bench CONFIG [bench args]  one bench line -> gpurun_out/b_CONFIG.log
+#   tools/gpu_task.sh bench CONFIG[@TAG] [bench args]  one bench line -> gpurun_out/b_CONFIG[_TAG].log
 #   tools/gpu_task.sh trace TAG [bench args]     rocprofv3 kernel trace + stats
 #   tools/gpu_task.sh pmc TAG SET [bench args]   one PMC set (mem | valu | wait | lds),
 #                                                one rocprofv3 pass per counter group
@@ -27,9 +27,9 @@ run_one() {
       timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" \
         > gpurun_out/smoke.log 2>&1 && echo smoke ok ;;
     bench)
-      local c=$1; shift
-      timeout -k 10 600 python -u bench.py --config $c "$@" > gpurun_out/b_$c.log 2>&1 && \
-        tail -1 gpurun_out/b_$c.log | cut -c1-200 ;;
+      local c=${1%%@*} n=${1/@/_}; shift
+      timeout -k 10 600 python -u bench.py --config $c "$@" > gpurun_out/b_$n.log 2>&1 && \
+        tail -1 gpurun_out/b_$n.log | cut -c1-200 ;;
     trace)
       local tag=$1; shift
       BARGS="$* --steps 3 --warmup 1" prof prof_${tag}_trace --kernel-trace --stats && \

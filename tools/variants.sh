@@ -76,6 +76,11 @@ declare -A V=(
   [lord]="-DCWQ_COOP_LOAD_ORDER=1"
   [nowma]="-DCWQ_WAVE_MAX_ASM=0"
   [noctile]="-DCWQ_COOP_CLASS_TILES=0"
+  [seed0]="-DCWQ_SEED_LOG2=0"
+  [seed14]="-DCWQ_SEED_LOG2=14"
+  [seed18]="-DCWQ_SEED_LOG2=18"
+  [seed20]="-DCWQ_SEED_LOG2=20"
+  [stats0]="-DCWQ_PRUNE_STATS -DCWQ_SEED_LOG2=0"
 )
 if [ "$1" = build ]; then
   mkdir -p $OUT
