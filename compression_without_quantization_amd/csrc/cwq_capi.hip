@@ -112,8 +112,11 @@ WsLayout ws_layout_uniform(int64_t nb, int64_t d) {
   return ws_layout(nb, nb * d, csr, d > CWQ_CSR_LDS_DIMS);
 }
 
+#ifndef CWQ_TARGET_TILES
+#define CWQ_TARGET_TILES 16384  // tiles per launch the tiling aims for (tuning builds)
+#endif
 void choose_tiling(int64_t nb, int64_t n_cand, int64_t* tiles_per_block, int64_t* cand_per_tile) {
-  const int64_t kTargetTiles = 16384;
+  const int64_t kTargetTiles = CWQ_TARGET_TILES;
   int64_t want = nb > 0 ? (kTargetTiles + nb - 1) / nb : 1;
   int64_t max_split = (n_cand + 255) / 256;  // at least one candidate per lane
   if (want > max_split) want = max_split;
@@ -359,6 +362,7 @@ int encode_impl(const float* t_loc, const float* t_scale, const float* p_loc,
   a.ud = ud;
   a.nb = nb;
   a.total_dims = total_dims;
+  a.max_d = block_off ? max_block_dim : ud;
   a.n_cand = (int64_t)1 << n_bits;
   choose_tiling(nb, a.n_cand, &a.tiles_per_block, &a.cand_per_tile);
   a.n_steps = n_steps;

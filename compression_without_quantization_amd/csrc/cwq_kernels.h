@@ -38,6 +38,7 @@ struct EncodeArgs {
   int64_t ud;
   int64_t nb;
   int64_t total_dims;
+  int64_t max_d;             // longest block (uniform: ud); -1: unknown
   int64_t n_cand;            // 2^n_bits_per_step
   int64_t tiles_per_block;
   int64_t cand_per_tile;     // multiple of 256

@@ -416,7 +416,10 @@ __global__ void __launch_bounds__(256, CWQ_PRUNE_MIN_WAVES) k_encode_prune(
     uint32_t n = (uint32_t)w0 + lane;
     int k = 0;
     float s = 0.0f;
-    float tau = -__builtin_inff();
+#ifndef CWQ_TAU_FROM_KEYS
+#define CWQ_TAU_FROM_KEYS 1  // INTER: start the lanes' tau at keys[g]'s value, not at the first share
+#endif
+    float tau = (INTER && CWQ_TAU_FROM_KEYS) ? unord_f32(tau_ord) : -__builtin_inff();
 #ifdef CWQ_PRUNE_STATS
     tau = tau_seed;
 #endif
@@ -1914,6 +1917,465 @@ __global__ void __launch_bounds__(256) k_small_survivors(
 }
 
 // ---------------------------------------------------------------------------
+// The small-candidate step fused into one kernel (round 4): a wave owns four
+// consecutive blocks (64 <= 2^b < 4096 candidates, d <= CWQ_FUSED_DMAX) and
+// does k_small_prep's constants, k_small_screen's rows, the exact scoring of
+// the survivors and k_encode_finalize's index + sample update itself, so a
+// step is k_prep_dims and this launch.  The three-kernel path ran ~650 waves
+// in each of its prep and survivor launches (latency-bound: 20 + 23 us for
+// C2's 41.5k blocks) and sent per-dim constants, headers and survivor slots
+// through HBM; a one-block-per-wave fusion left every per-block latency chain
+// exposed (113 us against 106).  Four blocks per wave:
+//   * constants: a 16-lane row per block, lanes over its dims (coalesced
+//     loads); the block sums are row-local DPP reductions (four steps), the
+//     bounds and the stream key are computed by every lane of the row;
+//   * screen: the blocks one after the other, as k_small_screen (a lane per
+//     4-row span of d whole Philox blocks, per-dim constants wave-uniform LDS
+//     reads); a block's rows whose upper bound reaches its final tau are
+//     listed in LDS.  A block with a single listed row needs no exact value:
+//     every other row's exact value is below tau <= that row's.
+//   * exact values of the other listed rows, lane-parallel over (row, dim):
+//     each lane computes one normal exactly (its Philox block and the one
+//     Box-Muller pair holding it) and its log-density into LDS; a lane per row
+//     then sums in the Eigen order (eval_row's values bit for bit) and folds
+//     its key into its block's LDS maximum;
+//   * finalize: best += the winning row, a row's lanes over the block's dims
+//     (k_encode_finalize's arithmetic).
+// Blocks whose constants leave the gate, or whose listed rows overflow the
+// list, are scored exactly (every candidate through eval_row).
+// ---------------------------------------------------------------------------
+#ifndef CWQ_FUSED_DMAX
+#define CWQ_FUSED_DMAX 64  // longest block of the fused kernel (a wave's 4 blocks: 256 LDS slots)
+#endif
+#ifndef CWQ_FUSED_LIST
+#define CWQ_FUSED_LIST 64  // listed rows per wave
+#endif
+#ifndef CWQ_FUSED_STAGE
+#define CWQ_FUSED_STAGE 256  // (row, dim) values per exact batch
+#endif
+#ifndef CWQ_FUSED_WAVES
+#define CWQ_FUSED_WAVES 8
+#endif
+static_assert(CWQ_FUSED_STAGE >= CWQ_FUSED_DMAX, "an exact batch holds at least one row");
+static_assert(CWQ_FUSED_LIST <= 64, "one listed row per lane");
+
+// Row-local (16-lane) DPP reduction of doubles: every lane of a row gets its
+// row's result.  The block sums of the fused kernel feed rigorous bounds whose
+// slack dwarfs double rounding, so their order does not matter.  Full exec mask.
+template <int CTRL>
+__device__ __forceinline__ double dpp_f64(double v) {
+  const uint64_t b = __builtin_bit_cast(uint64_t, v);
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)b, CTRL, 0xf, 0xf, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)(b >> 32), CTRL, 0xf, 0xf, false);
+  return __builtin_bit_cast(double, ((uint64_t)(uint32_t)hi << 32) | (uint64_t)(uint32_t)lo);
+}
+template <bool MAX>
+__device__ __forceinline__ double row16_red_f64(double v) {
+  auto op = [](double a, double b) { return MAX ? (a > b ? a : b) : a + b; };
+  v = op(v, dpp_f64<0xb1>(v));   // quad_perm [1,0,3,2]
+  v = op(v, dpp_f64<0x4e>(v));   // quad_perm [2,3,0,1]
+  v = op(v, dpp_f64<0x141>(v));  // row_half_mirror
+  v = op(v, dpp_f64<0x140>(v));  // row_mirror
+  return v;
+}
+
+// Exact normal k of a block's stream: its Philox block and the one
+// Box-Muller pair that holds it (normal4_dev's element k & 3, bit for bit).
+__device__ __forceinline__ float exact_normal(const PhiloxStream& st, uint64_t k,
+                                              const double* logtab) {
+  const U4 x = philox_block_dev(st, k >> 2);
+  const bool hi = (k & 2u) != 0;
+  float f0, f1;
+  box_muller_dev(hi ? x.z : x.x, hi ? x.w : x.y, logtab, f0, f1);
+  return (k & 1u) ? f1 : f0;
+}
+
+// LDS written by some lanes of a wave and read by others: order the wave's
+// accesses (no workgroup barrier: the four waves work independently)
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
+__device__ __forceinline__ uint32_t lane_rank(uint64_t m) {  // set lanes of m below this one
+  return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+__device__ __forceinline__ int64_t readlane_i64(int64_t v, int l) {
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)((uint64_t)v >> 32), l);
+  return (int64_t)(((uint64_t)hi << 32) | lo);
+}
+__device__ __forceinline__ float readlane_f32(float v, int l) {
+  return u2f((uint32_t)__builtin_amdgcn_readlane((int)f2u(v), l));
+}
+__device__ __forceinline__ uint32_t readlane_u32(uint32_t v, int l) {
+  return (uint32_t)__builtin_amdgcn_readlane((int)v, l);
+}
+
+// Per-block record of the fused kernel (LDS, one per block of the wave)
+struct QuadBlk {
+  int64_t off;
+  uint32_t d, k0, k1, c2, c3, idx;  // idx: the block's index once decided
+  uint32_t state;                   // kQuad*
+  float bf, c1, c2f, as, pq;        // screening bound constants
+  uint32_t rel;                     // first dim, relative to the quad's
+};
+constexpr uint32_t kQuadKnown = 0;   // idx decided (empty block, or a single listed row)
+constexpr uint32_t kQuadListed = 1;  // listed rows scored exactly (s_key)
+constexpr uint32_t kQuadExact = 2;   // every candidate scored exactly
+
+#ifndef CWQ_FUSED_NOINLINE
+#define CWQ_FUSED_NOINLINE 1  // the rare whole-block exact path out of line (its registers)
+#endif
+#if CWQ_FUSED_NOINLINE
+#define CWQ_RARE __device__ __noinline__
+#else
+#define CWQ_RARE __device__ __forceinline__
+#endif
+// Every candidate of a block exactly (eval_row, a lane per row): the fused
+// kernel's fallback for blocks outside the screening gate or with a full list.
+// Returns the wave's best argmax key.
+template <bool STEP0>
+CWQ_RARE unsigned long long quad_exact_block(const QuadBlk r, const float* __restrict__ t_loc,
+                                             const float* __restrict__ t_scale,
+                                             const float* __restrict__ loc_s,
+                                             const float* __restrict__ scale_s,
+                                             const float* __restrict__ lognorm,
+                                             const float* __restrict__ best, int64_t n_cand,
+                                             const double* logtab) {
+  const uint32_t lane = threadIdx.x & 63u;
+  const PhiloxStream se{r.k0, r.k1, r.c2, r.c3};
+  const int64_t ob = r.off;
+  const int db = (int)r.d;
+  uint64_t bestk = 0;
+  for (int rr = 0; rr < 4; ++rr) {  // rows n = rr (mod 4): one alignment class per pass
+    const int align = (int)(((uint64_t)rr * (uint64_t)db) & 3u);
+    for (int64_t n = rr + 4 * (int64_t)lane; n < n_cand; n += 256) {
+      const float v = eval_row<0, STEP0>(se, (uint64_t)n * (uint64_t)db, db, align, loc_s + ob,
+                                         scale_s + ob, t_loc + ob, t_scale + ob, lognorm + ob,
+                                         STEP0 ? nullptr : best + ob, logtab);
+      const uint64_t kk = argmax_key(v, (uint32_t)n);
+      bestk = kk > bestk ? kk : bestk;
+    }
+  }
+  return wave_max_u64(bestk);
+}
+
+template <bool STEP0>
+__global__ void __launch_bounds__(256, CWQ_FUSED_WAVES) k_small_fused(
+    const float* __restrict__ t_loc, const float* __restrict__ t_scale,
+    const float* __restrict__ loc_s, const float* __restrict__ scale_s,
+    const float* __restrict__ lognorm, float* __restrict__ best,
+    const int64_t* __restrict__ block_off, int64_t ud, int64_t nb, int64_t n_cand, SeedSpec sd,
+    int32_t step, int n_steps, int32_t* __restrict__ out_idx) {
+  __shared__ double logtab[32];
+  __shared__ float2 s_ab[4][4 * CWQ_FUSED_DMAX];   // the 4 blocks' (sA, sB), by dim offset
+  __shared__ uint32_t s_ln[4][CWQ_FUSED_LIST];     // listed rows
+  __shared__ float s_lu[4][CWQ_FUSED_LIST];        // their upper bounds
+  __shared__ uint32_t s_lk[4][CWQ_FUSED_LIST];     // their block (0..3)
+  __shared__ uint32_t s_pre[4][CWQ_FUSED_LIST + 1];  // first exact item of each listed row
+  __shared__ float s_lp[4][CWQ_FUSED_STAGE];       // exact batch: log-densities
+  __shared__ unsigned long long s_key[4][4];       // best exact key per block
+  __shared__ QuadBlk s_bk[4][4];
+  fill_logtab(logtab);
+  const uint32_t wv = wave_id();
+  const uint32_t lane0 = threadIdx.x & 63u;
+  const int64_t nwaves = (int64_t)gridDim.x * 4;
+  float2* ab = s_ab[wv];
+  uint32_t* ln = s_ln[wv];
+  float* lu = s_lu[wv];
+  uint32_t* lk = s_lk[wv];
+  uint32_t* pre = s_pre[wv];
+  float* lpv = s_lp[wv];
+  unsigned long long* kmax = s_key[wv];
+  QuadBlk* bk = s_bk[wv];
+  for (int64_t q = (int64_t)blockIdx.x * 4 + wv; 4 * q < nb; q += nwaves) {
+    uint32_t lane = lane0;  // re-derived per quad (see k_small_screen)
+    asm volatile("" : "+v"(lane));
+    const uint32_t k = lane >> 4, slot = lane & 15u;
+    const int64_t g0 = 4 * q;
+    const int nq = (int)(nb - g0 < 4 ? nb - g0 : 4);  // blocks of this quad
+    const int64_t g = g0 + (int64_t)k;
+    const bool valid = (int)k < nq;
+    const BlockSpan sp = block_span(block_off, ud, valid ? g : g0);
+    const int64_t off = sp.off;
+    const int d = valid ? (int)sp.d : 0;
+    const int64_t base = readlane_i64(off, 0);  // block g0's first dim
+    const int64_t rel = off - base;
+    const bool fits = d <= CWQ_FUSED_DMAX && rel + d <= 4 * CWQ_FUSED_DMAX;
+
+    // (1) per-dim constants and each block's bound (k_small_prep), a row per block
+    double sm = 0.0, sa = 0.0, sk = 0.0, s2 = 0.0, cs = 0.0, mx = 0.0;
+    int okl = 1;
+    if (fits) {
+      for (int j = (int)slot; j < d; j += 16) {
+        const CsrDim o = csr_dim<STEP0>(loc_s[off + j], scale_s[off + j], t_loc[off + j],
+                                        t_scale[off + j], lognorm[off + j],
+                                        STEP0 ? 0.0f : best[off + j]);
+        ab[rel + j] = float2{o.sa, o.sb};
+        sm += o.M;
+        sa += __builtin_fabs(o.M);
+        sk += __builtin_fabs(o.M) + o.M;
+        s2 += (double)o.A * (double)o.A;
+        cs += (double)o.C;
+        mx = (double)o.A > mx ? (double)o.A : mx;
+        okl &= o.ok ? 1 : 0;
+      }
+    }
+    sm = row16_red_f64<false>(sm);
+    sa = row16_red_f64<false>(sa);
+    sk = row16_red_f64<false>(sk);
+    s2 = row16_red_f64<false>(s2);
+    cs = row16_red_f64<false>(cs);
+    mx = row16_red_f64<true>(mx);
+    const bool row_ok = ((__ballot(okl == 0) >> (16u * k)) & 0xffffull) == 0ull;
+    const double h_s = (double)d, h_e = (double)d / 8.0 + 8.0;
+    const double gam = 1.01 * ((h_s > h_e ? h_s : h_e) + 1.0) * 0x1p-24;
+    const double sl = (3.0 * gam + 0x1p-20) * (__builtin_fabs(sm) + sa + sk) + 0x1p-126;
+    const float bf = round_up_f32(sm + cs * (1.0 + 0x1p-20) + sl);
+    const float c1 = round_dn_f32(1.0 - 3.0 * gam - 0x1p-22);
+    const float c2 = round_up_f32(1.0 + 3.0 * gam + 0x1p-14);
+    const float as = round_dn_f32(sm - sl - 1.01 * s2 * (1.0 + 0x1p-11));
+    const float pq = round_up_f32(2.01 * mx * __builtin_sqrt((double)(d > 0 ? d : 1)) *
+                                  (1.0 + 0x1p-11));
+    const bool screen = fits && row_ok && d > 0 && as - as == 0.0f && pq - pq == 0.0f &&
+                        bf - bf == 0.0f;
+    if (slot == 0u && valid) {
+      const PhiloxStream st = generate_key(step_seed(sd.of(g), step), 42);
+      QuadBlk r;
+      r.off = off;
+      r.d = (uint32_t)d;
+      r.k0 = st.k0;
+      r.k1 = st.k1;
+      r.c2 = st.c2;
+      r.c3 = st.c3;
+      r.idx = 0u;
+      r.state = d == 0 ? kQuadKnown : (screen ? kQuadListed : kQuadExact);
+      r.bf = bf;
+      r.c1 = c1;
+      r.c2f = c2;
+      r.as = as;
+      r.pq = pq;
+      r.rel = (uint32_t)rel;
+      bk[k] = r;
+      kmax[k] = 0ull;
+    }
+    wave_lds_sync();
+
+    // (2) screen the blocks' rows (k_small_screen's spans), list those that can win
+    uint32_t used = 0;  // listed rows of the wave (uniform)
+    for (int kb = 0; kb < nq; ++kb) {
+      const QuadBlk rb = bk[kb];  // wave-uniform LDS reads, into SGPRs
+      auto ufirst = [](uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); };
+      auto ffirst = [&](float v) { return u2f(ufirst(f2u(v))); };
+      if (ufirst(rb.state) != kQuadListed) continue;
+      const int db = (int)ufirst(rb.d);
+      const float2* abk = ab + ufirst(rb.rel);
+      const float bfb = ffirst(rb.bf), c1b = ffirst(rb.c1), c2b = ffirst(rb.c2f);
+      const float asb = ffirst(rb.as), pqb = ffirst(rb.pq);
+      PhiloxStream sb;
+      sb.k0 = ufirst(rb.k0);
+      sb.k1 = ufirst(rb.k1);
+      sb.c2 = ufirst(rb.c2);
+      sb.c3 = ufirst(rb.c3);
+      const PhiloxLo K = philox_lo_key(sb);  // n_cand * d / 4 < 2^32 here (launch_small)
+      float tau = -__builtin_inff();
+      const uint32_t first = used;
+      bool over = false;
+      for (int64_t m0 = 0; 256 * m0 < n_cand; ++m0) {
+        const int64_t ns = 4 * ((int64_t)lane + 64 * m0);
+        const uint32_t b0 = (uint32_t)((uint64_t)ns * (uint64_t)db / 4u);
+        float rs[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+        float cur = 0.0f;
+        int j = 0, qd = 0;
+        for (int b = 0; b < db; ++b) {
+          const U4 x = philox10_lo(b0 + (uint32_t)b, K, sb.k0, sb.k1);
+          float z[4];
+          box_muller_screen(x.x, x.y, z[0], z[1]);
+          box_muller_screen(x.z, x.w, z[2], z[3]);
+#pragma unroll
+          for (int t = 0; t < 4; ++t) {
+            const float2 e = abk[j];
+            const float a = __builtin_fmaf(e.x, z[t], e.y);
+            cur = __builtin_fmaf(-a, a, cur);
+            if (++j == db) {  // wave-uniform: a row of the span is complete
+              if (qd == 0) rs[0] = cur;
+              else if (qd == 1) rs[1] = cur;
+              else if (qd == 2) rs[2] = cur;
+              else rs[3] = cur;
+              cur = 0.0f;
+              j = 0;
+              ++qd;
+            }
+          }
+        }
+        // tau from the lane's best valid row (the lower bound is monotone in s)
+        float smax = -__builtin_inff();
+        bool any = false;
+#pragma unroll
+        for (int qq = 0; qq < 4; ++qq)
+          if (ns + qq < n_cand) {
+            smax = fmaxf(smax, rs[qq]);
+            any = true;
+          }
+        const float lower =
+            any ? __builtin_fmaf(smax, c2b, asb) - pqb * __builtin_amdgcn_sqrtf(-smax)
+                : -__builtin_inff();
+        tau = fmaxf(tau, wave_max_f32(lower));
+        uint64_t m[4];
+        uint32_t cnt = 0;
+#pragma unroll
+        for (int qq = 0; qq < 4; ++qq) {
+          m[qq] = __ballot(ns + qq < n_cand && __builtin_fmaf(rs[qq], c1b, bfb) >= tau);
+          cnt += (uint32_t)__builtin_popcountll(m[qq]);
+        }
+        if (cnt == 0) continue;
+        if (used + cnt > CWQ_FUSED_LIST) {  // drop this block's rows the raised tau excludes
+          const bool have = lane >= first && lane < used;
+          const uint32_t nl = have ? ln[lane] : 0u;
+          const float ul = have ? lu[lane] : 0.0f;
+          const uint64_t keep = __ballot(have && ul >= tau);
+          if ((keep >> lane) & 1ull) {
+            const uint32_t r = first + lane_rank(keep);
+            ln[r] = nl;
+            lu[r] = ul;
+          }
+          used = first + (uint32_t)__builtin_popcountll(keep);
+          wave_lds_sync();
+        }
+        if (used + cnt > CWQ_FUSED_LIST) {  // list full (near-ties): score the block exactly
+          over = true;
+          break;
+        }
+        uint32_t at = used;
+#pragma unroll
+        for (int qq = 0; qq < 4; ++qq) {
+          const uint64_t mq = m[qq];
+          if ((mq >> lane) & 1ull) {
+            const uint32_t slot_i = at + lane_rank(mq);
+            ln[slot_i] = (uint32_t)(ns + qq);
+            lu[slot_i] = __builtin_fmaf(rs[qq], c1b, bfb);
+            lk[slot_i] = (uint32_t)kb;
+          }
+          at += (uint32_t)__builtin_popcountll(mq);
+        }
+        used = at;
+        wave_lds_sync();
+      }
+      if (over) {
+        used = first;
+        if (lane == 0) bk[kb].state = kQuadExact;
+        wave_lds_sync();
+        continue;
+      }
+      // keep the rows whose upper bound reaches the block's final tau
+      const bool have = lane >= first && lane < used;
+      const uint32_t nl = have ? ln[lane] : 0u;
+      const uint64_t keep = __ballot(have && lu[have ? lane : 0] >= tau);
+      const uint32_t nk = (uint32_t)__builtin_popcountll(keep);
+      if (nk == 1u) {  // the single listed row is the argmax: no exact value needed
+        if ((keep >> lane) & 1ull) {
+          bk[kb].idx = nl;
+          bk[kb].state = kQuadKnown;
+        }
+        used = first;
+      } else {
+        if ((keep >> lane) & 1ull) {
+          const uint32_t r = first + lane_rank(keep);
+          ln[r] = nl;
+          lk[r] = (uint32_t)kb;
+        }
+        used = first + nk;
+        if (nk == 0u && lane == 0) bk[kb].state = kQuadExact;  // (never: the best lower bound's row is listed)
+      }
+      wave_lds_sync();
+    }
+
+    // (3) exact values of the listed rows, lane-parallel over (row, dim)
+    if (used > 0) {
+      // prefix of the rows' dims: pre[e] = first item of row e
+      const bool have = lane < used;
+      const uint32_t de = have ? bk[lk[lane]].d : 0u;
+      uint32_t inc = de;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t t = (uint32_t)__shfl_up((int)inc, (unsigned)o, 64);
+        if (lane >= (uint32_t)o) inc += t;
+      }
+      if (have) pre[lane + 1] = inc;
+      if (lane == 0) pre[0] = 0u;
+      wave_lds_sync();
+      for (uint32_t e0 = 0; e0 < used;) {
+        // rows [e0, e1) whose items fit one batch (a row's d <= the batch)
+        uint32_t e1 = e0 + 1;
+        while (e1 < used && pre[e1 + 1] - pre[e0] <= (uint32_t)CWQ_FUSED_STAGE) ++e1;
+        const uint32_t i0 = pre[e0], i1 = pre[e1];
+        for (uint32_t it = i0 + lane; it < i1; it += 64) {
+          uint32_t e = e0;
+          while (pre[e + 1] <= it) ++e;
+          const QuadBlk r = bk[lk[e]];
+          const uint32_t j = it - pre[e];
+          const int64_t ei = r.off + j;
+          const PhiloxStream se{r.k0, r.k1, r.c2, r.c3};
+          const float zz = exact_normal(se, (uint64_t)ln[e] * (uint64_t)r.d + j, logtab);
+          float sv = scale_s[ei] * zz;  // misc.py:14
+          sv = loc_s[ei] + sv;          // misc.py:15
+          const float tv = STEP0 ? sv : best[ei] + sv;  // :57
+          lpv[it - i0] = log_prob(tv, t_loc[ei], t_scale[ei], lognorm[ei]);
+        }
+        wave_lds_sync();
+        const uint32_t e = e0 + lane;
+        if (e < e1) {  // a lane per row: the Eigen-order sum (eval_row_f)
+          const float* x = lpv + (pre[e] - i0);
+          const int dr = (int)(pre[e + 1] - pre[e]);
+          const int vec = dr & ~7;
+          float p[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+          for (int jj = 0; jj < vec; jj += 8) {
+#pragma unroll
+            for (int l = 0; l < 8; ++l) p[l] = p[l] + x[jj + l];
+          }
+          float t = 0.0f;
+          for (int jj = vec; jj < dr; ++jj) t = t + x[jj];
+          const float q0 = p[0] + p[4], q1 = p[1] + p[5], q2 = p[2] + p[6], q3 = p[3] + p[7];
+          atomicMax(&kmax[lk[e]], (unsigned long long)argmax_key(t + ((q0 + q2) + (q1 + q3)),
+                                                                 ln[e]));
+        }
+        wave_lds_sync();
+        e0 = e1;
+      }
+    }
+
+    // blocks scored exactly: every candidate (constants outside the gate, list full)
+    for (int kb = 0; kb < nq; ++kb) {
+      if (bk[kb].state != kQuadExact) continue;
+      const unsigned long long bestk =
+          quad_exact_block<STEP0>(bk[kb], t_loc, t_scale, loc_s, scale_s, lognorm, best, n_cand,
+                                  logtab);
+      if (lane == 0) kmax[kb] = bestk;
+      wave_lds_sync();
+    }
+
+    // (4) index and best += the winning row (k_encode_finalize), a row per block
+    if (valid) {
+      const QuadBlk r = bk[k];
+      uint32_t idx = r.idx;
+      if (r.state != kQuadKnown) {  // ArgMaxTupleReducer: a key at the clamp level is index 0
+        const unsigned long long kb = kmax[k];
+        idx = (kb >> 32) > kArgmaxClampOrd ? argmax_key_index(kb) : 0u;
+      }
+      if (slot == 0u) out_idx[g * n_steps + step] = (int32_t)idx;
+      const PhiloxStream st{r.k0, r.k1, r.c2, r.c3};
+      for (int j = (int)slot; j < d; j += 16) {
+        const float zz = exact_normal(st, (uint64_t)idx * (uint64_t)d + (uint32_t)j, logtab);
+        float sv = scale_s[off + j] * zz;
+        sv = loc_s[off + j] + sv;
+        best[off + j] = (STEP0 ? 0.0f : best[off + j]) + sv;
+      }
+    }
+    wave_lds_sync();  // the next quad reuses the wave's LDS
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Encoder, end of a step: index -> out_idx; best += winning candidate (:63).
 // General shapes (CSR groups, uniform d the float4 kernel does not take): one
 // thread per flat dim i, which finds its block by binary search in block_off
@@ -2377,7 +2839,7 @@ static void launch_prune_t(const EncodeArgs& a, int step, hipStream_t stream) {
   // best).  The sample's rows are scored again by the main launch: its keys
   // are exact, so the final argmax is unchanged.
 #ifndef CWQ_SEED_LOG2
-#define CWQ_SEED_LOG2 16
+#define CWQ_SEED_LOG2 0  // off: measured no gain
 #endif
 #ifndef CWQ_SEED_TILE
 #define CWQ_SEED_TILE 4096
@@ -2389,7 +2851,7 @@ static void launch_prune_t(const EncodeArgs& a, int step, hipStream_t stream) {
   const bool seeded = CWQ_TILE_INTERLEAVE && seed_n > 0 && a.tiles_per_block >= CWQ_SEED_MIN_TPB &&
                       a.n_cand >= 4 * seed_n;
   if (seeded) {
-    const int64_t cpt_s = seed_n < CWQ_SEED_TILE ? seed_n : CWQ_SEED_TILE;
+    const int64_t cpt_s = seed_n < CWQ_SEED_TILE ? (seed_n > 0 ? seed_n : 1) : CWQ_SEED_TILE;
     const int64_t nt_s = a.nb * (seed_n / cpt_s);
     hipLaunchKernelGGL((k_encode_prune<D, STEP0, true>),
                        dim3((unsigned)(nt_s < kPruneGrid ? nt_s : kPruneGrid)), dim3(256), 0,
@@ -2464,8 +2926,19 @@ static void launch_prune_csr(const EncodeArgs& a, int step, hipStream_t stream) 
                        coop_min_d, (const float4*)a.abp);
 }
 
+#ifndef CWQ_SMALL_FUSED
+#define CWQ_SMALL_FUSED 1  // 0: the three-kernel path for every block length
+#endif
+// true: the launch also wrote the step's indices and sample (k_small_fused)
 template <bool STEP0>
-static void launch_small(const EncodeArgs& a, int step, hipStream_t stream) {
+static bool launch_small(const EncodeArgs& a, int step, hipStream_t stream) {
+  if (CWQ_SMALL_FUSED && a.max_d >= 0 && a.max_d <= CWQ_FUSED_DMAX && a.n_cand < 4096) {
+    hipLaunchKernelGGL((k_small_fused<STEP0>), dim3(grid_for(a.nb, 16, 1u << 20)), dim3(256), 0,
+                       stream, a.t_loc, a.t_scale, a.loc_s, a.scale_s, a.lognorm, a.out_sample,
+                       a.block_off, a.ud, a.nb, a.n_cand, seeds_of(a), step, a.n_steps,
+                       a.out_idx);
+    return true;
+  }
   const int64_t ntiles = a.nb * a.tiles_per_block;
   hipLaunchKernelGGL((k_small_prep<STEP0>), dim3(grid_for(a.nb, 4 * 64, 16384)), dim3(256), 0,
                      stream, a.t_loc, a.t_scale, a.loc_s, a.scale_s, a.lognorm, a.out_sample,
@@ -2480,41 +2953,45 @@ static void launch_small(const EncodeArgs& a, int step, hipStream_t stream) {
                      a.out_sample, a.block_off, a.ud, a.nb, a.n_cand, seeds_of(a), step,
                      (const float4*)a.grp, (const uint32_t*)a.gtau, (const uint32_t*)a.ordu,
                      (const uint2*)a.slist, (const float*)a.bpre, a.keys);
+  return false;
 }
 
+// Scoring launches of one step; true when they also finalized it (indices and
+// sample written), false when k_encode_finalize must follow.
 template <bool STEP0>
-static void launch_eval_dc(const EncodeArgs& a, int step, hipStream_t stream) {
+static bool launch_eval_dc(const EncodeArgs& a, int step, hipStream_t stream) {
   // pruned path: uniform D % 8 == 0, D <= 64, Philox block index n*D/4 < 2^32
   if (a.block_off == nullptr && a.prune && a.ud % 8 == 0 && a.ud >= 8 && a.ud <= 64 &&
       a.n_cand * (a.ud / 4) <= (1LL << 32)) {
     switch (a.ud) {
-      case 8: return launch_prune_t<8, STEP0>(a, step, stream);
-      case 16: return launch_prune_t<16, STEP0>(a, step, stream);
-      case 24: return launch_prune_t<24, STEP0>(a, step, stream);
-      case 32: return launch_prune_t<32, STEP0>(a, step, stream);
-      case 40: return launch_prune_t<40, STEP0>(a, step, stream);
-      case 48: return launch_prune_t<48, STEP0>(a, step, stream);
-      case 56: return launch_prune_t<56, STEP0>(a, step, stream);
-      case 64: return launch_prune_t<64, STEP0>(a, step, stream);
+      case 8: return launch_prune_t<8, STEP0>(a, step, stream), false;
+      case 16: return launch_prune_t<16, STEP0>(a, step, stream), false;
+      case 24: return launch_prune_t<24, STEP0>(a, step, stream), false;
+      case 32: return launch_prune_t<32, STEP0>(a, step, stream), false;
+      case 40: return launch_prune_t<40, STEP0>(a, step, stream), false;
+      case 48: return launch_prune_t<48, STEP0>(a, step, stream), false;
+      case 56: return launch_prune_t<56, STEP0>(a, step, stream), false;
+      case 64: return launch_prune_t<64, STEP0>(a, step, stream), false;
       default: break;
     }
   }
   // general pruned path (screening): CSR or other uniform d, >= 4096 candidates
   if (a.prune >= 2 && a.sab != nullptr && a.n_cand >= 4096)
-    return launch_prune_csr<STEP0>(a, step, stream);
+    return launch_prune_csr<STEP0>(a, step, stream), false;
   // screened small-candidate path (k_small_*): few candidates per block
   if (a.prune >= 2 && a.sab != nullptr && a.slist != nullptr && a.ordu != nullptr &&
       a.n_cand >= CWQ_SMALL_MIN_CAND)
     return launch_small<STEP0>(a, step, stream);
   if (a.block_off == nullptr) {
     switch (a.ud) {
-      case 8: return launch_eval_t<8, STEP0>(a, step, stream);
-      case 16: return launch_eval_t<16, STEP0>(a, step, stream);
-      case 32: return launch_eval_t<32, STEP0>(a, step, stream);
+      case 8: return launch_eval_t<8, STEP0>(a, step, stream), false;
+      case 16: return launch_eval_t<16, STEP0>(a, step, stream), false;
+      case 32: return launch_eval_t<32, STEP0>(a, step, stream), false;
       default: break;
     }
   }
   launch_eval_t<0, STEP0>(a, step, stream);
+  return false;
 }
 
 // The step loop of one block range on one stream: reset the argmax keys, score
@@ -2536,16 +3013,15 @@ static hipError_t encode_steps(const EncodeArgs& a, hipStream_t stream, bool eve
       e = hipEventRecord((hipEvent_t)a.ev_start, stream);
       if (e != hipSuccess) return e;
     }
-    if (s == 0)
-      launch_eval_dc<true>(a, s, stream);
-    else
-      launch_eval_dc<false>(a, s, stream);
+    const bool finalized =
+        s == 0 ? launch_eval_dc<true>(a, s, stream) : launch_eval_dc<false>(a, s, stream);
     if (events && s == a.n_steps - 1 && a.ev_stop) {
       e = hipEventRecord((hipEvent_t)a.ev_stop, stream);
       if (e != hipSuccess) return e;
     }
     e = hipGetLastError();
     if (e != hipSuccess) return e;
+    if (finalized) continue;
     if (q4_shape(a.block_off, a.ud) && aligned16(a.loc_s, a.scale_s, a.out_sample)) {
       const uint32_t qpb = (uint32_t)(a.ud / 4), bpw = 64u / qpb;
       hipLaunchKernelGGL(k_encode_finalize_q4, dim3(grid_for(a.nb, 4 * (int64_t)bpw, 1u << 20)),

@@ -8,6 +8,8 @@
 #   tools/gpu_task.sh pmc TAG SET [bench args]   one PMC set (mem | valu | wait | lds),
 #                                                one rocprofv3 pass per counter group
 #   tools/gpu_task.sh stress [N]                 CSR + small-path stress sweeps
+#   tools/gpu_task.sh variants TAG "V1 V2" [bench args]   tools/variants.sh run -> gpurun_out/v_TAG.log
+#   tools/gpu_task.sh stats TAG VARIANT NB D BITS        tools/prune_stats.py on a stats build
 # Several tasks can be chained: tools/gpu_task.sh tests -- pmc c2 wait --config c2
 set -o pipefail
 cd "$(dirname "$0")/.."
@@ -49,7 +51,17 @@ run_one() {
       timeout -k 10 300 python -u tools/stress_csr.py $n ${STRESS_SEED:-20000} 200 \
         > gpurun_out/stress_csr.log 2>&1 && tail -1 gpurun_out/stress_csr.log && \
       STRESS_BITS=6,11 timeout -k 10 300 python -u tools/stress_csr.py $n ${STRESS_SEED:-20000} 200 \
-        > gpurun_out/stress_small.log 2>&1 && tail -1 gpurun_out/stress_small.log ;;
+        > gpurun_out/stress_small.log 2>&1 && tail -1 gpurun_out/stress_small.log && \
+      STRESS_SMALL=1 STRESS_BITS=6,11 timeout -k 10 300 python -u tools/stress_csr.py $n ${STRESS_SEED:-20000} 200 \
+        > gpurun_out/stress_fused.log 2>&1 && tail -1 gpurun_out/stress_fused.log ;;
+    variants)
+      local tag=$1 vs=$2; shift 2
+      VARIANTS="$vs" BENCH_ARGS="$*" timeout -k 10 900 bash tools/variants.sh run \
+        > gpurun_out/v_$tag.log 2>&1 && cat gpurun_out/v_$tag.log ;;
+    stats)
+      local tag=$1 v=$2 nb=$3 d=$4 bits=$5
+      CWQ_LIB_PATH=$PWD/tools/variants/libcwq_$v.so PS_D=$d PS_BITS=$bits timeout -k 10 300 \
+        python -u tools/prune_stats.py $nb > gpurun_out/s_$tag.log 2>&1 && head -3 gpurun_out/s_$tag.log ;;
     *) echo "unknown task $task"; return 2 ;;
   esac
 }

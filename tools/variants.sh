@@ -81,6 +81,16 @@ declare -A V=(
   [seed18]="-DCWQ_SEED_LOG2=18"
   [seed20]="-DCWQ_SEED_LOG2=20"
   [stats0]="-DCWQ_PRUNE_STATS -DCWQ_SEED_LOG2=0"
+  [fw7]="-DCWQ_FUSED_WAVES=7"
+  [fw6]="-DCWQ_FUSED_WAVES=6"
+  [nofuse]="-DCWQ_SMALL_FUSED=0"
+  [ni0]="-DCWQ_FUSED_NOINLINE=0"
+  [tt8k]="-DCWQ_TARGET_TILES=8192"
+  [tt32k]="-DCWQ_TARGET_TILES=32768"
+  [tt64k]="-DCWQ_TARGET_TILES=65536"
+  [tauold]="-DCWQ_TAU_FROM_KEYS=0"
+  [seed16]="-DCWQ_SEED_LOG2=16"
+  [fw7ni0]="-DCWQ_FUSED_WAVES=7 -DCWQ_FUSED_NOINLINE=0"
 )
 if [ "$1" = build ]; then
   mkdir -p $OUT
