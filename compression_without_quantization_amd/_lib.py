@@ -113,6 +113,10 @@ SIGNATURES = {
 # Tools-only entry points (csrc/cwq_debug.h, not in include/cwq.h).
 TOOL_SIGNATURES = {
     "cwq_debug_prune_stats": (c_int, [c_vp, c_int]),
+    "cwq_debug_tile_times": (c_int, [c_vp, c_vp, c_vp, c_int]),
+    "cwq_debug_partition_workspace_size": (c_size, [c_i64]),
+    "cwq_debug_group_starts_device": (c_i64, [c_vp, c_i64, c_i64, c_f64, c_vp, c_vp, c_size,
+                                              c_vp, c_vp]),
 }
 
 # CWQ_ABI_VERSION of the include/cwq.h these signatures mirror: a library

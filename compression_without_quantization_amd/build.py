@@ -6,7 +6,8 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 OUT = os.path.join(HERE, "libcwq.so")
-SOURCES = ["cwq_kernels.hip", "cwq_importance.hip", "cwq_pln.hip", "cwq_capi.hip", "cwq_ac.cpp"]
+SOURCES = ["cwq_kernels.hip", "cwq_importance.hip", "cwq_pln.hip", "cwq_partition.hip", "cwq_capi.hip",
+           "cwq_ac.cpp"]
 HEADERS = ["cwq_math.h", "cwq_kernels.h", "cwq_device.h", "cwq_debug.h"]
 
 # -ffp-contract=off: every FMA in the arithmetic is explicit (bit-exactness).

@@ -163,6 +163,17 @@ void scan_sse(const float* kl, int64_t i0, int64_t i1, float thr, int64_t size_t
   }
 }
 
+// The smallest float32 thr with (double)thr >= n_nats (> when strict): the
+// reference's float64 comparison of a float32 sum s is then s >= thr.
+float group_thr(double n_nats, bool strict) {
+  auto cond = [&](float f) { return strict ? ((double)f > n_nats) : ((double)f >= n_nats); };
+  float thr = (float)n_nats;
+  while (!cond(thr) && thr < __builtin_inff()) thr = nextafterf(thr, __builtin_inff());
+  while (cond(nextafterf(thr, -__builtin_inff())) && thr > -__builtin_inff())
+    thr = nextafterf(thr, -__builtin_inff());
+  return thr;
+}
+
 // coded_greedy_sampler.py:207-252 (strict=false) and
 // coded_importance_sampler.py:178-203 (strict=true).
 int64_t group_starts_impl(const float* kl, int64_t D, int64_t size_threshold, double n_nats,
@@ -198,11 +209,7 @@ int64_t group_starts_impl(const float* kl, int64_t D, int64_t size_threshold, do
   // when strict).  For a float s that equals s >= thr with thr the smallest
   // float satisfying the comparison, so the scan stays in float32, and it is
   // branch-free (group boundaries are data-dependent: a branch mispredicts).
-  auto cond = [&](float f) { return strict ? ((double)f > n_nats) : ((double)f >= n_nats); };
-  float thr = (float)n_nats;
-  while (!cond(thr) && thr < __builtin_inff()) thr = nextafterf(thr, __builtin_inff());
-  while (cond(nextafterf(thr, -__builtin_inff())) && thr > -__builtin_inff())
-    thr = nextafterf(thr, -__builtin_inff());
+  const float thr = group_thr(n_nats, strict);
   if (D < 8 * 1024) {
     int64_t ns = 1;
     starts[0] = 0;
@@ -532,7 +539,7 @@ int cwq_destandardise(const float* sample, const float* p_loc, const float* p_sc
 // ---------------------------------------------------------------------------
 namespace {
 struct GroupedWs {
-  size_t t_loc, t_scale, kl, zeros, ones, sample, out, offs, idx, enc, total;
+  size_t t_loc, t_scale, kl, zeros, ones, sample, out, offs, idx, part, pinfo, enc, total;
 };
 // D dims in at most max_groups groups (a partition of D dims has at most D + 1:
 // the reference's forced boundary at D - 1 can leave an empty first group)
@@ -555,6 +562,8 @@ GroupedWs grouped_ws(int64_t D, int n_steps, int64_t max_groups) {
   const int64_t G = max_groups > 1 ? max_groups : 1;
   l.offs = take((size_t)(G + 1) * 8);
   l.idx = take((size_t)G * (size_t)(n_steps > 0 ? n_steps : 1) * 4);
+  l.part = take(cwq::partition_workspace_size(D > 0 ? D : 0));  // device partition scratch
+  l.pinfo = take(16 * sizeof(unsigned long long));  // partition info[8] + item info[2]
   l.enc = take(ws_layout_csr(G, D, D).total);
   l.total = o;
   return l;
@@ -615,6 +624,16 @@ hipError_t wait_event(hipEvent_t e) {
 }
 thread_local std::vector<float> g_kl_host;
 thread_local std::vector<int32_t> g_idx_host;
+thread_local unsigned long long g_part_info[16];  // info[8], then item 0's (G + 1, largest)
+// CWQ_HOST_PARTITION=1: the host partition loop even where the device one
+// applies (A/B timing; the results are identical)
+bool device_partition_enabled() {
+  static const bool on = [] {
+    const char* e = getenv("CWQ_HOST_PARTITION");
+    return !(e && e[0] == '1');
+  }();
+  return on;
+}
 // :81-87, :288 (and binary_io.py:41-53) each of n indices as n_bits LSB-first
 // '0'/'1' chars; returns n * n_bits, or CWQ_ERR_INVALID for an index that does
 // not fit (to_bit_string raises there).
@@ -699,6 +718,11 @@ int64_t grouped_begin(const float* q_loc, const float* q_scale, const float* p_l
   int32_t* idx = (int32_t*)(w + l.idx);
   hipError_t e = hipSuccess;
   int rc;
+  // :207-252 the partition: on the device when it applies (cwq_partition.hip,
+  // bit-identical to the loop; no KL round trip), else the host loop
+  bool dev_part = false;
+  int64_t n = 0, maxd = 0;
+  bool kl_on_host = false;
   if (D > 0) {
     // :193-199 standardise; :201, :210 per-dim KL(target || proposal)
     if ((rc = cwq_standardise(q_loc, q_scale, p_loc, p_scale, D, t_loc, t_scale, stream)) < 0)
@@ -707,11 +731,36 @@ int64_t grouped_begin(const float* q_loc, const float* q_scale, const float* p_l
     if ((e = hipMemsetAsync(zeros, 0, (size_t)D * 4, s)) != hipSuccess) return hip_fail(e, "memset");
     if ((e = hipMemsetD32Async((hipDeviceptr_t)ones, 0x3f800000u, (size_t)D, s)) != hipSuccess)
       return hip_fail(e, "memset");
-    g_kl_host.resize((size_t)D);
-    if ((e = hipMemcpyAsync(g_kl_host.data(), kl, (size_t)D * 4, hipMemcpyDeviceToHost, s)) !=
-        hipSuccess)
-      return hip_fail(e, "KL to host");
-    if ((e = hipStreamSynchronize(s)) != hipSuccess) return hip_fail(e, "sync");
+    if (device_partition_enabled() && cwq::partition_applies(D, size_threshold)) {
+      unsigned long long* info_d = (unsigned long long*)(w + l.pinfo);
+      if ((e = cwq::launch_partition(kl, D, nullptr, 1, size_threshold, group_thr(n_nats, false),
+                                     offs, (int64_t*)(info_d + 8), w + l.part, info_d, s)) !=
+              hipSuccess ||
+          (e = hipMemcpyAsync(g_part_info, info_d, sizeof(g_part_info), hipMemcpyDeviceToHost,
+                              s)) != hipSuccess)
+        return hip_fail(e, "device partition");
+      if (kl_sum_out) {  // the log line's total KL only
+        g_kl_host.resize((size_t)D);
+        if ((e = hipMemcpyAsync(g_kl_host.data(), kl, (size_t)D * 4, hipMemcpyDeviceToHost, s)) !=
+            hipSuccess)
+          return hip_fail(e, "KL to host");
+        kl_on_host = true;
+      }
+      if ((e = hipStreamSynchronize(s)) != hipSuccess) return hip_fail(e, "sync");
+      if (!cwq::partition_fell_back(g_part_info)) {
+        dev_part = true;
+        n = (int64_t)g_part_info[8];
+        maxd = (int64_t)g_part_info[9];
+      }
+    }
+    if (!dev_part && !kl_on_host) {
+      g_kl_host.resize((size_t)D);
+      if ((e = hipMemcpyAsync(g_kl_host.data(), kl, (size_t)D * 4, hipMemcpyDeviceToHost, s)) !=
+          hipSuccess)
+        return hip_fail(e, "KL to host");
+      if ((e = hipStreamSynchronize(s)) != hipSuccess) return hip_fail(e, "sync");
+      kl_on_host = true;
+    }
   }
   lap("kl");
   if (kl_sum_out) {  // log line only: four independent accumulators
@@ -722,10 +771,16 @@ int64_t grouped_begin(const float* q_loc, const float* q_scale, const float* p_l
     for (; i < D; ++i) t[0] += (double)g_kl_host[(size_t)i];
     *kl_sum_out = (t[0] + t[2]) + (t[1] + t[3]);
   }
-  // :207-252 the sequential partition (host, exact reference semantics)
-  const int64_t n = group_starts_impl(D > 0 ? g_kl_host.data() : nullptr, D, size_threshold, n_nats,
-                                      starts_host, starts_cap, false);
-  if (n < 0) return n;
+  if (!dev_part) {
+    // :207-252 the sequential partition (host, exact reference semantics)
+    n = group_starts_impl(D > 0 ? g_kl_host.data() : nullptr, D, size_threshold, n_nats,
+                          starts_host, starts_cap, false);
+    if (n < 0) return n;
+    for (int64_t g = 0; g + 1 < n; ++g) {
+      const int64_t dg = starts_host[g + 1] - starts_host[g];
+      maxd = dg > maxd ? dg : maxd;
+    }
+  }
   const int64_t G = n - 1;
   lap("group");
   if (n_bits_cap_check && bits_cap < G * (int64_t)n_steps * n_bits_per_step)
@@ -735,13 +790,9 @@ int64_t grouped_begin(const float* q_loc, const float* q_scale, const float* p_l
   if (idx_cap < G * (int64_t)n_steps || !idx_host)
     return fail(CWQ_ERR_CAPACITY, "%s: index buffer %lld < %lld", who, (long long)idx_cap,
                 (long long)(G * n_steps));
-  int64_t maxd = 0;
-  for (int64_t g = 0; g < G; ++g) {
-    const int64_t dg = starts_host[g + 1] - starts_host[g];
-    maxd = dg > maxd ? dg : maxd;
-  }
-  if ((e = hipMemcpyAsync(offs, starts_host, (size_t)(G + 1) * 8, hipMemcpyHostToDevice, s)) !=
-      hipSuccess)
+  if (!dev_part &&
+      (e = hipMemcpyAsync(offs, starts_host, (size_t)(G + 1) * 8, hipMemcpyHostToDevice, s)) !=
+          hipSuccess)
     return hip_fail(e, "offsets to device");
   // :273-284 one greedy coder per group, seed + g
   if (o.eval_ms_out && (!tev->made(2, s, hipEventDefault) ||
@@ -763,6 +814,18 @@ int64_t grouped_begin(const float* q_loc, const float* q_scale, const float* p_l
   if ((e = hipMemcpyAsync(sample_host, out, (size_t)D * 4, hipMemcpyDeviceToHost, s)) !=
       hipSuccess)
     return hip_fail(e, "sample to host");
+  if (dev_part) {
+    // the group starts to the caller now (it reads them before _end), on a copy
+    // stream beside the encode: the partition has completed (synchronised above)
+    hipStream_t d2h = cwq::copy_stream(s, 0);
+    if (!d2h) d2h = s;
+    if ((e = hipMemcpyAsync(starts_host, offs, (size_t)(G + 1) * 8, hipMemcpyDeviceToHost,
+                            d2h)) != hipSuccess ||
+        (e = hipStreamSynchronize(d2h)) != hipSuccess) {
+      (void)hipStreamSynchronize(s);
+      return hip_fail(e, "starts to host");
+    }
+  }
   lap("enqueued");
   return G;
 }
@@ -890,14 +953,20 @@ namespace {
 // D + 2 n + 1 entries, indices / seeds D + n.
 struct BatchWs {
   GroupedWs g;
-  size_t seeds, total;
+  size_t seeds, ioff, dstarts, iinfo, itab, total;
 };
 BatchWs batch_ws(int64_t D, int64_t n_items, int n_steps) {
   BatchWs l;
   const int64_t n = n_items > 0 ? n_items : 0;
   l.g = grouped_ws(D, n_steps, D + 2 * n + 1);
   l.seeds = l.g.total;
-  l.total = align_up(l.seeds + (size_t)(D + n + 1) * 4, 256);
+  // the device partition: item offsets, the items' start lists (the host
+  // layout: item i at item_off[i] + 2 i), per-item counts, the layout table
+  l.ioff = align_up(l.seeds + (size_t)(D + n + 1) * 4, 256);
+  l.dstarts = align_up(l.ioff + (size_t)(n + 1) * 8, 256);
+  l.iinfo = align_up(l.dstarts + (size_t)(D + 2 * n + 1) * 8, 256);
+  l.itab = align_up(l.iinfo + (size_t)(2 * n + 2) * 8, 256);
+  l.total = align_up(l.itab + (size_t)(n + 1) * sizeof(cwq::BatchItem), 256);
   return l;
 }
 // Host staging of the batch (the caller's pinned memory, or thread-local
@@ -955,6 +1024,211 @@ int64_t batch_chunks() {
   return n;
 }
 thread_local std::vector<char> g_batch_host;
+thread_local std::vector<unsigned long long> g_batch_info;
+thread_local std::vector<cwq::BatchItem> g_batch_items;
+
+constexpr int64_t kBatchFellBack = INT64_MIN;
+
+// cwq_code_grouped_greedy_batch with every item's partition on the device
+// (cwq_partition.hip) and the chunks' group layouts built there too
+// (k_batch_layout): after one small copy of the items' group counts the host
+// only enqueues the chunks' encodes and writes the bitcode, on its threads, as
+// each chunk's indices arrive.  Returns kBatchFellBack (nothing written) when
+// the device partition does not cover the batch; the caller then runs the host
+// path.  Standardisation and KL are already queued on s.
+int64_t batch_device_path(int64_t n_items, const int64_t* item_off, int64_t D, int n_steps,
+                          int n_bits_per_step, const int32_t* seeds, float rho,
+                          int64_t size_threshold, double n_nats, float* sample_host,
+                          char* bits_host, int64_t bits_cap, int64_t* bits_off,
+                          int64_t* starts_host, int64_t* n_starts, char* w, size_t workspace_bytes,
+                          const BatchWs& bl, const cwq_options& o, const std::vector<int64_t>& ci,
+                          const float* t_loc, const float* t_scale, const float* kl,
+                          const float* zeros, const float* ones, float* sample, float* out,
+                          int64_t* offs, int32_t* idx, int32_t* bseed, int32_t* idx_h,
+                          CallEvents& evs, CallEvents& tev, const float* p_loc,
+                          const float* p_scale, hipStream_t s, hipStream_t d2h, hipStream_t h2d) {
+  const GroupedWs& l = bl.g;
+  const int64_t K = (int64_t)ci.size() - 1;
+  int64_t* ioff_d = (int64_t*)(w + bl.ioff);
+  int64_t* dst = (int64_t*)(w + bl.dstarts);
+  int64_t* iinfo_d = (int64_t*)(w + bl.iinfo);
+  cwq::BatchItem* itab_d = (cwq::BatchItem*)(w + bl.itab);
+  unsigned long long* info_d = (unsigned long long*)(w + l.pinfo);
+  hipEvent_t* done_ev = evs.ev.data() + K;
+  hipEvent_t* res_ev = evs.ev.data() + 3 * K;
+  auto drain = [&]() {
+    (void)hipStreamSynchronize(s);
+    (void)hipStreamSynchronize(d2h);
+    (void)hipStreamSynchronize(h2d);
+  };
+  hipError_t e;
+  g_batch_info.resize((size_t)(8 + 2 * n_items));
+  unsigned long long* hi = g_batch_info.data();
+  if ((e = hipMemcpyAsync(ioff_d, item_off, (size_t)(n_items + 1) * 8, hipMemcpyHostToDevice,
+                          s)) != hipSuccess ||
+      (e = cwq::launch_partition(kl, D, ioff_d, n_items, size_threshold, group_thr(n_nats, false),
+                                 dst, iinfo_d, w + l.part, info_d, s)) != hipSuccess ||
+      (e = hipMemcpyAsync(hi, info_d, 8 * 8, hipMemcpyDeviceToHost, s)) != hipSuccess ||
+      (e = hipMemcpyAsync(hi + 8, iinfo_d, (size_t)(2 * n_items) * 8, hipMemcpyDeviceToHost, s)) !=
+          hipSuccess ||
+      (e = hipStreamSynchronize(s)) != hipSuccess) {
+    drain();
+    return hip_fail(e, "cwq_code_grouped_greedy_batch: device partition");
+  }
+  if (cwq::partition_fell_back(hi)) return kBatchFellBack;
+  // the items' group counts; per chunk its groups, largest group and layout
+  std::vector<int64_t> gl((size_t)n_items), chunk_of((size_t)n_items);
+  std::vector<int64_t> cG((size_t)K, 0), cmaxd((size_t)K, 0);
+  g_batch_items.resize((size_t)n_items);
+  for (int64_t c = 0; c < K; ++c) {
+    const int64_t a = item_off[ci[(size_t)c]], gb = a + ci[(size_t)c];
+    int64_t g = 0;
+    for (int64_t i = ci[(size_t)c]; i < ci[(size_t)c + 1]; ++i) {
+      n_starts[i] = (int64_t)hi[8 + 2 * i];
+      const int64_t Gi = n_starts[i] - 1 > 0 ? n_starts[i] - 1 : 0;
+      gl[(size_t)i] = g;
+      chunk_of[(size_t)i] = c;
+      cmaxd[(size_t)c] = std::max<int64_t>(cmaxd[(size_t)c], (int64_t)hi[9 + 2 * i]);
+      cwq::BatchItem& it = g_batch_items[(size_t)i];
+      it.src = item_off[i] + 2 * i;
+      it.rel = item_off[i] - a;
+      it.go = gb + c + g;
+      it.gs = gb + g;
+      it.G = Gi;
+      it.seed = seeds[i];
+      it.pad = 0;
+      it.term = -1;
+      it.dc = 0;
+      g += Gi;
+      bits_off[i + 1] = bits_off[i] + Gi * (int64_t)n_steps * n_bits_per_step;
+    }
+    cG[(size_t)c] = g;
+    cwq::BatchItem& last = g_batch_items[(size_t)(ci[(size_t)c + 1] - 1)];
+    last.term = gb + c + g;  // the chunk's closing offset: its dims
+    last.dc = item_off[ci[(size_t)c + 1]] - a;
+  }
+  if (bits_off[n_items] > bits_cap) {
+    drain();
+    return fail(CWQ_ERR_CAPACITY, "cwq_code_grouped_greedy_batch: bits_cap %lld < %lld",
+                (long long)bits_cap, (long long)bits_off[n_items]);
+  }
+  if ((e = hipMemcpyAsync(itab_d, g_batch_items.data(), (size_t)n_items * sizeof(cwq::BatchItem),
+                          hipMemcpyHostToDevice, s)) != hipSuccess ||
+      (e = cwq::launch_batch_layout(itab_d, n_items, dst, offs, bseed, s)) != hipSuccess) {
+    drain();
+    return hip_fail(e, "cwq_code_grouped_greedy_batch: layout");
+  }
+  // the chunks: encode, destandardise, results to the host behind the next chunk
+  int64_t Gtot = 0;
+  int rc = CWQ_OK;
+  int64_t c_done = 0;
+  for (int64_t c = 0; c < K && rc == CWQ_OK; ++c) {
+    const int64_t a = item_off[ci[(size_t)c]], Dc = item_off[ci[(size_t)c + 1]] - a;
+    const int64_t gb = a + ci[(size_t)c], Gc = cG[(size_t)c];
+    Gtot += Gc;
+    if (o.eval_start_event && c == 0 &&
+        (e = hipEventRecord((hipEvent_t)o.eval_start_event, s)) != hipSuccess)
+      rc = hip_fail(e, "event");
+    if (rc == CWQ_OK && Gc > 0) {
+      if (o.eval_ms_out && (e = hipEventRecord(tev.ev[(size_t)(2 * c)], s)) != hipSuccess)
+        rc = hip_fail(e, "event");
+      cwq_options oc = o;
+      oc.eval_start_event = oc.eval_stop_event = nullptr;
+      oc.eval_ms_out = nullptr;
+      if (rc == CWQ_OK)  // :273-284 the chunk's groups in one launch sequence
+        rc = encode_impl(t_loc + a, t_scale + a, zeros + a, ones + a, offs + gb + c, 0, Gc, Dc,
+                         cmaxd[(size_t)c], n_bits_per_step, n_steps, 0, rho, 0,
+                         idx + gb * n_steps, sample + a, w + l.enc, workspace_bytes - l.enc, &oc,
+                         s, bseed + gb);
+      if (rc == CWQ_OK && o.eval_ms_out &&
+          (e = hipEventRecord(tev.ev[(size_t)(2 * c + 1)], s)) != hipSuccess)
+        rc = hip_fail(e, "event");
+      if (rc == CWQ_OK)  // :292 destandardise
+        rc = cwq_destandardise(sample + a, p_loc + a, p_scale + a, Dc, out + a, s);
+    } else if (rc == CWQ_OK && Dc > 0 &&
+               (e = hipMemsetAsync(out + a, 0, (size_t)Dc * 4, s)) != hipSuccess) {
+      rc = hip_fail(e, "memset");
+    }
+    if (rc == CWQ_OK && o.eval_stop_event && c == K - 1 &&
+        (e = hipEventRecord((hipEvent_t)o.eval_stop_event, s)) != hipSuccess)
+      rc = hip_fail(e, "event");
+    if (rc == CWQ_OK && ((e = hipEventRecord(res_ev[c], s)) != hipSuccess ||
+                         (e = hipStreamWaitEvent(d2h, res_ev[c], 0)) != hipSuccess))
+      rc = hip_fail(e, "event");
+    if (rc == CWQ_OK && Gc > 0 &&
+        (e = hipMemcpyAsync(idx_h + gb * n_steps, idx + gb * n_steps, (size_t)(Gc * n_steps) * 4,
+                            hipMemcpyDeviceToHost, d2h)) != hipSuccess)
+      rc = hip_fail(e, "indices to host");
+    if (rc == CWQ_OK && Dc > 0 &&
+        (e = hipMemcpyAsync(sample_host + a, out + a, (size_t)Dc * 4, hipMemcpyDeviceToHost,
+                            d2h)) != hipSuccess)
+      rc = hip_fail(e, "sample to host");
+    if (rc == CWQ_OK && (e = hipEventRecord(done_ev[c], d2h)) != hipSuccess)
+      rc = hip_fail(e, "event");
+    if (rc == CWQ_OK) c_done = c + 1;
+  }
+  // the items' start lists to the caller, beside the coding (the partition has
+  // completed: synchronised above)
+  for (int64_t i = 0; i < n_items && rc == CWQ_OK; ++i)
+    if ((e = hipMemcpyAsync(starts_host + item_off[i] + 2 * i, dst + item_off[i] + 2 * i,
+                            (size_t)n_starts[i] * 8, hipMemcpyDeviceToHost, h2d)) != hipSuccess)
+      rc = hip_fail(e, "starts to host");
+  // bitcode (:81-87, :288) item by item as its chunk's indices arrive, on the
+  // host threads and the calling thread
+  std::atomic<int64_t> next{0};
+  std::atomic<int> err{0};
+  auto bits_worker = [&]() {
+    for (;;) {
+      const int64_t i = next.fetch_add(1);
+      if (i >= n_items || err.load()) return;
+      const int64_t c = chunk_of[(size_t)i];
+      if (c >= c_done) return;
+      if (wait_event(done_ev[c]) != hipSuccess) {
+        int z = 0;
+        err.compare_exchange_strong(z, fail(CWQ_ERR_HIP, "results copy failed"));
+        return;
+      }
+      const int64_t gb = item_off[ci[(size_t)c]] + ci[(size_t)c];
+      const int64_t Gi = n_starts[i] - 1 > 0 ? n_starts[i] - 1 : 0;
+      const int64_t nw = write_bitcode(idx_h + (gb + gl[(size_t)i]) * n_steps, Gi * n_steps,
+                                       n_bits_per_step, bits_host + bits_off[i]);
+      if (nw < 0) {
+        int z = 0;
+        err.compare_exchange_strong(z, (int)nw);
+        return;
+      }
+      if (o.item_ready) __atomic_store_n(o.item_ready + i, 1, __ATOMIC_RELEASE);
+    }
+  };
+  std::vector<std::thread> pool;
+  if (rc == CWQ_OK) {
+    const int64_t nw = std::min<int64_t>(host_threads() - 1, n_items - 1);
+    try {
+      for (int64_t t = 0; t < nw; ++t) pool.emplace_back(bits_worker);
+    } catch (...) {
+    }
+    bits_worker();
+  }
+  for (auto& th : pool) th.join();
+  drain();
+  if (rc < 0) return rc;
+  if (err.load() < 0) return err.load();
+  if ((e = hipStreamSynchronize(s)) != hipSuccess) return hip_fail(e, "sync");
+  if (o.eval_ms_out) {
+    float tot = 0.0f;
+    for (int64_t c = 0; c < K; ++c) {
+      if (cG[(size_t)c] <= 0) continue;
+      float ms = 0.0f;
+      if ((e = hipEventElapsedTime(&ms, tev.ev[(size_t)(2 * c)], tev.ev[(size_t)(2 * c + 1)])) !=
+          hipSuccess)
+        return hip_fail(e, "event time");
+      tot += ms;
+    }
+    *o.eval_ms_out = tot;
+  }
+  cwq::set_error(CWQ_OK, "");
+  return Gtot;
+}
 
 }  // namespace
 
@@ -1096,6 +1370,18 @@ int64_t cwq_code_grouped_greedy_batch(
   if (D > 0 && (e = hipMemsetD32Async((hipDeviceptr_t)ones, 0x3f800000u, (size_t)D, s)) !=
                    hipSuccess)
     return hip_fail(e, "memset");
+  if (device_partition_enabled() && cwq::partition_applies(D, size_threshold)) {
+    // :207-252 every item's partition on the device (cwq_partition.hip: one walk
+    // over the batch, bit-identical to the host loop), then the chunks' group
+    // layouts on the device too: the host only sequences launches and writes the
+    // bitcode.  Falls through to the host path when the device one does not apply.
+    const int64_t r = batch_device_path(
+        n_items, item_off, D, n_steps, n_bits_per_step, seeds, rho, size_threshold, n_nats,
+        sample_host, bits_host, bits_cap, bits_off, starts_host, n_starts, w, workspace_bytes, bl,
+        o, ci, t_loc, t_scale, kl, zeros, ones, sample, out, offs, idx, bseed, idx_h, evs, tev,
+        p_loc, p_scale, s, d2h, h2d);
+    if (r != kBatchFellBack) return r;
+  }
   if ((e = hipEventRecord(kl_ready, s)) == hipSuccess) e = hipStreamWaitEvent(d2h, kl_ready, 0);
   for (int64_t c = 0; c < K && e == hipSuccess; ++c) {
     const int64_t a = a_of(c), n = a_of(c + 1) - a;
@@ -1617,6 +1903,44 @@ int cwq_selftest_screen_tables(uint32_t m0, int64_t count, float* radius, float*
       cwq::launch_selftest_screen(m0, count, radius, sin_out, cos_out, (hipStream_t)stream);
   if (e != hipSuccess) return hip_fail(e, "cwq_selftest_screen_tables");
   return ok();
+}
+
+size_t cwq_debug_partition_workspace_size(int64_t D) {
+  return D < 0 ? 0 : cwq::partition_workspace_size(D) + 16 * sizeof(unsigned long long);
+}
+
+int64_t cwq_debug_group_starts_device(const float* kl, int64_t D, int64_t size_threshold,
+                                      double n_nats, int64_t* starts, void* workspace,
+                                      size_t workspace_bytes, unsigned long long* info_host,
+                                      void* stream) {
+  if (!kl || !starts || !workspace || !info_host || D < 0)
+    return fail(CWQ_ERR_INVALID, "cwq_debug_group_starts_device: bad arguments");
+  if (!cwq::partition_applies(D, size_threshold)) return 0;
+  if (workspace_bytes < cwq_debug_partition_workspace_size(D))
+    return fail(CWQ_ERR_WORKSPACE, "cwq_debug_group_starts_device: workspace too small");
+  hipStream_t s = (hipStream_t)stream;
+  unsigned long long* info_d =
+      (unsigned long long*)((char*)workspace + cwq::partition_workspace_size(D));
+  hipError_t e = cwq::launch_partition(kl, D, nullptr, 1, size_threshold, group_thr(n_nats, false),
+                                       starts, (int64_t*)(info_d + 8), workspace, info_d, s);
+  unsigned long long h[16];
+  if (e == hipSuccess)
+    e = hipMemcpyAsync(h, info_d, sizeof(h), hipMemcpyDeviceToHost, s);
+  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  if (e != hipSuccess) return hip_fail(e, "cwq_debug_group_starts_device");
+  ok();
+  for (int i = 0; i < 8; ++i) info_host[i] = h[i];
+  info_host[0] = h[8] - 1;  // G
+  info_host[1] = h[9];      // largest group
+  return cwq::partition_fell_back(h) ? 0 : (int64_t)h[8];
+}
+
+int cwq_debug_tile_times(unsigned long long* t0, unsigned long long* t1, unsigned int* wg,
+                         int n) {
+  if (!t0 || !t1 || !wg || n < 0) return fail(CWQ_ERR_INVALID, "cwq_debug_tile_times: bad args");
+  const int r = cwq::tile_times(t0, t1, wg, n);
+  if (r < 0) return fail(CWQ_ERR_HIP, "cwq_debug_tile_times: symbol copy failed");
+  return r;
 }
 
 int cwq_debug_prune_stats(unsigned long long* out72, int flags) {

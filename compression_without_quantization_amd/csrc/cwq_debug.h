@@ -5,6 +5,9 @@
 #ifndef CWQ_DEBUG_H_
 #define CWQ_DEBUG_H_
 
+#include <stddef.h>
+#include <stdint.h>
+
 #ifdef __cplusplus
 extern "C" {
 #endif
@@ -18,6 +21,24 @@ extern "C" {
  * experiment on / off (later launches start each tile at the best value the
  * last launch found for it). */
 int cwq_debug_prune_stats(unsigned long long* out72, int flags);
+
+/* Per-tile wall clock of the last k_encode_prune launch (s_memrealtime ticks,
+ * 100 MHz) and the workgroup that ran each tile, filled only by builds compiled
+ * with -DCWQ_TILE_TIMES (tools/tile_times.py); returns the entries copied (0 in
+ * other builds). */
+int cwq_debug_tile_times(unsigned long long* t0, unsigned long long* t1, unsigned int* wg, int n);
+
+/* The grouped coder's device partition (cwq_partition.hip) on a device KL
+ * array: starts (device, D + 2 int64) as cwq_group_starts computes them on the
+ * host.  Returns the number of starts, or 0 when the device path does not cover
+ * the input (info_host[2] / info_host[4]: the caller uses the host loop), or a
+ * negative code.  info_host: 8 entries (G, largest group, fallback, dup, longest
+ * jump). */
+size_t cwq_debug_partition_workspace_size(int64_t D);
+int64_t cwq_debug_group_starts_device(const float* kl, int64_t D, int64_t size_threshold,
+                                      double n_nats, int64_t* starts, void* workspace,
+                                      size_t workspace_bytes, unsigned long long* info_host,
+                                      void* stream);
 
 #ifdef __cplusplus
 }

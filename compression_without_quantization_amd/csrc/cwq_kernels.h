@@ -97,6 +97,29 @@ hipError_t launch_kl(const float* q_loc, const float* q_scale, const float* p_lo
 hipError_t launch_destandardise(const float* sample, const float* p_loc, const float* p_scale,
                                 int64_t n, float* out, hipStream_t stream);
 
+// The grouped coder's greedy partition on the device (cwq_partition.hip), of
+// one item (item_off == nullptr, n_items == 1) or of each item [item_off[k],
+// item_off[k+1]) of a batch (device offsets): item k's starts at starts +
+// item_off[k] + 2 k, iinfo[2k] their count (G + 1), iinfo[2k + 1] its largest
+// group.  partition_fell_back(info copied to the host): not covered, the caller
+// runs the host loop (the results never depend on which path ran).
+size_t partition_workspace_size(int64_t D);
+bool partition_applies(int64_t D, int64_t size_threshold);
+// One item of a batch in the device layout of its chunk's encode: its G groups
+// go to offs[go ...] (block offsets relative to the chunk's first dim: rel +
+// its starts at dstarts[src ...]) and seeds[gs ...] (seed + g, :282); term >= 0:
+// offs[term] = dc, the chunk's closing offset (written with the chunk's last item).
+struct BatchItem {
+  int64_t src, rel, go, gs, G, term, dc;
+  int32_t seed, pad;
+};
+hipError_t launch_batch_layout(const BatchItem* items, int64_t n_items, const int64_t* dstarts,
+                               int64_t* offs, int32_t* seeds, hipStream_t stream);
+hipError_t launch_partition(const float* kl, int64_t D, const int64_t* item_off, int64_t n_items,
+                            int64_t size_threshold, float thr, int64_t* starts, int64_t* iinfo,
+                            void* ws, unsigned long long* info, hipStream_t stream);
+bool partition_fell_back(const unsigned long long* info_host);
+
 size_t importance_workspace_size(int64_t nb, int64_t total_dims);
 hipError_t launch_imp_outliers(const float* kl, int64_t n, float limit, float* t_loc,
                                float* t_scale, uint8_t* keep, hipStream_t stream);
@@ -116,6 +139,7 @@ hipError_t launch_selftest_bm(uint32_t m0, int64_t count, float* rad, float* sn,
 hipError_t launch_selftest_screen(uint32_t m0, int64_t count, float* rad, float* sn, float* cs,
                                   hipStream_t stream);
 int prune_stats(unsigned long long* out72, int reset);
+int tile_times(unsigned long long* t0, unsigned long long* t1, unsigned int* wg, int n);
 hipError_t launch_selftest_wave_max(const float* x, int64_t nw, float* out, hipStream_t stream);
 hipError_t launch_selftest_div(const float* a, const float* b, int64_t n, float* out,
                                hipStream_t stream);

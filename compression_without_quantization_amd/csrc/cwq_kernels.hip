@@ -199,6 +199,13 @@ constexpr double kScreenPhi = (1.0 - kScreenEps) * (1.0 - 0x1p-21);
 constexpr double kScreenKappa = 0.7070958018530696;  // sqrt(phi (1 - 2^-24) / 2), rounded down
 
 
+#ifdef CWQ_TILE_TIMES
+// timing builds only (tools/tile_times.py): per tile of k_encode_prune its
+// start / end wall clock (s_memrealtime, 100 MHz) and the workgroup that ran it
+constexpr int kTileTimes = 1 << 18;
+__device__ unsigned long long g_tile_t0[kTileTimes], g_tile_t1[kTileTimes];
+__device__ unsigned int g_tile_wg[kTileTimes];
+#endif
 #ifdef CWQ_PRUNE_STATS
 // tuning builds only (tools/prune_stats.py): [0..64] candidates finished after
 // k units, [65] completed rows, [66] survivors pushed, [67] screened tiles;
@@ -262,6 +269,12 @@ __global__ void __launch_bounds__(256, CWQ_PRUNE_MIN_WAVES) k_encode_prune(
     // tile loop and spilled under the 6-waves/SIMD register budget
     uint32_t tid = threadIdx.x;
     asm volatile("" : "+v"(tid));
+#ifdef CWQ_TILE_TIMES
+    if (tid == 0 && tile < kTileTimes) {
+      g_tile_t0[tile] = __builtin_amdgcn_s_memrealtime();
+      g_tile_wg[tile] = blockIdx.x;
+    }
+#endif
     const int64_t g = inter ? tile % nbt : tile / tiles_per_block;
     const int64_t tt = inter ? tile / nbt : tile - g * tiles_per_block;
     const int64_t off = g * D;
@@ -575,6 +588,9 @@ __global__ void __launch_bounds__(256, CWQ_PRUNE_MIN_WAVES) k_encode_prune(
       if (mk) atomicMax(&keys[g], (unsigned long long)mk);
 #ifdef CWQ_PRUNE_STATS
       if (!g_seed_tau && g < kDbgBlocks) g_dbg_best[g] = mk;
+#endif
+#ifdef CWQ_TILE_TIMES
+      if (tile < kTileTimes) g_tile_t1[tile] = __builtin_amdgcn_s_memrealtime();
 #endif
     }
 #ifdef CWQ_PRUNE_STATS
@@ -3242,6 +3258,20 @@ hipError_t launch_selftest_screen(uint32_t m0, int64_t count, float* rad, float*
   hipLaunchKernelGGL(k_selftest_screen, dim3(grid_for(count, 256, 65536)), dim3(256), 0, stream,
                      m0, count, rad, sn, cs);
   return hipGetLastError();
+}
+
+int tile_times(unsigned long long* t0, unsigned long long* t1, unsigned int* wg, int n) {
+#ifdef CWQ_TILE_TIMES
+  if (n > kTileTimes) n = kTileTimes;
+  if (hipMemcpyFromSymbol(t0, HIP_SYMBOL(g_tile_t0), (size_t)n * 8) != hipSuccess ||
+      hipMemcpyFromSymbol(t1, HIP_SYMBOL(g_tile_t1), (size_t)n * 8) != hipSuccess ||
+      hipMemcpyFromSymbol(wg, HIP_SYMBOL(g_tile_wg), (size_t)n * 4) != hipSuccess)
+    return -1;
+  return n;
+#else
+  (void)t0; (void)t1; (void)wg; (void)n;
+  return 0;
+#endif
 }
 
 int prune_stats(unsigned long long* out72, int reset) {

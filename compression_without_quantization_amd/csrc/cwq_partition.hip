@@ -1,0 +1,391 @@
+// cwq_partition.hip -- the grouped coder's greedy partition on the device
+// (coded_greedy_sampler.py:223-252), bit-identical to the sequential loop.
+//
+// The loop walks the dims once, carrying (float32 group KL, group size), and
+// starts a group at idx when size >= size_threshold, or kl + kl[idx] >= the
+// threshold, or idx == D - 1.  The carried state restarts at every group
+// start, so the loop is a walk through the functional graph
+//     nxt(i) = the next start after a start at i
+// from node 0: the starts are 0, nxt(0), nxt(nxt(0)), ... up to D - 1 (always a
+// start), preceded by the reference's [0] and, when dim 0 alone already trips
+// the test ("dup"), a second 0 (an empty first group).  Four launches:
+//   k_part_next   every nxt(i) (a thread per dim scanning forward; a scan
+//                 longer than kPartMaxJump dims marks the input "long" and
+//                 the caller partitions on the host);
+//   k_part_exit   per chunk of kPartW dims: for every dim i of the chunk
+//                 ex(i) = the first node at or past the chunk's end on the
+//                 walk from i (pointer jumping in LDS).  The walk enters chunk
+//                 c at some node within [b_c, M_c], M_c the farthest nxt(s)
+//                 of a dim s before b_c; when every candidate entry leads to
+//                 the same exit the chunk is "converged" and its exit does not
+//                 depend on which one it is (walks merge at a shared start);
+//   k_part_mark   per chunk: its entry (the exit of the nearest converged
+//                 chunk before it, followed through at most kPartRun others
+//                 by their stored ex of the entry), then the walk's nodes in
+//                 the chunk marked by pointer jumping in LDS, counted and
+//                 compacted;
+//   k_part_emit   per chunk: the global rank of its first node (sum of the
+//                 earlier chunks' counts), the walk's nodes in rank order;
+//   k_part_items  per item: its nodes (a rank range found by binary search)
+//                 as its own start list, group count and largest group.
+// Several items (the batch coder's latent sets) are one walk: an item's last
+// dim is a forced start whose group is that dim alone, so nxt of it is the
+// next item's first dim, which is therefore on the walk too.
+// Inputs the scheme does not cover (a group longer than kPartMaxJump, walks
+// that do not merge within kPartRun chunks) set info[2]; the caller then runs
+// the host loop, so the result never depends on which path ran.
+// ---------------------------------------------------------------------------
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "cwq_kernels.h"
+
+namespace cwq {
+
+constexpr int kPartW = 1024;        // dims per chunk
+constexpr int kPartMaxJump = 512;   // longest group the device path takes
+constexpr int kPartRun = 8;         // non-converged chunks a walk may cross
+constexpr int kPartThreads = 256;
+
+// info[0] nodes on the walk, info[2] fallback flag, info[4] longest nxt(i) - i
+// (when above kPartMaxJump: fallback).  Per item k: iinfo[2k] its starts (G + 1),
+// iinfo[2k + 1] its largest group.
+__device__ __forceinline__ int64_t item_end(const int64_t* __restrict__ item_off, int64_t n_items,
+                                            int64_t D, int64_t i) {
+  if (!item_off) return D;
+  int64_t lo = 0, hi = n_items;  // item_off[lo] <= i < item_off[hi]
+  while (hi - lo > 1) {
+    const int64_t m = (lo + hi) >> 1;
+    if (item_off[m] <= i) lo = m; else hi = m;
+  }
+  // empty items share their offset with the next one: skip to the last match
+  return item_off[hi];
+}
+
+template <class T>
+__device__ __forceinline__ T block_max(T v, T* red);
+
+__global__ void __launch_bounds__(256) k_part_next(const float* __restrict__ kl, int64_t D,
+                                                   const int64_t* __restrict__ item_off,
+                                                   int64_t n_items, int64_t T, float thr,
+                                                   int32_t* __restrict__ nxt,
+                                                   unsigned long long* __restrict__ info) {
+  __shared__ int32_t red[256];
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  int32_t jump = 0;
+  if (i < D) {
+    const int64_t iend = item_end(item_off, n_items, D, i);
+    int64_t j = i + 1;
+    if (i < iend - 1) {
+      float cur = kl[i];  // a group started at i: (kl[i], size 1)
+      int64_t size = 1;
+      for (; j < iend - 1; ++j) {  // the item's last dim always starts a group (:234)
+        const float s = cur + kl[j];  // float32 running sum (:233, :243)
+        if (size >= T || s >= thr) break;
+        cur = s;
+        ++size;
+        if (j - i >= kPartMaxJump) {  // longer than the device path takes
+          ++j;                        // (jump > kPartMaxJump: the fallback)
+          break;
+        }
+      }
+    }  // i == iend - 1: the item's last group is that dim; the walk goes on at iend
+    jump = (int32_t)(j - i);  // > kPartMaxJump: not covered (the scan stopped early)
+    nxt[i] = (int32_t)j;
+  }
+  const int32_t mj = block_max(jump, red);  // one atomic per workgroup
+  if (threadIdx.x == 0 && mj > 32) atomicMax(&info[4], (unsigned long long)mj);
+}
+
+template <class T>
+__device__ __forceinline__ T block_max(T v, T* red) {
+  red[threadIdx.x] = v;
+  __syncthreads();
+  for (int w = kPartThreads / 2; w > 0; w >>= 1) {
+    if ((int)threadIdx.x < w) red[threadIdx.x] = red[threadIdx.x] > red[threadIdx.x + w]
+                                                     ? red[threadIdx.x]
+                                                     : red[threadIdx.x + w];
+    __syncthreads();
+  }
+  const T r = red[0];
+  __syncthreads();
+  return r;
+}
+
+// p[l] := the first node >= lim (the chunk's end, or D) on the walk from
+// b + l (in place: every update replaces a node of the walk by a later one,
+// never past the exit)
+__device__ __forceinline__ void part_jump(int32_t* p, int64_t b, int32_t lim, int n) {
+  for (int r = 0; r < 11; ++r) {  // 2^11 > kPartW
+    for (int l = threadIdx.x; l < n; l += kPartThreads) {
+      const int32_t v = p[l];
+      if (v < lim) p[l] = p[v - b];
+    }
+    __syncthreads();
+  }
+}
+
+__global__ void __launch_bounds__(256) k_part_exit(const int32_t* __restrict__ nxt, int64_t D,
+                                                   int32_t* __restrict__ exg,
+                                                   int32_t* __restrict__ conv,
+                                                   const unsigned long long* __restrict__ info) {
+  __shared__ int32_t p[kPartW];
+  __shared__ int32_t red[kPartThreads];
+  if (info[4] > (unsigned long long)kPartMaxJump) return;  // host path
+  const int64_t c = blockIdx.x;
+  const int64_t b = c * kPartW;
+  const int n = (int)(D - b < kPartW ? D - b : kPartW);
+  const int32_t lim = (int32_t)(b + n);  // the chunk's end (the last chunk: D)
+  for (int l = threadIdx.x; l < n; l += kPartThreads) p[l] = nxt[b + l];
+  __syncthreads();
+  // M_c: the farthest node a dim before the chunk jumps to (chunk 0: entry 0)
+  int32_t m = (int32_t)b;
+  if (c > 0)
+    for (int64_t s = b - kPartMaxJump + threadIdx.x; s < b; s += kPartThreads)
+      if (s >= 0) m = nxt[s] > m ? nxt[s] : m;
+  const int32_t mc = block_max(m, red);
+  part_jump(p, b, lim, n);
+  // candidate entries [b, mc]: their exits, and whether they agree
+  const int ne = (int)(mc - b) + 1 < n ? (int)(mc - b) + 1 : n;
+  const int32_t e0 = p[0];
+  int32_t diff = 0;
+  for (int l = threadIdx.x; l < ne; l += kPartThreads) {
+    exg[b + l] = p[l];
+    diff |= p[l] != e0 ? 1 : 0;
+  }
+  const int32_t any = block_max(diff, red);
+  if (threadIdx.x == 0) conv[c] = any ? 0 : 1;
+}
+
+__global__ void __launch_bounds__(256) k_part_mark(const int32_t* __restrict__ nxt, int64_t D,
+                                                   const int32_t* __restrict__ exg,
+                                                   const int32_t* __restrict__ conv,
+                                                   int32_t* __restrict__ node,
+                                                   int32_t* __restrict__ cnt,
+                                                   unsigned long long* __restrict__ info) {
+  __shared__ int32_t ja[kPartW], jb[kPartW];
+  __shared__ uint8_t mark[kPartW];
+  __shared__ int32_t red[kPartThreads];
+  __shared__ int32_t s_entry;
+  if (info[4] > (unsigned long long)kPartMaxJump) return;
+  const int64_t c = blockIdx.x;
+  const int64_t b = c * kPartW;
+  const int n = (int)(D - b < kPartW ? D - b : kPartW);
+  const int32_t lim = (int32_t)(b + n);
+  if (threadIdx.x == 0) {
+    // the entry: the exit of the nearest converged chunk k < c (chunk 0 enters
+    // at node 0), followed through the chunks between by their stored exits
+    int32_t e = 0;
+    if (c > 0) {
+      int64_t k = c - 1;
+      int run = 0;
+      while (k > 0 && !conv[k] && run < kPartRun) {
+        --k;
+        ++run;
+      }
+      if (k > 0 && !conv[k]) {
+        info[2] = 1ull;  // walks that do not merge: host path
+        e = -1;
+      } else {
+        e = exg[k * kPartW];  // converged (or chunk 0): its exit, from its first dim
+        for (int64_t k2 = k + 1; k2 < c && e >= 0; ++k2) e = exg[e];  // e in [b_k2, M_k2]
+      }
+    }
+    s_entry = e;
+  }
+  for (int l = threadIdx.x; l < n; l += kPartThreads) {
+    ja[l] = nxt[b + l];
+    mark[l] = 0;
+  }
+  __syncthreads();
+  const int32_t e = s_entry;
+  if (e < 0) return;
+  if (e < lim) {
+    if (threadIdx.x == 0) mark[e - b] = 1;
+    __syncthreads();
+    // pointer jumping: after round r every node within 2^(r+1) - 1 steps of
+    // the entry is marked (J_r = nxt^(2^r), double-buffered)
+    int32_t* J = ja;
+    int32_t* J2 = jb;
+    for (int r = 0; r < 11; ++r) {
+      for (int l = threadIdx.x; l < n; l += kPartThreads) {
+        const int32_t v = J[l];
+        if (mark[l] && v < lim) mark[v - b] = 1;
+      }
+      __syncthreads();
+      for (int l = threadIdx.x; l < n; l += kPartThreads) {
+        const int32_t v = J[l];
+        J2[l] = v < lim ? J[v - b] : v;
+      }
+      __syncthreads();
+      int32_t* t = J;
+      J = J2;
+      J2 = t;
+    }
+  }
+  // compact the marked nodes in order: per-thread runs of 4 consecutive dims
+  constexpr int kPer = kPartW / kPartThreads;
+  int mine = 0;
+  for (int q = 0; q < kPer; ++q) {
+    const int l = threadIdx.x * kPer + q;
+    mine += (l < n && mark[l]) ? 1 : 0;
+  }
+  red[threadIdx.x] = mine;
+  __syncthreads();
+  for (int o = 1; o < kPartThreads; o <<= 1) {  // inclusive scan
+    const int32_t t = (int)threadIdx.x >= o ? red[threadIdx.x - o] : 0;
+    __syncthreads();
+    red[threadIdx.x] += t;
+    __syncthreads();
+  }
+  int at = red[threadIdx.x] - mine;
+  for (int q = 0; q < kPer; ++q) {
+    const int l = threadIdx.x * kPer + q;
+    if (l < n && mark[l]) node[b + at++] = (int32_t)(b + l);
+  }
+  if (threadIdx.x == kPartThreads - 1) cnt[c] = red[threadIdx.x];
+}
+
+__global__ void __launch_bounds__(256) k_part_emit(int64_t nchunks,
+                                                   const int32_t* __restrict__ node,
+                                                   const int32_t* __restrict__ cnt,
+                                                   int32_t* __restrict__ gnode,
+                                                   unsigned long long* __restrict__ info) {
+  __shared__ int64_t red[kPartThreads];
+  if (info[4] > (unsigned long long)kPartMaxJump || info[2]) return;
+  const int64_t c = blockIdx.x;
+  const int64_t b = c * kPartW;
+  // rank of the chunk's first node: the earlier chunks' counts
+  int64_t s = 0;
+  for (int64_t k = threadIdx.x; k < c; k += kPartThreads) s += cnt[k];
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int w = kPartThreads / 2; w > 0; w >>= 1) {
+    if ((int)threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+    __syncthreads();
+  }
+  const int64_t r0 = red[0];
+  const int nc = cnt[c];
+  for (int q = threadIdx.x; q < nc; q += kPartThreads) gnode[r0 + q] = node[b + q];
+  if (threadIdx.x == 0 && c == nchunks - 1) info[0] = (unsigned long long)(r0 + nc);
+}
+
+__device__ __forceinline__ int64_t lower_bound_i32(const int32_t* __restrict__ a, int64_t n,
+                                                   int64_t v) {
+  int64_t lo = 0, hi = n;
+  while (lo < hi) {
+    const int64_t m = (lo + hi) >> 1;
+    if ((int64_t)a[m] < v) lo = m + 1; else hi = m;
+  }
+  return lo;
+}
+
+// Item k's start list (coded_greedy_sampler.py:207-252 on its dims alone) at
+// starts + item_off[k] + 2 k: [0], a second 0 when its first dim alone trips
+// the test (:232-233 from the loop's initial (size 0, kl 0)), its walk nodes
+// relative to its first dim, then its dim count (:252).
+__global__ void __launch_bounds__(256) k_part_items(const float* __restrict__ kl, int64_t D,
+                                                    const int64_t* __restrict__ item_off,
+                                                    int64_t T, float thr,
+                                                    const int32_t* __restrict__ nxt,
+                                                    const int32_t* __restrict__ gnode,
+                                                    int64_t* __restrict__ starts,
+                                                    int64_t* __restrict__ iinfo,
+                                                    const unsigned long long* __restrict__ info) {
+  __shared__ int32_t redi[kPartThreads];
+  __shared__ int64_t s_r[2];
+  if (info[4] > (unsigned long long)kPartMaxJump || info[2]) return;
+  const int64_t k = blockIdx.x;
+  const int64_t a = item_off ? item_off[k] : 0;
+  const int64_t e = item_off ? item_off[k + 1] : D;
+  const int64_t Dk = e - a;
+  int64_t* st = starts + a + 2 * k;
+  if (Dk == 0) {  // the loop never runs: [0, 0]
+    if (threadIdx.x == 0) {
+      st[0] = 0;
+      st[1] = 0;
+      iinfo[2 * k] = 2;
+      iinfo[2 * k + 1] = 0;
+    }
+    return;
+  }
+  const int64_t total = (int64_t)info[0];
+  if (threadIdx.x < 2) s_r[threadIdx.x] = lower_bound_i32(gnode, total, threadIdx.x ? e : a);
+  __syncthreads();
+  const int64_t r0 = s_r[0], cnt = s_r[1] - s_r[0];
+  const int64_t dup = (T <= 0 || kl[a] >= thr || Dk == 1) ? 1 : 0;
+  int32_t md = 0;
+  for (int64_t q = threadIdx.x; q < cnt; q += kPartThreads) {
+    const int32_t v = gnode[r0 + q];
+    st[dup + q] = v - a;  // st[dup + rank] = the rank-th node (rank 0: the first dim)
+    const int32_t gsz = nxt[v] - v;
+    md = gsz > md ? gsz : md;
+  }
+  const int32_t mdb = block_max(md, redi);
+  if (threadIdx.x == 0) {
+    st[0] = 0;              // the reference's initial [0]
+    st[dup + cnt] = Dk;     // :252
+    iinfo[2 * k] = dup + cnt + 1;
+    iinfo[2 * k + 1] = mdb;
+  }
+}
+
+__global__ void __launch_bounds__(256) k_batch_layout(const BatchItem* __restrict__ items,
+                                                      const int64_t* __restrict__ dstarts,
+                                                      int64_t* __restrict__ offs,
+                                                      int32_t* __restrict__ seeds) {
+  const BatchItem it = items[blockIdx.x];
+  for (int64_t g = threadIdx.x; g < it.G; g += blockDim.x) {
+    offs[it.go + g] = it.rel + dstarts[it.src + g];
+    seeds[it.gs + g] = (int32_t)((uint32_t)it.seed + (uint32_t)g);  // :282, int32 wrap
+  }
+  if (threadIdx.x == 0 && it.term >= 0) offs[it.term] = it.dc;
+}
+
+hipError_t launch_batch_layout(const BatchItem* items, int64_t n_items, const int64_t* dstarts,
+                               int64_t* offs, int32_t* seeds, hipStream_t stream) {
+  if (n_items <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_batch_layout, dim3((unsigned)n_items), dim3(256), 0, stream, items,
+                     dstarts, offs, seeds);
+  return hipGetLastError();
+}
+
+size_t partition_workspace_size(int64_t D) {
+  const int64_t nch = (D + kPartW - 1) / kPartW;
+  return (size_t)(4 * (D + 64) + 2 * (nch + 64)) * 4 + 64 * 8;
+}
+
+bool partition_fell_back(const unsigned long long* info) {
+  return info[4] > (unsigned long long)kPartMaxJump || info[2] != 0ull || info[0] == 0ull;
+}
+
+bool partition_applies(int64_t D, int64_t size_threshold) {
+  return D >= 2 && D < (1LL << 30) && size_threshold >= 1;
+}
+
+hipError_t launch_partition(const float* kl, int64_t D, const int64_t* item_off, int64_t n_items,
+                            int64_t size_threshold, float thr, int64_t* starts, int64_t* iinfo,
+                            void* ws, unsigned long long* info, hipStream_t stream) {
+  const int64_t nch = (D + kPartW - 1) / kPartW;
+  int32_t* nxt = (int32_t*)ws;
+  int32_t* exg = nxt + (D + 64);
+  int32_t* node = exg + (D + 64);
+  int32_t* gnode = node + (D + 64);
+  int32_t* conv = gnode + (D + 64);
+  int32_t* cnt = conv + (nch + 64);
+  hipError_t e = hipMemsetAsync(info, 0, 8 * sizeof(unsigned long long), stream);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k_part_next, dim3((unsigned)((D + 255) / 256)), dim3(256), 0, stream, kl, D,
+                     item_off, n_items, size_threshold, thr, nxt, info);
+  hipLaunchKernelGGL(k_part_exit, dim3((unsigned)nch), dim3(kPartThreads), 0, stream, nxt, D, exg,
+                     conv, info);
+  hipLaunchKernelGGL(k_part_mark, dim3((unsigned)nch), dim3(kPartThreads), 0, stream, nxt, D, exg,
+                     conv, node, cnt, info);
+  hipLaunchKernelGGL(k_part_emit, dim3((unsigned)nch), dim3(kPartThreads), 0, stream, nch, node,
+                     cnt, gnode, info);
+  hipLaunchKernelGGL(k_part_items, dim3((unsigned)n_items), dim3(kPartThreads), 0, stream, kl, D,
+                     item_off, size_threshold, thr, nxt, gnode, starts, iinfo, info);
+  return hipGetLastError();
+}
+
+}  // namespace cwq

@@ -1,0 +1,140 @@
+"""The grouped coder's device partition (csrc/cwq_partition.hip) against the
+host loop (cwq_group_starts, itself checked against the reference loop of
+coded_greedy_sampler.py:223-252 in tests/test_oracle.py): identical starts on
+every input the device path takes, and the documented fallback (return 0) on
+the inputs it does not (groups longer than 512 dims, walks that never merge)."""
+import ctypes
+
+import numpy as np
+import pytest
+import torch
+
+import compression_without_quantization_amd as C  # noqa: F401
+import compression_without_quantization_amd.coded_greedy_sampler as S
+from compression_without_quantization_amd import _lib
+
+pytestmark = pytest.mark.gpu
+
+
+def _host(kl, T, n_nats):
+    lib = _lib.load()
+    starts = np.empty(kl.size + 2, np.int64)
+    n = lib.cwq_group_starts(kl.ctypes.data, kl.size, T, float(n_nats), starts.ctypes.data,
+                             starts.size)
+    assert n > 0
+    return starts[:n]
+
+
+def _device(kl, T, n_nats):
+    lib = _lib.load()
+    D = kl.size
+    kd = torch.from_numpy(kl).cuda()
+    st = torch.full((D + 2,), -7, dtype=torch.int64, device="cuda")
+    wsz = int(lib.cwq_debug_partition_workspace_size(D))
+    ws = torch.empty(max(wsz, 1), dtype=torch.uint8, device="cuda")
+    info = np.zeros(8, np.uint64)
+    n = lib.cwq_debug_group_starts_device(kd.data_ptr(), D, T, float(n_nats), st.data_ptr(),
+                                          ws.data_ptr(), wsz, info.ctypes.data,
+                                          torch.cuda.current_stream().cuda_stream)
+    assert n >= 0, _lib.load().cwq_last_error()
+    return (st[:n].cpu().numpy() if n else None), info
+
+
+def _check(kl, bits=8, mgsb=12, expect_device=None):
+    kl = np.ascontiguousarray(kl, dtype=np.float32)
+    T = S.group_size_threshold(mgsb)
+    n_nats = bits * np.log(2) - 1
+    want = _host(kl, T, n_nats)
+    got, info = _device(kl, T, n_nats)
+    if expect_device is not None:
+        assert (got is not None) == expect_device, (kl.size, info)
+    if got is not None:
+        assert np.array_equal(got, want), (kl.size, got[:20], want[:20])
+        G = want.size - 1
+        assert int(info[0]) == G
+        assert int(info[1]) == int(np.diff(want).max())
+    return got is not None
+
+
+def test_partition_random_sizes():
+    rng = np.random.default_rng(5)
+    for D in (2, 3, 4, 5, 7, 63, 100, 1023, 1024, 1025, 2047, 2048, 2049, 5000, 65536):
+        kl = rng.exponential(0.8, D)
+        _check(kl, expect_device=True)
+
+
+def test_partition_c2_sized_latents():
+    """A C2-like image (196,608 dims, 8 bits per group): the device path covers it."""
+    from compression_without_quantization_amd.synthetic import make_latents
+    q_loc, q_scale, p_loc, p_scale = make_latents(196608, bits_per_dim=1.1, seed=3)
+    kl = (np.log(p_scale / q_scale) + (q_scale ** 2 + (q_loc - p_loc) ** 2) / (2 * p_scale ** 2)
+          - 0.5).astype(np.float32)
+    assert _check(kl, expect_device=True)
+    # the c2cli rate (30 x 14 bits per group: ~376-dim groups) fits too
+    _check(kl, bits=420)
+
+
+def test_partition_dup_and_edges():
+    rng = np.random.default_rng(9)
+    n_nats = 8 * np.log(2) - 1
+    for D in (2, 3, 10, 3000):
+        kl = rng.exponential(0.5, D).astype(np.float32)
+        kl[0] = np.float32(n_nats + 1.0)  # dim 0 alone trips the test: an empty first group
+        _check(kl)
+        kl[0] = np.float32(n_nats)        # exactly at the threshold (>=)
+        _check(kl)
+        kl[-1] = np.float32(50.0)         # huge last dims
+        kl[-2] = np.float32(50.0)
+        _check(kl)
+    # zeros, negatives, NaN and inf in the KL (the float compares as the loop's)
+    kl = rng.exponential(0.7, 4000).astype(np.float32)
+    kl[::97] = 0.0
+    kl[5::131] = -0.25
+    kl[7::499] = np.nan
+    kl[11::777] = np.inf
+    _check(kl)
+
+
+def test_partition_size_threshold_groups():
+    """Small size thresholds (max_group_size_bits 2..4): groups cut by size."""
+    rng = np.random.default_rng(13)
+    for mgsb in (2, 3, 4):
+        kl = rng.exponential(0.3, 20000).astype(np.float32)
+        _check(kl, mgsb=mgsb)
+
+
+def test_partition_fallbacks():
+    """Inputs the device path leaves to the host loop: equal-length groups whose
+    walks never merge, and groups longer than 512 dims."""
+    kl = np.full(10000, 1.0, np.float32)  # every group 5 dims from wherever it starts
+    assert _check(kl) in (False, True)    # identical when taken, host loop otherwise
+    kl = np.full(5000, 1e-4, np.float32)  # groups of thousands of dims
+    assert _check(kl, expect_device=False) is False
+
+
+def test_grouped_coder_device_partition_equals_host(monkeypatch):
+    """The whole grouped pipeline with the device partition equals the host
+    loop's (CWQ_HOST_PARTITION=1 in a subprocess) on a C2-sized image."""
+    import json
+    import os
+    import subprocess
+    import sys
+    code = (
+        "import json, numpy as np, torch\n"
+        "import compression_without_quantization_amd as C\n"
+        "import compression_without_quantization_amd.coded_greedy_sampler as S\n"
+        "from compression_without_quantization_amd.synthetic import make_latents\n"
+        "S.VERBOSE = False\n"
+        "q, qs, p, ps = make_latents(50000, bits_per_dim=1.1, seed=21)\n"
+        "t = C.Normal(torch.from_numpy(q).cuda(), torch.from_numpy(qs).cuda())\n"
+        "r = C.Normal(torch.from_numpy(p).cuda(), torch.from_numpy(ps).cuda())\n"
+        "s, b, st = C.code_grouped_greedy_sample(None, t, r, 1, 8, 42)\n"
+        "print(json.dumps([int(np.asarray(s).view(np.uint32).astype(np.uint64).sum()), b, st]))\n")
+    outs = []
+    for host in ("0", "1"):
+        env = dict(os.environ, CWQ_HOST_PARTITION=host)
+        r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True,
+                           timeout=240)
+        assert r.returncode == 0, r.stderr[-2000:]
+        outs.append(json.loads(r.stdout.strip().splitlines()[-1]))
+    assert outs[0] == outs[1]

@@ -10,6 +10,7 @@
 #   tools/gpu_task.sh stress [N]                 CSR + small-path stress sweeps
 #   tools/gpu_task.sh variants TAG "V1 V2" [bench args]   tools/variants.sh run -> gpurun_out/v_TAG.log
 #   tools/gpu_task.sh stats TAG VARIANT NB D BITS        tools/prune_stats.py on a stats build
+#   tools/gpu_task.sh tiles TAG NB D BITS                tools/tile_times.py on the tt build
 # Several tasks can be chained: tools/gpu_task.sh tests -- pmc c2 wait --config c2
 set -o pipefail
 cd "$(dirname "$0")/.."
@@ -62,6 +63,16 @@ run_one() {
       local tag=$1 v=$2 nb=$3 d=$4 bits=$5
       CWQ_LIB_PATH=$PWD/tools/variants/libcwq_$v.so PS_D=$d PS_BITS=$bits timeout -k 10 300 \
         python -u tools/prune_stats.py $nb > gpurun_out/s_$tag.log 2>&1 && head -3 gpurun_out/s_$tag.log ;;
+    c2parts)
+      timeout -k 10 300 python -u tools/c2_parts.py > gpurun_out/c2parts.log 2>&1 && cat gpurun_out/c2parts.log && \
+      CWQ_LIB_PATH=$PWD/tools/variants/libcwq_phases.so timeout -k 10 300 python -u bench.py --config c2 \
+        --no-cpu --no-e2e --steps 5 > gpurun_out/c2phases.log 2>&1 && grep cwq gpurun_out/c2phases.log | tail -8 && \
+      CWQ_LIB_PATH=$PWD/tools/variants/libcwq_phases.so timeout -k 10 300 python -u bench.py --config c3 \
+        --batch-only --no-cpu --no-e2e --steps 3 > gpurun_out/c3phases.log 2>&1 && grep -c cwq gpurun_out/c3phases.log ;;
+    tiles)
+      local tag=$1 nb=$2 d=$3 bits=$4
+      CWQ_LIB_PATH=$PWD/tools/variants/libcwq_tt.so timeout -k 10 300 \
+        python -u tools/tile_times.py $nb $d $bits > gpurun_out/tt_$tag.log 2>&1 && head -6 gpurun_out/tt_$tag.log ;;
     *) echo "unknown task $task"; return 2 ;;
   esac
 }

@@ -90,13 +90,14 @@ declare -A V=(
   [tt64k]="-DCWQ_TARGET_TILES=65536"
   [tauold]="-DCWQ_TAU_FROM_KEYS=0"
   [seed16]="-DCWQ_SEED_LOG2=16"
+  [tt]="-DCWQ_TILE_TIMES"
   [fw7ni0]="-DCWQ_FUSED_WAVES=7 -DCWQ_FUSED_NOINLINE=0"
 )
 if [ "$1" = build ]; then
   mkdir -p $OUT
   for k in ${VARIANTS:-"${!V[@]}"}; do
     [ "${V[$k]}" = prebuilt ] && continue  # built by hand from an older commit
-    hipcc $FLAGS ${V[$k]} -o $OUT/libcwq_$k.so $CSRC/cwq_kernels.hip $CSRC/cwq_importance.hip $CSRC/cwq_pln.hip $CSRC/cwq_capi.hip $CSRC/cwq_ac.cpp &
+    hipcc $FLAGS ${V[$k]} -o $OUT/libcwq_$k.so $CSRC/cwq_kernels.hip $CSRC/cwq_importance.hip $CSRC/cwq_pln.hip $CSRC/cwq_partition.hip $CSRC/cwq_capi.hip $CSRC/cwq_ac.cpp &
   done
   wait
 else
