@@ -372,7 +372,13 @@ def code_grouped_greedy_sample(sess, target, proposal, n_steps, n_bits_per_step,
             # two halves: the ~D/5-element Python list of group starts (~0.3 ms
             # for a Kodak image's 41k groups) is built while the device codes;
             # the sample comes back into page-locked memory it keeps alive
-            sample_h = torch.empty(max(D, 1), dtype=torch.float32, pin_memory=True).numpy()[:D]
+            # the group starts and the sample share one page-locked block (the
+            # starts arrive by DMA while the encode runs; the sample view keeps
+            # the block alive for the caller)
+            blk = torch.empty((D + 2) * 8 + max(D, 1) * 4, dtype=torch.uint8,
+                              pin_memory=True).numpy()
+            starts_h = blk[:(D + 2) * 8].view(np.int64)
+            sample_h = blk[(D + 2) * 8:].view(np.float32)[:D]
             idx_h = _pinned_scratch((D + 1) * n_steps * 4)
             G = _lib.check(lib.cwq_code_grouped_greedy_begin(
                 *args, sample_h.ctypes.data, idx_h.data_ptr(), (D + 1) * n_steps,

@@ -794,6 +794,17 @@ int64_t grouped_begin(const float* q_loc, const float* q_scale, const float* p_l
       (e = hipMemcpyAsync(offs, starts_host, (size_t)(G + 1) * 8, hipMemcpyHostToDevice, s)) !=
           hipSuccess)
     return hip_fail(e, "offsets to device");
+  // device partition: the group starts go to the caller (who reads them before
+  // _end) on a copy stream, queued before the encode's own copies so they do
+  // not wait behind it; the partition has completed (synchronised above)
+  hipStream_t d2h_starts = nullptr;
+  if (dev_part) {
+    d2h_starts = cwq::copy_stream(s, 0);
+    if (!d2h_starts) d2h_starts = s;
+    if ((e = hipMemcpyAsync(starts_host, offs, (size_t)(G + 1) * 8, hipMemcpyDeviceToHost,
+                            d2h_starts)) != hipSuccess)
+      return hip_fail(e, "starts to host");
+  }
   // :273-284 one greedy coder per group, seed + g
   if (o.eval_ms_out && (!tev->made(2, s, hipEventDefault) ||
                         hipEventRecord(tev->ev[0], s) != hipSuccess))
@@ -814,17 +825,9 @@ int64_t grouped_begin(const float* q_loc, const float* q_scale, const float* p_l
   if ((e = hipMemcpyAsync(sample_host, out, (size_t)D * 4, hipMemcpyDeviceToHost, s)) !=
       hipSuccess)
     return hip_fail(e, "sample to host");
-  if (dev_part) {
-    // the group starts to the caller now (it reads them before _end), on a copy
-    // stream beside the encode: the partition has completed (synchronised above)
-    hipStream_t d2h = cwq::copy_stream(s, 0);
-    if (!d2h) d2h = s;
-    if ((e = hipMemcpyAsync(starts_host, offs, (size_t)(G + 1) * 8, hipMemcpyDeviceToHost,
-                            d2h)) != hipSuccess ||
-        (e = hipStreamSynchronize(d2h)) != hipSuccess) {
-      (void)hipStreamSynchronize(s);
-      return hip_fail(e, "starts to host");
-    }
+  if (d2h_starts && (e = hipStreamSynchronize(d2h_starts)) != hipSuccess) {
+    (void)hipStreamSynchronize(s);
+    return hip_fail(e, "starts to host");
   }
   lap("enqueued");
   return G;
@@ -871,9 +874,11 @@ int64_t cwq_code_grouped_greedy(const float* q_loc, const float* q_scale, const 
                                   starts_cap, kl_sum_out, workspace, workspace_bytes, opts, o,
                                   &tev, 1, bits_cap, stream, who);
   if (G < 0) {
-    // work grouped_begin queued (the encode, the copies into g_idx_host) may
-    // still be in flight: drain it before g_idx_host or the events are reused
+    // work grouped_begin queued (the encode, the copies into g_idx_host and
+    // starts_host) may still be in flight: drain it before g_idx_host or the
+    // events are reused
     (void)hipStreamSynchronize((hipStream_t)stream);
+    if (hipStream_t c = cwq::copy_stream((hipStream_t)stream, 0)) (void)hipStreamSynchronize(c);
     return G;
   }
   hipError_t e;
@@ -910,8 +915,9 @@ int64_t cwq_code_grouped_greedy_begin(const float* q_loc, const float* q_scale,
                                   seed, rho, size_threshold, n_nats, sample_host, idx_host,
                                   idx_cap, starts_host, starts_cap, kl_sum_out, workspace,
                                   workspace_bytes, opts, o, nullptr, 0, 0, stream, who);
-  if (G < 0) {
-    (void)hipStreamSynchronize((hipStream_t)stream);  // nothing queued may outlive an error
+  if (G < 0) {  // nothing queued may outlive an error
+    (void)hipStreamSynchronize((hipStream_t)stream);
+    if (hipStream_t c = cwq::copy_stream((hipStream_t)stream, 0)) (void)hipStreamSynchronize(c);
     return G;
   }
   cwq::set_error(CWQ_OK, "");
@@ -965,7 +971,7 @@ BatchWs batch_ws(int64_t D, int64_t n_items, int n_steps) {
   l.ioff = align_up(l.seeds + (size_t)(D + n + 1) * 4, 256);
   l.dstarts = align_up(l.ioff + (size_t)(n + 1) * 8, 256);
   l.iinfo = align_up(l.dstarts + (size_t)(D + 2 * n + 1) * 8, 256);
-  l.itab = align_up(l.iinfo + (size_t)(2 * n + 2) * 8, 256);
+  l.itab = align_up(l.iinfo + (size_t)(4 * n + 4) * 8, 256);
   l.total = align_up(l.itab + (size_t)(n + 1) * sizeof(cwq::BatchItem), 256);
   return l;
 }

@@ -101,7 +101,7 @@ hipError_t launch_destandardise(const float* sample, const float* p_loc, const f
 // one item (item_off == nullptr, n_items == 1) or of each item [item_off[k],
 // item_off[k+1]) of a batch (device offsets): item k's starts at starts +
 // item_off[k] + 2 k, iinfo[2k] their count (G + 1), iinfo[2k + 1] its largest
-// group.  partition_fell_back(info copied to the host): not covered, the caller
+// group (iinfo holds 4 n_items entries: the rest is scratch).  partition_fell_back(info copied to the host): not covered, the caller
 // runs the host loop (the results never depend on which path ran).
 size_t partition_workspace_size(int64_t D);
 bool partition_applies(int64_t D, int64_t size_threshold);

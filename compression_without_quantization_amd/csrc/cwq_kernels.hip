@@ -158,6 +158,9 @@ constexpr float kPruneC1 = 0x1p-14f;
 #ifndef CWQ_PRUNE_MIN_WAVES
 #define CWQ_PRUNE_MIN_WAVES 6  // waves/SIMD the register allocator must allow (tools/variants.sh)
 #endif
+#ifndef CWQ_XCD_BALANCE
+#define CWQ_XCD_BALANCE 1  // INTER tiles: each XCD runs every block (see k_encode_prune)
+#endif
 #ifndef CWQ_TAU_SHARE_MASK
 #define CWQ_TAU_SHARE_MASK 15u  // share tau across the workgroup every 16 units
 #endif
@@ -226,7 +229,7 @@ __global__ void __launch_bounds__(256, CWQ_PRUNE_MIN_WAVES) k_encode_prune(
     const float* __restrict__ loc_s, const float* __restrict__ scale_s,
     const float* __restrict__ lognorm, const float* __restrict__ best, int64_t ntiles,
     int64_t tiles_per_block, int64_t cand_per_tile, int64_t n_cand, SeedSpec sd, int32_t step,
-    int allow_screen, unsigned long long* __restrict__ keys) {
+    int allow_screen, unsigned long long* __restrict__ keys, int64_t tail_from, int tail_div) {
   static_assert(D % 8 == 0 && D >= 8 && D <= 64, "pruned path: D % 8 == 0, D <= 64");
   constexpr int G = D / 4;
   constexpr int NF = STEP0 ? 6 : 7;  // loc_s, scale_s, mu, sigma, c, 1/sigma[, best]
@@ -272,14 +275,38 @@ __global__ void __launch_bounds__(256, CWQ_PRUNE_MIN_WAVES) k_encode_prune(
 #ifdef CWQ_TILE_TIMES
     if (tid == 0 && tile < kTileTimes) {
       g_tile_t0[tile] = __builtin_amdgcn_s_memrealtime();
-      g_tile_wg[tile] = blockIdx.x;
+      // HW_REG_XCC_ID (hwreg 20), bits [3:0]: the XCD this workgroup runs on
+      const uint32_t xcc = (uint32_t)__builtin_amdgcn_s_getreg((20) | (0 << 6) | ((4 - 1) << 11));
+      g_tile_wg[tile] = (xcc << 24) | (blockIdx.x & 0xffffffu);
     }
 #endif
-    const int64_t g = inter ? tile % nbt : tile / tiles_per_block;
-    const int64_t tt = inter ? tile / nbt : tile - g * tiles_per_block;
+    // XCD balance (INTER): workgroups go to the 8 XCDs round-robin by id, so
+    // with the block-interleaved order XCD x would run only the blocks == x
+    // (mod 8), and with few blocks per XCD their uneven pruning left XCDs idle
+    // at the end (tools/tile_times.py: 84% of the slots busy on 128 blocks).
+    // XCD x instead runs the x-th eighth of the interleaved order: every block,
+    // a contiguous range of its tiles.
+    // Only the full-size tiles are spread so: the short tail tiles (below) come
+    // last in their natural order, so every XCD gets its share of them too.
+    int64_t tord = tile;
+    const int64_t treg = inter ? nbt * tail_from : 0;  // full-size tiles
+    if (inter && CWQ_XCD_BALANCE && tile < treg && (treg & 7) == 0 && (gridDim.x & 7u) == 0)
+      tord = (tile & 7) * (treg >> 3) + (tile >> 3);
+    const int64_t g = inter ? tord % nbt : tile / tiles_per_block;
+    const int64_t tt = inter ? tord / nbt : tile - g * tiles_per_block;
     const int64_t off = g * D;
-    const int64_t n0 = tt * cand_per_tile;
-    const int64_t n1 = (n0 + cand_per_tile < n_cand) ? n0 + cand_per_tile : n_cand;
+    // a block's tiles from tail_from on are tail_div times smaller: the last
+    // rounds of the launch drain in short tiles (INTER; tail_div 1: no tail)
+    int64_t n0, csz;
+    if (tt < tail_from) {
+      n0 = tt * cand_per_tile;
+      csz = cand_per_tile;
+    } else {
+      csz = cand_per_tile / tail_div;
+      n0 = tail_from * cand_per_tile + (tt - tail_from) * csz;
+    }
+    const int64_t n1 = (n0 + csz < n_cand) ? n0 + csz : n_cand;
+    if (n0 >= n1) continue;  // (uniform) a tail piece past the block's candidates
     const PhiloxStream st =
         generate_key(step_seed(sd.of(g), step), 42);
 
@@ -2660,6 +2687,124 @@ __global__ void __launch_bounds__(256, CWQ_DECODE_MIN_WAVES) k_decode_q4(
   }
 }
 
+// Single-step decode with the chunks' inputs streamed into LDS by LDS-DMA
+// (global_load_lds, 16 B per lane; round 4).  The same group / chunk mapping
+// as k_decode_q4, but chunk j + 2's p_loc / p_scale / index rows are in
+// flight while chunk j's exact Box-Muller runs: the loads hold no VGPRs, so
+// the ~90-VGPR arithmetic no longer caps how many are outstanding.  A ring of
+// three slots per wave; a counted `s_waitcnt vmcnt` retires chunk j (the
+// count covers only the younger chunks' loads, so the stores issued in
+// between can only make it wait longer).  All LDS is one array (logf table
+// first): a second __shared__ object makes hipcc wait vmcnt(0) before every
+// LDS read (cdna_hip_programming.md, "three .s-level traps").
+#ifndef CWQ_DECODE_GLDS
+#define CWQ_DECODE_GLDS 1  // 0: the register-prefetch decoder for single-step codes too
+#endif
+#ifndef CWQ_GLDS_SLOTS
+#define CWQ_GLDS_SLOTS 2  // ring slots per wave (chunks in flight: slots - 1)
+#endif
+constexpr int kGldsSlots = CWQ_GLDS_SLOTS;
+static_assert(kGldsSlots == 2 || kGldsSlots == 3, "1 or 2 chunks ahead");
+constexpr int kGldsSlot = 1024 + 1024 + 256;  // p_loc, p_scale (64 x 16 B), index (64 x 4 B)
+#ifndef CWQ_GLDS_MIN_WAVES
+#define CWQ_GLDS_MIN_WAVES 7  // 69 VGPRs, 2 x 2.3 KB ring per wave (tools/variants.sh glds*)
+#endif
+__global__ void __launch_bounds__(256, CWQ_GLDS_MIN_WAVES) k_decode_q4_glds(
+    const int32_t* __restrict__ idx, const float4* __restrict__ p_loc,
+    const float4* __restrict__ p_scale, uint32_t qpb, uint32_t bpw, int64_t nb, int64_t n_cand,
+    float rho, int32_t seed, int64_t block_id_base, float4* __restrict__ out_sample) {
+  __shared__ __attribute__((aligned(16))) char lds[256 + 4 * kGldsSlots * kGldsSlot];
+  double* logtab = reinterpret_cast<double*>(lds);
+  if (threadIdx.x < 32) logtab[threadIdx.x] = kLogTabConst[threadIdx.x];
+  __syncthreads();
+  const Q4Lane L = q4_lane(qpb, bpw);
+  const uint32_t lane = threadIdx.x & 63u;
+  char* ring = lds + 256 + wave_id() * (kGldsSlots * kGldsSlot);
+  const int64_t B = (int64_t)bpw * qpb;
+  const int64_t ngroups = (nb + B - 1) / B;
+  const int64_t nwaves = (int64_t)gridDim.x * 4;
+  for (int64_t grp = (int64_t)blockIdx.x * 4 + wave_id(); grp < ngroups; grp += nwaves) {
+    const int64_t gb0 = grp * B;
+    const PhiloxStream kl = generate_key(step_seed(block_seed(seed, block_id_base + gb0 + lane), 0), 42);
+    const uint32_t J = qpb;
+    // chunk j's rows: lane -> block gb0 + j bpw + lb, Philox block q (contiguous
+    // float4s); lanes past nb or the group read row 0 (valid memory, unused)
+    auto issue = [&](uint32_t j) {
+      char* slot = ring + (j % kGldsSlots) * kGldsSlot;
+      const int64_t g = gb0 + (int64_t)(j * bpw + L.lb);
+      const bool ok = L.active && g < nb;
+      const int64_t t = ok ? g * qpb + L.q : 0;
+      __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(p_loc + t),
+                                       (__attribute__((address_space(3))) void*)(slot),
+                                       16, 0, 0);
+      __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(p_scale + t),
+                                       (__attribute__((address_space(3))) void*)(slot + 1024),
+                                       16, 0, 0);
+      __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(idx + (ok ? g : 0)),
+                                       (__attribute__((address_space(3))) void*)(slot + 2048),
+                                       4, 0, 0);
+    };
+    constexpr uint32_t kAhead = kGldsSlots - 1;
+    for (uint32_t j = 0; j < kAhead && j < J; ++j) issue(j);
+    for (uint32_t j = 0; j < J; ++j) {
+      if (j + kAhead < J) issue(j + kAhead);
+      // retire chunk j: at most the younger chunks' loads (3 each) may stay in flight
+      const uint32_t younger = (J - 1 - j) < kAhead ? (J - 1 - j) : kAhead;
+      if (younger >= 2)
+        asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+      else if (younger == 1)
+        asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+      else
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      // the slot's rows by inline-asm LDS reads: hipcc would put a vmcnt(0)
+      // (every chunk in flight) in front of ordinary reads of DMA-written LDS
+      char* slot = ring + (j % kGldsSlots) * kGldsSlot;
+      const uint32_t a16 =
+          (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)(slot) + lane * 16u;
+      const uint32_t a4 =
+          (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)(slot + 2048) + lane * 4u;
+      float4 cl, cs;
+      int32_t n;
+      asm volatile(
+          "ds_read_b128 %0, %3\n\t"
+          "ds_read_b128 %1, %3 offset:1024\n\t"
+          "ds_read_b32 %2, %4\n\t"
+          "s_waitcnt lgkmcnt(0)"
+          : "=&v"(cl), "=&v"(cs), "=&v"(n)
+          : "v"(a16), "v"(a4)
+          : "memory");
+      const uint32_t src = j * bpw + L.lb;  // the lane holding this block's key
+      const PhiloxStream ku{(uint32_t)__shfl((int)kl.k0, (int)src, 64),
+                            (uint32_t)__shfl((int)kl.k1, (int)src, 64),
+                            (uint32_t)__shfl((int)kl.c2, (int)src, 64),
+                            (uint32_t)__shfl((int)kl.c3, (int)src, 64)};
+      const int64_t g = gb0 + (int64_t)src;
+      if (L.active && g < nb) {
+        float v[4];
+        if (n < 0 || n >= n_cand) {
+          v[0] = v[1] = v[2] = v[3] = __builtin_nanf("");
+        } else {
+          const F4 z = normal4_dev(ku, (uint64_t)n * qpb + L.q, logtab);
+          const float zz[4] = {z.a, z.b, z.c, z.d};
+          const float ls[4] = {cl.x, cl.y, cl.z, cl.w};
+          const float ss[4] = {rho * cs.x, rho * cs.y, rho * cs.z, rho * cs.w};
+#pragma unroll
+          for (int w = 0; w < 4; ++w) {
+            float sv = ss[w] * zz[w];
+            sv = ls[w] + sv;
+            v[w] = 0.0f + sv;  // :153 tile(sample) + samples, from tf.zeros (:143)
+          }
+        }
+        typedef float nt4 __attribute__((ext_vector_type(4)));
+        const nt4 vo = {v[0], v[1], v[2], v[3]};
+        __builtin_nontemporal_store(vo, reinterpret_cast<nt4*>(out_sample) + g * qpb + L.q);
+      }
+      // the slot is rewritten by issue(j + 3) next iteration: this wave's reads are done
+      __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
+    }
+  }
+}
+
 // ---------------------------------------------------------------------------
 // misc.py:3-17 materialised: out[n*d+j] = loc[j] + scale[j] * (z*1 + 0).
 // ---------------------------------------------------------------------------
@@ -2873,18 +3018,35 @@ static void launch_prune_t(const EncodeArgs& a, int step, hipStream_t stream) {
                        dim3((unsigned)(nt_s < kPruneGrid ? nt_s : kPruneGrid)), dim3(256), 0,
                        stream, a.t_loc, a.t_scale, a.loc_s, a.scale_s, a.lognorm, a.out_sample,
                        nt_s, seed_n / cpt_s, cpt_s, seed_n, seeds_of(a), step,
-                       a.prune >= 2 ? 1 : 0, a.keys);
+                       a.prune >= 2 ? 1 : 0, a.keys, seed_n / cpt_s, 1);
   }
-  if (CWQ_TILE_INTERLEAVE && (a.tiles_per_block > 1 || seeded))
-    hipLaunchKernelGGL((k_encode_prune<D, STEP0, true>), dim3(grid), dim3(256), 0, stream,
-                       a.t_loc, a.t_scale, a.loc_s, a.scale_s, a.lognorm, a.out_sample, ntiles,
-                       a.tiles_per_block, a.cand_per_tile, a.n_cand, seeds_of(a), step,
-                       a.prune >= 2 ? 1 : 0, a.keys);
-  else
+  if (CWQ_TILE_INTERLEAVE && (a.tiles_per_block > 1 || seeded)) {
+    // tail: the last tile of each block's few last tiles split in CWQ_TAIL_SPLIT,
+    // about two resident rounds (1,536 workgroups) of short tiles at the end
+#ifndef CWQ_TAIL_SPLIT
+#define CWQ_TAIL_SPLIT 4
+#endif
+    const int64_t tpb = a.tiles_per_block;
+    int64_t from = tpb, div = 1;
+    if (CWQ_TAIL_SPLIT > 1 && tpb >= 2 && a.cand_per_tile % (256 * CWQ_TAIL_SPLIT) == 0) {
+      div = CWQ_TAIL_SPLIT;
+      int64_t L = (2 * 1536 + div * a.nb - 1) / (div * a.nb);
+      L = L < tpb / 2 ? L : tpb / 2;
+      from = tpb - L;
+    }
+    const int64_t tpb2 = from + (tpb - from) * div;
+    const int64_t nt2 = a.nb * tpb2;
+    hipLaunchKernelGGL((k_encode_prune<D, STEP0, true>),
+                       dim3((unsigned)(nt2 < kPruneGrid ? nt2 : kPruneGrid)), dim3(256), 0,
+                       stream, a.t_loc, a.t_scale, a.loc_s, a.scale_s, a.lognorm, a.out_sample,
+                       nt2, tpb2, a.cand_per_tile, a.n_cand, seeds_of(a), step,
+                       a.prune >= 2 ? 1 : 0, a.keys, from, (int)div);
+  } else {
     hipLaunchKernelGGL((k_encode_prune<D, STEP0, false>), dim3(grid), dim3(256), 0, stream,
                        a.t_loc, a.t_scale, a.loc_s, a.scale_s, a.lognorm, a.out_sample, ntiles,
                        a.tiles_per_block, a.cand_per_tile, a.n_cand, seeds_of(a), step,
-                       a.prune >= 2 ? 1 : 0, a.keys);
+                       a.prune >= 2 ? 1 : 0, a.keys, a.tiles_per_block, 1);
+  }
 }
 
 template <bool STEP0>
@@ -3197,6 +3359,12 @@ hipError_t launch_decode(const int32_t* idx, const float* p_loc, const float* p_
   if (q4_shape(block_off, ud) && aligned16(p_loc, p_scale, out_sample)) {
     const uint32_t qpb = (uint32_t)(ud / 4), bpw = 64u / qpb;
     const int64_t ngroups = (nb + (int64_t)bpw * qpb - 1) / ((int64_t)bpw * qpb);
+    if (CWQ_DECODE_GLDS && n_steps == 1) {
+      hipLaunchKernelGGL(k_decode_q4_glds, dim3(grid_for(ngroups, 4, 1u << 20)), dim3(256), 0,
+                         stream, idx, (const float4*)p_loc, (const float4*)p_scale, qpb, bpw, nb,
+                         (int64_t)1 << n_bits, rho, seed, block_id_base, (float4*)out_sample);
+      return hipGetLastError();
+    }
     hipLaunchKernelGGL(k_decode_q4, dim3(grid_for(ngroups, 4, 1u << 20)), dim3(256), 0,
                        stream, idx, (const float4*)p_loc, (const float4*)p_scale, qpb, bpw, nb,
                        n_steps, (int64_t)1 << n_bits, nst, sdiv, rho, seed, block_id_base,

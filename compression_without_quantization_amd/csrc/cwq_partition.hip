@@ -26,8 +26,9 @@
 //                 compacted;
 //   k_part_emit   per chunk: the global rank of its first node (sum of the
 //                 earlier chunks' counts), the walk's nodes in rank order;
-//   k_part_items  per item: its nodes (a rank range found by binary search)
-//                 as its own start list, group count and largest group.
+//   k_part_ihdr / k_part_ibody  per item: its nodes (a rank range found by
+//                 binary search) as its own start list, group count and
+//                 largest group.
 // Several items (the batch coder's latent sets) are one walk: an item's last
 // dim is a forced start whose group is that dim alone, so nxt of it is the
 // next item's first dim, which is therefore on the walk too.
@@ -283,51 +284,80 @@ __device__ __forceinline__ int64_t lower_bound_i32(const int32_t* __restrict__ a
 // Item k's start list (coded_greedy_sampler.py:207-252 on its dims alone) at
 // starts + item_off[k] + 2 k: [0], a second 0 when its first dim alone trips
 // the test (:232-233 from the loop's initial (size 0, kl 0)), its walk nodes
-// relative to its first dim, then its dim count (:252).
-__global__ void __launch_bounds__(256) k_part_items(const float* __restrict__ kl, int64_t D,
-                                                    const int64_t* __restrict__ item_off,
-                                                    int64_t T, float thr,
+// relative to its first dim, then its dim count (:252).  k_part_ihdr: a thread
+// per item (its rank range by binary search, the ends of its list, its count);
+// k_part_ibody: a thread per walk node (its entry and group size).
+// iinfo: [2k] the item's starts (G + 1), [2k + 1] its largest group; scratch
+// [2n + 2k] its first node's rank, [2n + 2k + 1] dup.
+__global__ void __launch_bounds__(256) k_part_ihdr(const float* __restrict__ kl, int64_t D,
+                                                   const int64_t* __restrict__ item_off,
+                                                   int64_t n_items, int64_t T, float thr,
+                                                   const int32_t* __restrict__ gnode,
+                                                   int64_t* __restrict__ starts,
+                                                   int64_t* __restrict__ iinfo,
+                                                   const unsigned long long* __restrict__ info) {
+  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n_items || info[4] > (unsigned long long)kPartMaxJump || info[2]) return;
+  const int64_t a = item_off ? item_off[k] : 0;
+  const int64_t e = item_off ? item_off[k + 1] : D;
+  const int64_t Dk = e - a;
+  int64_t* st = starts + a + 2 * k;
+  iinfo[2 * k + 1] = 0;
+  if (Dk == 0) {  // the loop never runs: [0, 0]
+    st[0] = 0;
+    st[1] = 0;
+    iinfo[2 * k] = 2;
+    return;
+  }
+  const int64_t total = (int64_t)info[0];
+  const int64_t r0 = lower_bound_i32(gnode, total, a);
+  const int64_t cnt = lower_bound_i32(gnode, total, e) - r0;
+  const int64_t dup = (T <= 0 || kl[a] >= thr || Dk == 1) ? 1 : 0;
+  st[0] = 0;           // the reference's initial [0] (and the empty first group's)
+  st[dup + cnt] = Dk;  // :252
+  iinfo[2 * k] = dup + cnt + 1;
+  iinfo[2 * n_items + 2 * k] = r0;
+  iinfo[2 * n_items + 2 * k + 1] = dup;
+}
+
+__global__ void __launch_bounds__(256) k_part_ibody(int64_t D, const int64_t* __restrict__ item_off,
+                                                    int64_t n_items,
                                                     const int32_t* __restrict__ nxt,
                                                     const int32_t* __restrict__ gnode,
                                                     int64_t* __restrict__ starts,
                                                     int64_t* __restrict__ iinfo,
                                                     const unsigned long long* __restrict__ info) {
-  __shared__ int32_t redi[kPartThreads];
-  __shared__ int64_t s_r[2];
+  __shared__ int32_t red[kPartThreads];
+  __shared__ int64_t s_k0;
   if (info[4] > (unsigned long long)kPartMaxJump || info[2]) return;
-  const int64_t k = blockIdx.x;
-  const int64_t a = item_off ? item_off[k] : 0;
-  const int64_t e = item_off ? item_off[k + 1] : D;
-  const int64_t Dk = e - a;
-  int64_t* st = starts + a + 2 * k;
-  if (Dk == 0) {  // the loop never runs: [0, 0]
-    if (threadIdx.x == 0) {
-      st[0] = 0;
-      st[1] = 0;
-      iinfo[2 * k] = 2;
-      iinfo[2 * k + 1] = 0;
-    }
-    return;
-  }
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t total = (int64_t)info[0];
-  if (threadIdx.x < 2) s_r[threadIdx.x] = lower_bound_i32(gnode, total, threadIdx.x ? e : a);
+  int64_t k = -1;
+  int32_t gsz = 0;
+  if (r < total) {
+    const int32_t v = gnode[r];
+    k = 0;
+    if (item_off) {  // the item holding dim v (empty items share offsets: the last match)
+      int64_t lo = 0, hi = n_items;
+      while (hi - lo > 1) {
+        const int64_t m = (lo + hi) >> 1;
+        if (item_off[m] <= v) lo = m; else hi = m;
+      }
+      k = lo;
+    }
+    const int64_t a = item_off ? item_off[k] : 0;
+    const int64_t r0 = iinfo[2 * n_items + 2 * k], dup = iinfo[2 * n_items + 2 * k + 1];
+    starts[a + 2 * k + dup + (r - r0)] = v - a;  // st[dup + rank] (rank 0: the first dim)
+    gsz = nxt[v] - v;
+  }
+  // the largest group per item: one atomic for the block's first item, own ones
+  // for the (rare) nodes of other items
+  if (threadIdx.x == 0) s_k0 = k;
   __syncthreads();
-  const int64_t r0 = s_r[0], cnt = s_r[1] - s_r[0];
-  const int64_t dup = (T <= 0 || kl[a] >= thr || Dk == 1) ? 1 : 0;
-  int32_t md = 0;
-  for (int64_t q = threadIdx.x; q < cnt; q += kPartThreads) {
-    const int32_t v = gnode[r0 + q];
-    st[dup + q] = v - a;  // st[dup + rank] = the rank-th node (rank 0: the first dim)
-    const int32_t gsz = nxt[v] - v;
-    md = gsz > md ? gsz : md;
-  }
-  const int32_t mdb = block_max(md, redi);
-  if (threadIdx.x == 0) {
-    st[0] = 0;              // the reference's initial [0]
-    st[dup + cnt] = Dk;     // :252
-    iinfo[2 * k] = dup + cnt + 1;
-    iinfo[2 * k + 1] = mdb;
-  }
+  const int64_t k0 = s_k0;
+  if (k >= 0 && k != k0) atomicMax((unsigned long long*)&iinfo[2 * k + 1], (unsigned long long)gsz);
+  const int32_t m0 = block_max(k == k0 ? gsz : 0, red);
+  if (threadIdx.x == 0 && k0 >= 0) atomicMax((unsigned long long*)&iinfo[2 * k0 + 1], (unsigned long long)m0);
 }
 
 __global__ void __launch_bounds__(256) k_batch_layout(const BatchItem* __restrict__ items,
@@ -383,8 +413,10 @@ hipError_t launch_partition(const float* kl, int64_t D, const int64_t* item_off,
                      conv, node, cnt, info);
   hipLaunchKernelGGL(k_part_emit, dim3((unsigned)nch), dim3(kPartThreads), 0, stream, nch, node,
                      cnt, gnode, info);
-  hipLaunchKernelGGL(k_part_items, dim3((unsigned)n_items), dim3(kPartThreads), 0, stream, kl, D,
-                     item_off, size_threshold, thr, nxt, gnode, starts, iinfo, info);
+  hipLaunchKernelGGL(k_part_ihdr, dim3((unsigned)((n_items + 255) / 256)), dim3(256), 0, stream,
+                     kl, D, item_off, n_items, size_threshold, thr, gnode, starts, iinfo, info);
+  hipLaunchKernelGGL(k_part_ibody, dim3((unsigned)((D + 255) / 256)), dim3(kPartThreads), 0, stream,
+                     D, item_off, n_items, nxt, gnode, starts, iinfo, info);
   return hipGetLastError();
 }
 

@@ -10,7 +10,8 @@
 #   tools/gpu_task.sh stress [N]                 CSR + small-path stress sweeps
 #   tools/gpu_task.sh variants TAG "V1 V2" [bench args]   tools/variants.sh run -> gpurun_out/v_TAG.log
 #   tools/gpu_task.sh stats TAG VARIANT NB D BITS        tools/prune_stats.py on a stats build
-#   tools/gpu_task.sh tiles TAG NB D BITS                tools/tile_times.py on the tt build
+#   tools/gpu_task.sh tiles TAG NB D BITS [VARIANT]      tools/tile_times.py on a tile-times build
+#   tools/gpu_task.sh decvar "V1 V2"                     decode tests + timing per variant build
 # Several tasks can be chained: tools/gpu_task.sh tests -- pmc c2 wait --config c2
 set -o pipefail
 cd "$(dirname "$0")/.."
@@ -69,9 +70,17 @@ run_one() {
         --no-cpu --no-e2e --steps 5 > gpurun_out/c2phases.log 2>&1 && grep cwq gpurun_out/c2phases.log | tail -8 && \
       CWQ_LIB_PATH=$PWD/tools/variants/libcwq_phases.so timeout -k 10 300 python -u bench.py --config c3 \
         --batch-only --no-cpu --no-e2e --steps 3 > gpurun_out/c3phases.log 2>&1 && grep -c cwq gpurun_out/c3phases.log ;;
+    decvar)  # decode timing per variant, after its decode tests against the oracle
+      for v in $1; do
+        CWQ_LIB_PATH=$PWD/tools/variants/libcwq_$v.so timeout -k 10 300 python -u -m pytest \
+          tests/test_gpu.py -q -x -k decode --timeout 120 --timeout-method thread \
+          > gpurun_out/decvar_$v.log 2>&1 && tail -1 gpurun_out/decvar_$v.log || return 1
+      done
+      VARIANTS="$1" timeout -k 10 600 bash tools/decode_variants.sh > gpurun_out/decvar.log 2>&1 && \
+        cat gpurun_out/decvar.log ;;
     tiles)
-      local tag=$1 nb=$2 d=$3 bits=$4
-      CWQ_LIB_PATH=$PWD/tools/variants/libcwq_tt.so timeout -k 10 300 \
+      local tag=$1 nb=$2 d=$3 bits=$4 v=${5:-tt}
+      CWQ_LIB_PATH=$PWD/tools/variants/libcwq_$v.so timeout -k 10 300 \
         python -u tools/tile_times.py $nb $d $bits > gpurun_out/tt_$tag.log 2>&1 && head -6 gpurun_out/tt_$tag.log ;;
     *) echo "unknown task $task"; return 2 ;;
   esac

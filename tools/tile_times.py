@@ -53,6 +53,13 @@ edges = np.linspace(0, span, 21)
 for lo, hi in zip(edges[:-1], edges[1:]):
     busy = (np.minimum(b, hi) - np.maximum(a, lo)).clip(min=0).sum() / (hi - lo)
     print(f"  {lo:8.1f}-{hi:8.1f} us: {busy:7.1f} tiles running")
+# per XCD (HW_REG_XCC_ID): tiles, busy time and when its last tile ended
+xcc = (wg[m] >> 24) & 0xf
+for x in range(8):
+    sel = xcc == x
+    if sel.any():
+        print(f"  XCD {x}: {int(sel.sum())} tiles, tile time {dur[sel].sum() / 1e3:.1f} ms, "
+              f"last end {b[sel].max():.1f} us")
 # tile index (interleaved: block t % nb, tile t // nb) against duration
 tt = np.nonzero(m)[0] // nb
 for q in range(0, int(tt.max()) + 1, max(1, (int(tt.max()) + 1) // 8)):

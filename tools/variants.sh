@@ -91,6 +91,13 @@ declare -A V=(
   [tauold]="-DCWQ_TAU_FROM_KEYS=0"
   [seed16]="-DCWQ_SEED_LOG2=16"
   [tt]="-DCWQ_TILE_TIMES"
+  [tt0]="-DCWQ_TILE_TIMES -DCWQ_XCD_BALANCE=0"
+  [xcd0]="-DCWQ_XCD_BALANCE=0"
+  [tail1]="-DCWQ_TAIL_SPLIT=1"
+  [tail2]="-DCWQ_TAIL_SPLIT=2"
+  [tail8]="-DCWQ_TAIL_SPLIT=8"
+  [glds0]="-DCWQ_DECODE_GLDS=0"
+  [glds3]="-DCWQ_GLDS_SLOTS=3 -DCWQ_GLDS_MIN_WAVES=5"
   [fw7ni0]="-DCWQ_FUSED_WAVES=7 -DCWQ_FUSED_NOINLINE=0"
 )
 if [ "$1" = build ]; then
