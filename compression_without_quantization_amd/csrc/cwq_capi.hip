@@ -1055,6 +1055,18 @@ int64_t batch_device_path(int64_t n_items, const int64_t* item_off, int64_t D, i
                           const float* p_scale, hipStream_t s, hipStream_t d2h, hipStream_t h2d) {
   const GroupedWs& l = bl.g;
   const int64_t K = (int64_t)ci.size() - 1;
+#ifdef CWQ_PHASE_TIMES  // tuning builds: per-phase host wall times to stderr
+  struct timespec ts_start;
+  clock_gettime(CLOCK_MONOTONIC, &ts_start);
+  auto lap = [&](const char* what) {
+    struct timespec t;
+    clock_gettime(CLOCK_MONOTONIC, &t);
+    fprintf(stderr, "[cwq batch dev] %-14s at %8.1f us\n", what,
+            (t.tv_sec - ts_start.tv_sec) * 1e6 + (t.tv_nsec - ts_start.tv_nsec) * 1e-3);
+  };
+#else
+  auto lap = [](const char*) {};
+#endif
   int64_t* ioff_d = (int64_t*)(w + bl.ioff);
   int64_t* dst = (int64_t*)(w + bl.dstarts);
   int64_t* iinfo_d = (int64_t*)(w + bl.iinfo);
@@ -1082,6 +1094,7 @@ int64_t batch_device_path(int64_t n_items, const int64_t* item_off, int64_t D, i
     return hip_fail(e, "cwq_code_grouped_greedy_batch: device partition");
   }
   if (cwq::partition_fell_back(hi)) return kBatchFellBack;
+  lap("partitioned");
   // the items' group counts; per chunk its groups, largest group and layout
   std::vector<int64_t> gl((size_t)n_items), chunk_of((size_t)n_items);
   std::vector<int64_t> cG((size_t)K, 0), cmaxd((size_t)K, 0);
@@ -1173,6 +1186,7 @@ int64_t batch_device_path(int64_t n_items, const int64_t* item_off, int64_t D, i
       rc = hip_fail(e, "event");
     if (rc == CWQ_OK) c_done = c + 1;
   }
+  lap("enqueued");
   // the items' start lists to the caller, beside the coding (the partition has
   // completed: synchronised above)
   for (int64_t i = 0; i < n_items && rc == CWQ_OK; ++i)
@@ -1216,7 +1230,9 @@ int64_t batch_device_path(int64_t n_items, const int64_t* item_off, int64_t D, i
     bits_worker();
   }
   for (auto& th : pool) th.join();
+  lap("bits written");
   drain();
+  lap("drained");
   if (rc < 0) return rc;
   if (err.load() < 0) return err.load();
   if ((e = hipStreamSynchronize(s)) != hipSuccess) return hip_fail(e, "sync");

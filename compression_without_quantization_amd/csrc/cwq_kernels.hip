@@ -2024,8 +2024,15 @@ __device__ __forceinline__ double row16_red_f64(double v) {
 
 // Exact normal k of a block's stream: its Philox block and the one
 // Box-Muller pair that holds it (normal4_dev's element k & 3, bit for bit).
-__device__ __forceinline__ float exact_normal(const PhiloxStream& st, uint64_t k,
-                                              const double* logtab) {
+#ifndef CWQ_EXACT_NOINLINE
+#define CWQ_EXACT_NOINLINE 1  // out of line: its f64 constants no longer spill the fused kernel
+#endif
+#if CWQ_EXACT_NOINLINE
+__device__ __noinline__
+#else
+__device__ __forceinline__
+#endif
+float exact_normal(const PhiloxStream& st, uint64_t k, const double* logtab) {
   const U4 x = philox_block_dev(st, k >> 2);
   const bool hi = (k & 2u) != 0;
   float f0, f1;
@@ -2397,21 +2404,30 @@ __global__ void __launch_bounds__(256, CWQ_FUSED_WAVES) k_small_fused(
       wave_lds_sync();
     }
 
-    // (4) index and best += the winning row (k_encode_finalize), a row per block
-    if (valid) {
-      const QuadBlk r = bk[k];
-      uint32_t idx = r.idx;
-      if (r.state != kQuadKnown) {  // ArgMaxTupleReducer: a key at the clamp level is index 0
-        const unsigned long long kb = kmax[k];
-        idx = (kb >> 32) > kArgmaxClampOrd ? argmax_key_index(kb) : 0u;
-      }
-      if (slot == 0u) out_idx[g * n_steps + step] = (int32_t)idx;
-      const PhiloxStream st{r.k0, r.k1, r.c2, r.c3};
-      for (int j = (int)slot; j < d; j += 16) {
-        const float zz = exact_normal(st, (uint64_t)idx * (uint64_t)d + (uint32_t)j, logtab);
-        float sv = scale_s[off + j] * zz;
-        sv = loc_s[off + j] + sv;
-        best[off + j] = (STEP0 ? 0.0f : best[off + j]) + sv;
+    // (4) index and best += the winning row (k_encode_finalize), a row per block;
+    // the row's values come back from its LDS record (nothing per-lane is kept
+    // across the screen: live values there were spilled to scratch)
+    {
+      uint32_t lane4 = lane0;
+      asm volatile("" : "+v"(lane4));
+      const uint32_t k4 = lane4 >> 4, slot4 = lane4 & 15u;
+      if ((int)k4 < nq) {
+        const QuadBlk r = bk[k4];
+        const int d4 = (int)r.d;
+        const int64_t off4 = r.off;
+        uint32_t idx = r.idx;
+        if (r.state != kQuadKnown) {  // ArgMaxTupleReducer: a key at the clamp level is index 0
+          const unsigned long long kb = kmax[k4];
+          idx = (kb >> 32) > kArgmaxClampOrd ? argmax_key_index(kb) : 0u;
+        }
+        if (slot4 == 0u) out_idx[(g0 + (int64_t)k4) * n_steps + step] = (int32_t)idx;
+        const PhiloxStream st{r.k0, r.k1, r.c2, r.c3};
+        for (int j = (int)slot4; j < d4; j += 16) {
+          const float zz = exact_normal(st, (uint64_t)idx * (uint64_t)d4 + (uint32_t)j, logtab);
+          float sv = scale_s[off4 + j] * zz;
+          sv = loc_s[off4 + j] + sv;
+          best[off4 + j] = (STEP0 ? 0.0f : best[off4 + j]) + sv;
+        }
       }
     }
     wave_lds_sync();  // the next quad reuses the wave's LDS

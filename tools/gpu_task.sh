@@ -69,7 +69,7 @@ run_one() {
       CWQ_LIB_PATH=$PWD/tools/variants/libcwq_phases.so timeout -k 10 300 python -u bench.py --config c2 \
         --no-cpu --no-e2e --steps 5 > gpurun_out/c2phases.log 2>&1 && grep cwq gpurun_out/c2phases.log | tail -8 && \
       CWQ_LIB_PATH=$PWD/tools/variants/libcwq_phases.so timeout -k 10 300 python -u bench.py --config c3 \
-        --batch-only --no-cpu --no-e2e --steps 3 > gpurun_out/c3phases.log 2>&1 && grep -c cwq gpurun_out/c3phases.log ;;
+        --batch-only --no-cpu --no-e2e --steps 3 > gpurun_out/c3phases.log 2>&1 && grep "cwq batch" gpurun_out/c3phases.log | tail -4 ;;
     decvar)  # decode timing per variant, after its decode tests against the oracle
       for v in $1; do
         CWQ_LIB_PATH=$PWD/tools/variants/libcwq_$v.so timeout -k 10 300 python -u -m pytest \

@@ -97,6 +97,9 @@ declare -A V=(
   [tail2]="-DCWQ_TAIL_SPLIT=2"
   [tail8]="-DCWQ_TAIL_SPLIT=8"
   [glds0]="-DCWQ_DECODE_GLDS=0"
+  [eni0]="-DCWQ_EXACT_NOINLINE=0"
+  [eni0fw6]="-DCWQ_EXACT_NOINLINE=0 -DCWQ_FUSED_WAVES=6"
+  [fw6]="-DCWQ_FUSED_WAVES=6"
   [glds3]="-DCWQ_GLDS_SLOTS=3 -DCWQ_GLDS_MIN_WAVES=5"
   [fw7ni0]="-DCWQ_FUSED_WAVES=7 -DCWQ_FUSED_NOINLINE=0"
 )
