@@ -237,7 +237,8 @@ def grouped_main(args):
                             "bytes (20 d + 4 n_steps per group) against HBM, as the north star "
                             "asks; the launches are bound by VALU issue (Philox + Box-Muller "
                             "per candidate), see `valu` and DESIGN.md 5c/5d",
-                "kernel": ("k_small_prep + k_small_screen + k_small_survivors" if small else
+                "kernel": ("k_small_fused (constants, screen, exact survivors and finalize in "
+                           "one launch per step; DESIGN.md 5e)" if small else
                            "k_csr_prep + k_encode_prune_csr (+ finalize between steps)"),
                 "kernel_ms": round(kernel_ms, 4),
                 "kernel_timing": "HIP events recorded on the launch stream around the "
