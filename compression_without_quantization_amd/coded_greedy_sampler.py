@@ -352,7 +352,6 @@ def code_grouped_greedy_sample(sess, target, proposal, n_steps, n_bits_per_step,
     need = int(lib.cwq_code_grouped_greedy_workspace_size(D, n_steps))
     ws = torch.empty(max(need, 1), dtype=torch.uint8, device=dev)
     bits_h = _scratch_bytes(max((D + 1) * n_bits_per_group, 1))  # <= D + 1 groups
-    starts_h = np.empty(D + 2, dtype=np.int64)
     kl_sum = ctypes.c_double(0.0)
     n_nats = n_bits_per_group * np.log(2) - 1
     seed32 = int(np.int32(np.uint32(int(seed) & 0xFFFFFFFF)))
@@ -363,6 +362,7 @@ def code_grouped_greedy_sample(sess, target, proposal, n_steps, n_bits_per_step,
     with torch.cuda.device(dev):
         if eval_ms_out is not None:  # the library times the encode: the one-shot call
             sample_h = np.empty(D, dtype=np.float32)
+            starts_h = np.empty(D + 2, dtype=np.int64)
             G = _lib.check(lib.cwq_code_grouped_greedy(
                 *args, sample_h.ctypes.data, bits_h.ctypes.data, bits_h.size,
                 starts_h.ctypes.data, starts_h.size, kls, ws.data_ptr(), ws.numel(), opts, stream),

@@ -51,7 +51,7 @@ int hip_fail(hipError_t e, const char* where) {
 size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
 
 struct WsLayout {
-  size_t keys, loc_s, scale_s, lognorm, sab, cdim, bpre, ordu, grp, gtau, abp, slist, total;
+  size_t keys, tq, loc_s, scale_s, lognorm, sab, cdim, bpre, ordu, grp, gtau, abp, slist, total;
   bool csr;   // has the general pruned kernel's arrays
   bool recs;  // ... and the visit-order records of blocks longer than CWQ_CSR_LDS_DIMS
 };
@@ -71,6 +71,8 @@ WsLayout ws_layout(int64_t nb, int64_t total_dims, bool csr, bool recs) {
   size_t o = 0;
   l.keys = o;
   o = align_up(o + (size_t)nb * 8, 256);
+  l.tq = o;  // k_encode_prune's tile queue counters
+  o = align_up(o + (size_t)cwq::kTileQueueSlots * 4, 256);
   l.loc_s = o;
   o = align_up(o + (size_t)total_dims * 4, 256);
   l.scale_s = o;
@@ -382,6 +384,7 @@ int encode_impl(const float* t_loc, const float* t_scale, const float* p_loc,
   a.out_sample = out_sample;
   char* w = (char*)workspace;
   a.keys = (unsigned long long*)(w + l.keys);
+  a.tq = (uint32_t*)(w + l.tq);
   a.loc_s = (float*)(w + l.loc_s);
   a.scale_s = (float*)(w + l.scale_s);
   a.lognorm = (float*)(w + l.lognorm);
@@ -624,7 +627,17 @@ hipError_t wait_event(hipEvent_t e) {
 }
 thread_local std::vector<float> g_kl_host;
 thread_local std::vector<int32_t> g_idx_host;
-thread_local unsigned long long g_part_info[16];  // info[8], then item 0's (G + 1, largest)
+// the device partition's info[8], then item 0's (G + 1, largest): pinned, so the
+// copy is a direct DMA (pageable memory is staged), per thread
+unsigned long long* part_info_host() {
+  thread_local unsigned long long* p = [] {
+    void* q = nullptr;
+    if (hipHostMalloc(&q, 16 * sizeof(unsigned long long), hipHostMallocDefault) != hipSuccess)
+      q = nullptr;
+    return (unsigned long long*)q;
+  }();
+  return p;
+}
 // CWQ_HOST_PARTITION=1: the host partition loop even where the device one
 // applies (A/B timing; the results are identical)
 bool device_partition_enabled() {
@@ -723,21 +736,23 @@ int64_t grouped_begin(const float* q_loc, const float* q_scale, const float* p_l
   bool dev_part = false;
   int64_t n = 0, maxd = 0;
   bool kl_on_host = false;
+  CallEvents pev;  // the partition info's and the starts' copies
   if (D > 0) {
-    // :193-199 standardise; :201, :210 per-dim KL(target || proposal)
-    if ((rc = cwq_standardise(q_loc, q_scale, p_loc, p_scale, D, t_loc, t_scale, stream)) < 0)
-      return rc;
-    if ((rc = cwq_kl_normal_normal(q_loc, q_scale, p_loc, p_scale, D, kl, stream)) < 0) return rc;
-    if ((e = hipMemsetAsync(zeros, 0, (size_t)D * 4, s)) != hipSuccess) return hip_fail(e, "memset");
-    if ((e = hipMemsetD32Async((hipDeviceptr_t)ones, 0x3f800000u, (size_t)D, s)) != hipSuccess)
-      return hip_fail(e, "memset");
-    if (device_partition_enabled() && cwq::partition_applies(D, size_threshold)) {
-      unsigned long long* info_d = (unsigned long long*)(w + l.pinfo);
+    // :193-199 standardise; :201, :210 per-dim KL(target || proposal); the
+    // standard prior (zeros, ones) and the partition's counters, one launch
+    unsigned long long* g_part_info = part_info_host();
+    const bool try_dev = device_partition_enabled() && cwq::partition_applies(D, size_threshold) &&
+                         g_part_info != nullptr;
+    unsigned long long* info_d = (unsigned long long*)(w + l.pinfo);
+    if ((e = cwq::launch_grouped_prep(q_loc, q_scale, p_loc, p_scale, D, t_loc, t_scale, kl, zeros,
+                                      ones, info_d, try_dev ? 16 : 0, s)) != hipSuccess)
+      return hip_fail(e, "standardise / KL");
+    if (try_dev) {
       if ((e = cwq::launch_partition(kl, D, nullptr, 1, size_threshold, group_thr(n_nats, false),
-                                     offs, (int64_t*)(info_d + 8), w + l.part, info_d, s)) !=
-              hipSuccess ||
-          (e = hipMemcpyAsync(g_part_info, info_d, sizeof(g_part_info), hipMemcpyDeviceToHost,
-                              s)) != hipSuccess)
+                                     offs, (int64_t*)(info_d + 8), w + l.part, info_d, s,
+                                     true)) != hipSuccess ||
+          (e = hipMemcpyAsync(g_part_info, info_d, 16 * sizeof(unsigned long long),
+                              hipMemcpyDeviceToHost, s)) != hipSuccess)
         return hip_fail(e, "device partition");
       if (kl_sum_out) {  // the log line's total KL only
         g_kl_host.resize((size_t)D);
@@ -746,7 +761,11 @@ int64_t grouped_begin(const float* q_loc, const float* q_scale, const float* p_l
           return hip_fail(e, "KL to host");
         kl_on_host = true;
       }
-      if ((e = hipStreamSynchronize(s)) != hipSuccess) return hip_fail(e, "sync");
+      // a polled event: the blocking wait's wake-up is of the order of the
+      // partition itself
+      if (!pev.made(1, s, hipEventDisableTiming) || hipEventRecord(pev.ev[0], s) != hipSuccess)
+        return fail(CWQ_ERR_HIP, "%s: events failed", who);
+      if ((e = wait_event(pev.ev[0])) != hipSuccess) return hip_fail(e, "sync");
       if (!cwq::partition_fell_back(g_part_info)) {
         dev_part = true;
         n = (int64_t)g_part_info[8];
@@ -804,6 +823,11 @@ int64_t grouped_begin(const float* q_loc, const float* q_scale, const float* p_l
     if ((e = hipMemcpyAsync(starts_host, offs, (size_t)(G + 1) * 8, hipMemcpyDeviceToHost,
                             d2h_starts)) != hipSuccess)
       return hip_fail(e, "starts to host");
+    if (pev.ev.size() != 1 || !pev.made(1, s, hipEventDisableTiming) ||
+        (e = hipEventRecord(pev.ev[1], d2h_starts)) != hipSuccess) {
+      (void)hipStreamSynchronize(d2h_starts);
+      return fail(CWQ_ERR_HIP, "%s: events failed", who);
+    }
   }
   // :273-284 one greedy coder per group, seed + g
   if (o.eval_ms_out && (!tev->made(2, s, hipEventDefault) ||
@@ -825,7 +849,7 @@ int64_t grouped_begin(const float* q_loc, const float* q_scale, const float* p_l
   if ((e = hipMemcpyAsync(sample_host, out, (size_t)D * 4, hipMemcpyDeviceToHost, s)) !=
       hipSuccess)
     return hip_fail(e, "sample to host");
-  if (d2h_starts && (e = hipStreamSynchronize(d2h_starts)) != hipSuccess) {
+  if (d2h_starts && (e = wait_event(pev.ev[1])) != hipSuccess) {
     (void)hipStreamSynchronize(s);
     return hip_fail(e, "starts to host");
   }

@@ -29,6 +29,8 @@ __host__ __device__ inline int64_t csr_rec_entries(int64_t total_dims) {
   return total_dims + 12 * (total_dims / (CWQ_CSR_LDS_DIMS + 1) + 1);
 }
 
+constexpr int kTileQueueSlots = 64;
+
 struct EncodeArgs {
   const float* t_loc;
   const float* t_scale;
@@ -52,6 +54,9 @@ struct EncodeArgs {
   float* out_sample;
   // workspace
   unsigned long long* keys;  // [nb]
+  // tile queue counters of k_encode_prune (kTileQueueSlots u32, one per fork
+  // part; nullptr: static tile loop); zeroed by the launcher before each launch
+  uint32_t* tq = nullptr;
   float* loc_s;              // [total_dims]
   float* scale_s;            // [total_dims]
   float* lognorm;            // [total_dims]
@@ -96,6 +101,12 @@ hipError_t launch_kl(const float* q_loc, const float* q_scale, const float* p_lo
                      const float* p_scale, int64_t n, float* out, hipStream_t stream);
 hipError_t launch_destandardise(const float* sample, const float* p_loc, const float* p_scale,
                                 int64_t n, float* out, hipStream_t stream);
+// standardise + KL + the standard prior's zeros/ones + nz zeroed u64 at zinfo
+// (nz <= 256), one launch (the grouped coder's first step)
+hipError_t launch_grouped_prep(const float* q_loc, const float* q_scale, const float* p_loc,
+                               const float* p_scale, int64_t n, float* t_loc, float* t_scale,
+                               float* kl, float* zeros, float* ones, unsigned long long* zinfo,
+                               int nz, hipStream_t stream);
 
 // The grouped coder's greedy partition on the device (cwq_partition.hip), of
 // one item (item_off == nullptr, n_items == 1) or of each item [item_off[k],
@@ -115,9 +126,12 @@ struct BatchItem {
 };
 hipError_t launch_batch_layout(const BatchItem* items, int64_t n_items, const int64_t* dstarts,
                                int64_t* offs, int32_t* seeds, hipStream_t stream);
+// info_zeroed: info[0..7] (and, single item, iinfo[0..1]) were zeroed on the
+// stream by the caller (launch_grouped_prep); otherwise a memset does it
 hipError_t launch_partition(const float* kl, int64_t D, const int64_t* item_off, int64_t n_items,
                             int64_t size_threshold, float thr, int64_t* starts, int64_t* iinfo,
-                            void* ws, unsigned long long* info, hipStream_t stream);
+                            void* ws, unsigned long long* info, hipStream_t stream,
+                            bool info_zeroed = false);
 bool partition_fell_back(const unsigned long long* info_host);
 
 size_t importance_workspace_size(int64_t nb, int64_t total_dims);

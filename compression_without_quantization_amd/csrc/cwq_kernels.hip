@@ -229,7 +229,8 @@ __global__ void __launch_bounds__(256, CWQ_PRUNE_MIN_WAVES) k_encode_prune(
     const float* __restrict__ loc_s, const float* __restrict__ scale_s,
     const float* __restrict__ lognorm, const float* __restrict__ best, int64_t ntiles,
     int64_t tiles_per_block, int64_t cand_per_tile, int64_t n_cand, SeedSpec sd, int32_t step,
-    int allow_screen, unsigned long long* __restrict__ keys, int64_t tail_from, int tail_div) {
+    int allow_screen, unsigned long long* __restrict__ keys, int64_t tail_from, int tail_div,
+    uint32_t* __restrict__ tq) {
   static_assert(D % 8 == 0 && D >= 8 && D <= 64, "pruned path: D % 8 == 0, D <= 64");
   constexpr int G = D / 4;
   constexpr int NF = STEP0 ? 6 : 7;  // loc_s, scale_s, mu, sigma, c, 1/sigma[, best]
@@ -250,6 +251,7 @@ __global__ void __launch_bounds__(256, CWQ_PRUNE_MIN_WAVES) k_encode_prune(
   __shared__ uint32_t sq_n[CWQ_SURVIVOR_CAP];
   __shared__ float sq_ub[CWQ_SURVIVOR_CAP];
   __shared__ unsigned long long wkey[4];
+  __shared__ uint32_t s_next;
 #ifdef CWQ_PRUNE_STATS
   // per-workgroup counters (LDS atomics), added to g_prune_stats once per tile:
   // one global atomic per finished candidate made C5-sized runs take minutes
@@ -266,7 +268,19 @@ __global__ void __launch_bounds__(256, CWQ_PRUNE_MIN_WAVES) k_encode_prune(
   // they left in keys[g] instead of from -inf
   constexpr bool inter = INTER;
   const int64_t nbt = INTER ? ntiles / tiles_per_block : 0;
-  for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+  // tile queue (tq != nullptr): a workgroup's first tile is its id, later ones
+  // come from one atomic counter, so workgroups stay resident until the queue
+  // is empty.  With one tile per workgroup the resident count fell from 1,514
+  // to 1,414 of 1,536 slots over a C5 launch as finished workgroups were
+  // replaced (tools/tile_times.py); the queue keeps every slot busy to the end.
+  auto next_tile = [&](int64_t cur) -> int64_t {
+    if (tq == nullptr) return cur + gridDim.x;
+    __syncthreads();
+    if (threadIdx.x == 0) s_next = gridDim.x + atomicAdd(tq, 1u);
+    __syncthreads();
+    return (int64_t)s_next;
+  };
+  for (int64_t tile = blockIdx.x; tile < ntiles; tile = next_tile(tile)) {
     // thread index re-derived per tile behind an opaque move: the per-thread
     // addresses below are then recomputed (cheap) instead of hoisted out of the
     // tile loop and spilled under the 6-waves/SIMD register budget
@@ -290,7 +304,8 @@ __global__ void __launch_bounds__(256, CWQ_PRUNE_MIN_WAVES) k_encode_prune(
     // last in their natural order, so every XCD gets its share of them too.
     int64_t tord = tile;
     const int64_t treg = inter ? nbt * tail_from : 0;  // full-size tiles
-    if (inter && CWQ_XCD_BALANCE && tile < treg && (treg & 7) == 0 && (gridDim.x & 7u) == 0)
+    if (inter && CWQ_XCD_BALANCE && tq == nullptr && tile < treg && (treg & 7) == 0 &&
+        (gridDim.x & 7u) == 0)
       tord = (tile & 7) * (treg >> 3) + (tile >> 3);
     const int64_t g = inter ? tord % nbt : tile / tiles_per_block;
     const int64_t tt = inter ? tord / nbt : tile - g * tiles_per_block;
@@ -2863,19 +2878,46 @@ __global__ void __launch_bounds__(256) k_standardise(
   }
 }
 
+__device__ __forceinline__ float kl_normal_normal_1(float a_loc, float a_scale, float b_loc,
+                                                    float b_scale) {
+  const float sa2 = a_scale * a_scale;
+  const float sb2 = b_scale * b_scale;
+  const float ratio = sa2 / sb2;
+  const float dl = a_loc - b_loc;
+  const float t1 = (dl * dl) / (2.0f * sb2);
+  const float t2 = 0.5f * ((ratio - 1.0f) - logf_full(ratio, kLogTabConst));
+  return t1 + t2;
+}
+
 __global__ void __launch_bounds__(256) k_kl_normal_normal(
     const float* __restrict__ a_loc, const float* __restrict__ a_scale,
     const float* __restrict__ b_loc, const float* __restrict__ b_scale, int64_t n,
     float* __restrict__ out) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x)
+    out[i] = kl_normal_normal_1(a_loc[i], a_scale[i], b_loc[i], b_scale[i]);
+}
+
+// The grouped coder's first launch (coded_greedy_sampler.py:193-201): the
+// standardised target (k_standardise's expressions), the per-dim KL
+// (k_kl_normal_normal's), the standard prior's zeros and ones, and zeroed
+// partition counters (nz u64 at zinfo), in one pass over the inputs.
+__global__ void __launch_bounds__(256) k_grouped_prep(
+    const float* __restrict__ q_loc, const float* __restrict__ q_scale,
+    const float* __restrict__ p_loc, const float* __restrict__ p_scale, int64_t n,
+    float* __restrict__ t_loc, float* __restrict__ t_scale, float* __restrict__ kl,
+    float* __restrict__ zeros, float* __restrict__ ones, unsigned long long* __restrict__ zinfo,
+    int nz) {
+  if (blockIdx.x == 0 && (int)threadIdx.x < nz) zinfo[threadIdx.x] = 0ull;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x) {
-    const float sa2 = a_scale[i] * a_scale[i];
-    const float sb2 = b_scale[i] * b_scale[i];
-    const float ratio = sa2 / sb2;
-    const float dl = a_loc[i] - b_loc[i];
-    const float t1 = (dl * dl) / (2.0f * sb2);
-    const float t2 = 0.5f * ((ratio - 1.0f) - logf_full(ratio, kLogTabConst));
-    out[i] = t1 + t2;
+    const float ql = q_loc[i], qs = q_scale[i], pl = p_loc[i], ps = p_scale[i];
+    const float dl = ql - pl;
+    t_loc[i] = dl / ps;
+    t_scale[i] = qs / ps;
+    kl[i] = kl_normal_normal_1(ql, qs, pl, ps);
+    zeros[i] = 0.0f;
+    ones[i] = 1.0f;
   }
 }
 
@@ -3004,7 +3046,6 @@ static void launch_prune_t(const EncodeArgs& a, int step, hipStream_t stream) {
 #endif
   constexpr int64_t kPruneGrid = CWQ_PRUNE_GRID;
   const int64_t ntiles = a.nb * a.tiles_per_block;
-  const unsigned grid = (unsigned)(ntiles < kPruneGrid ? ntiles : kPruneGrid);
 #ifndef CWQ_TILE_INTERLEAVE
 #define CWQ_TILE_INTERLEAVE 1
 #endif
@@ -3034,8 +3075,24 @@ static void launch_prune_t(const EncodeArgs& a, int step, hipStream_t stream) {
                        dim3((unsigned)(nt_s < kPruneGrid ? nt_s : kPruneGrid)), dim3(256), 0,
                        stream, a.t_loc, a.t_scale, a.loc_s, a.scale_s, a.lognorm, a.out_sample,
                        nt_s, seed_n / cpt_s, cpt_s, seed_n, seeds_of(a), step,
-                       a.prune >= 2 ? 1 : 0, a.keys, seed_n / cpt_s, 1);
+                       a.prune >= 2 ? 1 : 0, a.keys, seed_n / cpt_s, 1, nullptr);
   }
+  // tile queue (k_encode_prune): a persistent grid of CWQ_QUEUE_GRID workgroups
+  // draws tiles from a counter in the workspace, zeroed here before the launch
+#ifndef CWQ_TILE_QUEUE
+#define CWQ_TILE_QUEUE 1
+#endif
+#ifndef CWQ_QUEUE_GRID
+#define CWQ_QUEUE_GRID 1536
+#endif
+  uint32_t* tq = nullptr;
+  if (CWQ_TILE_QUEUE && a.tq != nullptr && ntiles < (1LL << 31)) {
+    if (hipMemsetAsync(a.tq, 0, sizeof(uint32_t), stream) == hipSuccess) tq = a.tq;
+  }
+  auto qgrid = [&](int64_t nt) -> unsigned {
+    const int64_t cap = tq ? (int64_t)CWQ_QUEUE_GRID : kPruneGrid;
+    return (unsigned)(nt < cap ? nt : cap);
+  };
   if (CWQ_TILE_INTERLEAVE && (a.tiles_per_block > 1 || seeded)) {
     // tail: the last tile of each block's few last tiles split in CWQ_TAIL_SPLIT,
     // about two resident rounds (1,536 workgroups) of short tiles at the end
@@ -3053,15 +3110,15 @@ static void launch_prune_t(const EncodeArgs& a, int step, hipStream_t stream) {
     const int64_t tpb2 = from + (tpb - from) * div;
     const int64_t nt2 = a.nb * tpb2;
     hipLaunchKernelGGL((k_encode_prune<D, STEP0, true>),
-                       dim3((unsigned)(nt2 < kPruneGrid ? nt2 : kPruneGrid)), dim3(256), 0,
+                       dim3(qgrid(nt2)), dim3(256), 0,
                        stream, a.t_loc, a.t_scale, a.loc_s, a.scale_s, a.lognorm, a.out_sample,
                        nt2, tpb2, a.cand_per_tile, a.n_cand, seeds_of(a), step,
-                       a.prune >= 2 ? 1 : 0, a.keys, from, (int)div);
+                       a.prune >= 2 ? 1 : 0, a.keys, from, (int)div, tq);
   } else {
-    hipLaunchKernelGGL((k_encode_prune<D, STEP0, false>), dim3(grid), dim3(256), 0, stream,
-                       a.t_loc, a.t_scale, a.loc_s, a.scale_s, a.lognorm, a.out_sample, ntiles,
-                       a.tiles_per_block, a.cand_per_tile, a.n_cand, seeds_of(a), step,
-                       a.prune >= 2 ? 1 : 0, a.keys, a.tiles_per_block, 1);
+    hipLaunchKernelGGL((k_encode_prune<D, STEP0, false>), dim3(qgrid(ntiles)), dim3(256), 0,
+                       stream, a.t_loc, a.t_scale, a.loc_s, a.scale_s, a.lognorm, a.out_sample,
+                       ntiles, a.tiles_per_block, a.cand_per_tile, a.n_cand, seeds_of(a), step,
+                       a.prune >= 2 ? 1 : 0, a.keys, a.tiles_per_block, 1, tq);
   }
 }
 
@@ -3337,6 +3394,7 @@ hipError_t launch_encode(const EncodeArgs& a, hipStream_t stream) {
     p.block_id_base = a.block_id_base + g0;
     if (a.seeds) p.seeds = a.seeds + g0;
     p.keys = a.keys + g0;
+    if (a.tq) p.tq = a.tq + i;  // its own tile queue counter
     p.out_idx = a.out_idx + g0 * a.n_steps;
     if (a.sab) p.sab = a.sab + 8 * g0;
     if (a.bpre) p.bpre = a.bpre + 12 * g0;
@@ -3417,6 +3475,18 @@ hipError_t launch_kl(const float* q_loc, const float* q_scale, const float* p_lo
   if (n <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_kl_normal_normal, dim3(grid_for(n, 256, 65536)), dim3(256), 0, stream,
                      q_loc, q_scale, p_loc, p_scale, n, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_grouped_prep(const float* q_loc, const float* q_scale, const float* p_loc,
+                               const float* p_scale, int64_t n, float* t_loc, float* t_scale,
+                               float* kl, float* zeros, float* ones, unsigned long long* zinfo,
+                               int nz, hipStream_t stream) {
+  if (n <= 0 && nz <= 0) return hipSuccess;
+  if (nz < 0 || nz > 256 || (nz > 0 && !zinfo)) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_grouped_prep, dim3(n > 0 ? grid_for(n, 256, 65536) : 1u), dim3(256), 0,
+                     stream, q_loc, q_scale, p_loc, p_scale, n, t_loc, t_scale, kl, zeros, ones,
+                     zinfo, nz);
   return hipGetLastError();
 }
 

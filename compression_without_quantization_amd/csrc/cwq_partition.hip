@@ -8,7 +8,7 @@
 //     nxt(i) = the next start after a start at i
 // from node 0: the starts are 0, nxt(0), nxt(nxt(0)), ... up to D - 1 (always a
 // start), preceded by the reference's [0] and, when dim 0 alone already trips
-// the test ("dup"), a second 0 (an empty first group).  Four launches:
+// the test ("dup"), a second 0 (an empty first group).  The launches:
 //   k_part_next   every nxt(i) (a thread per dim scanning forward; a scan
 //                 longer than kPartMaxJump dims marks the input "long" and
 //                 the caller partitions on the host);
@@ -25,7 +25,9 @@
 //                 the chunk marked by pointer jumping in LDS, counted and
 //                 compacted;
 //   k_part_emit   per chunk: the global rank of its first node (sum of the
-//                 earlier chunks' counts), the walk's nodes in rank order;
+//                 earlier chunks' counts), the walk's nodes in rank order (one
+//                 item: straight into its start list, with its largest group,
+//                 and the two launches below are skipped);
 //   k_part_ihdr / k_part_ibody  per item: its nodes (a rank range found by
 //                 binary search) as its own start list, group count and
 //                 largest group.
@@ -247,12 +249,22 @@ __global__ void __launch_bounds__(256) k_part_mark(const int32_t* __restrict__ n
   if (threadIdx.x == kPartThreads - 1) cnt[c] = red[threadIdx.x];
 }
 
+// SINGLE (one item, no item_off): the chunk's nodes go straight to the start
+// list (st[dup + rank]; the last chunk adds st[0] = 0 and st[dup + total] = D)
+// and the largest group to iinfo[1], so k_part_ihdr / k_part_ibody are not run.
+template <bool SINGLE>
 __global__ void __launch_bounds__(256) k_part_emit(int64_t nchunks,
                                                    const int32_t* __restrict__ node,
                                                    const int32_t* __restrict__ cnt,
                                                    int32_t* __restrict__ gnode,
-                                                   unsigned long long* __restrict__ info) {
+                                                   unsigned long long* __restrict__ info,
+                                                   const float* __restrict__ kl, int64_t D,
+                                                   int64_t T, float thr,
+                                                   const int32_t* __restrict__ nxt,
+                                                   int64_t* __restrict__ starts,
+                                                   int64_t* __restrict__ iinfo) {
   __shared__ int64_t red[kPartThreads];
+  __shared__ int32_t redm[kPartThreads];
   if (info[4] > (unsigned long long)kPartMaxJump || info[2]) return;
   const int64_t c = blockIdx.x;
   const int64_t b = c * kPartW;
@@ -267,8 +279,31 @@ __global__ void __launch_bounds__(256) k_part_emit(int64_t nchunks,
   }
   const int64_t r0 = red[0];
   const int nc = cnt[c];
-  for (int q = threadIdx.x; q < nc; q += kPartThreads) gnode[r0 + q] = node[b + q];
-  if (threadIdx.x == 0 && c == nchunks - 1) info[0] = (unsigned long long)(r0 + nc);
+  if (!SINGLE) {
+    for (int q = threadIdx.x; q < nc; q += kPartThreads) gnode[r0 + q] = node[b + q];
+    if (threadIdx.x == 0 && c == nchunks - 1) info[0] = (unsigned long long)(r0 + nc);
+    return;
+  }
+  // as k_part_ihdr's dup: dim 0 alone trips the test (:232-233), or D == 1
+  const int64_t dup = (T <= 0 || kl[0] >= thr || D == 1) ? 1 : 0;
+  int32_t mx = 0;
+  for (int q = threadIdx.x; q < nc; q += kPartThreads) {
+    const int32_t v = node[b + q];
+    starts[dup + r0 + q] = v;  // rank 0 is dim 0
+    const int32_t gsz = nxt[v] - v;
+    mx = gsz > mx ? gsz : mx;
+  }
+  const int32_t m = block_max(mx, redm);
+  if (threadIdx.x == 0) {
+    if (m > 0) atomicMax((unsigned long long*)&iinfo[1], (unsigned long long)m);
+    if (c == nchunks - 1) {
+      const int64_t total = r0 + nc;
+      starts[0] = 0;
+      starts[dup + total] = D;
+      iinfo[0] = dup + total + 1;
+      info[0] = (unsigned long long)total;
+    }
+  }
 }
 
 __device__ __forceinline__ int64_t lower_bound_i32(const int32_t* __restrict__ a, int64_t n,
@@ -395,7 +430,8 @@ bool partition_applies(int64_t D, int64_t size_threshold) {
 
 hipError_t launch_partition(const float* kl, int64_t D, const int64_t* item_off, int64_t n_items,
                             int64_t size_threshold, float thr, int64_t* starts, int64_t* iinfo,
-                            void* ws, unsigned long long* info, hipStream_t stream) {
+                            void* ws, unsigned long long* info, hipStream_t stream,
+                            bool info_zeroed) {
   const int64_t nch = (D + kPartW - 1) / kPartW;
   int32_t* nxt = (int32_t*)ws;
   int32_t* exg = nxt + (D + 64);
@@ -403,16 +439,25 @@ hipError_t launch_partition(const float* kl, int64_t D, const int64_t* item_off,
   int32_t* gnode = node + (D + 64);
   int32_t* conv = gnode + (D + 64);
   int32_t* cnt = conv + (nch + 64);
-  hipError_t e = hipMemsetAsync(info, 0, 8 * sizeof(unsigned long long), stream);
-  if (e != hipSuccess) return e;
+  const bool single = item_off == nullptr && n_items == 1;
+  if (!info_zeroed) {
+    hipError_t e = hipMemsetAsync(info, 0, 8 * sizeof(unsigned long long), stream);
+    if (e == hipSuccess && single) e = hipMemsetAsync(iinfo, 0, 2 * sizeof(int64_t), stream);
+    if (e != hipSuccess) return e;
+  }
   hipLaunchKernelGGL(k_part_next, dim3((unsigned)((D + 255) / 256)), dim3(256), 0, stream, kl, D,
                      item_off, n_items, size_threshold, thr, nxt, info);
   hipLaunchKernelGGL(k_part_exit, dim3((unsigned)nch), dim3(kPartThreads), 0, stream, nxt, D, exg,
                      conv, info);
   hipLaunchKernelGGL(k_part_mark, dim3((unsigned)nch), dim3(kPartThreads), 0, stream, nxt, D, exg,
                      conv, node, cnt, info);
-  hipLaunchKernelGGL(k_part_emit, dim3((unsigned)nch), dim3(kPartThreads), 0, stream, nch, node,
-                     cnt, gnode, info);
+  if (single) {
+    hipLaunchKernelGGL(k_part_emit<true>, dim3((unsigned)nch), dim3(kPartThreads), 0, stream, nch,
+                       node, cnt, gnode, info, kl, D, size_threshold, thr, nxt, starts, iinfo);
+    return hipGetLastError();
+  }
+  hipLaunchKernelGGL(k_part_emit<false>, dim3((unsigned)nch), dim3(kPartThreads), 0, stream, nch,
+                     node, cnt, gnode, info, kl, D, size_threshold, thr, nxt, starts, iinfo);
   hipLaunchKernelGGL(k_part_ihdr, dim3((unsigned)((n_items + 255) / 256)), dim3(256), 0, stream,
                      kl, D, item_off, n_items, size_threshold, thr, gnode, starts, iinfo, info);
   hipLaunchKernelGGL(k_part_ibody, dim3((unsigned)((D + 255) / 256)), dim3(kPartThreads), 0, stream,

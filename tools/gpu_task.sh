@@ -12,6 +12,8 @@
 #   tools/gpu_task.sh stats TAG VARIANT NB D BITS        tools/prune_stats.py on a stats build
 #   tools/gpu_task.sh tiles TAG NB D BITS [VARIANT]      tools/tile_times.py on a tile-times build
 #   tools/gpu_task.sh decvar "V1 V2"                     decode tests + timing per variant build
+#   tools/gpu_task.sh py TAG SCRIPT [args]               a tools/ script -> gpurun_out/py_TAG.log
+#   tools/gpu_task.sh timeline TAG [bench args]          kernel + copy trace -> tools/timeline.py
 # Several tasks can be chained: tools/gpu_task.sh tests -- pmc c2 wait --config c2
 set -o pipefail
 cd "$(dirname "$0")/.."
@@ -82,6 +84,14 @@ run_one() {
       local tag=$1 nb=$2 d=$3 bits=$4 v=${5:-tt}
       CWQ_LIB_PATH=$PWD/tools/variants/libcwq_$v.so timeout -k 10 300 \
         python -u tools/tile_times.py $nb $d $bits > gpurun_out/tt_$tag.log 2>&1 && head -6 gpurun_out/tt_$tag.log ;;
+    py)  # py TAG SCRIPT [args]: a tools/ script -> gpurun_out/py_TAG.log
+      local tag=$1; shift
+      timeout -k 10 300 python -u "$@" > gpurun_out/py_$tag.log 2>&1 && tail -4 gpurun_out/py_$tag.log ;;
+    timeline)  # kernel + copy trace of a bench run, then tools/timeline.py on it
+      local tag=$1; shift
+      BARGS="$* --steps 3 --warmup 1" prof prof_${tag}_tl --kernel-trace --memory-copy-trace --stats && \
+        python3 tools/timeline.py gpurun_out/prof_${tag}_tl ${TL_MS:-12} > gpurun_out/tl_$tag.txt && \
+        tail -3 gpurun_out/tl_$tag.txt ;;
     *) echo "unknown task $task"; return 2 ;;
   esac
 }

@@ -94,6 +94,10 @@ declare -A V=(
   [tt0]="-DCWQ_TILE_TIMES -DCWQ_XCD_BALANCE=0"
   [xcd0]="-DCWQ_XCD_BALANCE=0"
   [tail1]="-DCWQ_TAIL_SPLIT=1"
+  [q0]="-DCWQ_TILE_QUEUE=0"
+  [qg3k]="-DCWQ_QUEUE_GRID=3072"
+  [qg6k]="-DCWQ_QUEUE_GRID=6144"
+  [qtail1]="-DCWQ_TAIL_SPLIT=1"
   [tail2]="-DCWQ_TAIL_SPLIT=2"
   [tail8]="-DCWQ_TAIL_SPLIT=8"
   [glds0]="-DCWQ_DECODE_GLDS=0"
