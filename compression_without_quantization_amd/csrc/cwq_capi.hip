@@ -1054,7 +1054,27 @@ int64_t batch_chunks() {
   return n;
 }
 thread_local std::vector<char> g_batch_host;
-thread_local std::vector<unsigned long long> g_batch_info;
+// page-locked per-thread buffer of at least `bytes` (the batch partition's
+// info; pageable memory would be staged), nullptr when allocation fails
+void* pinned_tl(size_t bytes) {
+  struct Buf {
+    void* p = nullptr;
+    size_t n = 0;
+  };
+  thread_local Buf b;
+  if (b.n < bytes) {
+    if (b.p) (void)hipHostFree(b.p);
+    b.p = nullptr;
+    b.n = 0;
+    const size_t want = bytes < 4096 ? 4096 : bytes * 2;
+    if (hipHostMalloc(&b.p, want, hipHostMallocDefault) != hipSuccess) {
+      b.p = nullptr;
+      return nullptr;
+    }
+    b.n = want;
+  }
+  return b.p;
+}
 thread_local std::vector<cwq::BatchItem> g_batch_items;
 
 constexpr int64_t kBatchFellBack = INT64_MIN;
@@ -1076,7 +1096,8 @@ int64_t batch_device_path(int64_t n_items, const int64_t* item_off, int64_t D, i
                           const float* zeros, const float* ones, float* sample, float* out,
                           int64_t* offs, int32_t* idx, int32_t* bseed, int32_t* idx_h,
                           CallEvents& evs, CallEvents& tev, const float* p_loc,
-                          const float* p_scale, hipStream_t s, hipStream_t d2h, hipStream_t h2d) {
+                          const float* p_scale, hipStream_t s, hipStream_t d2h, hipStream_t h2d,
+                          hipEvent_t part_ev) {
   const GroupedWs& l = bl.g;
   const int64_t K = (int64_t)ci.size() - 1;
 #ifdef CWQ_PHASE_TIMES  // tuning builds: per-phase host wall times to stderr
@@ -1104,16 +1125,18 @@ int64_t batch_device_path(int64_t n_items, const int64_t* item_off, int64_t D, i
     (void)hipStreamSynchronize(h2d);
   };
   hipError_t e;
-  g_batch_info.resize((size_t)(8 + 2 * n_items));
-  unsigned long long* hi = g_batch_info.data();
+  unsigned long long* hi =
+      (unsigned long long*)pinned_tl((size_t)(8 + 2 * n_items) * sizeof(unsigned long long));
+  if (!hi) return kBatchFellBack;
+  // info[0..7] were zeroed by the caller's k_grouped_prep; the wait polls
   if ((e = hipMemcpyAsync(ioff_d, item_off, (size_t)(n_items + 1) * 8, hipMemcpyHostToDevice,
                           s)) != hipSuccess ||
       (e = cwq::launch_partition(kl, D, ioff_d, n_items, size_threshold, group_thr(n_nats, false),
-                                 dst, iinfo_d, w + l.part, info_d, s)) != hipSuccess ||
+                                 dst, iinfo_d, w + l.part, info_d, s, true)) != hipSuccess ||
       (e = hipMemcpyAsync(hi, info_d, 8 * 8, hipMemcpyDeviceToHost, s)) != hipSuccess ||
       (e = hipMemcpyAsync(hi + 8, iinfo_d, (size_t)(2 * n_items) * 8, hipMemcpyDeviceToHost, s)) !=
           hipSuccess ||
-      (e = hipStreamSynchronize(s)) != hipSuccess) {
+      (e = hipEventRecord(part_ev, s)) != hipSuccess || (e = wait_event(part_ev)) != hipSuccess) {
     drain();
     return hip_fail(e, "cwq_code_grouped_greedy_batch: device partition");
   }
@@ -1408,15 +1431,13 @@ int64_t cwq_code_grouped_greedy_batch(
   int rc;
   // :193-210 for every item at once (elementwise), then the KL to the host chunk
   // by chunk, so the first chunk's partitions start before the rest arrives
-  if ((rc = cwq_standardise(q_loc, q_scale, p_loc, p_scale, D, t_loc, t_scale, stream)) < 0)
-    return rc;
-  if ((rc = cwq_kl_normal_normal(q_loc, q_scale, p_loc, p_scale, D, kl, stream)) < 0) return rc;
-  if (D > 0 && (e = hipMemsetAsync(zeros, 0, (size_t)D * 4, s)) != hipSuccess)
-    return hip_fail(e, "memset");
-  if (D > 0 && (e = hipMemsetD32Async((hipDeviceptr_t)ones, 0x3f800000u, (size_t)D, s)) !=
-                   hipSuccess)
-    return hip_fail(e, "memset");
-  if (device_partition_enabled() && cwq::partition_applies(D, size_threshold)) {
+  // (one launch: standardise, KL, the standard prior, the partition's counters)
+  const bool try_dev = device_partition_enabled() && cwq::partition_applies(D, size_threshold);
+  if ((e = cwq::launch_grouped_prep(q_loc, q_scale, p_loc, p_scale, D, t_loc, t_scale, kl, zeros,
+                                    ones, (unsigned long long*)(w + l.pinfo), try_dev ? 8 : 0,
+                                    s)) != hipSuccess)
+    return hip_fail(e, "cwq_code_grouped_greedy_batch: standardise / KL");
+  if (try_dev) {
     // :207-252 every item's partition on the device (cwq_partition.hip: one walk
     // over the batch, bit-identical to the host loop), then the chunks' group
     // layouts on the device too: the host only sequences launches and writes the
@@ -1425,7 +1446,7 @@ int64_t cwq_code_grouped_greedy_batch(
         n_items, item_off, D, n_steps, n_bits_per_step, seeds, rho, size_threshold, n_nats,
         sample_host, bits_host, bits_cap, bits_off, starts_host, n_starts, w, workspace_bytes, bl,
         o, ci, t_loc, t_scale, kl, zeros, ones, sample, out, offs, idx, bseed, idx_h, evs, tev,
-        p_loc, p_scale, s, d2h, h2d);
+        p_loc, p_scale, s, d2h, h2d, kl_ready);
     if (r != kBatchFellBack) return r;
   }
   if ((e = hipEventRecord(kl_ready, s)) == hipSuccess) e = hipStreamWaitEvent(d2h, kl_ready, 0);
