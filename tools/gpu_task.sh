@@ -50,6 +50,9 @@ run_one() {
         lds)  prof prof_${tag}_lds --pmc SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_SMEM SQ_WAVES ;;
         *) echo "unknown PMC set $set"; return 2 ;;
       esac && echo pmc $tag $set ok ;;
+    vpmc)  # vpmc TAG VARIANT SET [bench args]: pmc on a tools/variants build
+      local tag=$1 v=$2; shift 2
+      ( export CWQ_LIB_PATH=$PWD/tools/variants/libcwq_$v.so; run_one pmc $tag "$@" ) ;;
     stress)
       local n=${1:-400}
       timeout -k 10 300 python -u tools/stress_csr.py $n ${STRESS_SEED:-20000} 200 \
