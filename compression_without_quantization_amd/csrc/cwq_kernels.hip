@@ -2356,6 +2356,9 @@ __global__ void __launch_bounds__(256, CWQ_FUSED_WAVES) k_small_fused(
     }
 
     // (3) exact values of the listed rows, lane-parallel over (row, dim)
+#ifdef CWQ_PROBE_NOEXACT  // timing probe only (wrong indices): listed rows not scored
+    used = 0;
+#endif
     if (used > 0) {
       // prefix of the rows' dims: pre[e] = first item of row e
       const bool have = lane < used;
@@ -2438,7 +2441,11 @@ __global__ void __launch_bounds__(256, CWQ_FUSED_WAVES) k_small_fused(
         if (slot4 == 0u) out_idx[(g0 + (int64_t)k4) * n_steps + step] = (int32_t)idx;
         const PhiloxStream st{r.k0, r.k1, r.c2, r.c3};
         for (int j = (int)slot4; j < d4; j += 16) {
+#ifdef CWQ_PROBE_NOFIN  // timing probe only (wrong samples): finalize without the exact normal
+          const float zz = (float)(idx + j);
+#else
           const float zz = exact_normal(st, (uint64_t)idx * (uint64_t)d4 + (uint32_t)j, logtab);
+#endif
           float sv = scale_s[off4 + j] * zz;
           sv = loc_s[off4 + j] + sv;
           best[off4 + j] = (STEP0 ? 0.0f : best[off4 + j]) + sv;

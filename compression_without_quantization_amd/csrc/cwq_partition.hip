@@ -49,6 +49,7 @@ constexpr int kPartW = 1024;        // dims per chunk
 constexpr int kPartMaxJump = 512;   // longest group the device path takes
 constexpr int kPartRun = 8;         // non-converged chunks a walk may cross
 constexpr int kPartThreads = 256;
+constexpr int kPartLdsItems = 1024;  // batches up to this many items search offsets in LDS
 
 // info[0] nodes on the walk, info[2] fallback flag, info[4] longest nxt(i) - i
 // (when above kPartMaxJump: fallback).  Per item k: iinfo[2k] its starts (G + 1),
@@ -78,14 +79,20 @@ __global__ void __launch_bounds__(256) k_part_next(const float* __restrict__ kl,
   // (coalesced): each thread's scan then reads LDS instead of a chain of
   // dependent global loads (C3's 9.6M dims: 72 us -> a few)
   __shared__ float skl[256 + kPartMaxJump + 1];
+  __shared__ int64_t soff[kPartLdsItems + 1];
   const int64_t b = (int64_t)blockIdx.x * blockDim.x;
   const int64_t i = b + threadIdx.x;
   for (int t = threadIdx.x; t < 256 + kPartMaxJump + 1; t += 256)
     skl[t] = b + t < D ? kl[b + t] : 0.0f;
+  // a batch's item offsets in LDS too (the binary search per dim is a chain of
+  // dependent loads: 66 us of C3's 9.6M dims from global memory)
+  const bool lds_off = item_off && n_items <= kPartLdsItems;
+  if (lds_off)
+    for (int t = threadIdx.x; t <= n_items; t += 256) soff[t] = item_off[t];
   __syncthreads();
   int32_t jump = 0;
   if (i < D) {
-    const int64_t iend = item_end(item_off, n_items, D, i);
+    const int64_t iend = item_end(lds_off ? soff : item_off, n_items, D, i);
     int64_t j = i + 1;
     if (i < iend - 1) {
       float cur = skl[i - b];  // a group started at i: (kl[i], size 1)
@@ -372,9 +379,15 @@ __global__ void __launch_bounds__(256) k_part_ibody(int64_t D, const int64_t* __
                                                     const unsigned long long* __restrict__ info) {
   __shared__ int32_t red[kPartThreads];
   __shared__ int64_t s_k0;
+  __shared__ int64_t soff[kPartLdsItems + 1];
   if (info[4] > (unsigned long long)kPartMaxJump || info[2]) return;
   const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t total = (int64_t)info[0];
+  const bool lds_off = item_off && n_items <= kPartLdsItems;
+  if (lds_off)
+    for (int t = threadIdx.x; t <= n_items; t += kPartThreads) soff[t] = item_off[t];
+  __syncthreads();
+  const int64_t* __restrict__ io = lds_off ? soff : item_off;
   int64_t k = -1;
   int32_t gsz = 0;
   if (r < total) {
@@ -384,11 +397,11 @@ __global__ void __launch_bounds__(256) k_part_ibody(int64_t D, const int64_t* __
       int64_t lo = 0, hi = n_items;
       while (hi - lo > 1) {
         const int64_t m = (lo + hi) >> 1;
-        if (item_off[m] <= v) lo = m; else hi = m;
+        if (io[m] <= v) lo = m; else hi = m;
       }
       k = lo;
     }
-    const int64_t a = item_off ? item_off[k] : 0;
+    const int64_t a = item_off ? io[k] : 0;
     const int64_t r0 = iinfo[2 * n_items + 2 * k], dup = iinfo[2 * n_items + 2 * k + 1];
     starts[a + 2 * k + dup + (r - r0)] = v - a;  // st[dup + rank] (rank 0: the first dim)
     gsz = nxt[v] - v;
@@ -407,19 +420,22 @@ __global__ void __launch_bounds__(256) k_batch_layout(const BatchItem* __restric
                                                       const int64_t* __restrict__ dstarts,
                                                       int64_t* __restrict__ offs,
                                                       int32_t* __restrict__ seeds) {
-  const BatchItem it = items[blockIdx.x];
-  for (int64_t g = threadIdx.x; g < it.G; g += blockDim.x) {
+  const BatchItem it = items[blockIdx.x];  // item blockIdx.x, slice blockIdx.y of its groups
+  const int64_t step = (int64_t)blockDim.x * gridDim.y;
+  for (int64_t g = (int64_t)blockIdx.y * blockDim.x + threadIdx.x; g < it.G; g += step) {
     offs[it.go + g] = it.rel + dstarts[it.src + g];
     seeds[it.gs + g] = (int32_t)((uint32_t)it.seed + (uint32_t)g);  // :282, int32 wrap
   }
-  if (threadIdx.x == 0 && it.term >= 0) offs[it.term] = it.dc;
+  if (blockIdx.y == 0 && threadIdx.x == 0 && it.term >= 0) offs[it.term] = it.dc;
 }
 
 hipError_t launch_batch_layout(const BatchItem* items, int64_t n_items, const int64_t* dstarts,
                                int64_t* offs, int32_t* seeds, hipStream_t stream) {
   if (n_items <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_batch_layout, dim3((unsigned)n_items), dim3(256), 0, stream, items,
-                     dstarts, offs, seeds);
+  // enough workgroups to fill the chip whatever the item count (48 C3 items: 16 each)
+  const unsigned ys = n_items >= 2048 ? 1u : (unsigned)((2048 + n_items - 1) / n_items);
+  hipLaunchKernelGGL(k_batch_layout, dim3((unsigned)n_items, ys > 64 ? 64u : ys), dim3(256), 0,
+                     stream, items, dstarts, offs, seeds);
   return hipGetLastError();
 }
 
