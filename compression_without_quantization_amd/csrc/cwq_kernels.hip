@@ -2014,9 +2014,6 @@ __global__ void __launch_bounds__(256) k_small_survivors(
 #ifndef CWQ_FUSED_WAVES
 #define CWQ_FUSED_WAVES 8
 #endif
-#ifndef CWQ_FUSED_MERGE_FIN
-#define CWQ_FUSED_MERGE_FIN 1  // decided blocks' sample update inside the exact pass
-#endif
 static_assert(CWQ_FUSED_STAGE >= CWQ_FUSED_DMAX, "an exact batch holds at least one row");
 static_assert(CWQ_FUSED_LIST <= 64, "one listed row per lane");
 
@@ -2090,7 +2087,6 @@ struct QuadBlk {
 constexpr uint32_t kQuadKnown = 0;   // idx decided (empty block, or a single listed row)
 constexpr uint32_t kQuadListed = 1;  // listed rows scored exactly (s_key)
 constexpr uint32_t kQuadExact = 2;   // every candidate scored exactly
-constexpr uint32_t kQuadDone = 3;    // idx decided and the sample updated in the exact pass
 
 #ifndef CWQ_FUSED_NOINLINE
 #define CWQ_FUSED_NOINLINE 1  // the rare whole-block exact path out of line (its registers)
@@ -2363,31 +2359,9 @@ __global__ void __launch_bounds__(256, CWQ_FUSED_WAVES) k_small_fused(
 #ifdef CWQ_PROBE_NOEXACT  // timing probe only (wrong indices): listed rows not scored
     used = 0;
 #endif
-    // the decided blocks' winning rows ride along (rows [used, nrow)): their
-    // items update the sample in this pass, so step (4) has no exact normals
-    // to draw for them (C2: the finalize pass was ~4% of the kernel)
-    uint32_t nrow = used;
-#if CWQ_FUSED_MERGE_FIN
-    {
-      const bool kn = (int)lane < nq && bk[lane < 4u ? lane : 0u].state == kQuadKnown &&
-                      bk[lane < 4u ? lane : 0u].d > 0u;
-      const uint64_t km = __ballot(kn);
-      const uint32_t nkn = (uint32_t)__builtin_popcountll(km);
-      if (nkn > 0u && used + nkn <= (uint32_t)CWQ_FUSED_LIST) {
-        if (kn) {
-          const uint32_t r = used + lane_rank(km);
-          ln[r] = bk[lane].idx;
-          lk[r] = lane;
-          bk[lane].state = kQuadDone;
-        }
-        nrow = used + nkn;
-        wave_lds_sync();
-      }
-    }
-#endif
-    if (nrow > 0) {
+    if (used > 0) {
       // prefix of the rows' dims: pre[e] = first item of row e
-      const bool have = lane < nrow;
+      const bool have = lane < used;
       const uint32_t de = have ? bk[lk[lane]].d : 0u;
       uint32_t inc = de;
 #pragma unroll
@@ -2398,10 +2372,10 @@ __global__ void __launch_bounds__(256, CWQ_FUSED_WAVES) k_small_fused(
       if (have) pre[lane + 1] = inc;
       if (lane == 0) pre[0] = 0u;
       wave_lds_sync();
-      for (uint32_t e0 = 0; e0 < nrow;) {
+      for (uint32_t e0 = 0; e0 < used;) {
         // rows [e0, e1) whose items fit one batch (a row's d <= the batch)
         uint32_t e1 = e0 + 1;
-        while (e1 < nrow && pre[e1 + 1] - pre[e0] <= (uint32_t)CWQ_FUSED_STAGE) ++e1;
+        while (e1 < used && pre[e1 + 1] - pre[e0] <= (uint32_t)CWQ_FUSED_STAGE) ++e1;
         const uint32_t i0 = pre[e0], i1 = pre[e1];
         for (uint32_t it = i0 + lane; it < i1; it += 64) {
           uint32_t e = e0;
@@ -2414,14 +2388,11 @@ __global__ void __launch_bounds__(256, CWQ_FUSED_WAVES) k_small_fused(
           float sv = scale_s[ei] * zz;  // misc.py:14
           sv = loc_s[ei] + sv;          // misc.py:15
           const float tv = STEP0 ? sv : best[ei] + sv;  // :57
-          if (e < used)
-            lpv[it - i0] = log_prob(tv, t_loc[ei], t_scale[ei], lognorm[ei]);
-          else  // a decided block's winning row: :63 best += the row (step 4's arithmetic)
-            best[ei] = STEP0 ? 0.0f + sv : tv;
+          lpv[it - i0] = log_prob(tv, t_loc[ei], t_scale[ei], lognorm[ei]);
         }
         wave_lds_sync();
         const uint32_t e = e0 + lane;
-        if (e < e1 && e < used) {  // a lane per row: the Eigen-order sum (eval_row_f)
+        if (e < e1) {  // a lane per row: the Eigen-order sum (eval_row_f)
           const float* x = lpv + (pre[e] - i0);
           const int dr = (int)(pre[e + 1] - pre[e]);
           const int vec = dr & ~7;
@@ -2463,14 +2434,13 @@ __global__ void __launch_bounds__(256, CWQ_FUSED_WAVES) k_small_fused(
         const int d4 = (int)r.d;
         const int64_t off4 = r.off;
         uint32_t idx = r.idx;
-        if (r.state != kQuadKnown && r.state != kQuadDone) {
-          // ArgMaxTupleReducer: a key at the clamp level is index 0
+        if (r.state != kQuadKnown) {  // ArgMaxTupleReducer: a key at the clamp level is index 0
           const unsigned long long kb = kmax[k4];
           idx = (kb >> 32) > kArgmaxClampOrd ? argmax_key_index(kb) : 0u;
         }
         if (slot4 == 0u) out_idx[(g0 + (int64_t)k4) * n_steps + step] = (int32_t)idx;
         const PhiloxStream st{r.k0, r.k1, r.c2, r.c3};
-        for (int j = (int)slot4; r.state != kQuadDone && j < d4; j += 16) {
+        for (int j = (int)slot4; j < d4; j += 16) {
 #ifdef CWQ_PROBE_NOFIN  // timing probe only (wrong samples): finalize without the exact normal
           const float zz = (float)(idx + j);
 #else
