@@ -433,31 +433,49 @@ def code_grouped_greedy_sample_batch(sess, targets, proposals, n_steps, n_bits_p
         raise ValueError("one seed per item")
     # int32 wrap of each seed (TF int32 arithmetic), as the single call's seed32
     seeds32 = (seeds64 & 0xFFFFFFFF).astype(np.uint64).astype(np.uint32).view(np.int32)
-    flat = [a for t, p in zip(targets, proposals) for a in (t.loc, t.scale, p.loc, p.scale)]
-    dev = _device_of(*flat)
-    # the common case (every array a contiguous float32 tensor on dev): no
-    # per-array conversion calls (48 items: ~0.2 ms of attribute checks)
-    fast = all(type(a) is torch.Tensor and a.dtype == torch.float32 and a.device == dev and
-               a.is_contiguous() for a in flat)
-    parts = []
-    for i, (t, p) in enumerate(zip(targets, proposals)):
-        if fast:
-            q_loc, q_scale, p_loc, p_scale = flat[4 * i:4 * i + 4]
-        else:
+    cols = ([t.loc for t in targets], [t.scale for t in targets], [p.loc for p in proposals],
+            [p.scale for p in proposals])
+    f32 = torch.float32
+    # the common case (float32 CUDA tensors): few attribute reads per array
+    # (48 items: ~0.1 ms instead of ~0.25 ms); torch.cat itself refuses mixed
+    # devices, and the concatenations' device is checked once
+    fast = all(type(a) is torch.Tensor and a.dtype is f32 and a.is_cuda for c in cols for a in c)
+    cat = None
+    if fast:
+        sz = [a.numel() for a in cols[0]]
+        if any([a.numel() for a in c] != sz for c in cols[1:]):
+            raise ValueError("target and proposal of an item must have the same size")
+        sizes = np.array(sz, dtype=np.int64)
+        try:
+            # concatenation along dim 0 of equal trailing shapes is the concatenation
+            # of the flattened arrays (1-D latents: always)
+            cat = [torch.cat(c).reshape(-1) for c in cols]
+        except RuntimeError:
+            cat = None
+        if cat is not None and any(int(x.numel()) != int(sizes.sum()) for x in cat):
+            cat = None
+        if cat is not None:
+            dev = cat[0].device
+            if any(x.device != dev for x in cat[1:]):
+                cat = None
+    if cat is None:
+        dev = _device_of(*[a for c in cols for a in c])
+        parts = []
+        for t, p in zip(targets, proposals):
             if not _is_float32(t.loc) or not _is_float32(t.scale):
                 raise Exception("Target datatype must be float32!")  # :183-187
             if not _is_float32(p.loc) or not _is_float32(p.scale):
                 raise Exception("Proposal datatype must be float32!")
             q_loc, q_scale = _dist_parts(t, dev, "Target")
             p_loc, p_scale = _dist_parts(p, dev, "Proposal")
-        if not (q_scale.numel() == p_loc.numel() == p_scale.numel() == q_loc.numel()):
-            raise ValueError("target and proposal of an item must have the same size")
-        parts.append((q_loc, q_scale, p_loc, p_scale))
-    sizes = np.array([pt[0].numel() for pt in parts], dtype=np.int64)
+            if not (q_scale.numel() == p_loc.numel() == p_scale.numel() == q_loc.numel()):
+                raise ValueError("target and proposal of an item must have the same size")
+            parts.append((q_loc, q_scale, p_loc, p_scale))
+        sizes = np.array([pt[0].numel() for pt in parts], dtype=np.int64)
+        cat = [torch.cat([pt[k] for pt in parts]) for k in range(4)]
     item_off = np.concatenate([[0], np.cumsum(sizes)]).astype(np.int64)
     D = int(item_off[-1])
-    cat = [torch.cat([x if x.dim() == 1 else x.reshape(-1) for x in (pt[k] for pt in parts)])
-           for k in range(4)]
+    cat = [x.contiguous() for x in cat]
     n_steps, n_bits_per_step = int(n_steps), int(n_bits_per_step)
     n_bits_per_group = n_bits_per_step * n_steps
     need = int(lib.cwq_code_grouped_greedy_batch_workspace_size(D, n_items, n_steps))

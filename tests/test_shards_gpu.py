@@ -498,3 +498,45 @@ def test_grouped_batch_wrapper_raises_from_helper_thread(cwq):
         s1, b1, st1 = cwq.code_grouped_greedy_sample(None, t, p, 1, 8, 5)
         assert bitcode == b1 and list(starts) == list(st1)
         assert np.array_equal(sample.view(np.uint32), np.asarray(s1).view(np.uint32))
+
+
+def test_grouped_batch_wrapper_argument_forms(cwq):
+    """The batch wrapper's fast argument path (float32 CUDA tensors, one
+    torch.cat per column) and its general path give the same results: 1-D and
+    multi-dim items of different shapes, numpy items, a mix; float64 inputs
+    and size mismatches raise as the single call does."""
+    rng = np.random.default_rng(17)
+    shapes = [(1, 4, 6, 8), (1, 2, 3, 5), (700,)]
+    arrs = []
+    for shp in shapes:
+        n = int(np.prod(shp))
+        pl = (0.1 * rng.standard_normal(n)).astype(np.float32).reshape(shp)
+        ps = rng.uniform(0.8, 1.2, n).astype(np.float32).reshape(shp)
+        ql = (pl + 0.5 * ps * rng.standard_normal(shp)).astype(np.float32)
+        qs = (ps * rng.uniform(0.3, 1.0, shp)).astype(np.float32)
+        arrs.append((ql, qs, pl, ps))
+
+    def run(conv):
+        tg = [cwq.Normal(conv(a[0]), conv(a[1])) for a in arrs]
+        pr = [cwq.Normal(conv(a[2]), conv(a[3])) for a in arrs]
+        return cwq.code_grouped_greedy_sample_batch(None, tg, pr, 1, 8, 11)
+    def same(r0, r1):
+        for (s0, b0, st0), (s1, b1, st1) in zip(r0, r1):
+            assert b0 == b1 and np.array_equal(st0, st1)
+            assert np.array_equal(np.asarray(s0).view(np.uint32), np.asarray(s1).view(np.uint32))
+    flat = run(lambda x: torch.from_numpy(x.reshape(-1).copy()).cuda())  # 1-D tensors
+    same(flat, run(lambda x: torch.from_numpy(x).cuda()))  # multi-dim, shapes differ
+    same(flat, run(lambda x: x))                           # numpy arrays
+    # non-contiguous views code their logical (flattened) order
+    tr = lambda x: torch.from_numpy(x).cuda().transpose(0, -1)  # noqa: E731
+    same(run(lambda x: tr(x).reshape(-1).contiguous()), run(tr))
+    tg = [cwq.Normal(torch.from_numpy(a[0]).cuda().double(), torch.from_numpy(a[1]).cuda())
+          for a in arrs]
+    pr = [cwq.Normal(torch.from_numpy(a[2]).cuda(), torch.from_numpy(a[3]).cuda()) for a in arrs]
+    with pytest.raises(Exception, match="float32"):
+        cwq.code_grouped_greedy_sample_batch(None, tg, pr, 1, 8, 11)
+    tg = [cwq.Normal(torch.from_numpy(a[0]).cuda(), torch.from_numpy(a[1]).cuda()) for a in arrs]
+    pr[1] = cwq.Normal(torch.from_numpy(arrs[1][2][..., :-1].copy()).cuda(),
+                       torch.from_numpy(arrs[1][3][..., :-1].copy()).cuda())
+    with pytest.raises(ValueError, match="same size"):
+        cwq.code_grouped_greedy_sample_batch(None, tg, pr, 1, 8, 11)
