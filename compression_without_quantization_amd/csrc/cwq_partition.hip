@@ -51,8 +51,8 @@ constexpr int kPartRun = 8;         // non-converged chunks a walk may cross
 constexpr int kPartThreads = 256;
 constexpr int kPartLdsItems = 1024;  // batches up to this many items search offsets in LDS
 
-// info[0] nodes on the walk, info[2] fallback flag, info[4] longest nxt(i) - i
-// (when above kPartMaxJump: fallback).  Per item k: iinfo[2k] its starts (G + 1),
+// info[0] nodes on the walk, info[2] fallback flag, info[4] a jump nxt(i) - i
+// above kPartMaxJump (the fallback; 0 when there is none).  Per item k: iinfo[2k] its starts (G + 1),
 // iinfo[2k + 1] its largest group.
 __device__ __forceinline__ int64_t item_end(const int64_t* __restrict__ item_off, int64_t n_items,
                                             int64_t D, int64_t i) {
@@ -112,7 +112,9 @@ __global__ void __launch_bounds__(256) k_part_next(const float* __restrict__ kl,
     nxt[i] = (int32_t)j;
   }
   const int32_t mj = block_max(jump, red);  // one atomic per workgroup
-  if (threadIdx.x == 0 && mj > 32) atomicMax(&info[4], (unsigned long long)mj);
+  // only a jump past kPartMaxJump matters (the fallback): an atomic from every
+  // workgroup on one address serialised C3's 37.6k workgroups (~60 us)
+  if (threadIdx.x == 0 && mj > kPartMaxJump) atomicMax(&info[4], (unsigned long long)mj);
 }
 
 template <class T>
@@ -411,9 +413,15 @@ __global__ void __launch_bounds__(256) k_part_ibody(int64_t D, const int64_t* __
   if (threadIdx.x == 0) s_k0 = k;
   __syncthreads();
   const int64_t k0 = s_k0;
-  if (k >= 0 && k != k0) atomicMax((unsigned long long*)&iinfo[2 * k + 1], (unsigned long long)gsz);
+  // (an atomic only when it can raise the value: few workgroups of an item
+  // contend for its address)
+  unsigned long long* im = (unsigned long long*)iinfo;
+  if (k >= 0 && k != k0 && (unsigned long long)gsz > __atomic_load_n(&im[2 * k + 1], __ATOMIC_RELAXED))
+    atomicMax(&im[2 * k + 1], (unsigned long long)gsz);
   const int32_t m0 = block_max(k == k0 ? gsz : 0, red);
-  if (threadIdx.x == 0 && k0 >= 0) atomicMax((unsigned long long*)&iinfo[2 * k0 + 1], (unsigned long long)m0);
+  if (threadIdx.x == 0 && k0 >= 0 &&
+      (unsigned long long)m0 > __atomic_load_n(&im[2 * k0 + 1], __ATOMIC_RELAXED))
+    atomicMax(&im[2 * k0 + 1], (unsigned long long)m0);
 }
 
 __global__ void __launch_bounds__(256) k_batch_layout(const BatchItem* __restrict__ items,
