@@ -3092,8 +3092,15 @@ static void launch_prune_t(const EncodeArgs& a, int step, hipStream_t stream) {
 #ifndef CWQ_QUEUE_GRID
 #define CWQ_QUEUE_GRID 1536
 #endif
+  // Only for tiles of real work: with tiny tiles (C1: 16 candidates) the memset
+  // and a counter round trip per tile cost more than the slots they keep busy
+  // (C1 0.039 -> 0.065 ms with the queue)
+#ifndef CWQ_QUEUE_MIN_CPT
+#define CWQ_QUEUE_MIN_CPT 4096
+#endif
   uint32_t* tq = nullptr;
-  if (CWQ_TILE_QUEUE && a.tq != nullptr && ntiles < (1LL << 31)) {
+  if (CWQ_TILE_QUEUE && a.tq != nullptr && ntiles < (1LL << 31) &&
+      a.cand_per_tile >= CWQ_QUEUE_MIN_CPT && ntiles > CWQ_QUEUE_GRID) {
     if (hipMemsetAsync(a.tq, 0, sizeof(uint32_t), stream) == hipSuccess) tq = a.tq;
   }
   auto qgrid = [&](int64_t nt) -> unsigned {
