@@ -2014,9 +2014,6 @@ __global__ void __launch_bounds__(256) k_small_survivors(
 #ifndef CWQ_FUSED_WAVES
 #define CWQ_FUSED_WAVES 8
 #endif
-#ifndef CWQ_FUSED_PAIR
-#define CWQ_FUSED_PAIR 1  // screen two Philox blocks per iteration
-#endif
 static_assert(CWQ_FUSED_STAGE >= CWQ_FUSED_DMAX, "an exact batch holds at least one row");
 static_assert(CWQ_FUSED_LIST <= 64, "one listed row per lane");
 
@@ -2255,7 +2252,11 @@ __global__ void __launch_bounds__(256, CWQ_FUSED_WAVES) k_small_fused(
         float rs[4] = {0.0f, 0.0f, 0.0f, 0.0f};
         float cur = 0.0f;
         int j = 0, qd = 0;
-        auto dims4 = [&](const float* z) {
+        for (int b = 0; b < db; ++b) {
+          const U4 x = philox10_lo(b0 + (uint32_t)b, K, sb.k0, sb.k1);
+          float z[4];
+          box_muller_screen(x.x, x.y, z[0], z[1]);
+          box_muller_screen(x.z, x.w, z[2], z[3]);
 #pragma unroll
           for (int t = 0; t < 4; ++t) {
             const float2 e = abk[j];
@@ -2271,32 +2272,6 @@ __global__ void __launch_bounds__(256, CWQ_FUSED_WAVES) k_small_fused(
               ++qd;
             }
           }
-        };
-#if CWQ_FUSED_PAIR
-        // two Philox blocks per iteration: their (independent) rounds and
-        // transcendentals interleave, where one block at a time left each
-        // Philox chain's latency exposed (the kernel runs far below VALU issue)
-        int b = 0;
-        for (; b + 1 < db; b += 2) {
-          const U4 x = philox10_lo(b0 + (uint32_t)b, K, sb.k0, sb.k1);
-          const U4 y = philox10_lo(b0 + (uint32_t)b + 1u, K, sb.k0, sb.k1);
-          float z[4], w[4];
-          box_muller_screen(x.x, x.y, z[0], z[1]);
-          box_muller_screen(y.x, y.y, w[0], w[1]);
-          box_muller_screen(x.z, x.w, z[2], z[3]);
-          box_muller_screen(y.z, y.w, w[2], w[3]);
-          dims4(z);
-          dims4(w);
-        }
-        if (b < db) {
-#else
-        for (int b = 0; b < db; ++b) {
-#endif
-          const U4 x = philox10_lo(b0 + (uint32_t)b, K, sb.k0, sb.k1);
-          float z[4];
-          box_muller_screen(x.x, x.y, z[0], z[1]);
-          box_muller_screen(x.z, x.w, z[2], z[3]);
-          dims4(z);
         }
         // tau from the lane's best valid row (the lower bound is monotone in s)
         float smax = -__builtin_inff();
