@@ -222,8 +222,9 @@ int64_t cwq_code_grouped_greedy(const float* q_loc, const float* q_scale, const 
 
 /* cwq_code_grouped_greedy in two halves, so the caller can work while the
  * device codes (the Python wrapper builds the reference's group_start_indices
- * list meanwhile).  _begin: the same inputs; synchronises once (after the KL),
- * writes starts_host[0..G] and returns G (or a negative error code), with the
+ * list meanwhile).  _begin: the same inputs; waits for the partition (on the
+ * device where it applies: its 128-byte result; else the KL copy and the host
+ * loop), writes starts_host[0..G] and returns G (or a negative error code), with the
  * encode, the destandardisation and the copies of the G * n_steps indices to
  * idx_host (idx_cap >= G * n_steps; D + 1 groups at most) and of the sample to
  * sample_host still in flight on the stream: both must stay valid until _end,
