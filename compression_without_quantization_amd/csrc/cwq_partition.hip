@@ -93,23 +93,28 @@ __global__ void __launch_bounds__(256) k_part_next(const float* __restrict__ kl,
   int32_t jump = 0;
   if (i < D) {
     const int64_t iend = item_end(lds_off ? soff : item_off, n_items, D, i);
-    int64_t j = i + 1;
+    // the loop from a start at i (kl[i], size 1) accepts dim i + k while the
+    // float32 running sum stays below the threshold (:233, :243), and stops at
+    // size T (size == k), at the item's last dim (a forced start, :234), or one
+    // past kPartMaxJump (longer than the device path takes: the fallback).
+    // Folding those three limits into klim leaves one add and one compare per
+    // dim (C3's low-KL stretches scan hundreds of dims from every start).
+    int32_t k = 1;
     if (i < iend - 1) {
-      float cur = skl[i - b];  // a group started at i: (kl[i], size 1)
-      int64_t size = 1;
-      for (; j < iend - 1; ++j) {  // the item's last dim always starts a group (:234)
-        const float s = cur + skl[j - b];  // float32 running sum (:233, :243); j - i <= kPartMaxJump
-        if (size >= T || s >= thr) break;
+      int64_t klim = iend - 1 - i;
+      klim = klim < T ? klim : T;
+      klim = klim < kPartMaxJump + 1 ? klim : kPartMaxJump + 1;
+      const int32_t kl32 = (int32_t)klim;
+      const float* row = skl + (i - b);  // row[k] = kl[i + k]; i + k - b <= 255 + 512
+      float cur = row[0];
+      for (; k < kl32; ++k) {
+        const float s = cur + row[k];
+        if (s >= thr) break;
         cur = s;
-        ++size;
-        if (j - i >= kPartMaxJump) {  // longer than the device path takes
-          ++j;                        // (jump > kPartMaxJump: the fallback)
-          break;
-        }
       }
     }  // i == iend - 1: the item's last group is that dim; the walk goes on at iend
-    jump = (int32_t)(j - i);  // > kPartMaxJump: not covered (the scan stopped early)
-    nxt[i] = (int32_t)j;
+    jump = k;  // > kPartMaxJump: not covered
+    nxt[i] = (int32_t)(i + k);
   }
   const int32_t mj = block_max(jump, red);  // one atomic per workgroup
   // only a jump past kPartMaxJump matters (the fallback): an atomic from every
