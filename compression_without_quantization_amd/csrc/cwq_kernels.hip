@@ -543,7 +543,9 @@ __global__ void __launch_bounds__(256, CWQ_PRUNE_MIN_WAVES) k_encode_prune(
         k += 1;
         const bool complete = (k == G);
         const bool below = upper < tau;
+#ifdef CWQ_PRUNE_STATS
         const bool prune = !complete && below;
+#endif
         const bool done = complete || below || !active;
         // the finished lanes' mask from the compares' own masks (SALU): a
         // ballot of the combined flag costs a v_cndmask + v_cmp to rebuild it
