@@ -128,3 +128,59 @@ def test_model_items_match_host_loop_per_item():
     for k in range(len(sizes)):
         want = host(kl[off[k]:off[k + 1]].copy(), T, n_nats) if sizes[k] else np.array([0, 0])
         assert np.array_equal(got[k], want), k
+
+
+def _next_loop(kl, i, iend, T, thr):
+    """nxt(i) as the reference loop restarts from a start at i (the shape of
+    k_part_next before round 4's rewrite): size and sum carried, three tests."""
+    j = i + 1
+    if i < iend - 1:
+        cur, size = kl[i], 1
+        while j < iend - 1:
+            s = np.float32(cur + kl[j])
+            if size >= T or s >= thr:
+                break
+            cur, size = s, size + 1
+            if j - i >= MAXJ:
+                j += 1
+                break
+            j += 1
+    return j
+
+
+def _next_folded(kl, i, iend, T, thr):
+    """k_part_next's scan (csrc/cwq_partition.hip): the three stops folded into
+    one bound klim = min(iend - 1 - i, T, MAXJ + 1), one add and compare per dim."""
+    k = 1
+    if i < iend - 1:
+        klim = min(iend - 1 - i, T, MAXJ + 1)
+        cur = kl[i]
+        while k < klim:
+            s = np.float32(cur + kl[i + k])
+            if s >= thr:
+                break
+            cur = s
+            k += 1
+    return i + k
+
+
+def test_folded_scan_equals_loop():
+    """The kernel's folded scan equals the loop's on every start: random and
+    near-zero KL (long groups up to and past MAXJ), size thresholds 1..5 and
+    large, NaN/inf entries, item ends at every distance."""
+    rng = np.random.default_rng(11)
+    n_nats = 8 * np.log(2) - 1
+    thr = thr_of(n_nats)
+    for trial in range(12):
+        D = int(rng.integers(2, 1400))
+        scale = [0.8, 0.02, 0.004, 1e-4][trial % 4]
+        kl = rng.exponential(scale, D).astype(np.float32)
+        if trial % 3 == 0:
+            kl[rng.integers(0, D, 5)] = np.float32(np.nan)
+            kl[rng.integers(0, D, 3)] = np.float32(np.inf)
+        for T in (1, 2, 3, 5, 4095):
+            for iend in (D, max(1, D // 2), min(D, 600)):
+                for i in range(0, iend):
+                    a = _next_loop(kl, i, iend, T, thr)
+                    b = _next_folded(kl, i, iend, T, thr)
+                    assert a == b, (trial, T, iend, i, a, b)
