@@ -1075,9 +1075,8 @@ __global__ void __launch_bounds__(256, COOP ? CWQ_CSR_COOP_MIN_WAVES : CWQ_CSR_R
     const float2* __restrict__ sab, const float* __restrict__ bpre,
     const uint32_t* __restrict__ ordu, const float4* __restrict__ grp,
     uint32_t* __restrict__ gtau, unsigned long long* __restrict__ keys, int64_t coop_min_d,
-    const float4* __restrict__ abp, uint32_t* __restrict__ tq) {
+    const float4* __restrict__ abp) {
   __shared__ double logtab[32];
-  __shared__ uint32_t s_next;
   __shared__ uint32_t tau_ord;
   __shared__ uint32_t sq_cnt;
   __shared__ uint32_t sq_n[CWQ_CSR_SURVIVOR_CAP];
@@ -1100,16 +1099,7 @@ __global__ void __launch_bounds__(256, COOP ? CWQ_CSR_COOP_MIN_WAVES : CWQ_CSR_R
   const uint32_t wv = wave_id();
   const uint32_t lane = threadIdx.x & 63u;
 
-  // tile queue (tq != nullptr, as k_encode_prune's): a resident grid whose
-  // workgroups take their first tile by id and the rest from one counter
-  auto next_tile = [&](int64_t cur) -> int64_t {
-    if (tq == nullptr) return cur + gridDim.x;
-    __syncthreads();
-    if (threadIdx.x == 0) s_next = gridDim.x + atomicAdd(tq, 1u);
-    __syncthreads();
-    return (int64_t)s_next;
-  };
-  for (int64_t tile = blockIdx.x; tile < ntiles; tile = next_tile(tile)) {
+  for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
     uint32_t tid = threadIdx.x;
     asm volatile("" : "+v"(tid));
     // tile-major order: a block's later tiles start after its first ones have
@@ -3186,32 +3176,21 @@ static void launch_prune_csr(const EncodeArgs& a, int step, hipStream_t stream) 
                      a.block_off, a.ud, a.nb, a.sab, a.cdim, a.bpre, a.ordu, a.grp, a.gtau,
                      a.abp, (int64_t)CWQ_CSR_LDS_DIMS, coop_min_d);
   constexpr int64_t kGrid = 1 << 20;
-  unsigned grid = (unsigned)(ntiles < kGrid ? ntiles : kGrid);
-#ifndef CWQ_CSR_QUEUE
-#define CWQ_CSR_QUEUE 1
-#endif
-  // the resident grid of the kernel's occupancy (6 or 4 waves/SIMD)
-  const int64_t qgrid = 256 * 4 * (coop ? CWQ_CSR_COOP_MIN_WAVES : CWQ_CSR_RUN_MIN_WAVES) / 4;
-  uint32_t* tq = nullptr;
-  if (CWQ_CSR_QUEUE && a.tq != nullptr && ntiles > qgrid && ntiles < (1LL << 31) &&
-      hipMemsetAsync(a.tq, 0, sizeof(uint32_t), stream) == hipSuccess) {
-    tq = a.tq;
-    grid = (unsigned)qgrid;
-  }
+  const unsigned grid = (unsigned)(ntiles < kGrid ? ntiles : kGrid);
   if (coop)
     hipLaunchKernelGGL((k_encode_prune_csr<STEP0, true>), dim3(grid), dim3(256), 0, stream,
                        a.t_loc, a.t_scale, a.loc_s, a.scale_s, a.lognorm, a.out_sample,
                        a.block_off, a.ud, ntiles, tpb, cpt, a.n_cand, seeds_of(a),
                        step, (const float2*)a.sab, (const float*)a.bpre,
                        (const uint32_t*)a.ordu, (const float4*)a.grp, a.gtau, a.keys,
-                       coop_min_d, (const float4*)a.abp, tq);
+                       coop_min_d, (const float4*)a.abp);
   else
     hipLaunchKernelGGL((k_encode_prune_csr<STEP0, false>), dim3(grid), dim3(256), 0, stream,
                        a.t_loc, a.t_scale, a.loc_s, a.scale_s, a.lognorm, a.out_sample,
                        a.block_off, a.ud, ntiles, tpb, cpt, a.n_cand, seeds_of(a),
                        step, (const float2*)a.sab, (const float*)a.bpre,
                        (const uint32_t*)a.ordu, (const float4*)a.grp, a.gtau, a.keys,
-                       coop_min_d, (const float4*)a.abp, tq);
+                       coop_min_d, (const float4*)a.abp);
 }
 
 #ifndef CWQ_SMALL_FUSED

@@ -82,7 +82,6 @@ declare -A V=(
   [seed20]="-DCWQ_SEED_LOG2=20"
   [stats0]="-DCWQ_PRUNE_STATS -DCWQ_SEED_LOG2=0"
   [fw7]="-DCWQ_FUSED_WAVES=7"
-  [csrq0]="-DCWQ_CSR_QUEUE=0"
   [pnofin]="-DCWQ_PROBE_NOFIN"
   [pnoex]="-DCWQ_PROBE_NOEXACT"
   [pnoboth]="-DCWQ_PROBE_NOFIN -DCWQ_PROBE_NOEXACT"
