@@ -290,7 +290,11 @@ def _uniform_encode(cwq, cwqlib, tl, ts, pl, ps, d, bits, n_steps, seed, rho, mo
     # 2^20+ candidates (many tiles per block, tau close to the best row):
     # multi-step (best carried), rho, group counts G = d / 4 from 2 to 16
     (16, 20, 1, 1, 1.0), (8, 20, 1, 3, 1.0), (16, 21, 2, 2, 0.9), (24, 20, 1, 2, 1.0),
-    (32, 20, 3, 2, 1.0), (64, 20, 1, 1, 1.0), (16, 22, 1, 2, 1.0)])
+    (32, 20, 3, 2, 1.0), (64, 20, 1, 1, 1.0), (16, 22, 1, 2, 1.0),
+    # the tile queue (tiles of >= 4096 candidates, more tiles than the resident
+    # grid): one tile per block (C4's shape), and block-interleaved tiles with
+    # the tail split (C5's shape), two steps
+    (16, 12, 1, 16384, 1.0), (16, 20, 2, 64, 1.0)])
 def test_pruned_matches_unpruned_and_oracle(cwq, cwqlib, oracle, d, bits, n_steps, nb, rho):
     from compression_without_quantization_amd.synthetic import make_blocks
     b = make_blocks(nb, d, bits, seed=77 + d + bits)
