@@ -142,17 +142,11 @@ __device__ __forceinline__ T block_max(T v, T* red) {
 // never past the exit)
 __device__ __forceinline__ void part_jump(int32_t* p, int64_t b, int32_t lim, int n) {
   for (int r = 0; r < 11; ++r) {  // 2^11 > kPartW
-    int open = 0;
     for (int l = threadIdx.x; l < n; l += kPartThreads) {
       const int32_t v = p[l];
-      if (v < lim) {
-        p[l] = p[v - b];
-        open = 1;
-      }
+      if (v < lim) p[l] = p[v - b];
     }
-    // every pointer at the exit: later rounds would change nothing (a chunk
-    // of ~5-dim groups is done after ~8 of the 11 rounds)
-    if (!__syncthreads_or(open)) break;
+    __syncthreads();
   }
 }
 
@@ -244,18 +238,14 @@ __global__ void __launch_bounds__(256) k_part_mark(const int32_t* __restrict__ n
         if (mark[l] && v < lim) mark[v - b] = 1;
       }
       __syncthreads();
-      int open = 0;
       for (int l = threadIdx.x; l < n; l += kPartThreads) {
         const int32_t v = J[l];
         J2[l] = v < lim ? J[v - b] : v;
-        open |= v < lim ? 1 : 0;
       }
-      // no pointer left inside the chunk: the marks are complete
-      const int more = __syncthreads_or(open);
+      __syncthreads();
       int32_t* t = J;
       J = J2;
       J2 = t;
-      if (!more) break;
     }
   }
   // compact the marked nodes in order: per-thread runs of 4 consecutive dims
