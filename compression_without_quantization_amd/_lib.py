@@ -114,6 +114,7 @@ SIGNATURES = {
 TOOL_SIGNATURES = {
     "cwq_debug_prune_stats": (c_int, [c_vp, c_int]),
     "cwq_debug_tile_times": (c_int, [c_vp, c_vp, c_vp, c_int]),
+    "cwq_debug_quad_times": (c_int, [c_vp, c_vp, c_int]),
     "cwq_debug_partition_workspace_size": (c_size, [c_i64]),
     "cwq_debug_group_starts_device": (c_i64, [c_vp, c_i64, c_i64, c_f64, c_vp, c_vp, c_size,
                                               c_vp, c_vp]),

@@ -51,7 +51,8 @@ int hip_fail(hipError_t e, const char* where) {
 size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
 
 struct WsLayout {
-  size_t keys, tq, loc_s, scale_s, lognorm, sab, cdim, bpre, ordu, grp, gtau, abp, slist, total;
+  size_t keys, tq, loc_s, scale_s, lognorm, sab, cdim, bpre, ordu, grp, gtau, abp, slist;
+  size_t sdmap, total;
   bool csr;   // has the general pruned kernel's arrays
   bool recs;  // ... and the visit-order records of blocks longer than CWQ_CSR_LDS_DIMS
 };
@@ -59,7 +60,7 @@ struct WsLayout {
 // Blocks the uniform fast pruned kernel takes (d % 8 == 0, 8 <= d <= 64) need
 // only keys + the per-dim shard constants; everything else (CSR, other d) also
 // gets the general pruned kernel's screening constants and the screened small-candidate
-// path's survivor slots (20 B/dim + 244 B/block),
+// path's survivor slots and the small-candidate pipeline's arrays (24 B/dim + 244 B/block),
 // and, when some block may exceed CWQ_CSR_LDS_DIMS dims, the visit-order
 // records of the long blocks (32 B/dim + 384 B per CWQ_CSR_LDS_DIMS + 1 dims,
 // csr_rec_entries: short blocks take no room, so a grouped call sized for
@@ -82,6 +83,7 @@ WsLayout ws_layout(int64_t nb, int64_t total_dims, bool csr, bool recs) {
   l.csr = csr;
   l.recs = csr && recs;
   l.sab = l.cdim = l.bpre = l.ordu = l.grp = l.gtau = l.abp = l.slist = o;
+  l.sdmap = o;
   if (csr) {
     l.slist = o;  // the screened small-candidate path's survivor slots (8 B each)
     o = align_up(o + (size_t)nb * CWQ_SLIST_PER_BLOCK * 8, 256);
@@ -97,6 +99,8 @@ WsLayout ws_layout(int64_t nb, int64_t total_dims, bool csr, bool recs) {
     o = align_up(o + (size_t)nb * 16, 256);
     l.gtau = o;
     o = align_up(o + (size_t)nb * 4 * CWQ_CSR_GTAU_STRIDE, 256);
+    l.sdmap = o;  // the small-candidate pipeline's dim -> block map
+    o = align_up(o + (size_t)total_dims * 4, 256);
     if (l.recs) {
       l.abp = o;
       o = align_up(o + (size_t)cwq::csr_rec_entries(total_dims) * 32, 256);
@@ -400,6 +404,7 @@ int encode_impl(const float* t_loc, const float* t_scale, const float* p_loc,
   a.abp = l.recs ? (float4*)(w + l.abp) : nullptr;
 #endif
   a.slist = l.csr ? (uint2*)(w + l.slist) : nullptr;
+  a.sdmap = l.csr ? (uint32_t*)(w + l.sdmap) : nullptr;
   a.ev_start = o.eval_start_event;
   a.ev_stop = o.eval_stop_event;
   hipError_t e = cwq::launch_encode(a, (hipStream_t)stream);
@@ -2007,6 +2012,13 @@ int cwq_debug_tile_times(unsigned long long* t0, unsigned long long* t1, unsigne
   if (!t0 || !t1 || !wg || n < 0) return fail(CWQ_ERR_INVALID, "cwq_debug_tile_times: bad args");
   const int r = cwq::tile_times(t0, t1, wg, n);
   if (r < 0) return fail(CWQ_ERR_HIP, "cwq_debug_tile_times: symbol copy failed");
+  return r;
+}
+
+int cwq_debug_quad_times(unsigned long long* t, unsigned int* info, int n) {
+  if (!t || !info || n < 0) return fail(CWQ_ERR_INVALID, "cwq_debug_quad_times: bad args");
+  const int r = cwq::quad_times(t, info, n);
+  if (r < 0) return fail(CWQ_ERR_HIP, "cwq_debug_quad_times: symbol copy failed");
   return r;
 }
 

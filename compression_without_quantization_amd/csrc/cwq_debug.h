@@ -28,6 +28,14 @@ int cwq_debug_prune_stats(unsigned long long* out72, int flags);
  * other builds). */
 int cwq_debug_tile_times(unsigned long long* t0, unsigned long long* t1, unsigned int* wg, int n);
 
+/* Per-quad wall clock of the last k_small_fused launch: t[6*q + i] is quad q's
+ * s_memrealtime at its start (i = 0) and after its constants, screen, exact
+ * rows, exact blocks and finalize (i = 1..5); info[4*q + ...] = HW_ID, XCC_ID,
+ * listed rows scored exactly, exact blocks | dims << 8.  Filled only by builds
+ * compiled with -DCWQ_QUAD_TIMES (tools/quad_times.py); returns the quads
+ * copied (0 in other builds). */
+int cwq_debug_quad_times(unsigned long long* t, unsigned int* info, int n);
+
 /* The grouped coder's device partition (cwq_partition.hip) on a device KL
  * array: starts (device, D + 2 int64) as cwq_group_starts computes them on the
  * host.  Returns the number of starts, or 0 when the device path does not cover

@@ -76,6 +76,11 @@ struct EncodeArgs {
   // optional profiling events around the eval launches (hipEvent_t)
   void* ev_start;
   void* ev_stop;
+  // the small-candidate pipeline (k_small_*; nullptr: not sized for it):
+  // per-dim screening constants (sA, sB) by absolute dim offset (a view of
+  // sab, set by launch_encode) and the dim -> block map [total_dims]
+  const float2* pre_ab = nullptr;
+  uint32_t* sdmap = nullptr;
 };
 
 #define CWQ_SLIST_PER_BLOCK 8
@@ -154,6 +159,7 @@ hipError_t launch_selftest_screen(uint32_t m0, int64_t count, float* rad, float*
                                   hipStream_t stream);
 int prune_stats(unsigned long long* out72, int reset);
 int tile_times(unsigned long long* t0, unsigned long long* t1, unsigned int* wg, int n);
+int quad_times(unsigned long long* t, unsigned int* info, int n);
 hipError_t launch_selftest_wave_max(const float* x, int64_t nw, float* out, hipStream_t stream);
 hipError_t launch_selftest_div(const float* a, const float* b, int64_t n, float* out,
                                hipStream_t stream);

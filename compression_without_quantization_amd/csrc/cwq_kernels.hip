@@ -1977,38 +1977,17 @@ __global__ void __launch_bounds__(256) k_small_survivors(
 }
 
 // ---------------------------------------------------------------------------
-// The small-candidate step fused into one kernel (round 4): a wave owns four
-// consecutive blocks (64 <= 2^b < 4096 candidates, d <= CWQ_FUSED_DMAX) and
-// does k_small_prep's constants, k_small_screen's rows, the exact scoring of
-// the survivors and k_encode_finalize's index + sample update itself, so a
-// step is k_prep_dims and this launch.  The three-kernel path ran ~650 waves
-// in each of its prep and survivor launches (latency-bound: 20 + 23 us for
-// C2's 41.5k blocks) and sent per-dim constants, headers and survivor slots
-// through HBM; a one-block-per-wave fusion left every per-block latency chain
-// exposed (113 us against 106).  Four blocks per wave:
-//   * constants: a 16-lane row per block, lanes over its dims (coalesced
-//     loads); the block sums are row-local DPP reductions (four steps), the
-//     bounds and the stream key are computed by every lane of the row;
-//   * screen: the blocks one after the other, as k_small_screen (a lane per
-//     4-row span of d whole Philox blocks, per-dim constants wave-uniform LDS
-//     reads); a block's rows whose upper bound reaches its final tau are
-//     listed in LDS.  A block with a single listed row needs no exact value:
-//     every other row's exact value is below tau <= that row's.
-//   * exact values of the other listed rows, lane-parallel over (row, dim):
-//     each lane computes one normal exactly (its Philox block and the one
-//     Box-Muller pair holding it) and its log-density into LDS; a lane per row
-//     then sums in the Eigen order (eval_row's values bit for bit) and folds
-//     its key into its block's LDS maximum;
-//   * finalize: best += the winning row, a row's lanes over the block's dims
-//     (k_encode_finalize's arithmetic).
-// Blocks whose constants leave the gate, or whose listed rows overflow the
-// list, are scored exactly (every candidate through eval_row).
+// The small-candidate shapes (64 <= 2^b < 4096 candidates, blocks of d <=
+// CWQ_FUSED_DMAX): shared pieces of the small pipeline below (k_small_*).
+// Round 4 ran these shapes as one kernel (k_small_fused: a wave per four
+// blocks doing constants, screen, exact survivors and finalize); round 5
+// split it (see "The small-candidate step as a pipeline").
 // ---------------------------------------------------------------------------
 #ifndef CWQ_FUSED_DMAX
-#define CWQ_FUSED_DMAX 64  // longest block of the fused kernel (a wave's 4 blocks: 256 LDS slots)
+#define CWQ_FUSED_DMAX 64  // longest block of the small pipeline
 #endif
 #ifndef CWQ_FUSED_LIST
-#define CWQ_FUSED_LIST 64  // listed rows per wave
+#define CWQ_FUSED_LIST 64  // listed rows per block
 #endif
 #ifndef CWQ_FUSED_STAGE
 #define CWQ_FUSED_STAGE 256  // (row, dim) values per exact batch
@@ -2019,30 +1998,10 @@ __global__ void __launch_bounds__(256) k_small_survivors(
 static_assert(CWQ_FUSED_STAGE >= CWQ_FUSED_DMAX, "an exact batch holds at least one row");
 static_assert(CWQ_FUSED_LIST <= 64, "one listed row per lane");
 
-// Row-local (16-lane) DPP reduction of doubles: every lane of a row gets its
-// row's result.  The block sums of the fused kernel feed rigorous bounds whose
-// slack dwarfs double rounding, so their order does not matter.  Full exec mask.
-template <int CTRL>
-__device__ __forceinline__ double dpp_f64(double v) {
-  const uint64_t b = __builtin_bit_cast(uint64_t, v);
-  const int lo = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)b, CTRL, 0xf, 0xf, false);
-  const int hi = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)(b >> 32), CTRL, 0xf, 0xf, false);
-  return __builtin_bit_cast(double, ((uint64_t)(uint32_t)hi << 32) | (uint64_t)(uint32_t)lo);
-}
-template <bool MAX>
-__device__ __forceinline__ double row16_red_f64(double v) {
-  auto op = [](double a, double b) { return MAX ? (a > b ? a : b) : a + b; };
-  v = op(v, dpp_f64<0xb1>(v));   // quad_perm [1,0,3,2]
-  v = op(v, dpp_f64<0x4e>(v));   // quad_perm [2,3,0,1]
-  v = op(v, dpp_f64<0x141>(v));  // row_half_mirror
-  v = op(v, dpp_f64<0x140>(v));  // row_mirror
-  return v;
-}
-
 // Exact normal k of a block's stream: its Philox block and the one
 // Box-Muller pair that holds it (normal4_dev's element k & 3, bit for bit).
 #ifndef CWQ_EXACT_NOINLINE
-#define CWQ_EXACT_NOINLINE 1  // out of line: its f64 constants no longer spill the fused kernel
+#define CWQ_EXACT_NOINLINE 0  // inline (k_small_one has no loop to hoist its constants out of)
 #endif
 #if CWQ_EXACT_NOINLINE
 __device__ __noinline__
@@ -2058,7 +2017,7 @@ float exact_normal(const PhiloxStream& st, uint64_t k, const double* logtab) {
 }
 
 // LDS written by some lanes of a wave and read by others: order the wave's
-// accesses (no workgroup barrier: the four waves work independently)
+// accesses (no workgroup barrier: a wave's LDS is its own)
 __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   __builtin_amdgcn_wave_barrier();
@@ -2066,28 +2025,14 @@ __device__ __forceinline__ void wave_lds_sync() {
 __device__ __forceinline__ uint32_t lane_rank(uint64_t m) {  // set lanes of m below this one
   return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
-__device__ __forceinline__ int64_t readlane_i64(int64_t v, int l) {
-  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l);
-  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)((uint64_t)v >> 32), l);
-  return (int64_t)(((uint64_t)hi << 32) | lo);
-}
-__device__ __forceinline__ float readlane_f32(float v, int l) {
-  return u2f((uint32_t)__builtin_amdgcn_readlane((int)f2u(v), l));
-}
-__device__ __forceinline__ uint32_t readlane_u32(uint32_t v, int l) {
-  return (uint32_t)__builtin_amdgcn_readlane((int)v, l);
-}
-
-// Per-block record of the fused kernel (LDS, one per block of the wave)
+// A block for quad_exact_block: its first dim, length and step stream
 struct QuadBlk {
   int64_t off;
-  uint32_t d, k0, k1, c2, c3, idx;  // idx: the block's index once decided
-  uint32_t state;                   // kQuad*
-  float bf, c1, c2f, as, pq;        // screening bound constants
-  uint32_t rel;                     // first dim, relative to the quad's
+  uint32_t d, k0, k1, c2, c3;
 };
+// a block's state in the small pipeline (SmallRec q0.w, then k_small_one's)
 constexpr uint32_t kQuadKnown = 0;   // idx decided (empty block, or a single listed row)
-constexpr uint32_t kQuadListed = 1;  // listed rows scored exactly (s_key)
+constexpr uint32_t kQuadListed = 1;  // screened; listed rows scored exactly
 constexpr uint32_t kQuadExact = 2;   // every candidate scored exactly
 
 #ifndef CWQ_FUSED_NOINLINE
@@ -2098,8 +2043,8 @@ constexpr uint32_t kQuadExact = 2;   // every candidate scored exactly
 #else
 #define CWQ_RARE __device__ __forceinline__
 #endif
-// Every candidate of a block exactly (eval_row, a lane per row): the fused
-// kernel's fallback for blocks outside the screening gate or with a full list.
+// Every candidate of a block exactly (eval_row, a lane per row): k_small_one's
+// fallback for blocks outside the screening gate or with a full list.
 // Returns the wave's best argmax key.
 template <bool STEP0>
 CWQ_RARE unsigned long long quad_exact_block(const QuadBlk r, const float* __restrict__ t_loc,
@@ -2127,126 +2072,198 @@ CWQ_RARE unsigned long long quad_exact_block(const QuadBlk r, const float* __res
   return wave_max_u64(bestk);
 }
 
+#ifdef CWQ_QUAD_TIMES
+// timing builds only (tools/quad_times.py --one): per block of k_small_one the
+// wall clock (s_memrealtime, 100 MHz) at its start [0], after its screen [1]
+// and at its end [2..5]; info = HW_ID, XCC_ID, listed rows scored exactly,
+// exact-block flag | d << 8
+constexpr int kQuadTimes = 1 << 16;
+__device__ unsigned long long g_quad_t[kQuadTimes][6];
+__device__ unsigned int g_quad_info[kQuadTimes][4];
+#endif
+
+// ---------------------------------------------------------------------------
+// The small-candidate step as a pipeline (round 5): blocks of d <= 64,
+// 64 <= 2^b < 4096 candidates (C2/C3's 8-bit groups).  tools/quad_times.py
+// showed where k_small_fused's time went on C2 (41.5k groups, 10.4k quads):
+// the quads ran at the chip's issue rate while 8 waves shared each SIMD, but
+// every quad took ~29 us, so the launch drained for ~35 us of its 62-69 us
+// at falling occupancy, and 35% of a quad's time went to its constants phase
+// (per-block f64 sums and bounds on 16-lane rows, DPP reductions, the stream
+// key).  Here the per-block work runs lane-parallel before the screen, and
+// the screen runs a block at a time on persistent waves fed by a counter:
+//   k_small_prep1     a workgroup per 256 blocks, a thread per dim: the shard
+//                     constants (step 0, k_prep_dims' arithmetic) and each
+//                     dim's screening constants (csr_dim), summed per block
+//                     in LDS; then a thread per block: bounds, stream key ->
+//                     a 64-byte record; dim -> block map; zeroes the counter
+//   k_small_one       persistent waves, a block at a time from the counter:
+//                     screen, exact survivors -> index
+//   k_small_finalize  a thread per dim: best += the winning row (:63)
+// ---------------------------------------------------------------------------
+struct SmallRec {  // 4 x uint4: q0 = (off lo, off hi, d, state), q1 = stream key,
+  uint4 q0, q1;    // q2 = (bf, c1, c2, As), q3 = (Pq, -, -, -)
+  uint4 q2, q3;
+};
+static_assert(sizeof(SmallRec) <= 8 * CWQ_SLIST_PER_BLOCK, "a record per block in slist");
+// blocks per k_small_prep1 workgroup of 256 threads: C2's 41.5k blocks make
+// 650 workgroups (with 256 per workgroup 163 of them ran 20 us, latency-bound)
+constexpr int kSmallPrepBlocks = 64;
+
+// The dims of a launch's blocks: [block_off[0], block_off[nb]) (absolute: a
+// forked part of a launch passes block_off + g0), or [0, nb ud) for uniform blocks
+__device__ __forceinline__ void dims_of(const int64_t* __restrict__ block_off, int64_t ud,
+                                        int64_t nb, int64_t& d0, int64_t& d1) {
+  d0 = block_off ? block_off[0] : 0;
+  d1 = block_off ? block_off[nb] : nb * ud;
+}
+
+// FIRST (step 0): also the shard constants and best = 0 (k_prep_dims).  The
+// block sums are LDS atomics in no fixed order, which the bounds' slack (far
+// above double rounding) covers, so the screen stays exact-safe.
+template <bool FIRST>
+__global__ void __launch_bounds__(256) k_small_prep1(
+    const float* __restrict__ t_loc, const float* __restrict__ t_scale,
+    const float* __restrict__ p_loc, const float* __restrict__ p_scale, float nst, float sdiv,
+    float rho, float* __restrict__ loc_s, float* __restrict__ scale_s,
+    float* __restrict__ lognorm, float* __restrict__ best, const int64_t* __restrict__ block_off,
+    int64_t ud, int64_t nb, SeedSpec sd, int32_t step, float2* __restrict__ pre_ab,
+    SmallRec* __restrict__ rec, uint32_t* __restrict__ dmap) {
+  constexpr int B = kSmallPrepBlocks;
+  constexpr int T = 256;
+  __shared__ int64_t boff[B + 1];
+  __shared__ double acc[5][B];  // sum M, sum |M|, sum |M| + M, sum A^2, sum C
+  __shared__ uint32_t amx[B], abad[B];
+  const int t = threadIdx.x;
+  const int64_t g0 = (int64_t)blockIdx.x * B;
+  const int n = (int)(nb - g0 < B ? nb - g0 : B);
+  for (int k = t; k <= n; k += T) boff[k] = block_off ? block_off[g0 + k] : (g0 + k) * ud;
+  if (t < B) {
+    for (int k = 0; k < 5; ++k) acc[k][t] = 0.0;
+    amx[t] = 0u;
+    abad[t] = 0u;
+  }
+  __syncthreads();
+  const int64_t i0 = boff[0], i1 = boff[n];
+  for (int64_t i = i0 + t; i < i1; i += T) {
+    int lo = 0, hi = n;  // boff[lo] <= i < boff[hi] (empty blocks are skipped)
+    while (hi - lo > 1) {
+      const int m = (lo + hi) >> 1;
+      if (boff[m] <= i) lo = m; else hi = m;
+    }
+    float ls, ss, c;
+    const float sg = t_scale[i];
+    if (FIRST) {  // k_prep_dims' arithmetic, bit for bit
+      ls = p_loc[i] / nst;
+      ss = (rho * p_scale[i]) / sdiv;
+      c = kHalfLog2Pi + logf_full(sg, kLogTabConst);
+      loc_s[i] = ls;
+      scale_s[i] = ss;
+      lognorm[i] = c;
+    } else {
+      ls = loc_s[i];
+      ss = scale_s[i];
+      c = lognorm[i];
+    }
+    const CsrDim o = csr_dim<FIRST>(ls, ss, t_loc[i], sg, c, FIRST ? 0.0f : best[i]);
+    pre_ab[i] = float2{o.sa, o.sb};
+    atomicAdd(&acc[0][lo], o.M);
+    atomicAdd(&acc[1][lo], __builtin_fabs(o.M));
+    atomicAdd(&acc[2][lo], __builtin_fabs(o.M) + o.M);
+    atomicAdd(&acc[3][lo], (double)o.A * (double)o.A);
+    atomicAdd(&acc[4][lo], (double)o.C);
+    atomicMax(&amx[lo], f2u(o.A));  // A >= 0: float order is uint order
+    if (!o.ok) atomicOr(&abad[lo], 1u);
+    dmap[i] = (uint32_t)(g0 + lo);
+  }
+  __syncthreads();
+  if (t >= n) return;
+  const int64_t g = g0 + t;
+  const int64_t off = boff[t];
+  const int d = (int)(boff[t + 1] - off);
+  const double sm = acc[0][t], sa = acc[1][t], sk = acc[2][t], s2 = acc[3][t], cs = acc[4][t];
+  const double mx = (double)u2f(amx[t]);
+  // the screening bound's block constants (round 4's k_small_fused, term for term)
+  const double h_s = (double)d, h_e = (double)d / 8.0 + 8.0;
+  const double gam = 1.01 * ((h_s > h_e ? h_s : h_e) + 1.0) * 0x1p-24;
+  const double sl = (3.0 * gam + 0x1p-20) * (__builtin_fabs(sm) + sa + sk) + 0x1p-126;
+  const float bf = round_up_f32(sm + cs * (1.0 + 0x1p-20) + sl);
+  const float c1 = round_dn_f32(1.0 - 3.0 * gam - 0x1p-22);
+  const float c2 = round_up_f32(1.0 + 3.0 * gam + 0x1p-14);
+  const float as = round_dn_f32(sm - sl - 1.01 * s2 * (1.0 + 0x1p-11));
+  const float pq = round_up_f32(2.01 * mx * __builtin_sqrt((double)(d > 0 ? d : 1)) *
+                                (1.0 + 0x1p-11));
+  const bool screen = abad[t] == 0u && d > 0 && d <= CWQ_FUSED_DMAX && as - as == 0.0f &&
+                      pq - pq == 0.0f && bf - bf == 0.0f && mx - mx == 0.0;
+  const PhiloxStream st = generate_key(step_seed(sd.of(g), step), 42);
+  SmallRec r;
+  r.q0 = uint4{(uint32_t)off, (uint32_t)((uint64_t)off >> 32), (uint32_t)d,
+               d == 0 ? kQuadKnown : (screen ? kQuadListed : kQuadExact)};
+  r.q1 = uint4{st.k0, st.k1, st.c2, st.c3};
+  r.q2 = uint4{f2u(bf), f2u(c1), f2u(c2), f2u(as)};
+  r.q3 = uint4{f2u(pq), 0u, 0u, 0u};
+  rec[g] = r;
+}
+
+// A wave (a 64-thread workgroup) per block: the screen (k_small_screen's spans)
+// and the exact scoring of the listed rows; writes the index (out_idx).  The
+// dispatcher hands a slot to the next wave as soon as one ends.  Measured
+// alternatives on C2
+// (tools/quad_times.py --one): persistent waves drawing blocks from one
+// atomic counter, 474 us (41.5k same-address atomics serialise at ~11 ns);
+// two blocks per wave in a loop, 69 us against 47 (the loop's spills);
+// longest blocks first (a counting sort by d), 41 us against 47 but the sort
+// cost a launch and a histogram that needed zeroing.
 template <bool STEP0>
-__global__ void __launch_bounds__(256, CWQ_FUSED_WAVES) k_small_fused(
+__global__ void __launch_bounds__(64, CWQ_FUSED_WAVES) k_small_one(
     const float* __restrict__ t_loc, const float* __restrict__ t_scale,
     const float* __restrict__ loc_s, const float* __restrict__ scale_s,
-    const float* __restrict__ lognorm, float* __restrict__ best,
-    const int64_t* __restrict__ block_off, int64_t ud, int64_t nb, int64_t n_cand, SeedSpec sd,
-    int32_t step, int n_steps, int32_t* __restrict__ out_idx) {
+    const float* __restrict__ lognorm, const float* __restrict__ best,
+    const SmallRec* __restrict__ rec, const float2* __restrict__ pre_ab, int64_t nb, int64_t u0,
+    int64_t n_cand, int32_t step, int n_steps, int32_t* __restrict__ out_idx) {
   __shared__ double logtab[32];
-  __shared__ float2 s_ab[4][4 * CWQ_FUSED_DMAX];   // the 4 blocks' (sA, sB), by dim offset
-  __shared__ uint32_t s_ln[4][CWQ_FUSED_LIST];     // listed rows
-  __shared__ float s_lu[4][CWQ_FUSED_LIST];        // their upper bounds
-  __shared__ uint32_t s_lk[4][CWQ_FUSED_LIST];     // their block (0..3)
-  __shared__ uint32_t s_pre[4][CWQ_FUSED_LIST + 1];  // first exact item of each listed row
-  __shared__ float s_lp[4][CWQ_FUSED_STAGE];       // exact batch: log-densities
-  __shared__ unsigned long long s_key[4][4];       // best exact key per block
-  __shared__ QuadBlk s_bk[4][4];
-  fill_logtab(logtab);
-  const uint32_t wv = wave_id();
-  const uint32_t lane0 = threadIdx.x & 63u;
-  const int64_t nwaves = (int64_t)gridDim.x * 4;
-  float2* ab = s_ab[wv];
-  uint32_t* ln = s_ln[wv];
-  float* lu = s_lu[wv];
-  uint32_t* lk = s_lk[wv];
-  uint32_t* pre = s_pre[wv];
-  float* lpv = s_lp[wv];
-  unsigned long long* kmax = s_key[wv];
-  QuadBlk* bk = s_bk[wv];
-  for (int64_t q = (int64_t)blockIdx.x * 4 + wv; 4 * q < nb; q += nwaves) {
-    uint32_t lane = lane0;  // re-derived per quad (see k_small_screen)
-    asm volatile("" : "+v"(lane));
-    const uint32_t k = lane >> 4, slot = lane & 15u;
-    const int64_t g0 = 4 * q;
-    const int nq = (int)(nb - g0 < 4 ? nb - g0 : 4);  // blocks of this quad
-    const int64_t g = g0 + (int64_t)k;
-    const bool valid = (int)k < nq;
-    const BlockSpan sp = block_span(block_off, ud, valid ? g : g0);
-    const int64_t off = sp.off;
-    const int d = valid ? (int)sp.d : 0;
-    const int64_t base = readlane_i64(off, 0);  // block g0's first dim
-    const int64_t rel = off - base;
-    const bool fits = d <= CWQ_FUSED_DMAX && rel + d <= 4 * CWQ_FUSED_DMAX;
-
-    // (1) per-dim constants and each block's bound (k_small_prep), a row per block
-    double sm = 0.0, sa = 0.0, sk = 0.0, s2 = 0.0, cs = 0.0, mx = 0.0;
-    int okl = 1;
-    if (fits) {
-      for (int j = (int)slot; j < d; j += 16) {
-        const CsrDim o = csr_dim<STEP0>(loc_s[off + j], scale_s[off + j], t_loc[off + j],
-                                        t_scale[off + j], lognorm[off + j],
-                                        STEP0 ? 0.0f : best[off + j]);
-        ab[rel + j] = float2{o.sa, o.sb};
-        sm += o.M;
-        sa += __builtin_fabs(o.M);
-        sk += __builtin_fabs(o.M) + o.M;
-        s2 += (double)o.A * (double)o.A;
-        cs += (double)o.C;
-        mx = (double)o.A > mx ? (double)o.A : mx;
-        okl &= o.ok ? 1 : 0;
-      }
-    }
-    sm = row16_red_f64<false>(sm);
-    sa = row16_red_f64<false>(sa);
-    sk = row16_red_f64<false>(sk);
-    s2 = row16_red_f64<false>(s2);
-    cs = row16_red_f64<false>(cs);
-    mx = row16_red_f64<true>(mx);
-    const bool row_ok = ((__ballot(okl == 0) >> (16u * k)) & 0xffffull) == 0ull;
-    const double h_s = (double)d, h_e = (double)d / 8.0 + 8.0;
-    const double gam = 1.01 * ((h_s > h_e ? h_s : h_e) + 1.0) * 0x1p-24;
-    const double sl = (3.0 * gam + 0x1p-20) * (__builtin_fabs(sm) + sa + sk) + 0x1p-126;
-    const float bf = round_up_f32(sm + cs * (1.0 + 0x1p-20) + sl);
-    const float c1 = round_dn_f32(1.0 - 3.0 * gam - 0x1p-22);
-    const float c2 = round_up_f32(1.0 + 3.0 * gam + 0x1p-14);
-    const float as = round_dn_f32(sm - sl - 1.01 * s2 * (1.0 + 0x1p-11));
-    const float pq = round_up_f32(2.01 * mx * __builtin_sqrt((double)(d > 0 ? d : 1)) *
-                                  (1.0 + 0x1p-11));
-    const bool screen = fits && row_ok && d > 0 && as - as == 0.0f && pq - pq == 0.0f &&
-                        bf - bf == 0.0f;
-    if (slot == 0u && valid) {
-      const PhiloxStream st = generate_key(step_seed(sd.of(g), step), 42);
-      QuadBlk r;
-      r.off = off;
-      r.d = (uint32_t)d;
-      r.k0 = st.k0;
-      r.k1 = st.k1;
-      r.c2 = st.c2;
-      r.c3 = st.c3;
-      r.idx = 0u;
-      r.state = d == 0 ? kQuadKnown : (screen ? kQuadListed : kQuadExact);
-      r.bf = bf;
-      r.c1 = c1;
-      r.c2f = c2;
-      r.as = as;
-      r.pq = pq;
-      r.rel = (uint32_t)rel;
-      bk[k] = r;
-      kmax[k] = 0ull;
-    }
+  // the block's (sA, sB) repeated 4 times: a lane's span of 4 rows is 4 d
+  // normals, so Philox block b covers abx[4 b .. 4 b + 3] (two b128 reads,
+  // issued ahead of the Philox rounds that hide their latency)
+  __shared__ float4 abx[2 * CWQ_FUSED_DMAX];
+  __shared__ uint32_t ln[CWQ_FUSED_LIST];
+  __shared__ float lu[CWQ_FUSED_LIST];
+  __shared__ float lpv[CWQ_FUSED_STAGE];
+  __shared__ unsigned long long kmax;
+  const uint32_t lane = threadIdx.x & 63u;
+  if (lane < 32) logtab[lane] = kLogTabConst[lane];
+  auto ufirst = [](uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); };
+  auto ffirst = [&](uint32_t v) { return u2f(ufirst(v)); };
+  const int64_t g = u0 + blockIdx.x;
+  {
+#ifdef CWQ_QUAD_TIMES  // tools/quad_times.py --one: per block start, after the screen, end
+    if (lane == 0u && g < kQuadTimes) g_quad_t[g][0] = __builtin_amdgcn_s_memrealtime();
+#endif
+    const uint4 q0 = rec[g].q0, q1 = rec[g].q1;
+    const int64_t off = (int64_t)(((uint64_t)ufirst(q0.y) << 32) | ufirst(q0.x));
+    const int db = (int)ufirst(q0.z);
+    uint32_t state = ufirst(q0.w);
+    PhiloxStream sb;
+    sb.k0 = ufirst(q1.x);
+    sb.k1 = ufirst(q1.y);
+    sb.c2 = ufirst(q1.z);
+    sb.c3 = ufirst(q1.w);
+    uint32_t idx = 0u;
+    uint32_t used = 0;
+    if (lane == 0) kmax = 0ull;
     wave_lds_sync();
-
-    // (2) screen the blocks' rows (k_small_screen's spans), list those that can win
-    uint32_t used = 0;  // listed rows of the wave (uniform)
-    for (int kb = 0; kb < nq; ++kb) {
-      const QuadBlk rb = bk[kb];  // wave-uniform LDS reads, into SGPRs
-      auto ufirst = [](uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); };
-      auto ffirst = [&](float v) { return u2f(ufirst(f2u(v))); };
-      if (ufirst(rb.state) != kQuadListed) continue;
-      const int db = (int)ufirst(rb.d);
-      const float2* abk = ab + ufirst(rb.rel);
-      const float bfb = ffirst(rb.bf), c1b = ffirst(rb.c1), c2b = ffirst(rb.c2f);
-      const float asb = ffirst(rb.as), pqb = ffirst(rb.pq);
-      PhiloxStream sb;
-      sb.k0 = ufirst(rb.k0);
-      sb.k1 = ufirst(rb.k1);
-      sb.c2 = ufirst(rb.c2);
-      sb.c3 = ufirst(rb.c3);
-      const PhiloxLo K = philox_lo_key(sb);  // n_cand * d / 4 < 2^32 here (launch_small)
+    if (state == kQuadListed) {
+      const uint4 q2 = rec[g].q2;
+      const float bfb = ffirst(q2.x), c1b = ffirst(q2.y), c2b = ffirst(q2.z);
+      const float asb = ffirst(q2.w), pqb = ffirst(rec[g].q3.x);
+      if ((int)lane < db) {  // d <= 64 (launch_small)
+        const float2 e = pre_ab[off + lane];
+        float2* ax = (float2*)abx;
+        for (int r = 0; r < 4; ++r) ax[r * db + (int)lane] = e;
+      }
+      wave_lds_sync();
+      const PhiloxLo K = philox_lo_key(sb);  // n_cand * d / 4 < 2^32 (d <= 64, < 4096 rows)
       float tau = -__builtin_inff();
-      const uint32_t first = used;
       bool over = false;
       for (int64_t m0 = 0; 256 * m0 < n_cand; ++m0) {
         const int64_t ns = 4 * ((int64_t)lane + 64 * m0);
@@ -2255,14 +2272,17 @@ __global__ void __launch_bounds__(256, CWQ_FUSED_WAVES) k_small_fused(
         float cur = 0.0f;
         int j = 0, qd = 0;
         for (int b = 0; b < db; ++b) {
+          const float4 e01 = abx[2 * b], e23 = abx[2 * b + 1];
           const U4 x = philox10_lo(b0 + (uint32_t)b, K, sb.k0, sb.k1);
           float z[4];
           box_muller_screen(x.x, x.y, z[0], z[1]);
           box_muller_screen(x.z, x.w, z[2], z[3]);
+          const float2 ev[4] = {float2{e01.x, e01.y}, float2{e01.z, e01.w},
+                                float2{e23.x, e23.y}, float2{e23.z, e23.w}};
 #pragma unroll
-          for (int t = 0; t < 4; ++t) {
-            const float2 e = abk[j];
-            const float a = __builtin_fmaf(e.x, z[t], e.y);
+          for (int tt = 0; tt < 4; ++tt) {
+            const float2 e = ev[tt];  // = (sA, sB) of dim j
+            const float a = __builtin_fmaf(e.x, z[tt], e.y);
             cur = __builtin_fmaf(-a, a, cur);
             if (++j == db) {  // wave-uniform: a row of the span is complete
               if (qd == 0) rs[0] = cur;
@@ -2284,9 +2304,9 @@ __global__ void __launch_bounds__(256, CWQ_FUSED_WAVES) k_small_fused(
             smax = fmaxf(smax, rs[qq]);
             any = true;
           }
-        const float lower =
-            any ? __builtin_fmaf(smax, c2b, asb) - pqb * __builtin_amdgcn_sqrtf(-smax)
-                : -__builtin_inff();
+        const float lower = any ? __builtin_fmaf(smax, c2b, asb) -
+                                      pqb * __builtin_amdgcn_sqrtf(-smax)
+                                : -__builtin_inff();
         tau = fmaxf(tau, wave_max_f32(lower));
         uint64_t m[4];
         uint32_t cnt = 0;
@@ -2296,17 +2316,17 @@ __global__ void __launch_bounds__(256, CWQ_FUSED_WAVES) k_small_fused(
           cnt += (uint32_t)__builtin_popcountll(m[qq]);
         }
         if (cnt == 0) continue;
-        if (used + cnt > CWQ_FUSED_LIST) {  // drop this block's rows the raised tau excludes
-          const bool have = lane >= first && lane < used;
+        if (used + cnt > CWQ_FUSED_LIST) {  // drop the rows the raised tau excludes
+          const bool have = lane < used;
           const uint32_t nl = have ? ln[lane] : 0u;
           const float ul = have ? lu[lane] : 0.0f;
           const uint64_t keep = __ballot(have && ul >= tau);
           if ((keep >> lane) & 1ull) {
-            const uint32_t r = first + lane_rank(keep);
+            const uint32_t r = lane_rank(keep);
             ln[r] = nl;
             lu[r] = ul;
           }
-          used = first + (uint32_t)__builtin_popcountll(keep);
+          used = (uint32_t)__builtin_popcountll(keep);
           wave_lds_sync();
         }
         if (used + cnt > CWQ_FUSED_LIST) {  // list full (near-ties): score the block exactly
@@ -2321,7 +2341,6 @@ __global__ void __launch_bounds__(256, CWQ_FUSED_WAVES) k_small_fused(
             const uint32_t slot_i = at + lane_rank(mq);
             ln[slot_i] = (uint32_t)(ns + qq);
             lu[slot_i] = __builtin_fmaf(rs[qq], c1b, bfb);
-            lk[slot_i] = (uint32_t)kb;
           }
           at += (uint32_t)__builtin_popcountll(mq);
         }
@@ -2329,132 +2348,120 @@ __global__ void __launch_bounds__(256, CWQ_FUSED_WAVES) k_small_fused(
         wave_lds_sync();
       }
       if (over) {
-        used = first;
-        if (lane == 0) bk[kb].state = kQuadExact;
-        wave_lds_sync();
-        continue;
-      }
-      // keep the rows whose upper bound reaches the block's final tau
-      const bool have = lane >= first && lane < used;
-      const uint32_t nl = have ? ln[lane] : 0u;
-      const uint64_t keep = __ballot(have && lu[have ? lane : 0] >= tau);
-      const uint32_t nk = (uint32_t)__builtin_popcountll(keep);
-      if (nk == 1u) {  // the single listed row is the argmax: no exact value needed
-        if ((keep >> lane) & 1ull) {
-          bk[kb].idx = nl;
-          bk[kb].state = kQuadKnown;
-        }
-        used = first;
+        state = kQuadExact;
+        used = 0;
       } else {
-        if ((keep >> lane) & 1ull) {
-          const uint32_t r = first + lane_rank(keep);
-          ln[r] = nl;
-          lk[r] = (uint32_t)kb;
+        // keep the rows whose upper bound reaches the block's final tau
+        const bool have = lane < used;
+        const uint32_t nl = have ? ln[lane] : 0u;
+        const uint64_t keep = __ballot(have && lu[have ? lane : 0] >= tau);
+        const uint32_t nk = (uint32_t)__builtin_popcountll(keep);
+        if (nk == 1u) {  // the single listed row is the argmax: no exact value needed
+          idx = ufirst((uint32_t)__builtin_amdgcn_readlane((int)nl, __builtin_ctzll(keep)));
+          state = kQuadKnown;
+          used = 0;
+        } else {
+          if ((keep >> lane) & 1ull) ln[lane_rank(keep)] = nl;
+          used = nk;
+          if (nk == 0u) state = kQuadExact;  // (never: the best lower bound's row is listed)
         }
-        used = first + nk;
-        if (nk == 0u && lane == 0) bk[kb].state = kQuadExact;  // (never: the best lower bound's row is listed)
+        wave_lds_sync();
       }
-      wave_lds_sync();
     }
-
-    // (3) exact values of the listed rows, lane-parallel over (row, dim)
-#ifdef CWQ_PROBE_NOEXACT  // timing probe only (wrong indices): listed rows not scored
-    used = 0;
+#ifdef CWQ_QUAD_TIMES
+    if (lane == 0u && g < kQuadTimes) {
+      g_quad_t[g][1] = __builtin_amdgcn_s_memrealtime();
+      g_quad_info[g][0] = (uint32_t)__builtin_amdgcn_s_getreg((4) | (0 << 6) | ((32 - 1) << 11));
+      g_quad_info[g][1] = (uint32_t)__builtin_amdgcn_s_getreg((20) | (0 << 6) | ((4 - 1) << 11));
+      g_quad_info[g][2] = used;
+      g_quad_info[g][3] = (state == kQuadExact ? 1u : 0u) | ((uint32_t)db << 8);
+    }
 #endif
-    if (used > 0) {
-      // prefix of the rows' dims: pre[e] = first item of row e
-      const bool have = lane < used;
-      const uint32_t de = have ? bk[lk[lane]].d : 0u;
-      uint32_t inc = de;
-#pragma unroll
-      for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t t = (uint32_t)__shfl_up((int)inc, (unsigned)o, 64);
-        if (lane >= (uint32_t)o) inc += t;
-      }
-      if (have) pre[lane + 1] = inc;
-      if (lane == 0) pre[0] = 0u;
-      wave_lds_sync();
-      for (uint32_t e0 = 0; e0 < used;) {
-        // rows [e0, e1) whose items fit one batch (a row's d <= the batch)
-        uint32_t e1 = e0 + 1;
-        while (e1 < used && pre[e1 + 1] - pre[e0] <= (uint32_t)CWQ_FUSED_STAGE) ++e1;
-        const uint32_t i0 = pre[e0], i1 = pre[e1];
-        for (uint32_t it = i0 + lane; it < i1; it += 64) {
-          uint32_t e = e0;
-          while (pre[e + 1] <= it) ++e;
-          const QuadBlk r = bk[lk[e]];
-          const uint32_t j = it - pre[e];
-          const int64_t ei = r.off + j;
-          const PhiloxStream se{r.k0, r.k1, r.c2, r.c3};
-          const float zz = exact_normal(se, (uint64_t)ln[e] * (uint64_t)r.d + j, logtab);
+    if (state == kQuadListed && used > 0) {
+      // exact values of the listed rows, lane-parallel over (row, dim): rows of d items
+      const uint32_t du = (uint32_t)db;
+      const uint32_t per = (uint32_t)CWQ_FUSED_STAGE / du;  // rows per batch (>= 1: d <= 64)
+      for (uint32_t e0 = 0; e0 < used; e0 += per) {
+        const uint32_t e1 = e0 + per < used ? e0 + per : used;
+        const uint32_t i1 = (e1 - e0) * du;
+        for (uint32_t it = lane; it < i1; it += 64) {
+          const uint32_t e = e0 + it / du;
+          const uint32_t j = it - (e - e0) * du;
+          const int64_t ei = off + j;
+          const float zz = exact_normal(sb, (uint64_t)ln[e] * (uint64_t)du + j, logtab);
           float sv = scale_s[ei] * zz;  // misc.py:14
           sv = loc_s[ei] + sv;          // misc.py:15
           const float tv = STEP0 ? sv : best[ei] + sv;  // :57
-          lpv[it - i0] = log_prob(tv, t_loc[ei], t_scale[ei], lognorm[ei]);
+          lpv[it] = log_prob(tv, t_loc[ei], t_scale[ei], lognorm[ei]);
         }
         wave_lds_sync();
         const uint32_t e = e0 + lane;
         if (e < e1) {  // a lane per row: the Eigen-order sum (eval_row_f)
-          const float* x = lpv + (pre[e] - i0);
-          const int dr = (int)(pre[e + 1] - pre[e]);
+          const float* x = lpv + (e - e0) * du;
+          const int dr = db;
           const int vec = dr & ~7;
           float p[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
           for (int jj = 0; jj < vec; jj += 8) {
 #pragma unroll
             for (int l = 0; l < 8; ++l) p[l] = p[l] + x[jj + l];
           }
-          float t = 0.0f;
-          for (int jj = vec; jj < dr; ++jj) t = t + x[jj];
-          const float q0 = p[0] + p[4], q1 = p[1] + p[5], q2 = p[2] + p[6], q3 = p[3] + p[7];
-          atomicMax(&kmax[lk[e]], (unsigned long long)argmax_key(t + ((q0 + q2) + (q1 + q3)),
-                                                                 ln[e]));
+          float s = 0.0f;
+          for (int jj = vec; jj < dr; ++jj) s = s + x[jj];
+          const float r0 = p[0] + p[4], r1 = p[1] + p[5], r2 = p[2] + p[6], r3 = p[3] + p[7];
+          atomicMax(&kmax, (unsigned long long)argmax_key(s + ((r0 + r2) + (r1 + r3)), ln[e]));
         }
         wave_lds_sync();
-        e0 = e1;
       }
     }
-
-    // blocks scored exactly: every candidate (constants outside the gate, list full)
-    for (int kb = 0; kb < nq; ++kb) {
-      if (bk[kb].state != kQuadExact) continue;
-      const unsigned long long bestk =
-          quad_exact_block<STEP0>(bk[kb], t_loc, t_scale, loc_s, scale_s, lognorm, best, n_cand,
-                                  logtab);
-      if (lane == 0) kmax[kb] = bestk;
+    if (state == kQuadExact) {  // every candidate exactly (constants outside the gate, list full)
+      QuadBlk r;
+      r.off = off;
+      r.d = (uint32_t)db;
+      r.k0 = sb.k0;
+      r.k1 = sb.k1;
+      r.c2 = sb.c2;
+      r.c3 = sb.c3;
+      const unsigned long long bk = quad_exact_block<STEP0>(r, t_loc, t_scale, loc_s, scale_s,
+                                                             lognorm, best, n_cand, logtab);
+      if (lane == 0) kmax = bk;
       wave_lds_sync();
     }
-
-    // (4) index and best += the winning row (k_encode_finalize), a row per block;
-    // the row's values come back from its LDS record (nothing per-lane is kept
-    // across the screen: live values there were spilled to scratch)
-    {
-      uint32_t lane4 = lane0;
-      asm volatile("" : "+v"(lane4));
-      const uint32_t k4 = lane4 >> 4, slot4 = lane4 & 15u;
-      if ((int)k4 < nq) {
-        const QuadBlk r = bk[k4];
-        const int d4 = (int)r.d;
-        const int64_t off4 = r.off;
-        uint32_t idx = r.idx;
-        if (r.state != kQuadKnown) {  // ArgMaxTupleReducer: a key at the clamp level is index 0
-          const unsigned long long kb = kmax[k4];
-          idx = (kb >> 32) > kArgmaxClampOrd ? argmax_key_index(kb) : 0u;
-        }
-        if (slot4 == 0u) out_idx[(g0 + (int64_t)k4) * n_steps + step] = (int32_t)idx;
-        const PhiloxStream st{r.k0, r.k1, r.c2, r.c3};
-        for (int j = (int)slot4; j < d4; j += 16) {
-#ifdef CWQ_PROBE_NOFIN  // timing probe only (wrong samples): finalize without the exact normal
-          const float zz = (float)(idx + j);
-#else
-          const float zz = exact_normal(st, (uint64_t)idx * (uint64_t)d4 + (uint32_t)j, logtab);
-#endif
-          float sv = scale_s[off4 + j] * zz;
-          sv = loc_s[off4 + j] + sv;
-          best[off4 + j] = (STEP0 ? 0.0f : best[off4 + j]) + sv;
-        }
-      }
+    if (state != kQuadKnown) {  // ArgMaxTupleReducer: a key at the clamp level is index 0
+      const unsigned long long kb = kmax;
+      idx = (kb >> 32) > kArgmaxClampOrd ? argmax_key_index(kb) : 0u;
     }
-    wave_lds_sync();  // the next quad reuses the wave's LDS
+    if (lane == 0) out_idx[g * n_steps + step] = (int32_t)idx;
+#ifdef CWQ_QUAD_TIMES
+    if (lane == 0u && g < kQuadTimes)
+      g_quad_t[g][2] = g_quad_t[g][3] = g_quad_t[g][4] = g_quad_t[g][5] =
+          __builtin_amdgcn_s_memrealtime();
+#endif
+  }
+}
+
+// A thread per dim of [d0, d0 + n): best += the winning row of its block (:63)
+template <bool STEP0>
+__global__ void __launch_bounds__(256) k_small_finalize(
+    const float* __restrict__ loc_s, const float* __restrict__ scale_s,
+    const SmallRec* __restrict__ rec, const uint32_t* __restrict__ dmap,
+    const int32_t* __restrict__ out_idx, int32_t step, int n_steps,
+    const int64_t* __restrict__ block_off, int64_t ud, int64_t nb, float* __restrict__ best) {
+  __shared__ double logtab[32];
+  fill_logtab(logtab);
+  int64_t d0, d1;
+  dims_of(block_off, ud, nb, d0, d1);
+  for (int64_t i = d0 + blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < d1;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const uint32_t g = dmap[i];
+    const uint4 q0 = rec[g].q0, q1 = rec[g].q1;
+    const int64_t off = (int64_t)(((uint64_t)q0.y << 32) | q0.x);
+    const uint32_t d = q0.z, j = (uint32_t)(i - off);
+    const PhiloxStream st{q1.x, q1.y, q1.z, q1.w};
+    const uint32_t idx = (uint32_t)out_idx[(int64_t)g * n_steps + step];  // k_small_one's
+    const float zz = exact_normal(st, (uint64_t)idx * (uint64_t)d + j, logtab);
+    float sv = scale_s[i] * zz;  // misc.py:14
+    sv = loc_s[i] + sv;          // misc.py:15
+    best[i] = (STEP0 ? 0.0f : best[i]) + sv;
   }
 }
 
@@ -3194,16 +3201,63 @@ static void launch_prune_csr(const EncodeArgs& a, int step, hipStream_t stream) 
 }
 
 #ifndef CWQ_SMALL_FUSED
-#define CWQ_SMALL_FUSED 1  // 0: the three-kernel path for every block length
+#define CWQ_SMALL_FUSED 1  // 0: the three-kernel path for every block length (d <= 64 too)
 #endif
-// true: the launch also wrote the step's indices and sample (k_small_fused)
+// true: the launches also wrote the step's indices and sample (the small pipeline)
+#ifndef CWQ_SMALL_PIPE
+#define CWQ_SMALL_PIPE 1  // 0: the three-kernel path for these shapes too
+#endif
+// launch_eval_dc's choices, shared with launch_encode (which leaves step 0's
+// prep to k_small_prep1 when the small pipeline runs)
+static bool takes_uniform_pruned(const EncodeArgs& a) {
+  // pruned path: uniform D % 8 == 0, D <= 64, Philox block index n*D/4 < 2^32
+  return a.block_off == nullptr && a.prune && a.ud % 8 == 0 && a.ud >= 8 && a.ud <= 64 &&
+         a.n_cand * (a.ud / 4) <= (1LL << 32);
+}
+static bool takes_small_path(const EncodeArgs& a) {  // launch_small's d <= 64 shapes
+  return !takes_uniform_pruned(a) && !(a.prune >= 2 && a.sab != nullptr && a.n_cand >= 4096) &&
+         a.prune >= 2 && a.sab != nullptr && a.slist != nullptr && a.ordu != nullptr &&
+         a.n_cand >= CWQ_SMALL_MIN_CAND && CWQ_SMALL_FUSED && a.max_d >= 0 &&
+         a.max_d <= CWQ_FUSED_DMAX && a.n_cand < 4096;
+}
+static bool small_pipe_ok(const EncodeArgs& a) {  // ... and the pipeline's arrays are there
+  return a.sdmap && a.sab && a.slist && a.nb < (1LL << 32);
+}
+static bool takes_small_pipe(const EncodeArgs& a) {
+  return CWQ_SMALL_PIPE && takes_small_path(a) && small_pipe_ok(a);
+}
+
 template <bool STEP0>
 static bool launch_small(const EncodeArgs& a, int step, hipStream_t stream) {
-  if (CWQ_SMALL_FUSED && a.max_d >= 0 && a.max_d <= CWQ_FUSED_DMAX && a.n_cand < 4096) {
-    hipLaunchKernelGGL((k_small_fused<STEP0>), dim3(grid_for(a.nb, 16, 1u << 20)), dim3(256), 0,
-                       stream, a.t_loc, a.t_scale, a.loc_s, a.scale_s, a.lognorm, a.out_sample,
-                       a.block_off, a.ud, a.nb, a.n_cand, seeds_of(a), step, a.n_steps,
-                       a.out_idx);
+  if (CWQ_SMALL_PIPE && CWQ_SMALL_FUSED && a.max_d >= 0 && a.max_d <= CWQ_FUSED_DMAX &&
+      a.n_cand < 4096 && small_pipe_ok(a)) {
+    // the small pipeline (k_small_*): constants, persistent screen, finalize
+    SmallRec* rec = (SmallRec*)a.slist;
+    float2* pab = const_cast<float2*>(a.pre_ab);  // by absolute dim (launch_encode)
+    const float nst = (float)a.n_steps;
+    const float sdiv = (float)__builtin_sqrt((double)a.n_steps);
+    const unsigned pgrid = grid_for(a.nb, kSmallPrepBlocks, 1u << 31);
+    if (STEP0)
+      hipLaunchKernelGGL(k_small_prep1<true>, dim3(pgrid), dim3(256), 0, stream, a.t_loc,
+                         a.t_scale, a.p_loc, a.p_scale, nst, sdiv, a.rho, a.loc_s, a.scale_s,
+                         a.lognorm, a.out_sample, a.block_off, a.ud, a.nb, seeds_of(a), step,
+                         pab, rec, a.sdmap);
+    else
+      hipLaunchKernelGGL(k_small_prep1<false>, dim3(pgrid), dim3(256), 0, stream, a.t_loc,
+                         a.t_scale, a.p_loc, a.p_scale, nst, sdiv, a.rho, a.loc_s, a.scale_s,
+                         a.lognorm, a.out_sample, a.block_off, a.ud, a.nb, seeds_of(a), step,
+                         pab, rec, a.sdmap);
+    const int64_t nu = a.nb;
+    for (int64_t u0 = 0; u0 < nu; u0 += (int64_t)1 << 30)
+      hipLaunchKernelGGL((k_small_one<STEP0>),
+                         dim3((unsigned)(nu - u0 < (1LL << 30) ? nu - u0 : (1LL << 30))),
+                         dim3(64), 0, stream, a.t_loc, a.t_scale, a.loc_s, a.scale_s, a.lognorm,
+                         a.out_sample, rec, a.pre_ab, a.nb, u0, a.n_cand, step, a.n_steps,
+                         a.out_idx);
+    const unsigned dgrid = grid_for(a.total_dims > a.nb ? a.total_dims : a.nb, 256, 16384);
+    hipLaunchKernelGGL((k_small_finalize<STEP0>), dim3(dgrid), dim3(256), 0, stream, a.loc_s,
+                       a.scale_s, rec, a.sdmap, a.out_idx, step, a.n_steps, a.block_off, a.ud,
+                       a.nb, a.out_sample);
     return true;
   }
   const int64_t ntiles = a.nb * a.tiles_per_block;
@@ -3227,9 +3281,7 @@ static bool launch_small(const EncodeArgs& a, int step, hipStream_t stream) {
 // sample written), false when k_encode_finalize must follow.
 template <bool STEP0>
 static bool launch_eval_dc(const EncodeArgs& a, int step, hipStream_t stream) {
-  // pruned path: uniform D % 8 == 0, D <= 64, Philox block index n*D/4 < 2^32
-  if (a.block_off == nullptr && a.prune && a.ud % 8 == 0 && a.ud >= 8 && a.ud <= 64 &&
-      a.n_cand * (a.ud / 4) <= (1LL << 32)) {
+  if (takes_uniform_pruned(a)) {
     switch (a.ud) {
       case 8: return launch_prune_t<8, STEP0>(a, step, stream), false;
       case 16: return launch_prune_t<16, STEP0>(a, step, stream), false;
@@ -3376,10 +3428,17 @@ hipStream_t copy_stream(hipStream_t stream, int which) {
   return f && which >= 0 && which < 2 ? f->cp[which] : nullptr;
 }
 
-hipError_t launch_encode(const EncodeArgs& a, hipStream_t stream) {
+hipError_t launch_encode(const EncodeArgs& a_in, hipStream_t stream) {
   hipError_t e;
-  e = launch_prep_dims(a.t_scale, a.p_loc, a.p_scale, a.total_dims, a.n_steps, a.rho, a.loc_s,
-                       a.scale_s, a.lognorm, a.out_sample, a.keys, a.nb, stream);
+  EncodeArgs a = a_in;
+  // the small pipeline's per-dim screening constants, by absolute dim offset: a
+  // view of sab (the other paths' scratch) taken before a fork shifts it per part
+  a.pre_ab = a.sab;
+  if (takes_small_pipe(a))
+    e = hipSuccess;  // its step 0 does k_prep_dims' work in k_small_prep1
+  else
+    e = launch_prep_dims(a.t_scale, a.p_loc, a.p_scale, a.total_dims, a.n_steps, a.rho, a.loc_s,
+                         a.scale_s, a.lognorm, a.out_sample, a.keys, a.nb, stream);
   if (e != hipSuccess) return e;
   if (a.nb == 0) return hipSuccess;
   ForkStreams* f = (CWQ_ENCODE_SPLIT > 1 && a.block_off != nullptr && a.n_steps > 1 &&
@@ -3419,6 +3478,7 @@ hipError_t launch_encode(const EncodeArgs& a, hipStream_t stream) {
     if (a.gtau) p.gtau = a.gtau + g0 * CWQ_CSR_GTAU_STRIDE;
     // abp is indexed by absolute dim offset alone (csr_rec_base): unshifted
     if (a.slist) p.slist = a.slist + CWQ_SLIST_PER_BLOCK * g0;
+    // sdmap is indexed by absolute dim offset (its values: the part's block numbers)
     if ((e = hipStreamWaitEvent(f->s[i], f->fork, 0)) != hipSuccess) break;
     forked = i + 1;
     e = encode_steps(p, f->s[i], false);
@@ -3540,6 +3600,19 @@ int tile_times(unsigned long long* t0, unsigned long long* t1, unsigned int* wg,
   return n;
 #else
   (void)t0; (void)t1; (void)wg; (void)n;
+  return 0;
+#endif
+}
+
+int quad_times(unsigned long long* t, unsigned int* info, int n) {
+#ifdef CWQ_QUAD_TIMES
+  if (n > kQuadTimes) n = kQuadTimes;
+  if (hipMemcpyFromSymbol(t, HIP_SYMBOL(g_quad_t), (size_t)n * 6 * 8) != hipSuccess ||
+      hipMemcpyFromSymbol(info, HIP_SYMBOL(g_quad_info), (size_t)n * 4 * 4) != hipSuccess)
+    return -1;
+  return n;
+#else
+  (void)t; (void)info; (void)n;
   return 0;
 #endif
 }

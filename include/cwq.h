@@ -126,7 +126,7 @@ typedef struct cwq_options {
 /* Workspace bytes needed by cwq_greedy_encode (CSR blocks) for nb blocks
  * holding total_dims dims in all, none longer than max_block_dim: the argmax
  * keys and per-dim shard constants plus the general pruned kernel's per-step
- * screening constants (20 B/dim + 244 B/block) and, when max_block_dim > 1024,
+ * screening constants (24 B/dim + 244 B/block) and, when max_block_dim > 1024,
  * their visit-order copies for the long blocks (32 B/dim + 384 B per 1025
  * dims).  A
  * CSR call given less returns CWQ_ERR_WORKSPACE (it never silently falls back

@@ -490,7 +490,18 @@ CWQO_API int cwqo_greedy_encode_lsig(const float* t_loc, const float* t_scale,
 /* ------------------------------------------------------------------------ */
 #define SEM_NFORM 2 /* 0: TFP<=0.7 (declared), 1: TFP>=0.8 squared_difference */
 #define SEM_NSUM 6  /* row-sum orders, see sem_rowsum */
-#define SEM_NV (SEM_NFORM * SEM_NSUM)
+/* RNG transcendentals (round 5): the declared form and order on
+ * normals a TF build with another logf / sincosf (a non-glibc libm, TF-GPU's
+ * device functions, Eigen numext) or another 2pi evaluation could have drawn:
+ *   0 ulp_hash  every Box-Muller output one ulp away from glibc's, up or down
+ *               by a hash of (stream, flat index): the proxy for a libm whose
+ *               results differ in the last place at random;
+ *   1 ulp_up    every output one ulp toward +inf;
+ *   2 ulp_down  every output one ulp toward -inf;
+ *   3 v1_f32    the angle in float, (2.0f * (float)M_PI) * U(x1), instead of
+ *               TF's double 2.0f * M_PI (a build whose constant is a float). */
+#define SEM_NRNG 4
+#define SEM_NV (SEM_NFORM * SEM_NSUM + SEM_NRNG)
 
 /* TFP >= 0.8 Normal._log_prob:
  *   -0.5 * squared_difference(x / scale, loc / scale) - (0.5 log 2pi + log scale)
@@ -557,6 +568,60 @@ static float sem_rowsum(const float* x, int64_t d, int order) {
 }
 
 CWQO_API int cwqo_sem_num_variants(void) { return SEM_NV; }
+
+static inline uint64_t mix64(uint64_t x) {  /* splitmix64 finaliser */
+  x ^= x >> 30;
+  x *= 0xbf58476d1ce4e5b9ull;
+  x ^= x >> 27;
+  x *= 0x94d049bb133111ebull;
+  return x ^ (x >> 31);
+}
+
+/* The normals of Philox group `grp` twice: z as declared (A.4) and zf with
+ * the float angle (RNG variant v1_f32). */
+static void normal_group_f32angle(const uint32_t key[2], const uint32_t ctr[4], uint64_t grp,
+                                  float z[4], float zf[4]) {
+  uint32_t c[4], x[4];
+  philox_skip(ctr, grp, c);
+  cwqo_philox4x32_10(c, key, x);
+  for (int h = 0; h < 2; ++h) {
+    const float u2 = cwqo_bm_radius(x[2 * h]);
+    float sn, cs;
+    cwqo_bm_sincos(x[2 * h + 1], &sn, &cs);
+    z[2 * h] = sn * u2;
+    z[2 * h + 1] = cs * u2;
+    const float v1f = (2.0f * (float)M_PI) * uint32_to_float(x[2 * h + 1]);
+    sincosf(v1f, &sn, &cs);
+    zf[2 * h] = sn * u2;
+    zf[2 * h + 1] = cs * u2;
+  }
+}
+
+typedef struct {
+  uint32_t key[2], ctr[4];
+  uint64_t cur_grp, sid;
+  int have;
+  float z[4], zf[4];
+} rng_stream;
+
+/* normal k of the stream under the declared generator (v < 0) or RNG
+ * variant v */
+static inline float rng_normal(rng_stream* st, uint64_t k, int v) {
+  const uint64_t g = k >> 2;
+  if (!st->have || st->cur_grp != g) {
+    normal_group_f32angle(st->key, st->ctr, g, st->z, st->zf);
+    st->cur_grp = g;
+    st->have = 1;
+  }
+  const float z = st->z[k & 3] * 1.0f + 0.0f;
+  switch (v) {
+    case 0: return nextafterf(z, (mix64(st->sid ^ mix64(k)) & 1u) ? INFINITY : -INFINITY);
+    case 1: return nextafterf(z, INFINITY);
+    case 2: return nextafterf(z, -INFINITY);
+    case 3: return st->zf[k & 3] * 1.0f + 0.0f;
+    default: return z;
+  }
+}
 CWQO_API float cwqo_sem_rowsum(const float* x, int64_t d, int order) {
   return sem_rowsum(x, d, order);
 }
@@ -591,21 +656,24 @@ CWQO_API int cwqo_greedy_encode_semvar(const float* t_loc, const float* t_scale,
     float* loc_s = (float*)malloc(db);
     float* scale_s = (float*)malloc(db);
     float* lognorm = (float*)malloc(db);
-    float* row = (float*)malloc(2 * db);
+    float* row = (float*)malloc((2 + SEM_NRNG) * db);
     if (!loc_s || !scale_s || !lognorm || !row) {
       free(loc_s); free(scale_s); free(lognorm); free(row);
       err |= 1;
       continue;
     }
     float* row8 = row + (d > 0 ? d : 1);
+    float* rowr = row8 + (d > 0 ? d : 1);  /* [SEM_NRNG][d]: the RNG variants' rows */
     shard_params(p_loc + o, p_scale + o, d, n_steps, rho, loc_s, scale_s);
     for (int64_t j = 0; j < d; ++j) lognorm[j] = cwqo_log_normalization(ts[j]);
     for (int64_t j = 0; j < d; ++j) best[j] = 0.0f;
     const int64_t n_samples = (int64_t)1 << n_bits_per_step;
     for (int i = 0; i < n_steps; ++i) {
-      normal_stream st;
+      rng_stream st;
       memset(&st, 0, sizeof(st));
       cwqo_generate_key(step_seed(sg, i), 42, st.key, st.ctr);
+      st.sid = mix64(((uint64_t)st.key[0] << 32 | st.key[1]) ^
+                     mix64((uint64_t)st.ctr[2] << 32 | st.ctr[3]));
       float bv[SEM_NV], bdev[SEM_NV];
       int64_t bi[SEM_NV];
       for (int v = 0; v < SEM_NV; ++v) { bv[v] = -FLT_MAX; bi[v] = 0; }
@@ -613,25 +681,33 @@ CWQO_API int cwqo_greedy_encode_semvar(const float* t_loc, const float* t_scale,
       for (int v = 0; v < SEM_NV; ++v) bdev[v] = 0.0f;
       for (int64_t n = 0; n < n_samples; ++n) {
         for (int64_t j = 0; j < d; ++j) {
-          float z = stream_normal(&st, (uint64_t)(n * d + j));
+          const uint64_t k = (uint64_t)(n * d + j);
+          float z = rng_normal(&st, k, -1);
           float s = scale_s[j] * z;
           s = loc_s[j] + s;
           float tv = best[j] + s;
           row[j] = log_prob_c(tv, tl[j], ts[j], lognorm[j]);
           row8[j] = log_prob_tfp08(tv, tl[j], ts[j], lognorm[j]);
+          for (int r = 0; r < SEM_NRNG; ++r) {
+            float sr = scale_s[j] * rng_normal(&st, k, r);
+            sr = loc_s[j] + sr;
+            rowr[r * d + j] = log_prob_c(best[j] + sr, tl[j], ts[j], lognorm[j]);
+          }
         }
         float vals[SEM_NV];
-        for (int f = 0; f < SEM_NFORM; ++f)
-          for (int ord = 0; ord < SEM_NSUM; ++ord) {
-            const int v = f * SEM_NSUM + ord;
-            const float val = sem_rowsum(f ? row8 : row, d, ord);
-            vals[v] = val;
-            if (v == 0) {
-              if (val > bv[0]) second = bv[0];
-              else if (val > second) second = val;
-            }
-            if (val > bv[v]) { bv[v] = val; bi[v] = n; }
+        for (int v = 0; v < SEM_NV; ++v) {
+          const int f = v < SEM_NFORM * SEM_NSUM ? v / SEM_NSUM : 0;
+          const int ord = v < SEM_NFORM * SEM_NSUM ? v % SEM_NSUM : 0;
+          const float* rv = v < SEM_NFORM * SEM_NSUM ? (f ? row8 : row)
+                                                     : rowr + (v - SEM_NFORM * SEM_NSUM) * d;
+          const float val = sem_rowsum(rv, d, ord);
+          vals[v] = val;
+          if (v == 0) {
+            if (val > bv[0]) second = bv[0];
+            else if (val > second) second = val;
           }
+          if (val > bv[v]) { bv[v] = val; bi[v] = n; }
+        }
         if (bi[0] == n) /* the declared best row so far: each variant's deviation on it */
           for (int v = 0; v < SEM_NV; ++v) bdev[v] = vals[v] - vals[0];
       }
@@ -641,7 +717,7 @@ CWQO_API int cwqo_greedy_encode_semvar(const float* t_loc, const float* t_scale,
         if (out_dev) out_dev[(g * n_steps + i) * SEM_NV + v] = bdev[v];
       }
       for (int64_t j = 0; j < d; ++j) {
-        float z = stream_normal(&st, (uint64_t)(bi[0] * d + j));
+        float z = rng_normal(&st, (uint64_t)(bi[0] * d + j), -1);
         float s = scale_s[j] * z;
         s = loc_s[j] + s;
         best[j] = best[j] + s;

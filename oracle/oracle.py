@@ -216,12 +216,15 @@ def greedy_encode_lsig(t_loc, t_scale, p_loc, p_scale, block_off, n_bits_per_ste
 
 SEM_FORMS = ("tfp07", "tfp08")
 SEM_ORDERS = ("avx8", "sse4", "avx8x2", "avx512", "seq", "tree")
+SEM_RNG = ("ulp_hash", "ulp_up", "ulp_down", "v1_f32")
 
 
 def sem_variant_names():
     """Names of the per-candidate semantics variants, in the oracle's order
-    v = form * len(SEM_ORDERS) + order; v = 0 ('tfp07/avx8') is declared."""
-    return [f + "/" + o for f in SEM_FORMS for o in SEM_ORDERS]
+    v = form * len(SEM_ORDERS) + order, then the RNG-transcendental variants
+    (declared form and order on other normals, cwq_oracle.c SEM_NRNG);
+    v = 0 ('tfp07/avx8') is declared."""
+    return [f + "/" + o for f in SEM_FORMS for o in SEM_ORDERS] + ["rng/" + r for r in SEM_RNG]
 
 
 def sem_rowsum(x, order):

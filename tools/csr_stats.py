@@ -1,6 +1,6 @@
 """Counters of the general pruned kernel (k_encode_prune_csr) on the grouped
 coder (run on the GPU box with a -DCWQ_PRUNE_STATS build through CWQ_LIB_PATH).
-Usage: CWQ_LIB_PATH=tools/variants/libcwq_stats.so python tools/csr_stats.py [config]"""
+Usage: CWQ_LIB_PATH=tools/vrun/libcwq_stats.so python tools/csr_stats.py [config]"""
 import ctypes, os, sys, time
 import numpy as np
 import torch

@@ -50,9 +50,9 @@ run_one() {
         lds)  prof prof_${tag}_lds --pmc SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_SMEM SQ_WAVES ;;
         *) echo "unknown PMC set $set"; return 2 ;;
       esac && echo pmc $tag $set ok ;;
-    vpmc)  # vpmc TAG VARIANT SET [bench args]: pmc on a tools/variants build
+    vpmc)  # vpmc TAG VARIANT SET [bench args]: pmc on a tools/vrun build
       local tag=$1 v=$2; shift 2
-      ( export CWQ_LIB_PATH=$PWD/tools/variants/libcwq_$v.so; run_one pmc $tag "$@" ) ;;
+      ( export CWQ_LIB_PATH=$PWD/tools/vrun/libcwq_$v.so; run_one pmc $tag "$@" ) ;;
     stress)
       local n=${1:-400}
       timeout -k 10 300 python -u tools/stress_csr.py $n ${STRESS_SEED:-20000} 200 \
@@ -67,17 +67,17 @@ run_one() {
         > gpurun_out/v_$tag.log 2>&1 && cat gpurun_out/v_$tag.log ;;
     stats)
       local tag=$1 v=$2 nb=$3 d=$4 bits=$5
-      CWQ_LIB_PATH=$PWD/tools/variants/libcwq_$v.so PS_D=$d PS_BITS=$bits timeout -k 10 300 \
+      CWQ_LIB_PATH=$PWD/tools/vrun/libcwq_$v.so PS_D=$d PS_BITS=$bits timeout -k 10 300 \
         python -u tools/prune_stats.py $nb > gpurun_out/s_$tag.log 2>&1 && head -3 gpurun_out/s_$tag.log ;;
     c2parts)
       timeout -k 10 300 python -u tools/c2_parts.py > gpurun_out/c2parts.log 2>&1 && cat gpurun_out/c2parts.log && \
-      CWQ_LIB_PATH=$PWD/tools/variants/libcwq_phases.so timeout -k 10 300 python -u bench.py --config c2 \
+      CWQ_LIB_PATH=$PWD/tools/vrun/libcwq_phases.so timeout -k 10 300 python -u bench.py --config c2 \
         --no-cpu --no-e2e --steps 5 > gpurun_out/c2phases.log 2>&1 && grep cwq gpurun_out/c2phases.log | tail -8 && \
-      CWQ_LIB_PATH=$PWD/tools/variants/libcwq_phases.so timeout -k 10 300 python -u bench.py --config c3 \
+      CWQ_LIB_PATH=$PWD/tools/vrun/libcwq_phases.so timeout -k 10 300 python -u bench.py --config c3 \
         --batch-only --no-cpu --no-e2e --steps 3 > gpurun_out/c3phases.log 2>&1 && grep "cwq batch" gpurun_out/c3phases.log | tail -4 ;;
     decvar)  # decode timing per variant, after its decode tests against the oracle
       for v in $1; do
-        CWQ_LIB_PATH=$PWD/tools/variants/libcwq_$v.so timeout -k 10 300 python -u -m pytest \
+        CWQ_LIB_PATH=$PWD/tools/vrun/libcwq_$v.so timeout -k 10 300 python -u -m pytest \
           tests/test_gpu.py -q -x -k decode --timeout 120 --timeout-method thread \
           > gpurun_out/decvar_$v.log 2>&1 && tail -1 gpurun_out/decvar_$v.log || return 1
       done
@@ -85,7 +85,7 @@ run_one() {
         cat gpurun_out/decvar.log ;;
     tiles)
       local tag=$1 nb=$2 d=$3 bits=$4 v=${5:-tt}
-      CWQ_LIB_PATH=$PWD/tools/variants/libcwq_$v.so timeout -k 10 300 \
+      CWQ_LIB_PATH=$PWD/tools/vrun/libcwq_$v.so timeout -k 10 300 \
         python -u tools/tile_times.py $nb $d $bits > gpurun_out/tt_$tag.log 2>&1 && head -6 gpurun_out/tt_$tag.log ;;
     py)  # py TAG SCRIPT [args]: a tools/ script -> gpurun_out/py_TAG.log
       local tag=$1; shift

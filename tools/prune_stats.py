@@ -1,6 +1,6 @@
 """Units-per-candidate histogram of the pruned encoder (run on the GPU box
 with a -DCWQ_PRUNE_STATS build selected through CWQ_LIB_PATH).
-Usage: CWQ_LIB_PATH=tools/variants/libcwq_stats.so python tools/prune_stats.py [nb] [mode]
+Usage: CWQ_LIB_PATH=tools/vrun/libcwq_stats.so python tools/prune_stats.py [nb] [mode]
 (PS_D / PS_BITS select the block shape; default the C4 shape d=32, 16 bits)"""
 import ctypes, os, sys
 import numpy as np

@@ -18,6 +18,17 @@ move an argmax.  The oracle scores every candidate under all
           seq                a scalar build: left to right
           tree               pairwise halving (a GPU tree reduction, representative)
 
+and, for the RNG's transcendentals, 4 generator variants on the
+declared form and order:
+
+  rng     ulp_hash           every Box-Muller output one ulp off glibc's, up or
+                             down by a hash of (stream, index): a libm (TF-GPU,
+                             Eigen numext, another C library) whose logf /
+                             sincosf differ in the last place
+          ulp_up, ulp_down   every output one ulp toward +inf / -inf
+          v1_f32             the angle in float, (2.0f * (float)M_PI) * U, not
+                             TF's double 2.0f * M_PI
+
 and records, per variant, how many indices differ from the declared encoder's
 given the same history (multi-step groups follow the declared chain), with the
 declared best - second-best gap of every index and of every flipped one.
@@ -29,11 +40,11 @@ Workloads (bench.py's synthetic generators, the bench's own seeds):
   c5     the first --c5-blocks C5 blocks (d=16, 24 bits)
   c2cli  --cli-groups evenly spaced groups of the C2 image at the CLI's
          greedy defaults (30 steps x 14 bits, ~376 dims per group)
-  c2low  --low-groups evenly spaced groups of the low-rate C2 image (30 x 14
-         bits, groups up to 4095 dims)
+  c2low  the low-rate C2 image's groups (30 x 14 bits, groups up to 4095
+         dims): all of them by default (--low-groups N: N evenly spaced)
 
 Usage: python tools/semantics_sensitivity.py [--c4-blocks 10000] [--c5-blocks 32]
-           [--cli-groups 48] [--low-groups 4] [--threads N] [--only c4,c2]
+           [--cli-groups 48] [--low-groups 0] [--threads N] [--only c4,c2]
 """
 import argparse
 import json
@@ -154,7 +165,7 @@ def main():
     ap.add_argument("--c4-blocks", type=int, default=10000)
     ap.add_argument("--c5-blocks", type=int, default=32)
     ap.add_argument("--cli-groups", type=int, default=48)
-    ap.add_argument("--low-groups", type=int, default=4)
+    ap.add_argument("--low-groups", type=int, default=0, help="0: every group")
     ap.add_argument("--threads", type=int, default=0)
     ap.add_argument("--only", default="c4,c2,c5,c2cli,c2low")
     ap.add_argument("--out", default=os.path.join(REPO, "profiles", "semantics_sensitivity.json"))
@@ -168,8 +179,9 @@ def main():
     res["variants"] = O.sem_variant_names()[1:]
     res["declared"] = O.sem_variant_names()[0]
     res["source"] = ("[ext] TFP 0.8 Normal._log_prob and Eigen 3.3/3.4 reducer packet orders "
-                     "recalled from their public sources (oracle/cwq_oracle.c "
-                     "cwqo_greedy_encode_semvar); unpinned, like SURVEY.md A.5-A.6")
+                     "recalled from their public sources, and proxies for a non-glibc "
+                     "logf/sincosf and a float 2*pi (oracle/cwq_oracle.c "
+                     "cwqo_greedy_encode_semvar); unpinned, like SURVEY.md A.4-A.6")
     if "c4" in only:
         (tl, ts, pl, ps), off = uniform(a.c4_blocks, 32, 16)
         res["c4"] = run("c4", tl, ts, pl, ps, off, 16, 1, a.threads,
@@ -186,7 +198,7 @@ def main():
         res["c2cli"] = run("c2cli", tl, ts, pl, ps, off, 14, 30, a.threads,
                            "C2 image 0 at 30 x 14 bits: " + note)
     if "c2low" in only:
-        (tl, ts, pl, ps), off, note = grouped(0.06, 14, 30, a.low_groups)
+        (tl, ts, pl, ps), off, note = grouped(0.06, 14, 30, a.low_groups or None)
         res["c2low"] = run("c2low", tl, ts, pl, ps, off, 14, 30, a.threads,
                            "low-rate C2 image 0 at 30 x 14 bits: " + note)
     with open(a.out, "w") as f:

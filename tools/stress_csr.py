@@ -45,7 +45,8 @@ VERBOSE = bool(os.environ.get("STRESS_VERBOSE"))
 # bits per step drawn from [BITS_LO, BITS_HI]: 12-16 reach the general pruned
 # kernel (>= 4096 candidates); STRESS_BITS=6,11 the screened small-candidate path
 BITS_LO, BITS_HI = (int(v) for v in os.environ.get("STRESS_BITS", "12,16").split(","))
-# STRESS_SMALL=1: short groups only (d <= 128: k_small_fused with STRESS_BITS=6,11)
+# STRESS_SMALL=1: short groups only (d <= 128; all <= 64 in a third of the trials:
+# k_small_fused with STRESS_BITS=6,11)
 SMALL = bool(os.environ.get("STRESS_SMALL"))
 
 
@@ -88,7 +89,7 @@ def main():
             sizes = np.full(nb, int(rng.choice([256, 300, 1024, 1025, 2048, 3001])))
         if SMALL:  # the fused small-candidate kernel's blocks (d <= 128), many of them
             nb = int(rng.integers(1, 3000))
-            sizes = rng.integers(0, int(rng.choice([3, 8, 33, 129])), nb)
+            sizes = rng.integers(0, int(rng.choice([3, 8, 33, 65, 65, 129])), nb)  # 65: max 64 (fused)
         sizes = [int(x) for x in sizes]
         if sum(sizes) == 0:
             sizes[0] = 1

@@ -1,6 +1,6 @@
 """Per-tile timeline of one pruned-encoder launch (run on the GPU box with a
 -DCWQ_TILE_TIMES build selected through CWQ_LIB_PATH).
-Usage: CWQ_LIB_PATH=tools/variants/libcwq_tt.so python tools/tile_times.py NB D BITS
+Usage: CWQ_LIB_PATH=tools/vrun/libcwq_tt.so python tools/tile_times.py NB D BITS
 Prints the launch span, how many tiles run at once over time, the tile
 durations of the first resident round against the later ones, and the drain
 at the end of the launch (the time from the last tile start to the last end)."""

@@ -1,11 +1,11 @@
 #!/bin/bash
-# Build compile-time tuning variants of libcwq.so into tools/variants/ and
+# Build compile-time tuning variants of libcwq.so into tools/vrun/ (built here just before a GPU call, removed after it; never shipped otherwise) and
 # time each on a bench config (run on the GPU box).
 # Usage: tools/variants.sh build | [VARIANTS="base t512"] [BENCH_ARGS="--config c2cli"] tools/variants.sh run
 set -e
 cd "$(dirname "$0")/.."
 CSRC=compression_without_quantization_amd/csrc
-OUT=${VOUT:-tools/variants}
+OUT=${VOUT:-tools/vrun}
 FLAGS="--offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -fno-fast-math -fPIC -shared"
 declare -A V=(
   [base]=""
@@ -96,6 +96,9 @@ declare -A V=(
   [tauold]="-DCWQ_TAU_FROM_KEYS=0"
   [seed16]="-DCWQ_SEED_LOG2=16"
   [tt]="-DCWQ_TILE_TIMES"
+  [qt]="-DCWQ_QUAD_TIMES"
+  [pipe0]="-DCWQ_SMALL_PIPE=0"
+  [lpt0]="-DCWQ_SMALL_LPT=0"
   [tt0]="-DCWQ_TILE_TIMES -DCWQ_XCD_BALANCE=0"
   [xcd0]="-DCWQ_XCD_BALANCE=0"
   [tail1]="-DCWQ_TAIL_SPLIT=1"
@@ -125,6 +128,8 @@ else
     [ "$k" = stats ] && continue  # counters only: tools/prune_stats.py
     [ "$k" = phases ] && continue  # host phase timings only
     echo "== $k ${V[$k]}"
-    CWQ_LIB_PATH=$PWD/$OUT/libcwq_$k.so timeout -k 10 300 python -u bench.py --no-cpu --no-e2e --steps 2 --warmup 1 $BENCH_ARGS | tail -1 | python -c "import json,sys; d=json.loads(sys.stdin.read()); print(d['value'], d['ms_per_step'], d.get('roofline', {}).get('kernel_ms'))"
+    lp=$PWD/$OUT/libcwq_$k.so
+    [ "$k" = main ] && lp=$PWD/compression_without_quantization_amd/libcwq.so  # the in-tree build
+    CWQ_LIB_PATH=$lp timeout -k 10 300 python -u bench.py --no-cpu --no-e2e --steps 2 --warmup 1 $BENCH_ARGS | tail -1 | python -c "import json,sys; d=json.loads(sys.stdin.read()); print(d['value'], d['ms_per_step'], d.get('roofline', {}).get('kernel_ms'))"
   done
 fi
