@@ -221,37 +221,15 @@ def grouped_main(args):
     # SURVEY.md 8(d) per group: 16 d (four f32 inputs) + 4 n_steps (indices) + 4 d (sample)
     alg = 20 * D_step + 4 * groups * n_steps
     cand_dims = (1 << bits) * n_steps * D_step
-    achieved = alg / (kernel_ms * 1e-3) / 1e9
-    traffic = valu = None
-    tf = os.path.join(REPO, "profiles", f"traffic_{args.config}.json")
-    if os.path.exists(tf):
-        with open(tf) as f:
-            tj = json.load(f)
-        if tj.get("blocks") == groups:
-            traffic = tj.get("hbm_bytes_per_launch")
-            valu = tj.get("valu")
     small = 64 <= (1 << bits) < 4096
-    roofline = {"bound": "valu", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS,
-                "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                "hbm_note": "achieved/peak/frac/traffic price the scoring launches' algorithmic "
-                            "bytes (20 d + 4 n_steps per group) against HBM, as the north star "
-                            "asks; the launches are bound by VALU issue (Philox + Box-Muller "
-                            "per candidate), see `valu` and DESIGN.md 5c/5d",
-                "kernel": ("k_small_fused (constants, screen, exact survivors and finalize in "
-                           "one launch per step; DESIGN.md 5e)" if small else
-                           "k_csr_prep + k_encode_prune_csr (+ finalize between steps)"),
-                "kernel_ms": round(kernel_ms, 4),
-                "kernel_timing": "HIP events recorded on the launch stream around the "
-                                 "candidate-scoring launches: the caller's cwq_options events "
-                                 "for single calls, cwq_options.eval_ms_out (per pipelined "
-                                 "chunk) for the batched call; summed over the calls of a step",
-                "algorithmic_bytes_per_launch": alg,
-                "valu": {"unit": "candidate-dims/s",
-                         "nominal_candidate_dims_per_s": cand_dims / (kernel_ms * 1e-3),
-                         "valu_issue_frac": (valu or {}).get("valu_issue_frac"),
-                         "valu_issue_source": "profiles/traffic_%s.json (rocprofv3 --pmc "
-                                              "SQ_INSTS_VALU GRBM_GUI_ACTIVE, the scoring "
-                                              "kernels)" % args.config if valu else None}}
+    roofline = scoring_roofline(
+        args.config, groups, alg, kernel_ms, cand_dims,
+        ("k_small_prep1 + k_small_one + k_small_finalize (the small-candidate pipeline, "
+         "DESIGN.md 5e; k_small_one dominant)" if small else
+         "k_csr_prep + k_encode_prune_csr (+ finalize between steps)"),
+        "HIP events recorded on the launch stream around the candidate-scoring launches: the "
+        "caller's cwq_options events for single calls, cwq_options.eval_ms_out (per "
+        "pipelined chunk) for the batched call; summed over the calls of a step")
     cpu = parity = None
     if not args.no_cpu:
         cpu, parity = grouped_cpu_baseline(args, lat_np, res[:len(dims)], bits, n_steps)
@@ -356,30 +334,46 @@ def importance_main(args):
     """I1/I2: the grouped importance pipeline per image
     (code_grouped_importance_sample): standardise + KL on the GPU, host
     grouping and N_g plan, the tiled candidate kernel, Elias-delta bitcode and
-    quint16 outliers.  Synthetic PLN-like latents."""
+    quint16 outliers.  Synthetic PLN-like latents.  The roofline prices the
+    candidate-scoring launches (cwq_options.eval_ms_out: HIP events around
+    them, summed over the step's calls); cpu_baseline / parity run the oracle's
+    whole pipeline (oracle.code_grouped_importance_sample) on image 0."""
+    import ctypes
     import compression_without_quantization_amd.coded_importance_sampler as I
     from compression_without_quantization_amd.synthetic import make_latents
     I.VERBOSE = False
     n_img, D, nbits, gbits, kl_lim, desc = IMPORTANCE[args.config]
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
-    lat = []
+    lat, lat_np = [], []
     for i in range(n_img):
         q_loc, q_scale, p_loc, p_scale = make_latents(D, seed=5000 + i)
+        if i == 0:
+            lat_np.append((q_loc, q_scale, p_loc, p_scale))
         lat.append((C.Normal(torch.from_numpy(q_loc).to(dev), torch.from_numpy(q_scale).to(dev)),
                     C.Normal(torch.from_numpy(p_loc).to(dev), torch.from_numpy(p_scale).to(dev))))
+    evq = []
 
-    def step():
-        return [I.code_grouped_importance_sample(None, t, p, 42, nbits, max_group_size_bits=gbits,
-                                                 dim_kl_bit_limit=kl_lim) for t, p in lat]
+    def step(timed=False):
+        out = []
+        for t, p in lat:
+            v = ctypes.c_float(0.0) if timed else None
+            out.append(I.code_grouped_importance_sample(None, t, p, 42, nbits,
+                                                        max_group_size_bits=gbits,
+                                                        dim_kl_bit_limit=kl_lim, eval_ms_out=v))
+            if v is not None:
+                evq.append(v)
+        return out
     for _ in range(args.warmup):
         res = step()
     torch.cuda.synchronize()
+    evq.clear()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        res = step()
+        res = step(True)
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
+    kernel_ms = sum(v.value for v in evq) / max(args.steps, 1)
     # work: sum over groups of N_g * d_g candidate-dims (the plan the coder used)
     cand_dims = 0
     for (t, p), r in zip(lat, res):
@@ -387,6 +381,16 @@ def importance_main(args):
         cand_dims += _importance_work(t, p, starts, kl_lim, dev)
     groups = sum(len(r[2]) - 1 for r in res)
     bitlen = sum(len(r[1]) for r in res)
+    # per group: 16 d (four f32 inputs) + 8 (int64 index) + 4 d (sample)
+    alg = 20 * D * n_img + 8 * groups
+    roofline = scoring_roofline(args.config, groups, alg, kernel_ms, cand_dims,
+                                "k_imp_prep + k_imp_tiles + k_imp_eval + k_imp_rows "
+                                "(DESIGN.md 8)", "cwq_options.eval_ms_out of each "
+                                "code_grouped_importance_sample call (HIP events around its "
+                                "candidate-scoring launches), summed over the step's calls")
+    cpu = parity = None
+    if not args.no_cpu:
+        cpu, parity = importance_cpu_baseline(args, lat_np[0], res[0], nbits, gbits, kl_lim)
     line = {"metric": "images coded/s (grouped importance pipeline)",
             "value": n_img * args.steps / el, "unit": "images/s", "n_gpus": 1,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": el / args.steps * 1e3,
@@ -395,8 +399,128 @@ def importance_main(args):
             "config": {"workload": desc, "groups_per_step": groups, "bits_per_step": bitlen,
                        "groups_per_s": groups * args.steps / el,
                        "candidate_dims_per_step": cand_dims,
-                       "candidate_dims_per_s": cand_dims * args.steps / el}}
+                       "candidate_dims_per_s": cand_dims * args.steps / el},
+            "roofline": roofline, "cpu_baseline": cpu, "parity": parity}
     print(json.dumps(line), flush=True)
+
+
+def scoring_roofline(config, groups, alg, kernel_ms, cand_dims, kernel, timing):
+    """The roofline block of a grouped line: the scoring launches' algorithmic
+    bytes over their HIP-event time against HBM, and the VALU issue fraction
+    and HBM traffic of the PMC evidence in profiles/traffic_CONFIG.json
+    (tools/collect_profile.py; recomputable from the CSVs it lists) when it
+    was taken on this workload (same group count)."""
+    achieved = alg / (kernel_ms * 1e-3) / 1e9 if kernel_ms > 0 else None
+    traffic = valu = agg = src = None
+    tf = os.path.join(REPO, "profiles", f"traffic_{config}.json")
+    if os.path.exists(tf):
+        with open(tf) as f:
+            tj = json.load(f)
+        if tj.get("blocks") == groups:
+            agg = tj.get("scoring") or {}
+            traffic = agg.get("hbm_bytes_per_step", tj.get("hbm_bytes_per_launch"))
+            valu = (tj.get("valu") or {}).get("valu_issue_frac")
+            src = tj.get("sources")
+    return {"bound": "valu", "achieved": None if achieved is None else round(achieved, 3),
+            "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": None if achieved is None else achieved / HBM_PEAK_GBS, "traffic": traffic,
+            "hbm_note": "achieved/peak/frac/traffic price the scoring launches' algorithmic "
+                        "bytes (20 d + 4 n_steps per group) against HBM, as the north star "
+                        "asks; the launches are bound by VALU issue (Philox + Box-Muller per "
+                        "candidate), see `valu`",
+            "kernel": kernel, "kernel_ms": round(kernel_ms, 4), "kernel_timing": timing,
+            "algorithmic_bytes_per_launch": alg,
+            "valu": {"unit": "candidate-dims/s",
+                     "nominal_candidate_dims_per_s": (cand_dims / (kernel_ms * 1e-3)
+                                                      if kernel_ms > 0 else None),
+                     "valu_issue_frac": valu,
+                     "valu_issue_frac_scoring_launches": (agg or {}).get("valu_issue_frac"),
+                     "valu_issue_source": (f"profiles/traffic_{config}.json: 2 * SQ_INSTS_VALU / "
+                                           "(1024 SIMDs x dispatch duration x 2.4 GHz), the "
+                                           "dominant kernel; _scoring_launches: every scoring "
+                                           "dispatch of the step; CSVs: " +
+                                           ", ".join((src or {}).get("pmc_csvs", []))
+                                           if valu is not None else None)}}
+
+
+def importance_cpu_baseline(args, lat0, res0, nbits, gbits, kl_lim):
+    """The oracle's grouped importance pipeline on image 0 (standardise, KL,
+    outliers, partition, plan, coder, destandardise) where it fits
+    ~cpu_seconds, else its coder on a prefix of the image's groups (the same
+    plan) with the rate scaled by the prefix's share of the candidate-dims.
+    The sampled groups' indices and sample words, the group starts and the
+    outliers are checked against the GPU's."""
+    from oracle import oracle as O
+    ncpu, quota = affinity_cores()
+    nthr = min(ncpu, int(np.ceil(quota))) if quota else ncpu
+    ql, qs, pl, ps = lat0
+    gs, gcode, gst, gout = res0
+    D = ql.size
+    tl, ts = O.standardise(ql, qs, pl, ps)
+    kl_bits = O.kl_normal_normal(ql, qs, pl, ps) / np.float32(np.log(2))
+    keep = kl_bits <= kl_lim
+    tl = np.where(keep, tl, np.float32(0)).astype(np.float32)
+    ts = np.where(keep, ts, np.float32(1)).astype(np.float32)
+    zeros, ones = np.zeros(D, np.float32), np.ones(D, np.float32)
+    kl_divs = O.kl_normal_normal(tl, ts, zeros, ones)
+    st = np.asarray(O.importance_group_starts(kl_divs, nbits, gbits), np.int64)
+    ns = np.asarray(O.importance_plan(kl_divs, st), np.int64)
+    starts_equal = bool(np.array_equal(st, np.asarray(gst, np.int64)))
+    G = st.size - 1
+    gidx = np.asarray(C.elias_delta_decode_many(gcode, len(gst) - 1)[0]
+                      if isinstance(gcode, str) else gcode, np.int64) - 1
+    work = np.diff(st) * np.maximum(ns, 1)
+    total = float(work.sum())
+
+    def prefix(k, threads):
+        e = int(st[k])
+        c0 = time.perf_counter()
+        wi, wsm = O.importance_encode(tl[:e], ts[:e], zeros[:e], ones[:e], st[:k + 1], ns[:k],
+                                      42, 0, threads)
+        dt = time.perf_counter() - c0
+        smp = np.where(keep[:e], O.destandardise(wsm, pl[:e], ps[:e]), gs[:e])
+        mi = int((wi != gidx[:k]).sum())
+        ms = int((smp.astype(np.float32).view(np.uint32) != gs[:e].view(np.uint32)).sum())
+        return dt, float(work[:k].sum()), mi, ms
+    k0 = max(1, G // 100)
+    dt, cd, _, _ = prefix(k0, nthr)
+    full_s = dt * total / max(cd, 1.0)
+    if full_s <= args.cpu_seconds:
+        reps = int(max(1, min(100, 3.0 / max(full_s, 1e-6))))  # short images: ~3 s of runs
+        c0 = time.perf_counter()
+        for _ in range(reps):
+            wsm, wi, wst, (oi, oq) = O.code_grouped_importance_sample(ql, qs, pl, ps, 42, nbits,
+                                                                     gbits, kl_lim, nthr)
+        dt = (time.perf_counter() - c0) / reps
+        mi = int((np.asarray(wi, np.int64) - 1 != gidx).sum()) if len(wi) == gidx.size else G
+        ms = int((wsm.view(np.uint32) != gs.view(np.uint32)).sum())
+        out_equal = bool(np.array_equal(oi, gout[0]) and np.array_equal(oq, gout[1]))
+        frac, kind, checked = 1.0, ("the whole pipeline (oracle.code_grouped_importance_sample: "
+                                    "standardise, KL, outliers, partition, plan, coder, "
+                                    f"destandardise), {reps} run(s), per image"), G
+    else:
+        frac_t = min(1.0, args.cpu_seconds / full_s)
+        k = max(1, int(np.searchsorted(np.cumsum(work), frac_t * total)))
+        dt, cd, mi, ms = prefix(k, nthr)
+        frac = cd / total
+        kind = (f"the coder (oracle.importance_encode) on the first {k} of the image's {G} "
+                f"groups ({frac:.2%} of its candidate-dims, the same plan); rate scaled by that "
+                "share")
+        out_equal, checked = None, k
+    k1 = max(1, min(G, int(np.searchsorted(np.cumsum(work), total * min(frac, 3.0 / max(
+        full_s * nthr, 1e-9))))))
+    dt1, cd1, _, _ = prefix(k1, 1)
+    cpu = {"value": frac / dt, "unit": "images/s", "cores": nthr, "kind": "port",
+           "sample": f"image 0 ({D} dims, {total:.3g} candidate-dims): {kind}, {dt:.3f} s, "
+                     "oracle/cwq_oracle.c OpenMP over groups",
+           "affinity_cpus": ncpu, "cgroup_cpu_quota": quota,
+           "one_core_value": (cd1 / total) / dt1,
+           "one_core_sample": f"{cd1 / total:.3%} of image 0's candidate-dims, {dt1:.2f} s"}
+    parity = {"groups_checked": checked, "index_mismatches": mi, "sample_word_mismatches": ms,
+              "group_starts_equal": starts_equal, "outliers_equal": out_equal,
+              "oracle": "oracle/cwq_oracle.c + oracle/oracle.py (CPU restatement of "
+                        "coded_importance_sampler.py:112-274; TF reference unpinned)"}
+    return cpu, parity
 
 
 def pln_main(args):
@@ -452,6 +576,31 @@ def pln_main(args):
         rec = decompress()
     torch.cuda.synchronize()
     eld = time.perf_counter() - t0
+    # one more (untimed) compress of image 0 capturing each level's coder
+    # inputs, results and scoring-launch milliseconds: the roofline prices
+    # those launches, the CPU oracle codes the same latents (parity)
+    cap = {}
+    model.code_image_greedy(None, imgs[0], 42, comp_file_path=paths[0], capture=cap, **kw)
+    torch.cuda.synchronize()
+    l1, l2 = cap["level1"], cap["level2"]
+    D1, D2 = l1["q_loc"].size, l2["q_loc"].size
+    G1, G2 = len(l1["result"][2]) - 1, len(l2["result"][2]) - 1
+    greedy1 = l1["kind"] == "greedy"
+    alg = (20 * D1 + (4 * kw["n_steps"] if greedy1 else 8) * G1) + (20 * D2 + 8 * G2)
+    kernel_ms = float(sum(cap["scoring_ms"]))
+    roofline = scoring_roofline(
+        args.config, G1 + G2, alg, kernel_ms, 0,
+        ("level 1: " + ("k_csr_prep + k_encode_prune_csr (+ finalize), 30 x 14 bits"
+                        if greedy1 else "k_imp_* (importance, 20 bits/group)") +
+         "; level 2: k_imp_* (importance, 20 bits/group)"),
+        "cwq_options.eval_ms_out of the two coders' calls (HIP events around their "
+        "candidate-scoring launches) in one compress of image 0, summed")
+    roofline["valu"]["nominal_candidate_dims_per_s"] = None
+    roofline["scoring_ms_by_level"] = {"level2": cap["scoring_ms"][0],
+                                       "level1": cap["scoring_ms"][1]}
+    cpu = parity = None
+    if not args.no_cpu:
+        cpu, parity = pln_cpu_baseline(args, cap, kw)
     line = {"metric": "images compressed/s (PLN codec, miracle.py compress)",
             "value": n_img * args.steps / el, "unit": "images/s", "n_gpus": 1,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": el / args.steps * 1e3,
@@ -463,8 +612,48 @@ def pln_main(args):
                        "kl_bits_level2": summ[0]["second_level_theoretical"] * 8,
                        "groups_level1": summ[0]["first_level_groups"],
                        "groups_level2": summ[0]["second_level_groups"],
-                       "reconstruction_shape": list(rec[0].shape)}}
+                       "reconstruction_shape": list(rec[0].shape)},
+            "roofline": roofline, "cpu_baseline": cpu, "parity": parity}
     print(json.dumps(line), flush=True)
+
+
+def pln_cpu_baseline(args, cap, kw):
+    """The CPU oracle coding image 0's two latent levels as the codec did
+    (level 2 importance; level 1 greedy 30 x 14 bits or importance), on the
+    coders' exact inputs captured from the GPU run: a per-level sample as in
+    grouped_cpu_baseline / importance_cpu_baseline, the image rate combining
+    the two levels' times.  The analysis / synthesis transforms (seeded random
+    weights, MIOpen) and the arithmetic coder are outside the sample."""
+    l1, l2 = cap["level1"], cap["level2"]
+    half = argparse.Namespace(**{**vars(args), "cpu_seconds": args.cpu_seconds / 2})
+    lat = lambda lv: (lv["q_loc"], lv["q_scale"], lv["p_loc"], lv["p_scale"])
+    c2, p2 = importance_cpu_baseline(half, lat(l2), l2["result"],
+                                     kw["second_level_n_bits_per_group"],
+                                     kw["second_level_max_group_size_bits"],
+                                     kw["second_level_dim_kl_bit_limit"])
+    if l1["kind"] == "greedy":
+        c1, p1 = grouped_cpu_baseline(half, [lat(l1)], [l1["result"]], kw["n_bits_per_step"],
+                                      kw["n_steps"])
+    else:
+        c1, p1 = importance_cpu_baseline(half, lat(l1), l1["result"],
+                                         kw["first_level_n_bits_per_group"],
+                                         kw["first_level_max_group_size_bits"],
+                                         kw["first_level_dim_kl_bit_limit"])
+    comb = lambda a, b: 1.0 / (1.0 / a + 1.0 / b)
+    cpu = {"value": comb(c1["value"], c2["value"]), "unit": "images/s", "cores": c1["cores"],
+           "kind": "port",
+           "sample": "image 0's latent coding on the CPU oracle (transforms and arithmetic "
+                     "coder excluded): level 1 " + c1["sample"] + "; level 2 " + c2["sample"],
+           "one_core_value": comb(c1["one_core_value"], c2["one_core_value"]),
+           "levels": {"level1": c1, "level2": c2}}
+    parity = {"level1": p1, "level2": p2,
+              "index_mismatches": p1["index_mismatches"] + p2["index_mismatches"],
+              "sample_word_mismatches": p1["sample_word_mismatches"] +
+              p2["sample_word_mismatches"],
+              "oracle": "oracle/cwq_oracle.c + oracle/oracle.py (CPU restatement; TF reference "
+                        "unpinned); the coders' inputs are the GPU codec's (random-weight "
+                        "transforms, TFC parity unpinned)"}
+    return cpu, parity
 
 
 def _importance_work(target, proposal, starts, kl_lim, dev):
@@ -681,6 +870,11 @@ def main():
         b0, b1 = rank * nb_cfg, (rank + 1) * nb_cfg
     nb = b1 - b0
     block_id_base = b0
+    shards = [[b0, b1]]
+    if dist:  # every rank's block range, for the line (contiguous, disjoint: checked in tests)
+        allr = [None] * world
+        dist.all_gather_object(allr, [b0, b1])
+        shards = allr
     seed = 42
     host = make_blocks_range(b0, b1, d, bits, seed=DEFAULT_SEED)
     t = {k: torch.from_numpy(v.reshape(-1)).to(dev) for k, v in host.items()}
@@ -804,6 +998,7 @@ def main():
     traffic = None
     valu = None
     units = None
+    tsrc = {}
     tf = os.path.join(REPO, "profiles", f"traffic_{args.config}.json")
     if os.path.exists(tf):
         with open(tf) as f:
@@ -811,6 +1006,7 @@ def main():
         if tj.get("blocks") == nb:
             traffic = tj.get("hbm_bytes_per_launch")
             valu = tj.get("valu")
+            tsrc = tj.get("sources") or {}
     pf = os.path.join(REPO, "profiles", f"prune_stats_{args.config}.json")
     if os.path.exists(pf):
         with open(pf) as f:
@@ -848,9 +1044,11 @@ def main():
                          "nominal_candidate_dims_per_s": cand_dims / (eval_ms * 1e-3),
                          "evaluated": evaluated,
                          "valu_issue_frac": (valu or {}).get("valu_issue_frac"),
-                         "valu_issue_source": "profiles/traffic_%s.json (rocprofv3 --pmc "
-                                              "SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE, same kernel)"
-                                              % args.config if valu else None}}
+                         "valu_issue_source": (f"profiles/traffic_{args.config}.json: 2 * "
+                                               "SQ_INSTS_VALU / (1024 SIMDs x dispatch duration "
+                                               "x 2.4 GHz) of the same kernel; CSVs: " +
+                                               ", ".join(tsrc.get("pmc_csvs", []))
+                                               if valu else None)}}
 
     cpu = None
     parity = None
@@ -952,6 +1150,7 @@ def main():
                        "parallelism": f"block-sharded x{world} ({scaling} scaling), "
                                       "no collective on the data path",
                        "world_size_checked": (dist.get_world_size() if dist else 1),
+                       "shards": shards,
                        "backend": (dist.get_backend() if dist else None),
                        "rank_devices": rank_devices},
             "roofline": roofline,

@@ -196,11 +196,14 @@ def _outlier_target_draw(dev, q_loc, q_scale, seed):
 def code_grouped_importance_sample(sess, target, proposal, seed, n_bits_per_group,
                                    max_group_size_bits=4, dim_kl_bit_limit=12,
                                    return_group_indices_only=False, return_indices=False,
-                                   return_indices_only=False, *, prune_mode=None):
+                                   return_indices_only=False, *, prune_mode=None,
+                                   eval_ms_out=None):
     """:112-274.  Returns (sample np.float32 [D], bitcode str | indices,
     group_start_indices np.ndarray, outlier_extras (indices int64, quint16)).
     ``prune_mode`` (keyword only, not in the reference): cwq_options.prune_mode
-    of the encoder; results never depend on it."""
+    of the encoder; results never depend on it.  ``eval_ms_out`` (keyword
+    only): a ctypes.c_float the fused call writes its candidate-scoring
+    launches' milliseconds to (bench.py's kernel timer)."""
     if not _is_float32(target.loc) or not _is_float32(target.scale):
         raise Exception("Target datatype must be float32!")
     if not _is_float32(proposal.loc) or not _is_float32(proposal.scale):
@@ -210,12 +213,13 @@ def code_grouped_importance_sample(sess, target, proposal, seed, n_bits_per_grou
         return _code_grouped_importance_on(dev, target, proposal, seed, n_bits_per_group,
                                            max_group_size_bits, dim_kl_bit_limit,
                                            return_group_indices_only, return_indices,
-                                           return_indices_only, prune_mode)
+                                           return_indices_only, prune_mode, eval_ms_out)
 
 
 def _code_grouped_importance_on(dev, target, proposal, seed, n_bits_per_group,
                                 max_group_size_bits, dim_kl_bit_limit, return_group_indices_only,
-                                return_indices, return_indices_only, prune_mode):
+                                return_indices, return_indices_only, prune_mode,
+                                eval_ms_out=None):
     lib = _lib.load()
     q_loc, q_scale = _f32(target.loc, dev, "target.loc"), _f32(target.scale, dev, "target.scale")
     p_loc, p_scale = _f32(proposal.loc, dev, "proposal.loc"), _f32(proposal.scale, dev,
@@ -224,7 +228,7 @@ def _code_grouped_importance_on(dev, target, proposal, seed, n_bits_per_group,
     if USE_FUSED and D > 0 and not (return_group_indices_only or return_indices_only):
         return _code_grouped_fused(lib, dev, q_loc, q_scale, p_loc, p_scale, D, seed,
                                    n_bits_per_group, max_group_size_bits, dim_kl_bit_limit,
-                                   return_indices, prune_mode)
+                                   return_indices, prune_mode, eval_ms_out)
     zeros = torch.zeros(D, dtype=torch.float32, device=dev)
     ones = torch.ones(D, dtype=torch.float32, device=dev)
     # :137-138 standardise
@@ -274,7 +278,8 @@ def _code_grouped_importance_on(dev, target, proposal, seed, n_bits_per_group,
 
 
 def _code_grouped_fused(lib, dev, q_loc, q_scale, p_loc, p_scale, D, seed, n_bits_per_group,
-                        max_group_size_bits, dim_kl_bit_limit, return_indices, prune_mode=None):
+                        max_group_size_bits, dim_kl_bit_limit, return_indices, prune_mode=None,
+                        eval_ms_out=None):
     """The common path of code_grouped_importance_sample in one native call
     (cwq_code_grouped_importance); same results as the step-by-step path."""
     need = int(lib.cwq_code_grouped_importance_workspace_size(D))
@@ -293,7 +298,7 @@ def _code_grouped_fused(lib, dev, q_loc, q_scale, p_loc, p_scale, D, seed, n_bit
         float(n_bits_per_group * np.log(2) - 1), sample_h.ctypes.data, index_h.ctypes.data,
         starts_h.ctypes.data, starts_h.size, out_i.ctypes.data, out_v.ctypes.data,
         n_out.ctypes.data, ctypes.byref(kl_sum) if VERBOSE else None, ws.data_ptr(), ws.numel(),
-        _lib.options(prune_mode), _stream(dev)),
+        _lib.options(prune_mode, eval_ms_out=eval_ms_out), _stream(dev)),
         "cwq_code_grouped_importance")
     if VERBOSE:
         total_kl_bits = kl_sum.value / np.log(2)

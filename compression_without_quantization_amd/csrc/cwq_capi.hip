@@ -1869,10 +1869,25 @@ int64_t cwq_code_grouped_importance(const float* q_loc, const float* q_scale,
         (e = hipMemcpyAsync(nsamp, g_imp_ns.data(), (size_t)G * 8, hipMemcpyHostToDevice, s)) !=
             hipSuccess)
       return hip_fail(e, "plan to device");
-    // :212-245 every group's importance coder, seed + g
+    // :212-245 every group's importance coder, seed + g; eval_ms_out: its
+    // launches timed with events of this call (the call synchronises anyway)
+    cwq_options oi;
+    if ((rc = read_options(opts, &oi)) != 0) return rc;
+    CallEvents tev;
+    if (oi.eval_ms_out) {
+      if (!tev.made(2, s, hipEventDefault))
+        return fail(CWQ_ERR_HIP, "cwq_code_grouped_importance: event creation failed");
+      oi.eval_start_event = tev.ev[0];
+      oi.eval_stop_event = tev.ev[1];
+    }
     if ((rc = cwq_importance_encode(t_loc, t_scale, zeros, ones, offs, nsamp, G, D, seed, 0, idx,
-                                    sample, w + l.enc, workspace_bytes - l.enc, opts, stream)) < 0)
+                                    sample, w + l.enc, workspace_bytes - l.enc, &oi, stream)) < 0)
       return rc;
+    if (oi.eval_ms_out) {
+      if ((e = hipEventSynchronize(tev.ev[1])) != hipSuccess ||
+          (e = hipEventElapsedTime(oi.eval_ms_out, tev.ev[0], tev.ev[1])) != hipSuccess)
+        return hip_fail(e, "event time");
+    }
   } else {
     if ((e = hipMemsetAsync(sample, 0, (size_t)D * 4, s)) != hipSuccess)
       return hip_fail(e, "memset");
@@ -1937,10 +1952,15 @@ int cwq_importance_encode(const float* t_loc, const float* t_scale, const float*
   const size_t need = cwq::importance_workspace_size(nb, total_dims);
   if (workspace_bytes < need || (need && !workspace))
     return fail(CWQ_ERR_WORKSPACE, "workspace %zu bytes < required %zu", workspace_bytes, need);
-  hipError_t e = cwq::launch_importance_encode(t_loc, t_scale, p_loc, p_scale, block_off,
-                                               n_samples, nb, total_dims, seed, block_id_base,
-                                               o.prune_mode >= 2 ? 1 : 0, out_index, out_sample,
-                                               workspace, (hipStream_t)stream);
+  hipError_t e = hipSuccess;
+  if (o.eval_start_event)  // the caller's timer around the candidate-scoring launches
+    e = hipEventRecord((hipEvent_t)o.eval_start_event, (hipStream_t)stream);
+  if (e == hipSuccess)
+    e = cwq::launch_importance_encode(t_loc, t_scale, p_loc, p_scale, block_off, n_samples, nb,
+                                      total_dims, seed, block_id_base, o.prune_mode >= 2 ? 1 : 0,
+                                      out_index, out_sample, workspace, (hipStream_t)stream);
+  if (e == hipSuccess && o.eval_stop_event)
+    e = hipEventRecord((hipEvent_t)o.eval_stop_event, (hipStream_t)stream);
   if (e != hipSuccess) return hip_fail(e, "cwq_importance_encode");
   return ok();
 }

@@ -2205,13 +2205,65 @@ __global__ void __launch_bounds__(256) k_small_prep1(
   rec[g] = r;
 }
 
+// The exact values of a block's listed rows (k_small_one), lane-parallel over
+// (row, dim): each lane computes one normal exactly (its Philox block and the
+// one Box-Muller pair holding it) and its log-density into lpv; a lane per row
+// then sums in the Eigen order (eval_row's values bit for bit).  Returns the
+// wave's best argmax key.  Out of line: its f64 Box-Muller constants would
+// otherwise occupy k_small_one's registers for the whole kernel.
+template <bool STEP0>
+CWQ_RARE unsigned long long small_listed_exact(
+    int64_t off, int db, const PhiloxStream sb, uint32_t used, const uint32_t* ln, float* lpv,
+    const double* logtab, const float* __restrict__ t_loc, const float* __restrict__ t_scale,
+    const float* __restrict__ loc_s, const float* __restrict__ scale_s,
+    const float* __restrict__ lognorm, const float* __restrict__ best) {
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t du = (uint32_t)db;
+  const uint32_t per = (uint32_t)CWQ_FUSED_STAGE / du;  // rows per batch (>= 1: d <= 64)
+  uint64_t bestk = 0;
+  for (uint32_t e0 = 0; e0 < used; e0 += per) {
+    const uint32_t e1 = e0 + per < used ? e0 + per : used;
+    const uint32_t i1 = (e1 - e0) * du;
+    for (uint32_t it = lane; it < i1; it += 64) {
+      const uint32_t e = e0 + it / du;
+      const uint32_t j = it - (e - e0) * du;
+      const int64_t ei = off + j;
+      const float zz = exact_normal(sb, (uint64_t)ln[e] * (uint64_t)du + j, logtab);
+      float sv = scale_s[ei] * zz;  // misc.py:14
+      sv = loc_s[ei] + sv;          // misc.py:15
+      const float tv = STEP0 ? sv : best[ei] + sv;  // :57
+      lpv[it] = log_prob(tv, t_loc[ei], t_scale[ei], lognorm[ei]);
+    }
+    wave_lds_sync();
+    const uint32_t e = e0 + lane;
+    if (e < e1) {  // a lane per row: the Eigen-order sum (eval_row_f)
+      const float* x = lpv + (e - e0) * du;
+      const int vec = db & ~7;
+      float p[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      for (int jj = 0; jj < vec; jj += 8) {
+#pragma unroll
+        for (int l = 0; l < 8; ++l) p[l] = p[l] + x[jj + l];
+      }
+      float sum = 0.0f;
+      for (int jj = vec; jj < db; ++jj) sum = sum + x[jj];
+      const float r0 = p[0] + p[4], r1 = p[1] + p[5], r2 = p[2] + p[6], r3 = p[3] + p[7];
+      const uint64_t k = argmax_key(sum + ((r0 + r2) + (r1 + r3)), ln[e]);
+      bestk = k > bestk ? k : bestk;
+    }
+    wave_lds_sync();
+  }
+  return wave_max_u64(bestk);
+}
+
 // A wave (a 64-thread workgroup) per block: the screen (k_small_screen's spans)
 // and the exact scoring of the listed rows; writes the index (out_idx).  The
 // dispatcher hands a slot to the next wave as soon as one ends.  Measured
 // alternatives on C2
 // (tools/quad_times.py --one): persistent waves drawing blocks from one
 // atomic counter, 474 us (41.5k same-address atomics serialise at ~11 ns);
-// two blocks per wave in a loop, 69 us against 47 (the loop's spills);
+// two blocks per wave in a loop, 69 us against 47 (the loop's spills), or
+// as straight-line copies (2 or 4 blocks, 6-8 waves/SIMD): no gain on C2 or
+// C3 (C3's scoring 1.11-1.20 ms per step in all five);
 // longest blocks first (a counting sort by d), 41 us against 47 but the sort
 // cost a launch and a histogram that needed zeroing.
 template <bool STEP0>
@@ -2377,41 +2429,11 @@ __global__ void __launch_bounds__(64, CWQ_FUSED_WAVES) k_small_one(
       g_quad_info[g][3] = (state == kQuadExact ? 1u : 0u) | ((uint32_t)db << 8);
     }
 #endif
-    if (state == kQuadListed && used > 0) {
-      // exact values of the listed rows, lane-parallel over (row, dim): rows of d items
-      const uint32_t du = (uint32_t)db;
-      const uint32_t per = (uint32_t)CWQ_FUSED_STAGE / du;  // rows per batch (>= 1: d <= 64)
-      for (uint32_t e0 = 0; e0 < used; e0 += per) {
-        const uint32_t e1 = e0 + per < used ? e0 + per : used;
-        const uint32_t i1 = (e1 - e0) * du;
-        for (uint32_t it = lane; it < i1; it += 64) {
-          const uint32_t e = e0 + it / du;
-          const uint32_t j = it - (e - e0) * du;
-          const int64_t ei = off + j;
-          const float zz = exact_normal(sb, (uint64_t)ln[e] * (uint64_t)du + j, logtab);
-          float sv = scale_s[ei] * zz;  // misc.py:14
-          sv = loc_s[ei] + sv;          // misc.py:15
-          const float tv = STEP0 ? sv : best[ei] + sv;  // :57
-          lpv[it] = log_prob(tv, t_loc[ei], t_scale[ei], lognorm[ei]);
-        }
-        wave_lds_sync();
-        const uint32_t e = e0 + lane;
-        if (e < e1) {  // a lane per row: the Eigen-order sum (eval_row_f)
-          const float* x = lpv + (e - e0) * du;
-          const int dr = db;
-          const int vec = dr & ~7;
-          float p[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-          for (int jj = 0; jj < vec; jj += 8) {
-#pragma unroll
-            for (int l = 0; l < 8; ++l) p[l] = p[l] + x[jj + l];
-          }
-          float s = 0.0f;
-          for (int jj = vec; jj < dr; ++jj) s = s + x[jj];
-          const float r0 = p[0] + p[4], r1 = p[1] + p[5], r2 = p[2] + p[6], r3 = p[3] + p[7];
-          atomicMax(&kmax, (unsigned long long)argmax_key(s + ((r0 + r2) + (r1 + r3)), ln[e]));
-        }
-        wave_lds_sync();
-      }
+    if (state == kQuadListed && used > 0) {  // rare (C2: 0.6% of the blocks): out of line
+      const unsigned long long bk = small_listed_exact<STEP0>(
+          off, db, sb, used, ln, lpv, logtab, t_loc, t_scale, loc_s, scale_s, lognorm, best);
+      if (lane == 0) kmax = bk;
+      wave_lds_sync();
     }
     if (state == kQuadExact) {  // every candidate exactly (constants outside the gate, list full)
       QuadBlk r;

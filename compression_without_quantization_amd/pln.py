@@ -41,6 +41,7 @@ Appendix B) or a non-determinism:
   sequence as the reference's ``np.random.seed(seed)``, without touching numpy's
   global state); nothing is written to hard-coded paths (:424, :754, :805).
 """
+import ctypes
 import math
 import os
 
@@ -454,13 +455,18 @@ class ProbabilisticLadderNetwork(nn.Module):
                           use_index_ac=False,
                           return_first_level_group_sizes=False, return_first_level_indices=False,
                           return_second_level_group_sizes=False,
-                          return_second_level_indices=False, verbose=False):
+                          return_second_level_indices=False, verbose=False, *,
+                          capture=None):
         """pln.py:213-627.  ``session`` is ignored.  Writes the .miracle file to
         comp_file_path and returns ((sample2, sample1), summaries), or what the
         return_* flags ask for.  Group-size count models are .npy paths or
         arrays (uniform over 1 + 2^max_group_size_bits symbols when empty);
         with use_index_ac the index coders are ArithmeticCoder objects or
-        count arrays (the reference unpickles them, :262-265)."""
+        count arrays (the reference unpickles them, :262-265).
+        ``capture`` (keyword only, not in the reference; bench.py): a dict that
+        receives each level's coder inputs (flattened, permuted float32 numpy
+        q/p loc and scale) and results under "level2" / "level1", and the
+        coders' candidate-scoring milliseconds under "scoring_ms"."""
         del session, backfitting_steps_level_1, backfitting_steps_level_2, use_log_prob
         if use_index_ac and not use_importance_sampling:
             raise ValueError("use_index_ac needs use_importance_sampling=True: the greedy "
@@ -479,13 +485,31 @@ class ProbabilisticLadderNetwork(nn.Module):
         q2p = Normal(permute_flatten(q2.loc, perm2_d), permute_flatten(q2.scale, perm2_d))
         p2p = Normal(torch.zeros(n2, device=dev), torch.ones(n2, device=dev))  # prior_2 = N(0, 1)
 
+        timers = []
+
+        def timer():  # capture: each coder's scoring milliseconds
+            if capture is None:
+                return {}
+            v = ctypes.c_float(0.0)
+            timers.append(v)
+            return {"eval_ms_out": v}
+
+        def keep(level, q, p, r, kind):
+            if capture is not None:
+                capture[level] = {"kind": kind, "result": r, **{
+                    k: x.detach().float().cpu().numpy().reshape(-1) for k, x in
+                    (("q_loc", q.loc), ("q_scale", q.scale), ("p_loc", p.loc),
+                     ("p_scale", p.scale))}}
+
         # Step 2a: level 2, grouped importance coder (:346-358)
         res = code_grouped_importance_sample(
             None, q2p, p2p, seed, second_level_n_bits_per_group,
             max_group_size_bits=second_level_max_group_size_bits,
             dim_kl_bit_limit=second_level_dim_kl_bit_limit,
             return_group_indices_only=return_second_level_group_sizes,
-            return_indices_only=return_second_level_indices, return_indices=use_index_ac)
+            return_indices_only=return_second_level_indices, return_indices=use_index_ac,
+            **timer())
+        keep("level2", q2p, p2p, res, "importance")
         if return_second_level_group_sizes:
             return res[0]
         if return_second_level_indices:
@@ -509,7 +533,9 @@ class ProbabilisticLadderNetwork(nn.Module):
                 max_group_size_bits=first_level_max_group_size_bits,
                 dim_kl_bit_limit=first_level_dim_kl_bit_limit,
                 return_group_indices_only=return_first_level_group_sizes,
-                return_indices_only=return_first_level_indices, return_indices=use_index_ac)
+                return_indices_only=return_first_level_indices, return_indices=use_index_ac,
+                **timer())
+            keep("level1", q1p, p1p, res, "importance")
             if return_first_level_group_sizes:
                 return res[0]
             if return_first_level_indices:
@@ -521,10 +547,13 @@ class ProbabilisticLadderNetwork(nn.Module):
         else:
             sample1, code1, group_indices1 = code_grouped_greedy_sample(
                 None, q1p, p1p, n_steps, n_bits_per_step, seed,
-                max_group_size_bits=greedy_max_group_size_bits, rho=rho)
+                max_group_size_bits=greedy_max_group_size_bits, rho=rho, **timer())
+            keep("level1", q1p, p1p, (sample1, code1, group_indices1), "greedy")
             if return_first_level_group_sizes:
                 return np.asarray(group_indices1)
             outlier_extras1 = None
+        if capture is not None:
+            capture["scoring_ms"] = [float(v.value) for v in timers]
         group_differences1 = _group_differences(group_indices1)
         bitcode = code1 + code2
 

@@ -40,7 +40,8 @@ def encode_blocks_host(t_loc, t_scale, p_loc, p_scale, n_bits_per_step, n_steps,
     last chunk's results are the copies left exposed (C4 on one MI355X,
     tools/stream_chunks.py: 65,536-block chunks 2.99e6 blocks/s, 131,072
     3.05e6, 262,144 3.04e6, 500,000 2.99e6; unpipelined 2.89e6,
-    device-resident 3.09e6).
+    device-resident 3.09e6).  A job of one chunk takes the plain copy-in /
+    encode / copy-out sequence.
     """
     arrs = [np.ascontiguousarray(np.asarray(a, dtype=np.float32).reshape(-1))
             for a in (t_loc, t_scale, p_loc, p_scale)]
@@ -62,6 +63,19 @@ def encode_blocks_host(t_loc, t_scale, p_loc, p_scale, n_bits_per_step, n_steps,
         chunk_blocks = max(131072, -(-nb // 8))
     cb = max(1, min(int(chunk_blocks), nb))
     n_chunks = (nb + cb - 1) // cb
+    if n_chunks == 1:
+        # nothing to overlap: one copy in, one encode, one copy out on the
+        # caller's stream (the pipeline's extra stream, events and slots only
+        # cost here: C5's 1,024 blocks ran 23.9k blocks/s through them against
+        # 28.1k for the plain sequence, round 4)
+        with torch.cuda.device(dev):
+            x = [torch.from_numpy(a).to(dev) for a in arrs]
+            idx, smp = encode_blocks(x[0], x[1], x[2], x[3], n_bits_per_step, n_steps, seed,
+                                     rho=rho, block_dim=d, block_id_base=int(block_id_base),
+                                     prune_mode=prune_mode)
+            idx_out[:] = idx.cpu().numpy().reshape(nb, n_steps)
+            sample_out[:] = smp.cpu().numpy().reshape(-1)
+        return idx_out, sample_out
     nslot = min(2, n_chunks)
     host_in = [torch.from_numpy(a) for a in arrs]
     host_idx, host_smp = torch.from_numpy(idx_out), torch.from_numpy(sample_out)

@@ -98,12 +98,12 @@ int cwq_stateless_normal_sample(const float* loc, const float* scale, int64_t d,
  *               recorded on the call's stream right before the first
  *               candidate-scoring launch and right after the last one, so a
  *               caller can time the dominant kernel alone (bench.py).
- *   eval_ms_out: HOST float, or NULL.  The fused grouped greedy calls
- *               (cwq_code_grouped_greedy[_batch]), which synchronise, write
- *               the summed milliseconds of their candidate-scoring launches
- *               (a pipelined batch codes in chunks: device gaps between them
- *               are excluded, unlike the event span).  Asynchronous entry
- *               points ignore it.
+ *   eval_ms_out: HOST float, or NULL.  The fused grouped calls
+ *               (cwq_code_grouped_greedy[_batch], cwq_code_grouped_importance),
+ *               which synchronise, write the summed milliseconds of their
+ *               candidate-scoring launches (a pipelined batch codes in chunks:
+ *               device gaps between them are excluded, unlike the event
+ *               span).  Asynchronous entry points ignore it.
  *   item_ready: HOST int32 array of n_items flags, zeroed by the caller, or
  *               NULL.  cwq_code_grouped_greedy_batch sets flag i to 1 (a
  *               release store) as soon as item i's sample, bitcode, bits_off

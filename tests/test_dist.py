@@ -1,4 +1,4 @@
-"""CPU: multi-rank block sharding over gloo (world_size 2 and 3), as bench.py
+"""CPU: multi-rank block sharding over gloo (world_size 2, 3 and 8), as bench.py
 --gpus N uses it (no collective on the data path; optional all-gather of
 indices).  Each rank codes its shard with the CPU oracle (the checker, allowed
 in tests) using block_id_base = its first global block; the gathered indices
@@ -62,7 +62,7 @@ def _worker(rank, world, port, nb, cost, out):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,balanced", [(2, False), (3, True), (3, "empty")])
+@pytest.mark.parametrize("world,balanced", [(2, False), (3, True), (3, "empty"), (8, True)])
 def test_gloo_ranks_gather_oracle_coded_shards(world, balanced):
     from oracle import oracle as O
     from compression_without_quantization_amd.synthetic import make_blocks_range

@@ -298,6 +298,7 @@ def test_bench_launches_two_ranks_itself(cwq):
     assert line["n_gpus"] == 2 and line["config"]["world_size_checked"] == 2
     assert line["scaling"] == "strong"
     assert line["config"]["blocks_total"] == 8192 and line["config"]["blocks_per_gpu"] == 4096
+    _check_shards(line, 2, 8192)
     assert line["parity"]["index_mismatches"] == 0
     assert line["parity"]["sample_word_mismatches"] == 0
     assert line["parity"]["blocks_checked"] >= 2 * 16
@@ -378,6 +379,36 @@ def test_ragged_shards_gathered(cwq):
         assert p.exitcode == 0
     assert 0 < n0 < off.size - 1  # rank 0's shard is a strict part: shards are unequal
     assert np.array_equal(got, want)
+
+
+def _check_shards(line, world, nb_total):
+    sh = line["config"]["shards"]
+    assert len(sh) == world
+    assert sh[0][0] == 0 and sh[-1][1] == nb_total
+    for (a0, a1), (b0, b1) in zip(sh[:-1], sh[1:]):
+        assert a1 == b0 and a0 < a1  # contiguous, non-empty, in rank order
+
+
+@pytest.mark.parametrize("config,blocks,check", [("c4", 8192, 4), ("c5", 64, 1)])
+def test_bench_eight_ranks_rehearsal(cwq, config, blocks, check):
+    """The scaling target's N = 8 on the box's one GPU: `bench.py --gpus 8`
+    starts its eight ranks itself (gloo: they share the device), cuts the
+    block set into 8 contiguous shards coded with block_id_base = their first
+    block (coded_greedy_sampler.py:282, seed + g), all-reduces the timing and
+    the oracle checks of every rank (first, last and evenly spaced blocks of
+    its shard): one line, world size 8, no mismatch.  C4-shaped (16 bits) and
+    C5-shaped (2^24 candidates per block, the multi-tile blocks) cases."""
+    line = _bench(["--gpus", "8", "--config", config, "--blocks", str(blocks), "--steps", "1",
+                   "--warmup", "0", "--no-e2e", "--check-blocks", str(check)], timeout=600)
+    assert line["n_gpus"] == 8 and line["config"]["world_size_checked"] == 8
+    assert line["scaling"] == "strong" and line["config"]["blocks_total"] == blocks
+    _check_shards(line, 8, blocks)
+    assert [m["rank"] for m in line["config"]["rank_devices"]] == list(range(8))
+    assert line["parity"]["index_mismatches"] == 0
+    assert line["parity"]["sample_word_mismatches"] == 0
+    assert line["parity"]["blocks_checked"] >= 8 * 2
+    assert line["decode_roundtrip_bit_exact"] is True
+    assert line["roofline"]["scope"].startswith("all 8 GPUs")
 
 
 def test_bench_weak_scaling_two_ranks(cwq):

@@ -1,59 +1,105 @@
-"""Turn tools/profile.sh output into the committed evidence under profiles/.
-Usage: python tools/collect_profile.py TAG CONFIG KERNEL_SUBSTR [BLOCKS ALG_BYTES]
-KERNEL_SUBSTR selects the priced kernels (every dispatch whose name contains
-it, counters summed: "k_small_" takes prep + screen + survivors).  BLOCKS (the
-blocks or groups of one launch) and ALG_BYTES default to the bench line of the
-trace run (config.blocks_per_gpu / groups_per_step, roofline's algorithmic
-bytes)."""
-import csv, glob, json, os, shutil, sys
+"""Turn a config's rocprofv3 runs (tools/gpu_task.sh trace TAG + pmc TAG mem /
+valu / wait, same bench arguments) into the committed evidence under
+profiles/ and the profiles/traffic_CONFIG.json that bench.py reads.
 
-tag, config, ksub = sys.argv[1], sys.argv[2], sys.argv[3]
-root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-src = os.path.join(root, "gpurun_out", "prof_" + tag)
-dst = os.path.join(root, "profiles")
-if len(sys.argv) > 5:
-    blocks, alg = int(sys.argv[4]), int(sys.argv[5])
-else:
-    line = [ln for ln in open(os.path.join(src, "trace.log")) if ln.startswith('{"metric"')][-1]
-    bl = json.loads(line)
-    blocks = bl["config"].get("blocks_per_gpu", bl["config"].get("groups_per_step"))
-    alg = bl["roofline"]["algorithmic_bytes_per_launch"]
+Usage: python tools/collect_profile.py CONFIG TAG DOMINANT [SCORING ...]
+
+DOMINANT selects the kernel the bench line's roofline prices (every dispatch
+whose name contains it); SCORING (default: DOMINANT) the substrings of every
+candidate-scoring launch of one step (e.g. k_small_prep1 k_small_one
+k_small_finalize for the small pipeline).  The PMC passes ran `bench.py
+--steps 1 --warmup 0`, so their dispatches are one step's.
+
+Fractions are computed over each dispatch's own duration (End - Start of its
+counter_collection.csv row), tools/pmc_frac.py:
+  valu_issue_frac = 2 * SQ_INSTS_VALU / (1024 SIMDs * duration * 2.4e9);
+  hbm bytes = (2 * FETCH_SIZE + WRITE_SIZE) * 1024 (gfx950 FETCH_SIZE x2).
+Everything in traffic_CONFIG.json can be recomputed from the CSVs it lists.
+"""
+import glob
+import json
+import os
+import shutil
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+import pmc_frac  # noqa: E402
+
+PASSES = ("fetch", "write", "valu", "wait")
 
 
 def one(pattern):
-    f = sorted(glob.glob(os.path.join(src, pattern), recursive=True))
-    assert f, pattern
-    return f[0]
+    f = sorted(glob.glob(pattern, recursive=True))
+    return f[0] if f else None
 
 
-shutil.copy(one("trace/**/*kernel_stats.csv"), os.path.join(dst, f"{tag}_kernel_stats.csv"))
-shutil.copy(one("trace/**/*kernel_trace.csv"), os.path.join(dst, f"{tag}_kernel_trace.csv"))
-vals = {}
-for pas in ("fetch", "write", "valu"):
-    f = one(f"{pas}/**/*counter_collection.csv")
-    shutil.copy(f, os.path.join(dst, f"{tag}_pmc_{pas}.csv"))
-    with open(f) as fh:
-        for row in csv.DictReader(fh):
-            if ksub in row["Kernel_Name"]:
-                vals.setdefault(row["Counter_Name"], 0.0)
-                vals[row["Counter_Name"]] += float(row["Counter_Value"])
-fetch_kb, write_kb = vals["FETCH_SIZE"], vals["WRITE_SIZE"]
-hbm = int((2 * fetch_kb + write_kb) * 1024)
-out = {"config": config, "blocks": blocks, "kernel": ksub, "FETCH_SIZE_kB": fetch_kb,
-       "WRITE_SIZE_kB": write_kb, "hbm_bytes_per_launch": hbm,
-       "algorithmic_bytes_per_launch": alg,
-       "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes of "
-                 "`python3 bench.py --steps 1 --warmup 0 --no-cpu --no-e2e` (one eval launch "
-                 "each); bytes = (2*FETCH_SIZE + WRITE_SIZE) * 1024 per MI355X_MICROARCH.md",
-       "valu": {k: vals.get(k) for k in ("SQ_INSTS_VALU", "SQ_INSTS_SALU",
-                                         "SQ_ACTIVE_INST_VALU", "GRBM_GUI_ACTIVE")}}
-v = out["valu"]
-if v.get("SQ_INSTS_VALU") and v.get("GRBM_GUI_ACTIVE"):
-    # a wave64 VALU instruction occupies its SIMD32 for 2 cycles (MI355X_MICROARCH.md);
-    # GRBM_GUI_ACTIVE sums the 8 XCDs' busy cycles
-    cycles = v["GRBM_GUI_ACTIVE"] / 8.0
-    v["kernel_cycles"] = cycles
-    v["valu_issue_frac"] = 2.0 * v["SQ_INSTS_VALU"] / (1024.0 * cycles)
-with open(os.path.join(dst, f"traffic_{config}.json"), "w") as fh:
-    json.dump(out, fh, indent=1)
-print(json.dumps(out, indent=1))
+def main():
+    config, tag, dom = sys.argv[1], sys.argv[2], sys.argv[3]
+    scoring = sys.argv[4:] or [dom]
+    src = os.path.join(ROOT, "gpurun_out")
+    dst = os.path.join(ROOT, "profiles")
+    files = {}
+    for what, pat in (("kernel_stats", f"prof_{tag}_trace/**/*kernel_stats.csv"),
+                      ("kernel_trace", f"prof_{tag}_trace/**/*kernel_trace.csv")):
+        f = one(os.path.join(src, pat))
+        if f:
+            files[what] = os.path.join("profiles", f"{tag}_{what}.csv")
+            shutil.copy(f, os.path.join(ROOT, files[what]))
+    csvs = []
+    for p in PASSES:
+        f = one(os.path.join(src, f"prof_{tag}_{p}/**/*counter_collection.csv"))
+        if not f:
+            continue
+        rel = os.path.join("profiles", f"{tag}_pmc_{p}.csv")
+        shutil.copy(f, os.path.join(ROOT, rel))
+        csvs.append(rel)
+    absf = [os.path.join(ROOT, c) for c in csvs]
+    d = pmc_frac.summarize(dom, absf)
+    # every scoring dispatch of the step: totals per pass, then the fractions
+    tot = {}
+    for sub in scoring:
+        s = pmc_frac.summarize(sub, absf)
+        if not s.get("dispatches"):
+            continue
+        for c, v in s["per_dispatch"].items():
+            n = s["counter_dispatches"][c]
+            tot.setdefault(c, [0.0, 0.0])
+            tot[c][0] += v * n
+            tot[c][1] += s["mean_duration_ns_by_pass"][c] * n
+    agg = {"kernels": scoring}
+    if "SQ_INSTS_VALU" in tot:
+        v, dur = tot["SQ_INSTS_VALU"]
+        agg["valu_instructions_per_step"] = v
+        agg["duration_ns_per_step"] = dur
+        agg["valu_issue_frac"] = 2.0 * v / (pmc_frac.SIMDS * dur * 1e-9 * pmc_frac.CLK)
+    if "FETCH_SIZE" in tot or "WRITE_SIZE" in tot:
+        agg["hbm_bytes_per_step"] = (2.0 * tot.get("FETCH_SIZE", [0.0])[0] +
+                                     tot.get("WRITE_SIZE", [0.0])[0]) * 1024.0
+    line = None
+    lf = os.path.join(src, f"prof_{tag}_trace.log")
+    if os.path.exists(lf):
+        for ln in open(lf):
+            if ln.startswith('{"metric"'):
+                line = json.loads(ln)
+    cfg = (line or {}).get("config", {})
+    out = {"config": config, "tag": tag,
+           "blocks": cfg.get("blocks_per_gpu", cfg.get("groups_per_step")),
+           "dominant": d, "scoring": agg,
+           "hbm_bytes_per_launch": d.get("hbm_bytes_per_dispatch"),
+           "valu": {"valu_issue_frac": d.get("valu_issue_frac"),
+                    "formula": d.get("valu_issue_formula")},
+           "sources": {"pmc_csvs": csvs, **files},
+           "method": "rocprofv3 --pmc passes (FETCH_SIZE | WRITE_SIZE | SQ_INSTS_VALU "
+                     "SQ_INSTS_SALU SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE | SQ_WAVE_CYCLES "
+                     "SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_BUSY_CYCLES SQ_WAVES) of `python3 "
+                     "bench.py --steps 1 --warmup 0 --no-cpu --no-e2e`, one pass each "
+                     "(tools/gpu_task.sh pmc); tools/collect_profile.py + tools/pmc_frac.py"}
+    with open(os.path.join(dst, f"traffic_{config}.json"), "w") as fh:
+        json.dump(out, fh, indent=1)
+    print(json.dumps({k: out[k] for k in ("config", "blocks", "hbm_bytes_per_launch", "valu",
+                                          "scoring")}, indent=1))
+
+
+if __name__ == "__main__":
+    main()
