@@ -350,7 +350,8 @@ int encode_impl(const float* t_loc, const float* t_scale, const float* p_loc,
                 int64_t total_dims, int64_t max_block_dim, int n_bits, int n_steps, int32_t seed, float rho,
                 int64_t block_id_base, int32_t* out_idx, float* out_sample, void* workspace,
                 size_t workspace_bytes, const cwq_options* opts, void* stream,
-                const int32_t* block_seeds = nullptr) {
+                const int32_t* block_seeds = nullptr, float* ds_out = nullptr,
+                const float* ds_loc = nullptr, const float* ds_scale = nullptr) {
   int rc = check_common(n_bits, n_steps, nb);
   if (rc) return rc;
   cwq_options o;
@@ -407,6 +408,9 @@ int encode_impl(const float* t_loc, const float* t_scale, const float* p_loc,
   a.sdmap = l.csr ? (uint32_t*)(w + l.sdmap) : nullptr;
   a.ev_start = o.eval_start_event;
   a.ev_stop = o.eval_stop_event;
+  a.ds_out = ds_out;
+  a.ds_loc = ds_loc;
+  a.ds_scale = ds_scale;
   hipError_t e = cwq::launch_encode(a, (hipStream_t)stream);
   if (e != hipSuccess) return hip_fail(e, "cwq_greedy_encode");
   return ok();
@@ -838,16 +842,15 @@ int64_t grouped_begin(const float* q_loc, const float* q_scale, const float* p_l
   if (o.eval_ms_out && (!tev->made(2, s, hipEventDefault) ||
                         hipEventRecord(tev->ev[0], s) != hipSuccess))
     return fail(CWQ_ERR_HIP, "%s: timing events failed", who);
-  if ((rc = cwq_greedy_encode(t_loc, t_scale, zeros, ones, offs, G, D, maxd, n_bits_per_step,
-                              n_steps, seed, rho, 0, idx, sample, w + l.enc,
-                              workspace_bytes - l.enc, opts, stream)) < 0)
+  // (and :292 destandardise into out, folded into the encoder's last launch)
+  if ((rc = encode_impl(t_loc, t_scale, zeros, ones, offs, 0, G, D, maxd, n_bits_per_step,
+                        n_steps, seed, rho, 0, idx, sample, w + l.enc, workspace_bytes - l.enc,
+                        opts, stream, nullptr, out, p_loc, p_scale)) < 0)
     return rc;
   if (o.eval_ms_out && (e = hipEventRecord(tev->ev[1], s)) != hipSuccess) {
     (void)hipStreamSynchronize(s);
     return hip_fail(e, "event");
   }
-  // :292 destandardise
-  if ((rc = cwq_destandardise(sample, p_loc, p_scale, D, out, stream)) < 0) return rc;
   if ((e = hipMemcpyAsync(idx_host, idx, (size_t)(G * n_steps) * 4, hipMemcpyDeviceToHost, s)) !=
       hipSuccess)
     return hip_fail(e, "indices to host");
@@ -988,7 +991,7 @@ namespace {
 // D + 2 n + 1 entries, indices / seeds D + n.
 struct BatchWs {
   GroupedWs g;
-  size_t seeds, ioff, dstarts, iinfo, itab, total;
+  size_t seeds, ioff, dstarts, iinfo, itab, pstarts, total;
 };
 BatchWs batch_ws(int64_t D, int64_t n_items, int n_steps) {
   BatchWs l;
@@ -1001,7 +1004,9 @@ BatchWs batch_ws(int64_t D, int64_t n_items, int n_steps) {
   l.dstarts = align_up(l.ioff + (size_t)(n + 1) * 8, 256);
   l.iinfo = align_up(l.dstarts + (size_t)(D + 2 * n + 1) * 8, 256);
   l.itab = align_up(l.iinfo + (size_t)(4 * n + 4) * 8, 256);
-  l.total = align_up(l.itab + (size_t)(n + 1) * sizeof(cwq::BatchItem), 256);
+  // the start lists packed back to back (at most D_i + 2 entries each)
+  l.pstarts = align_up(l.itab + (size_t)(n + 1) * sizeof(cwq::BatchItem), 256);
+  l.total = align_up(l.pstarts + (size_t)(D + 2 * n + 1) * 8, 256);
   return l;
 }
 // Host staging of the batch (the caller's pinned memory, or thread-local
@@ -1102,7 +1107,7 @@ int64_t batch_device_path(int64_t n_items, const int64_t* item_off, int64_t D, i
                           int64_t* offs, int32_t* idx, int32_t* bseed, int32_t* idx_h,
                           CallEvents& evs, CallEvents& tev, const float* p_loc,
                           const float* p_scale, hipStream_t s, hipStream_t d2h, hipStream_t h2d,
-                          hipEvent_t part_ev) {
+                          hipEvent_t part_ev, int64_t* pstage) {
   const GroupedWs& l = bl.g;
   const int64_t K = (int64_t)ci.size() - 1;
 #ifdef CWQ_PHASE_TIMES  // tuning builds: per-phase host wall times to stderr
@@ -1121,8 +1126,11 @@ int64_t batch_device_path(int64_t n_items, const int64_t* item_off, int64_t D, i
   int64_t* dst = (int64_t*)(w + bl.dstarts);
   int64_t* iinfo_d = (int64_t*)(w + bl.iinfo);
   cwq::BatchItem* itab_d = (cwq::BatchItem*)(w + bl.itab);
+  int64_t* pst_d = (int64_t*)(w + bl.pstarts);
   unsigned long long* info_d = (unsigned long long*)(w + l.pinfo);
   hipEvent_t* done_ev = evs.ev.data() + K;
+  // (the host path's per-chunk KL / layout events are free here)
+  hipEvent_t layout_ev = evs.ev[0], pst_ev = evs.ev[(size_t)(2 * K)];
   hipEvent_t* res_ev = evs.ev.data() + 3 * K;
   auto drain = [&]() {
     (void)hipStreamSynchronize(s);
@@ -1151,11 +1159,13 @@ int64_t batch_device_path(int64_t n_items, const int64_t* item_off, int64_t D, i
   std::vector<int64_t> gl((size_t)n_items), chunk_of((size_t)n_items);
   std::vector<int64_t> cG((size_t)K, 0), cmaxd((size_t)K, 0);
   g_batch_items.resize((size_t)n_items);
+  std::vector<int64_t> pk((size_t)n_items + 1, 0);  // packed start-list offsets
   for (int64_t c = 0; c < K; ++c) {
     const int64_t a = item_off[ci[(size_t)c]], gb = a + ci[(size_t)c];
     int64_t g = 0;
     for (int64_t i = ci[(size_t)c]; i < ci[(size_t)c + 1]; ++i) {
       n_starts[i] = (int64_t)hi[8 + 2 * i];
+      pk[(size_t)i + 1] = pk[(size_t)i] + n_starts[i];
       const int64_t Gi = n_starts[i] - 1 > 0 ? n_starts[i] - 1 : 0;
       gl[(size_t)i] = g;
       chunk_of[(size_t)i] = c;
@@ -1168,6 +1178,8 @@ int64_t batch_device_path(int64_t n_items, const int64_t* item_off, int64_t D, i
       it.G = Gi;
       it.seed = seeds[i];
       it.pad = 0;
+      it.pk = pk[(size_t)i];
+      it.ns = n_starts[i];
       it.term = -1;
       it.dc = 0;
       g += Gi;
@@ -1185,10 +1197,29 @@ int64_t batch_device_path(int64_t n_items, const int64_t* item_off, int64_t D, i
   }
   if ((e = hipMemcpyAsync(itab_d, g_batch_items.data(), (size_t)n_items * sizeof(cwq::BatchItem),
                           hipMemcpyHostToDevice, s)) != hipSuccess ||
-      (e = cwq::launch_batch_layout(itab_d, n_items, dst, offs, bseed, s)) != hipSuccess) {
+      (e = cwq::launch_batch_layout(itab_d, n_items, dst, offs, bseed, pst_d, s)) !=
+          hipSuccess) {
     drain();
     return hip_fail(e, "cwq_code_grouped_greedy_batch: layout");
   }
+  // the items' start lists go to the caller in one copy on d2h, queued behind
+  // the first chunk's coding (one copy per item took ~21 us each, serialised
+  // after the coding: ~1 ms of C3's 48 items; one copy ahead of the first
+  // chunk delayed its coding by the copy's 145 us); the bitcode workers unpack
+  const int64_t npk = pk[(size_t)n_items];
+  if (npk > 0 && (e = hipEventRecord(layout_ev, s)) != hipSuccess) {
+    drain();
+    return hip_fail(e, "cwq_code_grouped_greedy_batch: layout event");
+  }
+  auto starts_copy = [&]() -> hipError_t {
+    hipError_t r = hipSuccess;
+    if (npk > 0 && ((r = hipStreamWaitEvent(d2h, layout_ev, 0)) != hipSuccess ||
+                    (r = hipMemcpyAsync(pstage, pst_d, (size_t)npk * 8, hipMemcpyDeviceToHost,
+                                        d2h)) != hipSuccess ||
+                    (r = hipEventRecord(pst_ev, d2h)) != hipSuccess))
+      return r;
+    return hipSuccess;
+  };
   // the chunks: encode, destandardise, results to the host behind the next chunk
   int64_t Gtot = 0;
   int rc = CWQ_OK;
@@ -1210,12 +1241,10 @@ int64_t batch_device_path(int64_t n_items, const int64_t* item_off, int64_t D, i
         rc = encode_impl(t_loc + a, t_scale + a, zeros + a, ones + a, offs + gb + c, 0, Gc, Dc,
                          cmaxd[(size_t)c], n_bits_per_step, n_steps, 0, rho, 0,
                          idx + gb * n_steps, sample + a, w + l.enc, workspace_bytes - l.enc, &oc,
-                         s, bseed + gb);
+                         s, bseed + gb, out + a, p_loc + a, p_scale + a);  // + :292
       if (rc == CWQ_OK && o.eval_ms_out &&
           (e = hipEventRecord(tev.ev[(size_t)(2 * c + 1)], s)) != hipSuccess)
         rc = hip_fail(e, "event");
-      if (rc == CWQ_OK)  // :292 destandardise
-        rc = cwq_destandardise(sample + a, p_loc + a, p_scale + a, Dc, out + a, s);
     } else if (rc == CWQ_OK && Dc > 0 &&
                (e = hipMemsetAsync(out + a, 0, (size_t)Dc * 4, s)) != hipSuccess) {
       rc = hip_fail(e, "memset");
@@ -1223,6 +1252,8 @@ int64_t batch_device_path(int64_t n_items, const int64_t* item_off, int64_t D, i
     if (rc == CWQ_OK && o.eval_stop_event && c == K - 1 &&
         (e = hipEventRecord((hipEvent_t)o.eval_stop_event, s)) != hipSuccess)
       rc = hip_fail(e, "event");
+    if (rc == CWQ_OK && c == 0 && (e = starts_copy()) != hipSuccess)
+      rc = hip_fail(e, "start lists to host");
     if (rc == CWQ_OK && ((e = hipEventRecord(res_ev[c], s)) != hipSuccess ||
                          (e = hipStreamWaitEvent(d2h, res_ev[c], 0)) != hipSuccess))
       rc = hip_fail(e, "event");
@@ -1239,14 +1270,8 @@ int64_t batch_device_path(int64_t n_items, const int64_t* item_off, int64_t D, i
     if (rc == CWQ_OK) c_done = c + 1;
   }
   lap("enqueued");
-  // the items' start lists to the caller, beside the coding (the partition has
-  // completed: synchronised above)
-  for (int64_t i = 0; i < n_items && rc == CWQ_OK; ++i)
-    if ((e = hipMemcpyAsync(starts_host + item_off[i] + 2 * i, dst + item_off[i] + 2 * i,
-                            (size_t)n_starts[i] * 8, hipMemcpyDeviceToHost, h2d)) != hipSuccess)
-      rc = hip_fail(e, "starts to host");
-  // bitcode (:81-87, :288) item by item as its chunk's indices arrive, on the
-  // host threads and the calling thread
+  // bitcode (:81-87, :288) and start list item by item as its chunk's
+  // indices arrive, on the host threads and the calling thread
   std::atomic<int64_t> next{0};
   std::atomic<int> err{0};
   auto bits_worker = [&]() {
@@ -1255,11 +1280,13 @@ int64_t batch_device_path(int64_t n_items, const int64_t* item_off, int64_t D, i
       if (i >= n_items || err.load()) return;
       const int64_t c = chunk_of[(size_t)i];
       if (c >= c_done) return;
-      if (wait_event(done_ev[c]) != hipSuccess) {
+      if ((npk > 0 && wait_event(pst_ev) != hipSuccess) || wait_event(done_ev[c]) != hipSuccess) {
         int z = 0;
         err.compare_exchange_strong(z, fail(CWQ_ERR_HIP, "results copy failed"));
         return;
       }
+      memcpy(starts_host + item_off[i] + 2 * i, pstage + pk[(size_t)i],
+             (size_t)n_starts[i] * 8);
       const int64_t gb = item_off[ci[(size_t)c]] + ci[(size_t)c];
       const int64_t Gi = n_starts[i] - 1 > 0 ? n_starts[i] - 1 : 0;
       const int64_t nw = write_bitcode(idx_h + (gb + gl[(size_t)i]) * n_steps, Gi * n_steps,
@@ -1451,7 +1478,7 @@ int64_t cwq_code_grouped_greedy_batch(
         n_items, item_off, D, n_steps, n_bits_per_step, seeds, rho, size_threshold, n_nats,
         sample_host, bits_host, bits_cap, bits_off, starts_host, n_starts, w, workspace_bytes, bl,
         o, ci, t_loc, t_scale, kl, zeros, ones, sample, out, offs, idx, bseed, idx_h, evs, tev,
-        p_loc, p_scale, s, d2h, h2d, kl_ready);
+        p_loc, p_scale, s, d2h, h2d, kl_ready, offs_h);
     if (r != kBatchFellBack) return r;
   }
   if ((e = hipEventRecord(kl_ready, s)) == hipSuccess) e = hipStreamWaitEvent(d2h, kl_ready, 0);
@@ -1649,12 +1676,11 @@ int64_t cwq_code_grouped_greedy_batch(
       if (rc == CWQ_OK)
         rc = encode_impl(t_loc + a, t_scale + a, zeros + a, ones + a, offs + gb + c, 0, ch.G, Dc,
                          ch.maxd, n_bits_per_step, n_steps, 0, rho, 0, idx + gb * n_steps,
-                         sample + a, w + l.enc, workspace_bytes - l.enc, &oc, stream, bseed + gb);
+                         sample + a, w + l.enc, workspace_bytes - l.enc, &oc, stream, bseed + gb,
+                         out + a, p_loc + a, p_scale + a);  // + :292 destandardise
       if (rc == CWQ_OK && o.eval_ms_out)
         if ((e = hipEventRecord(tev.ev[(size_t)(2 * c + 1)], s)) != hipSuccess)
           rc = hip_fail(e, "event");
-      if (rc == CWQ_OK)  // :292 destandardise
-        rc = cwq_destandardise(sample + a, p_loc + a, p_scale + a, Dc, out + a, stream);
     } else if (rc == CWQ_OK && Dc > 0) {  // no groups (empty items only): the sample is zeros
       if ((e = hipMemsetAsync(out + a, 0, (size_t)Dc * 4, s)) != hipSuccess)
         rc = hip_fail(e, "memset");

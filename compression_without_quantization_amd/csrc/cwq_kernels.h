@@ -81,6 +81,12 @@ struct EncodeArgs {
   // sab, set by launch_encode) and the dim -> block map [total_dims]
   const float2* pre_ab = nullptr;
   uint32_t* sdmap = nullptr;
+  // grouped pipelines (coded_greedy_sampler.py:292): also ds_out[i] =
+  // ds_scale[i] * sample[i] + ds_loc[i] after the last step, folded into the
+  // small pipeline's finalize where it runs, else one k_destandardise
+  float* ds_out = nullptr;
+  const float* ds_loc = nullptr;
+  const float* ds_scale = nullptr;
 };
 
 #define CWQ_SLIST_PER_BLOCK 8
@@ -127,10 +133,14 @@ bool partition_applies(int64_t D, int64_t size_threshold);
 // offs[term] = dc, the chunk's closing offset (written with the chunk's last item).
 struct BatchItem {
   int64_t src, rel, go, gs, G, term, dc;
+  int64_t pk, ns;  // the item's start list: packed offset and length (pstarts)
   int32_t seed, pad;
 };
+// pstarts (may be nullptr): every item's start list packed back to back, for
+// one device-to-host copy
 hipError_t launch_batch_layout(const BatchItem* items, int64_t n_items, const int64_t* dstarts,
-                               int64_t* offs, int32_t* seeds, hipStream_t stream);
+                               int64_t* offs, int32_t* seeds, int64_t* pstarts,
+                               hipStream_t stream);
 // info_zeroed: info[0..7] (and, single item, iinfo[0..1]) were zeroed on the
 // stream by the caller (launch_grouped_prep); otherwise a memset does it
 hipError_t launch_partition(const float* kl, int64_t D, const int64_t* item_off, int64_t n_items,

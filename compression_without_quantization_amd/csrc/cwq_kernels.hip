@@ -2106,9 +2106,17 @@ struct SmallRec {  // 4 x uint4: q0 = (off lo, off hi, d, state), q1 = stream ke
   uint4 q2, q3;
 };
 static_assert(sizeof(SmallRec) <= 8 * CWQ_SLIST_PER_BLOCK, "a record per block in slist");
-// blocks per k_small_prep1 workgroup of 256 threads: C2's 41.5k blocks make
-// 650 workgroups (with 256 per workgroup 163 of them ran 20 us, latency-bound)
-constexpr int kSmallPrepBlocks = 64;
+// blocks per k_small_prep1 workgroup of CWQ_PREP1_THREADS threads: C2's 41.5k
+// blocks make 650 workgroups (with 256 per workgroup 163 of them ran 20 us,
+// latency-bound)
+#ifndef CWQ_PREP1_BLOCKS
+#define CWQ_PREP1_BLOCKS 64
+#endif
+#ifndef CWQ_PREP1_THREADS
+#define CWQ_PREP1_THREADS 256
+#endif
+constexpr int kSmallPrepBlocks = CWQ_PREP1_BLOCKS;
+static_assert(CWQ_PREP1_BLOCKS <= CWQ_PREP1_THREADS, "a thread per block in the block phase");
 
 // The dims of a launch's blocks: [block_off[0], block_off[nb]) (absolute: a
 // forked part of a launch passes block_off + g0), or [0, nb ud) for uniform blocks
@@ -2122,7 +2130,7 @@ __device__ __forceinline__ void dims_of(const int64_t* __restrict__ block_off, i
 // block sums are LDS atomics in no fixed order, which the bounds' slack (far
 // above double rounding) covers, so the screen stays exact-safe.
 template <bool FIRST>
-__global__ void __launch_bounds__(256) k_small_prep1(
+__global__ void __launch_bounds__(CWQ_PREP1_THREADS) k_small_prep1(
     const float* __restrict__ t_loc, const float* __restrict__ t_scale,
     const float* __restrict__ p_loc, const float* __restrict__ p_scale, float nst, float sdiv,
     float rho, float* __restrict__ loc_s, float* __restrict__ scale_s,
@@ -2130,7 +2138,7 @@ __global__ void __launch_bounds__(256) k_small_prep1(
     int64_t ud, int64_t nb, SeedSpec sd, int32_t step, float2* __restrict__ pre_ab,
     SmallRec* __restrict__ rec, uint32_t* __restrict__ dmap) {
   constexpr int B = kSmallPrepBlocks;
-  constexpr int T = 256;
+  constexpr int T = CWQ_PREP1_THREADS;
   __shared__ int64_t boff[B + 1];
   __shared__ double acc[5][B];  // sum M, sum |M|, sum |M| + M, sum A^2, sum C
   __shared__ uint32_t amx[B], abad[B];
@@ -2467,7 +2475,9 @@ __global__ void __launch_bounds__(256) k_small_finalize(
     const float* __restrict__ loc_s, const float* __restrict__ scale_s,
     const SmallRec* __restrict__ rec, const uint32_t* __restrict__ dmap,
     const int32_t* __restrict__ out_idx, int32_t step, int n_steps,
-    const int64_t* __restrict__ block_off, int64_t ud, int64_t nb, float* __restrict__ best) {
+    const int64_t* __restrict__ block_off, int64_t ud, int64_t nb, float* __restrict__ best,
+    float* __restrict__ ds_out, const float* __restrict__ ds_loc,
+    const float* __restrict__ ds_scale) {
   __shared__ double logtab[32];
   fill_logtab(logtab);
   int64_t d0, d1;
@@ -2483,7 +2493,12 @@ __global__ void __launch_bounds__(256) k_small_finalize(
     const float zz = exact_normal(st, (uint64_t)idx * (uint64_t)d + j, logtab);
     float sv = scale_s[i] * zz;  // misc.py:14
     sv = loc_s[i] + sv;          // misc.py:15
-    best[i] = (STEP0 ? 0.0f : best[i]) + sv;
+    const float b = (STEP0 ? 0.0f : best[i]) + sv;
+    best[i] = b;
+    if (ds_out) {  // :292 destandardise (k_destandardise's arithmetic)
+      const float m = ds_scale[i] * b;
+      ds_out[i] = m + ds_loc[i];
+    }
   }
 }
 
@@ -3260,12 +3275,12 @@ static bool launch_small(const EncodeArgs& a, int step, hipStream_t stream) {
     const float sdiv = (float)__builtin_sqrt((double)a.n_steps);
     const unsigned pgrid = grid_for(a.nb, kSmallPrepBlocks, 1u << 31);
     if (STEP0)
-      hipLaunchKernelGGL(k_small_prep1<true>, dim3(pgrid), dim3(256), 0, stream, a.t_loc,
+      hipLaunchKernelGGL(k_small_prep1<true>, dim3(pgrid), dim3(CWQ_PREP1_THREADS), 0, stream, a.t_loc,
                          a.t_scale, a.p_loc, a.p_scale, nst, sdiv, a.rho, a.loc_s, a.scale_s,
                          a.lognorm, a.out_sample, a.block_off, a.ud, a.nb, seeds_of(a), step,
                          pab, rec, a.sdmap);
     else
-      hipLaunchKernelGGL(k_small_prep1<false>, dim3(pgrid), dim3(256), 0, stream, a.t_loc,
+      hipLaunchKernelGGL(k_small_prep1<false>, dim3(pgrid), dim3(CWQ_PREP1_THREADS), 0, stream, a.t_loc,
                          a.t_scale, a.p_loc, a.p_scale, nst, sdiv, a.rho, a.loc_s, a.scale_s,
                          a.lognorm, a.out_sample, a.block_off, a.ud, a.nb, seeds_of(a), step,
                          pab, rec, a.sdmap);
@@ -3279,7 +3294,8 @@ static bool launch_small(const EncodeArgs& a, int step, hipStream_t stream) {
     const unsigned dgrid = grid_for(a.total_dims > a.nb ? a.total_dims : a.nb, 256, 16384);
     hipLaunchKernelGGL((k_small_finalize<STEP0>), dim3(dgrid), dim3(256), 0, stream, a.loc_s,
                        a.scale_s, rec, a.sdmap, a.out_idx, step, a.n_steps, a.block_off, a.ud,
-                       a.nb, a.out_sample);
+                       a.nb, a.out_sample, step == a.n_steps - 1 ? a.ds_out : nullptr, a.ds_loc,
+                       a.ds_scale);
     return true;
   }
   const int64_t ntiles = a.nb * a.tiles_per_block;
@@ -3463,11 +3479,22 @@ hipError_t launch_encode(const EncodeArgs& a_in, hipStream_t stream) {
                          a.scale_s, a.lognorm, a.out_sample, a.keys, a.nb, stream);
   if (e != hipSuccess) return e;
   if (a.nb == 0) return hipSuccess;
+  // :292 destandardise after the last step: the small pipeline's finalize
+  // does it, anything else one k_destandardise on the caller's stream
+  const bool ds_after = a.ds_out != nullptr && !takes_small_pipe(a);
+  auto ds = [&]() -> hipError_t {
+    if (!ds_after) return hipSuccess;
+    return launch_destandardise(a.out_sample, a.ds_loc, a.ds_scale, a.total_dims, a.ds_out,
+                                stream);
+  };
   ForkStreams* f = (CWQ_ENCODE_SPLIT > 1 && a.block_off != nullptr && a.n_steps > 1 &&
                     a.nb >= 2)
                        ? fork_streams(stream)
                        : nullptr;
-  if (f == nullptr) return encode_steps(a, stream, true);
+  if (f == nullptr) {
+    if ((e = encode_steps(a, stream, true)) != hipSuccess) return e;
+    return ds();
+  }
   // k parts of the block range: block-indexed arrays move by g0, the padded
   // per-block regions of the general kernel by 8 g0 / 12 g0 (their layout is
   // off + 8 g / off + 12 g with absolute dim offsets off).  Launches of few
@@ -3517,7 +3544,7 @@ hipError_t launch_encode(const EncodeArgs& a_in, hipStream_t stream) {
   }
   if (e != hipSuccess) return e;
   if (a.ev_stop && (e = hipEventRecord((hipEvent_t)a.ev_stop, stream)) != hipSuccess) return e;
-  return hipSuccess;
+  return ds();
 }
 
 hipError_t launch_decode(const int32_t* idx, const float* p_loc, const float* p_scale,

@@ -435,23 +435,28 @@ __global__ void __launch_bounds__(256) k_part_ibody(int64_t D, const int64_t* __
 __global__ void __launch_bounds__(256) k_batch_layout(const BatchItem* __restrict__ items,
                                                       const int64_t* __restrict__ dstarts,
                                                       int64_t* __restrict__ offs,
-                                                      int32_t* __restrict__ seeds) {
+                                                      int32_t* __restrict__ seeds,
+                                                      int64_t* __restrict__ pstarts) {
   const BatchItem it = items[blockIdx.x];  // item blockIdx.x, slice blockIdx.y of its groups
   const int64_t step = (int64_t)blockDim.x * gridDim.y;
   for (int64_t g = (int64_t)blockIdx.y * blockDim.x + threadIdx.x; g < it.G; g += step) {
     offs[it.go + g] = it.rel + dstarts[it.src + g];
     seeds[it.gs + g] = (int32_t)((uint32_t)it.seed + (uint32_t)g);  // :282, int32 wrap
   }
+  if (pstarts)
+    for (int64_t g = (int64_t)blockIdx.y * blockDim.x + threadIdx.x; g < it.ns; g += step)
+      pstarts[it.pk + g] = dstarts[it.src + g];
   if (blockIdx.y == 0 && threadIdx.x == 0 && it.term >= 0) offs[it.term] = it.dc;
 }
 
 hipError_t launch_batch_layout(const BatchItem* items, int64_t n_items, const int64_t* dstarts,
-                               int64_t* offs, int32_t* seeds, hipStream_t stream) {
+                               int64_t* offs, int32_t* seeds, int64_t* pstarts,
+                               hipStream_t stream) {
   if (n_items <= 0) return hipSuccess;
   // enough workgroups to fill the chip whatever the item count (48 C3 items: 16 each)
   const unsigned ys = n_items >= 2048 ? 1u : (unsigned)((2048 + n_items - 1) / n_items);
   hipLaunchKernelGGL(k_batch_layout, dim3((unsigned)n_items, ys > 64 ? 64u : ys), dim3(256), 0,
-                     stream, items, dstarts, offs, seeds);
+                     stream, items, dstarts, offs, seeds, pstarts);
   return hipGetLastError();
 }
 
