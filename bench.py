@@ -562,9 +562,18 @@ def pln_main(args):
     tmp = tempfile.mkdtemp()
     paths = [os.path.join(tmp, f"img{i}.miracle") for i in range(n_img)]
 
+    # the first compress (a warmup one when --warmup > 0) captures image 0's
+    # coder inputs, results and scoring-launch milliseconds: the roofline
+    # prices those launches, the CPU oracle codes the same latents (parity).
+    # Capturing inside a compress that runs anyway keeps a `--steps 1
+    # --warmup 0` PMC pass at exactly one compress per step.
+    cap = {}
+
     def compress():
-        return [model.code_image_greedy(None, im, 42, comp_file_path=p, **kw)[1]
-                for im, p in zip(imgs, paths)]
+        c = None if cap else cap
+        return [model.code_image_greedy(None, im, 42, comp_file_path=p,
+                                        capture=(c if i == 0 else None), **kw)[1]
+                for i, (im, p) in enumerate(zip(imgs, paths))]
 
     def decompress():
         return [model.decode_image_greedy(None, p, use_importance_sampling=kw[
@@ -584,12 +593,6 @@ def pln_main(args):
         rec = decompress()
     torch.cuda.synchronize()
     eld = time.perf_counter() - t0
-    # one more (untimed) compress of image 0 capturing each level's coder
-    # inputs, results and scoring-launch milliseconds: the roofline prices
-    # those launches, the CPU oracle codes the same latents (parity)
-    cap = {}
-    model.code_image_greedy(None, imgs[0], 42, comp_file_path=paths[0], capture=cap, **kw)
-    torch.cuda.synchronize()
     l1, l2 = cap["level1"], cap["level2"]
     D1, D2 = l1["q_loc"].size, l2["q_loc"].size
     G1, G2 = len(l1["result"][2]) - 1, len(l2["result"][2]) - 1
@@ -597,7 +600,7 @@ def pln_main(args):
     alg = (20 * D1 + (4 * kw["n_steps"] if greedy1 else 8) * G1) + (20 * D2 + 8 * G2)
     kernel_ms = float(sum(cap["scoring_ms"]))
     roofline = scoring_roofline(
-        args.config, G1 + G2, alg, kernel_ms, 0,
+        args.config, (G1 + G2) * n_img, alg, kernel_ms, 0,
         ("level 1: " + ("k_csr_prep + k_encode_prune_csr (+ finalize), 30 x 14 bits"
                         if greedy1 else "k_imp_* (importance, 20 bits/group)") +
          "; level 2: k_imp_* (importance, 20 bits/group)"),
@@ -614,7 +617,8 @@ def pln_main(args):
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": el / args.steps * 1e3,
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
             "data": "synthetic image, seeded random PLN weights (no checkpoint offline)",
-            "config": {"workload": desc, "decompress_images_per_s": n_img * args.steps / eld,
+            "config": {"workload": desc, "groups_per_step": (G1 + G2) * n_img,
+                       "decompress_images_per_s": n_img * args.steps / eld,
                        "bytes": summ[0]["actual_byte_size"], "bpp": summ[0]["bpp"],
                        "kl_bits_level1": summ[0]["first_level_theoretical"] * 8,
                        "kl_bits_level2": summ[0]["second_level_theoretical"] * 8,

@@ -638,14 +638,32 @@ thread_local std::vector<float> g_kl_host;
 thread_local std::vector<int32_t> g_idx_host;
 // the device partition's info[8], then item 0's (G + 1, largest): pinned, so the
 // copy is a direct DMA (pageable memory is staged), per thread
+// A thread's page-locked buffer, freed when the thread ends (the main
+// thread's at exit, before the HIP runtime's own teardown)
+struct PinnedTl {
+  void* p = nullptr;
+  size_t n = 0;
+  void* get(size_t bytes, size_t want) {
+    if (n < bytes) {
+      if (p) (void)hipHostFree(p);
+      p = nullptr;
+      n = 0;
+      if (hipHostMalloc(&p, want, hipHostMallocDefault) != hipSuccess) {
+        p = nullptr;
+        return nullptr;
+      }
+      n = want;
+    }
+    return p;
+  }
+  ~PinnedTl() {
+    if (p) (void)hipHostFree(p);
+  }
+};
 unsigned long long* part_info_host() {
-  thread_local unsigned long long* p = [] {
-    void* q = nullptr;
-    if (hipHostMalloc(&q, 16 * sizeof(unsigned long long), hipHostMallocDefault) != hipSuccess)
-      q = nullptr;
-    return (unsigned long long*)q;
-  }();
-  return p;
+  thread_local PinnedTl b;
+  constexpr size_t kBytes = 16 * sizeof(unsigned long long);
+  return (unsigned long long*)b.get(kBytes, kBytes);
 }
 // CWQ_HOST_PARTITION=1: the host partition loop even where the device one
 // applies (A/B timing; the results are identical)
@@ -1067,23 +1085,8 @@ thread_local std::vector<char> g_batch_host;
 // page-locked per-thread buffer of at least `bytes` (the batch partition's
 // info; pageable memory would be staged), nullptr when allocation fails
 void* pinned_tl(size_t bytes) {
-  struct Buf {
-    void* p = nullptr;
-    size_t n = 0;
-  };
-  thread_local Buf b;
-  if (b.n < bytes) {
-    if (b.p) (void)hipHostFree(b.p);
-    b.p = nullptr;
-    b.n = 0;
-    const size_t want = bytes < 4096 ? 4096 : bytes * 2;
-    if (hipHostMalloc(&b.p, want, hipHostMallocDefault) != hipSuccess) {
-      b.p = nullptr;
-      return nullptr;
-    }
-    b.n = want;
-  }
-  return b.p;
+  thread_local PinnedTl b;
+  return b.get(bytes, bytes < 4096 ? 4096 : bytes * 2);
 }
 thread_local std::vector<cwq::BatchItem> g_batch_items;
 

@@ -1995,6 +1995,20 @@ __global__ void __launch_bounds__(256) k_small_survivors(
 #ifndef CWQ_FUSED_WAVES
 #define CWQ_FUSED_WAVES 8
 #endif
+#ifndef CWQ_SMALL_RARE
+#define CWQ_SMALL_RARE 1  // k_small_one leaves blocks needing exact values to k_small_rare
+#endif
+#ifndef CWQ_RARE_GRID
+#define CWQ_RARE_GRID 1024  // k_small_rare's waves
+#endif
+#ifndef CWQ_ONE_GRID
+#define CWQ_ONE_GRID 0  // k_small_one workgroups, each striding the blocks (0: one per block)
+#endif
+#ifndef CWQ_ONE_WPG
+#define CWQ_ONE_WPG 1  // waves (blocks) per k_small_one workgroup
+#endif
+static_assert(CWQ_ONE_WPG >= 1 && (CWQ_ONE_WPG & (CWQ_ONE_WPG - 1)) == 0 && CWQ_ONE_WPG <= 16,
+              "k_small_one: a power-of-two number of waves per workgroup (launch_small's chunks)");
 static_assert(CWQ_FUSED_STAGE >= CWQ_FUSED_DMAX, "an exact batch holds at least one row");
 static_assert(CWQ_FUSED_LIST <= 64, "one listed row per lane");
 
@@ -2091,15 +2105,17 @@ __device__ unsigned int g_quad_info[kQuadTimes][4];
 // at falling occupancy, and 35% of a quad's time went to its constants phase
 // (per-block f64 sums and bounds on 16-lane rows, DPP reductions, the stream
 // key).  Here the per-block work runs lane-parallel before the screen, and
-// the screen runs a block at a time on persistent waves fed by a counter:
-//   k_small_prep1     a workgroup per 256 blocks, a thread per dim: the shard
-//                     constants (step 0, k_prep_dims' arithmetic) and each
-//                     dim's screening constants (csr_dim), summed per block
-//                     in LDS; then a thread per block: bounds, stream key ->
-//                     a 64-byte record; dim -> block map; zeroes the counter
-//   k_small_one       persistent waves, a block at a time from the counter:
+// the screen runs a wave per block:
+//   k_small_prep1     a workgroup per CWQ_PREP1_BLOCKS blocks, a thread per
+//                     dim: the shard constants (step 0, k_prep_dims'
+//                     arithmetic) and each dim's screening constants
+//                     (csr_dim), summed per block in LDS; then a thread per
+//                     block: bounds, stream key -> a 64-byte record; the
+//                     dim -> block map
+//   k_small_one       a wave per block (CWQ_ONE_WPG waves per workgroup):
 //                     screen, exact survivors -> index
-//   k_small_finalize  a thread per dim: best += the winning row (:63)
+//   k_small_finalize  a thread per dim: best += the winning row (:63), and
+//                     at the last step the destandardised sample (:292)
 // ---------------------------------------------------------------------------
 struct SmallRec {  // 4 x uint4: q0 = (off lo, off hi, d, state), q1 = stream key,
   uint4 q0, q1;    // q2 = (bf, c1, c2, As), q3 = (Pq, -, -, -)
@@ -2136,7 +2152,7 @@ __global__ void __launch_bounds__(CWQ_PREP1_THREADS) k_small_prep1(
     float rho, float* __restrict__ loc_s, float* __restrict__ scale_s,
     float* __restrict__ lognorm, float* __restrict__ best, const int64_t* __restrict__ block_off,
     int64_t ud, int64_t nb, SeedSpec sd, int32_t step, float2* __restrict__ pre_ab,
-    SmallRec* __restrict__ rec, uint32_t* __restrict__ dmap) {
+    SmallRec* __restrict__ rec, uint32_t* __restrict__ dmap, uint32_t* __restrict__ rare) {
   constexpr int B = kSmallPrepBlocks;
   constexpr int T = CWQ_PREP1_THREADS;
   __shared__ int64_t boff[B + 1];
@@ -2145,6 +2161,7 @@ __global__ void __launch_bounds__(CWQ_PREP1_THREADS) k_small_prep1(
   const int t = threadIdx.x;
   const int64_t g0 = (int64_t)blockIdx.x * B;
   const int n = (int)(nb - g0 < B ? nb - g0 : B);
+  if (blockIdx.x == 0 && t == 0) rare[0] = 0u;  // k_small_one's rare list, empty
   for (int k = t; k <= n; k += T) boff[k] = block_off ? block_off[g0 + k] : (g0 + k) * ud;
   if (t < B) {
     for (int k = 0; k < 5; ++k) acc[k][t] = 0.0;
@@ -2274,30 +2291,28 @@ CWQ_RARE unsigned long long small_listed_exact(
 // C3 (C3's scoring 1.11-1.20 ms per step in all five);
 // longest blocks first (a counting sort by d), 41 us against 47 but the sort
 // cost a launch and a histogram that needed zeroing.
-template <bool STEP0>
-__global__ void __launch_bounds__(64, CWQ_FUSED_WAVES) k_small_one(
-    const float* __restrict__ t_loc, const float* __restrict__ t_scale,
+// One block of the screen (a wave): FULL scores the listed rows / the whole
+// block exactly where the screen leaves more than one candidate (the two
+// out-of-line paths); otherwise such a block goes on the rare list (rare[0]
+// the count, rare[1..] block numbers) for k_small_rare, so k_small_one makes
+// no calls: without them it needs 32 VGPRs and no scratch (the calls' ABI took
+// 64 and 496 B/lane of scratch)
+template <bool STEP0, bool FULL>
+__device__ __forceinline__ void small_block(
+    const int64_t g, const float* __restrict__ t_loc, const float* __restrict__ t_scale,
     const float* __restrict__ loc_s, const float* __restrict__ scale_s,
     const float* __restrict__ lognorm, const float* __restrict__ best,
-    const SmallRec* __restrict__ rec, const float2* __restrict__ pre_ab, int64_t nb, int64_t u0,
-    int64_t n_cand, int32_t step, int n_steps, int32_t* __restrict__ out_idx) {
-  __shared__ double logtab[32];
-  // the block's (sA, sB) repeated 4 times: a lane's span of 4 rows is 4 d
-  // normals, so Philox block b covers abx[4 b .. 4 b + 3] (two b128 reads,
-  // issued ahead of the Philox rounds that hide their latency)
-  __shared__ float4 abx[2 * CWQ_FUSED_DMAX];
-  __shared__ uint32_t ln[CWQ_FUSED_LIST];
-  __shared__ float lu[CWQ_FUSED_LIST];
-  __shared__ float lpv[CWQ_FUSED_STAGE];
-  __shared__ unsigned long long kmax;
+    const SmallRec* __restrict__ rec, const float2* __restrict__ pre_ab, int64_t n_cand,
+    int32_t step, int n_steps, int32_t* __restrict__ out_idx, uint32_t* __restrict__ rare,
+    double* logtab, float4* abx, uint32_t* ln, float* lu, float* lpv,
+    unsigned long long& kmax) {
   const uint32_t lane = threadIdx.x & 63u;
-  if (lane < 32) logtab[lane] = kLogTabConst[lane];
   auto ufirst = [](uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); };
   auto ffirst = [&](uint32_t v) { return u2f(ufirst(v)); };
-  const int64_t g = u0 + blockIdx.x;
   {
 #ifdef CWQ_QUAD_TIMES  // tools/quad_times.py --one: per block start, after the screen, end
-    if (lane == 0u && g < kQuadTimes) g_quad_t[g][0] = __builtin_amdgcn_s_memrealtime();
+    constexpr bool kTimes = !(FULL && CWQ_SMALL_RARE);  // k_small_one's launch only
+    if (kTimes && lane == 0u && g < kQuadTimes) g_quad_t[g][0] = __builtin_amdgcn_s_memrealtime();
 #endif
     const uint4 q0 = rec[g].q0, q1 = rec[g].q1;
     const int64_t off = (int64_t)(((uint64_t)ufirst(q0.y) << 32) | ufirst(q0.x));
@@ -2429,7 +2444,7 @@ __global__ void __launch_bounds__(64, CWQ_FUSED_WAVES) k_small_one(
       }
     }
 #ifdef CWQ_QUAD_TIMES
-    if (lane == 0u && g < kQuadTimes) {
+    if (kTimes && lane == 0u && g < kQuadTimes) {
       g_quad_t[g][1] = __builtin_amdgcn_s_memrealtime();
       g_quad_info[g][0] = (uint32_t)__builtin_amdgcn_s_getreg((4) | (0 << 6) | ((32 - 1) << 11));
       g_quad_info[g][1] = (uint32_t)__builtin_amdgcn_s_getreg((20) | (0 << 6) | ((4 - 1) << 11));
@@ -2437,36 +2452,117 @@ __global__ void __launch_bounds__(64, CWQ_FUSED_WAVES) k_small_one(
       g_quad_info[g][3] = (state == kQuadExact ? 1u : 0u) | ((uint32_t)db << 8);
     }
 #endif
-    if (state == kQuadListed && used > 0) {  // rare (C2: 0.6% of the blocks): out of line
-      const unsigned long long bk = small_listed_exact<STEP0>(
-          off, db, sb, used, ln, lpv, logtab, t_loc, t_scale, loc_s, scale_s, lognorm, best);
-      if (lane == 0) kmax = bk;
-      wave_lds_sync();
-    }
-    if (state == kQuadExact) {  // every candidate exactly (constants outside the gate, list full)
-      QuadBlk r;
-      r.off = off;
-      r.d = (uint32_t)db;
-      r.k0 = sb.k0;
-      r.k1 = sb.k1;
-      r.c2 = sb.c2;
-      r.c3 = sb.c3;
-      const unsigned long long bk = quad_exact_block<STEP0>(r, t_loc, t_scale, loc_s, scale_s,
-                                                             lognorm, best, n_cand, logtab);
-      if (lane == 0) kmax = bk;
-      wave_lds_sync();
-    }
-    if (state != kQuadKnown) {  // ArgMaxTupleReducer: a key at the clamp level is index 0
-      const unsigned long long kb = kmax;
-      idx = (kb >> 32) > kArgmaxClampOrd ? argmax_key_index(kb) : 0u;
+    if (!FULL) {
+      if (state != kQuadKnown) {  // exact values needed: k_small_rare's (C2: 0.2% of the blocks)
+        if (lane == 0) rare[1 + atomicAdd(rare, 1u)] = (uint32_t)g;
+#ifdef CWQ_QUAD_TIMES
+        if (lane == 0u && g < kQuadTimes)
+          g_quad_t[g][2] = g_quad_t[g][3] = g_quad_t[g][4] = g_quad_t[g][5] =
+              __builtin_amdgcn_s_memrealtime();
+#endif
+        return;
+      }
+    } else {
+      if (state == kQuadListed && used > 0) {  // the listed rows' exact values
+        const unsigned long long bk = small_listed_exact<STEP0>(
+            off, db, sb, used, ln, lpv, logtab, t_loc, t_scale, loc_s, scale_s, lognorm, best);
+        if (lane == 0) kmax = bk;
+        wave_lds_sync();
+      }
+      if (state == kQuadExact) {  // every candidate exactly (constants outside the gate, list full)
+        QuadBlk r;
+        r.off = off;
+        r.d = (uint32_t)db;
+        r.k0 = sb.k0;
+        r.k1 = sb.k1;
+        r.c2 = sb.c2;
+        r.c3 = sb.c3;
+        const unsigned long long bk = quad_exact_block<STEP0>(r, t_loc, t_scale, loc_s, scale_s,
+                                                               lognorm, best, n_cand, logtab);
+        if (lane == 0) kmax = bk;
+        wave_lds_sync();
+      }
+      if (state != kQuadKnown) {  // ArgMaxTupleReducer: a key at the clamp level is index 0
+        const unsigned long long kb = kmax;
+        idx = (kb >> 32) > kArgmaxClampOrd ? argmax_key_index(kb) : 0u;
+      }
     }
     if (lane == 0) out_idx[g * n_steps + step] = (int32_t)idx;
 #ifdef CWQ_QUAD_TIMES
-    if (lane == 0u && g < kQuadTimes)
+    if (kTimes && lane == 0u && g < kQuadTimes)
       g_quad_t[g][2] = g_quad_t[g][3] = g_quad_t[g][4] = g_quad_t[g][5] =
           __builtin_amdgcn_s_memrealtime();
 #endif
   }
+}
+
+
+template <bool STEP0>
+__global__ void __launch_bounds__(64 * CWQ_ONE_WPG, CWQ_FUSED_WAVES) k_small_one(
+    const float* __restrict__ t_loc, const float* __restrict__ t_scale,
+    const float* __restrict__ loc_s, const float* __restrict__ scale_s,
+    const float* __restrict__ lognorm, const float* __restrict__ best,
+    const SmallRec* __restrict__ rec, const float2* __restrict__ pre_ab, int64_t nb, int64_t u0,
+    int64_t n_cand, int32_t step, int n_steps, int32_t* __restrict__ out_idx,
+    uint32_t* __restrict__ rare) {
+  // every wave of the workgroup its own block and its own LDS (no barrier
+  // between the waves: a wave whose block is past nb just ends)
+  constexpr int W = CWQ_ONE_WPG;
+  __shared__ double logtab_w[W][32];
+  // the block's (sA, sB) repeated 4 times: a lane's span of 4 rows is 4 d
+  // normals, so Philox block b covers abx[4 b .. 4 b + 3] (two b128 reads,
+  // issued ahead of the Philox rounds that hide their latency)
+  __shared__ float4 abx_w[W][2 * CWQ_FUSED_DMAX];
+  __shared__ uint32_t ln_w[W][CWQ_FUSED_LIST];
+  __shared__ float lu_w[W][CWQ_FUSED_LIST];
+  __shared__ float lpv_w[W][CWQ_SMALL_RARE ? 1 : CWQ_FUSED_STAGE];
+  __shared__ unsigned long long kmax_w[W];
+  const int wv = W == 1 ? 0 : (int)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const uint32_t lane = threadIdx.x & 63u;
+  const int64_t g = u0 + (int64_t)blockIdx.x * W + wv;
+  if (W > 1 && g >= nb) return;
+  if (lane < 32) logtab_w[wv][lane] = kLogTabConst[lane];
+#if CWQ_ONE_GRID
+  // a fixed grid, each wave striding the chunk's blocks
+  const int64_t u1 = nb - u0 < (1LL << 30) ? nb : u0 + (1LL << 30);
+  for (int64_t gg = g; gg < u1; gg += (int64_t)gridDim.x * W)
+    small_block<STEP0, !CWQ_SMALL_RARE>(gg, t_loc, t_scale, loc_s, scale_s, lognorm, best, rec,
+                                        pre_ab, n_cand, step, n_steps, out_idx, rare,
+                                        logtab_w[wv], abx_w[wv], ln_w[wv], lu_w[wv], lpv_w[wv],
+                                        kmax_w[wv]);
+#else
+  small_block<STEP0, !CWQ_SMALL_RARE>(g, t_loc, t_scale, loc_s, scale_s, lognorm, best, rec,
+                                      pre_ab, n_cand, step, n_steps, out_idx, rare,
+                                      logtab_w[wv], abx_w[wv], ln_w[wv], lu_w[wv], lpv_w[wv],
+                                      kmax_w[wv]);
+#endif
+}
+
+// The blocks k_small_one put on the rare list: the same screen again (the same
+// list), then the exact scoring of the listed rows or of the whole block.  A
+// wave per listed block; the grid's waves stride the list, whose length only
+// the device knows.
+template <bool STEP0>
+__global__ void __launch_bounds__(64) k_small_rare(
+    const float* __restrict__ t_loc, const float* __restrict__ t_scale,
+    const float* __restrict__ loc_s, const float* __restrict__ scale_s,
+    const float* __restrict__ lognorm, const float* __restrict__ best,
+    const SmallRec* __restrict__ rec, const float2* __restrict__ pre_ab, int64_t n_cand,
+    int32_t step, int n_steps, int32_t* __restrict__ out_idx, uint32_t* __restrict__ rare) {
+  __shared__ double logtab[32];
+  __shared__ float4 abx[2 * CWQ_FUSED_DMAX];
+  __shared__ uint32_t ln[CWQ_FUSED_LIST];
+  __shared__ float lu[CWQ_FUSED_LIST];
+  __shared__ float lpv[CWQ_FUSED_STAGE];
+  __shared__ unsigned long long kmax;
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t n = rare[0];
+  if (blockIdx.x >= n) return;
+  if (lane < 32) logtab[lane] = kLogTabConst[lane];
+  for (uint32_t i = blockIdx.x; i < n; i += gridDim.x)
+    small_block<STEP0, true>((int64_t)rare[1 + i], t_loc, t_scale, loc_s, scale_s, lognorm, best,
+                             rec, pre_ab, n_cand, step, n_steps, out_idx, rare, logtab, abx, ln,
+                             lu, lpv, kmax);
 }
 
 // A thread per dim of [d0, d0 + n): best += the winning row of its block (:63)
@@ -3258,7 +3354,7 @@ static bool takes_small_path(const EncodeArgs& a) {  // launch_small's d <= 64 s
          a.max_d <= CWQ_FUSED_DMAX && a.n_cand < 4096;
 }
 static bool small_pipe_ok(const EncodeArgs& a) {  // ... and the pipeline's arrays are there
-  return a.sdmap && a.sab && a.slist && a.nb < (1LL << 32);
+  return a.sdmap && a.sab && a.slist && a.ordu && a.nb < (1LL << 32);
 }
 static bool takes_small_pipe(const EncodeArgs& a) {
   return CWQ_SMALL_PIPE && takes_small_path(a) && small_pipe_ok(a);
@@ -3278,19 +3374,30 @@ static bool launch_small(const EncodeArgs& a, int step, hipStream_t stream) {
       hipLaunchKernelGGL(k_small_prep1<true>, dim3(pgrid), dim3(CWQ_PREP1_THREADS), 0, stream, a.t_loc,
                          a.t_scale, a.p_loc, a.p_scale, nst, sdiv, a.rho, a.loc_s, a.scale_s,
                          a.lognorm, a.out_sample, a.block_off, a.ud, a.nb, seeds_of(a), step,
-                         pab, rec, a.sdmap);
+                         pab, rec, a.sdmap, a.ordu);
     else
       hipLaunchKernelGGL(k_small_prep1<false>, dim3(pgrid), dim3(CWQ_PREP1_THREADS), 0, stream, a.t_loc,
                          a.t_scale, a.p_loc, a.p_scale, nst, sdiv, a.rho, a.loc_s, a.scale_s,
                          a.lognorm, a.out_sample, a.block_off, a.ud, a.nb, seeds_of(a), step,
-                         pab, rec, a.sdmap);
+                         pab, rec, a.sdmap, a.ordu);
     const int64_t nu = a.nb;
-    for (int64_t u0 = 0; u0 < nu; u0 += (int64_t)1 << 30)
-      hipLaunchKernelGGL((k_small_one<STEP0>),
-                         dim3((unsigned)(nu - u0 < (1LL << 30) ? nu - u0 : (1LL << 30))),
-                         dim3(64), 0, stream, a.t_loc, a.t_scale, a.loc_s, a.scale_s, a.lognorm,
+    for (int64_t u0 = 0; u0 < nu; u0 += (int64_t)1 << 30) {
+      int64_t nw = ((nu - u0 < (1LL << 30) ? nu - u0 : (1LL << 30)) + CWQ_ONE_WPG - 1) /
+                   CWQ_ONE_WPG;
+      if (CWQ_ONE_GRID && nw > CWQ_ONE_GRID) nw = CWQ_ONE_GRID;
+      hipLaunchKernelGGL((k_small_one<STEP0>), dim3((unsigned)nw),
+                         dim3(64 * CWQ_ONE_WPG), 0, stream, a.t_loc, a.t_scale, a.loc_s, a.scale_s, a.lognorm,
                          a.out_sample, rec, a.pre_ab, a.nb, u0, a.n_cand, step, a.n_steps,
-                         a.out_idx);
+                         a.out_idx, a.ordu);
+    }
+    // the rare list (a.ordu: the pipeline leaves that scratch unused; a forked
+    // part's view is its own)
+    if (CWQ_SMALL_RARE)
+      hipLaunchKernelGGL((k_small_rare<STEP0>),
+                         dim3((unsigned)(a.nb < CWQ_RARE_GRID ? a.nb : CWQ_RARE_GRID)), dim3(64),
+                         0, stream, a.t_loc, a.t_scale, a.loc_s, a.scale_s, a.lognorm,
+                         a.out_sample, rec, a.pre_ab, a.n_cand, step, a.n_steps, a.out_idx,
+                         a.ordu);
     const unsigned dgrid = grid_for(a.total_dims > a.nb ? a.total_dims : a.nb, 256, 16384);
     hipLaunchKernelGGL((k_small_finalize<STEP0>), dim3(dgrid), dim3(256), 0, stream, a.loc_s,
                        a.scale_s, rec, a.sdmap, a.out_idx, step, a.n_steps, a.block_off, a.ud,

@@ -24,8 +24,11 @@
 //                 by their stored ex of the entry), then the walk's nodes in
 //                 the chunk marked by pointer jumping in LDS, counted and
 //                 compacted;
-//   k_part_emit   per chunk: the global rank of its first node (sum of the
-//                 earlier chunks' counts), the walk's nodes in rank order (one
+//   k_part_emit   per chunk: the global rank of its first node (the earlier
+//                 superchunks' sums, which k_part_mark adds its count to, plus
+//                 the earlier chunks of its own superchunk of kPartSuper: per
+//                 chunk O(nch / kPartSuper + kPartSuper) loads, not O(nch)),
+//                 the walk's nodes in rank order (one
 //                 item: straight into its start list, with its largest group,
 //                 and the two launches below are skipped);
 //   k_part_ihdr / k_part_ibody  per item: its nodes (a rank range found by
@@ -50,6 +53,7 @@ constexpr int kPartMaxJump = 512;   // longest group the device path takes
 constexpr int kPartRun = 8;         // non-converged chunks a walk may cross
 constexpr int kPartThreads = 256;
 constexpr int kPartLdsItems = 1024;  // batches up to this many items search offsets in LDS
+constexpr int kPartSuper = 256;      // chunks per superchunk (k_part_mark's sums)
 
 // info[0] nodes on the walk, info[2] fallback flag, info[4] a jump nxt(i) - i
 // above kPartMaxJump (the fallback; 0 when there is none).  Per item k: iinfo[2k] its starts (G + 1),
@@ -73,7 +77,8 @@ __global__ void __launch_bounds__(256) k_part_next(const float* __restrict__ kl,
                                                    const int64_t* __restrict__ item_off,
                                                    int64_t n_items, int64_t T, float thr,
                                                    int32_t* __restrict__ nxt,
-                                                   unsigned long long* __restrict__ info) {
+                                                   unsigned long long* __restrict__ info,
+                                                   int32_t* __restrict__ sup, int64_t nsup) {
   __shared__ int32_t red[256];
   // the workgroup's 256 dims and the kPartMaxJump after them, staged in LDS
   // (coalesced): each thread's scan then reads LDS instead of a chain of
@@ -82,6 +87,7 @@ __global__ void __launch_bounds__(256) k_part_next(const float* __restrict__ kl,
   __shared__ int64_t soff[kPartLdsItems + 1];
   const int64_t b = (int64_t)blockIdx.x * blockDim.x;
   const int64_t i = b + threadIdx.x;
+  if (i < nsup) sup[i] = 0;  // k_part_mark's superchunk sums (D >= nsup threads)
   for (int t = threadIdx.x; t < 256 + kPartMaxJump + 1; t += 256)
     skl[t] = b + t < D ? kl[b + t] : 0.0f;
   // a batch's item offsets in LDS too (the binary search per dim is a chain of
@@ -187,7 +193,8 @@ __global__ void __launch_bounds__(256) k_part_mark(const int32_t* __restrict__ n
                                                    const int32_t* __restrict__ conv,
                                                    int32_t* __restrict__ node,
                                                    int32_t* __restrict__ cnt,
-                                                   unsigned long long* __restrict__ info) {
+                                                   unsigned long long* __restrict__ info,
+                                                   int32_t* __restrict__ sup) {
   __shared__ int32_t ja[kPartW], jb[kPartW];
   __shared__ uint8_t mark[kPartW];
   __shared__ int32_t red[kPartThreads];
@@ -268,7 +275,10 @@ __global__ void __launch_bounds__(256) k_part_mark(const int32_t* __restrict__ n
     const int l = threadIdx.x * kPer + q;
     if (l < n && mark[l]) node[b + at++] = (int32_t)(b + l);
   }
-  if (threadIdx.x == kPartThreads - 1) cnt[c] = red[threadIdx.x];
+  if (threadIdx.x == kPartThreads - 1) {
+    cnt[c] = red[threadIdx.x];
+    if (red[threadIdx.x]) atomicAdd(&sup[c / kPartSuper], red[threadIdx.x]);
+  }
 }
 
 // SINGLE (one item, no item_off): the chunk's nodes go straight to the start
@@ -278,6 +288,7 @@ template <bool SINGLE>
 __global__ void __launch_bounds__(256) k_part_emit(int64_t nchunks,
                                                    const int32_t* __restrict__ node,
                                                    const int32_t* __restrict__ cnt,
+                                                   const int32_t* __restrict__ sup,
                                                    int32_t* __restrict__ gnode,
                                                    unsigned long long* __restrict__ info,
                                                    const float* __restrict__ kl, int64_t D,
@@ -290,9 +301,12 @@ __global__ void __launch_bounds__(256) k_part_emit(int64_t nchunks,
   if (info[4] > (unsigned long long)kPartMaxJump || info[2]) return;
   const int64_t c = blockIdx.x;
   const int64_t b = c * kPartW;
-  // rank of the chunk's first node: the earlier chunks' counts
+  // rank of the chunk's first node: the earlier superchunks' sums, then the
+  // earlier chunks of its own superchunk
+  const int64_t c0 = c - c % kPartSuper;
   int64_t s = 0;
-  for (int64_t k = threadIdx.x; k < c; k += kPartThreads) s += cnt[k];
+  for (int64_t k = threadIdx.x; k < c / kPartSuper; k += kPartThreads) s += sup[k];
+  for (int64_t k = c0 + threadIdx.x; k < c; k += kPartThreads) s += cnt[k];
   red[threadIdx.x] = s;
   __syncthreads();
   for (int w = kPartThreads / 2; w > 0; w >>= 1) {
@@ -462,7 +476,9 @@ hipError_t launch_batch_layout(const BatchItem* items, int64_t n_items, const in
 
 size_t partition_workspace_size(int64_t D) {
   const int64_t nch = (D + kPartW - 1) / kPartW;
-  return (size_t)(4 * (D + 64) + 2 * (nch + 64)) * 4 + 64 * 8;
+  const int64_t nsup = (nch + kPartSuper - 1) / kPartSuper;
+  const size_t b = (size_t)(4 * (D + 64) + 2 * (nch + 64) + (nsup + 64)) * 4 + 64 * 8;
+  return (b + 255) & ~(size_t)255;  // callers place 8-byte words right after it
 }
 
 bool partition_fell_back(const unsigned long long* info) {
@@ -484,6 +500,8 @@ hipError_t launch_partition(const float* kl, int64_t D, const int64_t* item_off,
   int32_t* gnode = node + (D + 64);
   int32_t* conv = gnode + (D + 64);
   int32_t* cnt = conv + (nch + 64);
+  int32_t* sup = cnt + (nch + 64);
+  const int64_t nsup = (nch + kPartSuper - 1) / kPartSuper;
   const bool single = item_off == nullptr && n_items == 1;
   if (!info_zeroed) {
     hipError_t e = hipMemsetAsync(info, 0, 8 * sizeof(unsigned long long), stream);
@@ -491,18 +509,18 @@ hipError_t launch_partition(const float* kl, int64_t D, const int64_t* item_off,
     if (e != hipSuccess) return e;
   }
   hipLaunchKernelGGL(k_part_next, dim3((unsigned)((D + 255) / 256)), dim3(256), 0, stream, kl, D,
-                     item_off, n_items, size_threshold, thr, nxt, info);
+                     item_off, n_items, size_threshold, thr, nxt, info, sup, nsup);
   hipLaunchKernelGGL(k_part_exit, dim3((unsigned)nch), dim3(kPartThreads), 0, stream, nxt, D, exg,
                      conv, info);
   hipLaunchKernelGGL(k_part_mark, dim3((unsigned)nch), dim3(kPartThreads), 0, stream, nxt, D, exg,
-                     conv, node, cnt, info);
+                     conv, node, cnt, info, sup);
   if (single) {
     hipLaunchKernelGGL(k_part_emit<true>, dim3((unsigned)nch), dim3(kPartThreads), 0, stream, nch,
-                       node, cnt, gnode, info, kl, D, size_threshold, thr, nxt, starts, iinfo);
+                       node, cnt, sup, gnode, info, kl, D, size_threshold, thr, nxt, starts, iinfo);
     return hipGetLastError();
   }
   hipLaunchKernelGGL(k_part_emit<false>, dim3((unsigned)nch), dim3(kPartThreads), 0, stream, nch,
-                     node, cnt, gnode, info, kl, D, size_threshold, thr, nxt, starts, iinfo);
+                     node, cnt, sup, gnode, info, kl, D, size_threshold, thr, nxt, starts, iinfo);
   hipLaunchKernelGGL(k_part_ihdr, dim3((unsigned)((n_items + 255) / 256)), dim3(256), 0, stream,
                      kl, D, item_off, n_items, size_threshold, thr, gnode, starts, iinfo, info);
   hipLaunchKernelGGL(k_part_ibody, dim3((unsigned)((D + 255) / 256)), dim3(kPartThreads), 0, stream,

@@ -235,6 +235,35 @@ def test_grouped_batch_equals_single_calls(cwq, sizes, seeds, bits, n_steps):
         assert np.array_equal(_u32(bs), _u32(sample)), k
 
 
+def test_grouped_batch_many_items(cwq):
+    """More items than the device partition keeps in LDS (1,024): 1,300 items
+    of 0..200 dims (empty and 1-dim ones among them, ~130k dims: the pipelined
+    path), each equal to code_grouped_greedy_sample on that item alone."""
+    cwq.coded_greedy_sampler.VERBOSE = False
+    rng = np.random.default_rng(1300)
+    sizes = rng.integers(0, 201, 1300)
+    sizes[::97] = 0
+    sizes[5::89] = 1
+    seeds = [int(x) for x in rng.integers(-2 ** 31, 2 ** 31, sizes.size)]
+    tg, pr = [], []
+    for D in sizes:
+        pl = (0.1 * rng.standard_normal(D)).astype(np.float32)
+        ps = rng.uniform(0.8, 1.2, D).astype(np.float32)
+        ql = (pl + ps * rng.standard_normal(D) * 0.7).astype(np.float32)
+        qs = (ps * rng.uniform(0.3, 1.0, D)).astype(np.float32)
+        tg.append(cwq.Normal(torch.from_numpy(ql).cuda(), torch.from_numpy(qs).cuda()))
+        pr.append(cwq.Normal(torch.from_numpy(pl).cuda(), torch.from_numpy(ps).cuda()))
+    got = cwq.code_grouped_greedy_sample_batch(None, tg, pr, 1, 8, seeds)
+    assert len(got) == sizes.size
+    for k in range(sizes.size):
+        sample, bitcode, starts = cwq.code_grouped_greedy_sample(None, tg[k], pr[k], 1, 8,
+                                                                 seeds[k])
+        bs, bb, bst = got[k]
+        assert bst.tolist() == starts, k
+        assert bb == bitcode, k
+        assert np.array_equal(_u32(bs), _u32(sample)), k
+
+
 @pytest.mark.parametrize("D,bits,n_steps", [(0, 8, 1), (1, 8, 1), (3000, 8, 1), (20000, 10, 2),
                                              (9000, 14, 3)])
 def test_grouped_two_halves_equal_one_shot(cwq, cwqlib, D, bits, n_steps):

@@ -2,13 +2,16 @@
 valu / wait, same bench arguments) into the committed evidence under
 profiles/ and the profiles/traffic_CONFIG.json that bench.py reads.
 
-Usage: python tools/collect_profile.py CONFIG TAG DOMINANT [SCORING ...]
+Usage: python tools/collect_profile.py [--runs R] CONFIG TAG DOMINANT [SCORING ...]
 
 DOMINANT selects the kernel the bench line's roofline prices (every dispatch
 whose name contains it); SCORING (default: DOMINANT) the substrings of every
 candidate-scoring launch of one step (e.g. k_small_prep1 k_small_one
 k_small_finalize for the small pipeline).  The PMC passes ran `bench.py
---steps 1 --warmup 0`, so their dispatches are one step's.
+--steps 1 --warmup 0`; R (default 1) is how many times that run executes
+the step: 2 for the grouped greedy configs (bench.py's timed() runs the step
+once without and once with the scoring timers), 1 for the importance and PLN
+lines.  Step totals are the PMC run's totals divided by R.
 
 Fractions are computed over each dispatch's own duration (End - Start of its
 counter_collection.csv row), tools/pmc_frac.py:
@@ -35,8 +38,12 @@ def one(pattern):
 
 
 def main():
-    config, tag, dom = sys.argv[1], sys.argv[2], sys.argv[3]
-    scoring = sys.argv[4:] or [dom]
+    argv = sys.argv[1:]
+    runs = 1
+    if argv[0] == "--runs":
+        runs, argv = int(argv[1]), argv[2:]
+    config, tag, dom = argv[0], argv[1], argv[2]
+    scoring = argv[3:] or [dom]
     src = os.path.join(ROOT, "gpurun_out")
     dst = os.path.join(ROOT, "profiles")
     files = {}
@@ -65,9 +72,9 @@ def main():
         for c, v in s["per_dispatch"].items():
             n = s["counter_dispatches"][c]
             tot.setdefault(c, [0.0, 0.0])
-            tot[c][0] += v * n
-            tot[c][1] += s["mean_duration_ns_by_pass"][c] * n
-    agg = {"kernels": scoring}
+            tot[c][0] += v * n / runs
+            tot[c][1] += s["mean_duration_ns_by_pass"][c] * n / runs
+    agg = {"kernels": scoring, "step_runs_in_pmc_pass": runs}
     if "SQ_INSTS_VALU" in tot:
         v, dur = tot["SQ_INSTS_VALU"]
         agg["valu_instructions_per_step"] = v

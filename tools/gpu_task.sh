@@ -14,6 +14,7 @@
 #   tools/gpu_task.sh decvar "V1 V2"                     decode tests + timing per variant build
 #   tools/gpu_task.sh py TAG SCRIPT [args]               a tools/ script -> gpurun_out/py_TAG.log
 #   tools/gpu_task.sh timeline TAG [bench args]          kernel + copy trace -> tools/timeline.py
+#   tools/gpu_task.sh vtrace TAG "V1 V2" [bench args]    kernel trace + stats per tools/vrun build
 # Several tasks can be chained: tools/gpu_task.sh tests -- pmc c2 wait --config c2
 set -o pipefail
 cd "$(dirname "$0")/.."
@@ -53,6 +54,13 @@ run_one() {
     vpmc)  # vpmc TAG VARIANT SET [bench args]: pmc on a tools/vrun build
       local tag=$1 v=$2; shift 2
       ( export CWQ_LIB_PATH=$PWD/tools/vrun/libcwq_$v.so; run_one pmc $tag "$@" ) ;;
+    vtrace)  # vtrace TAG "V1 V2" [bench args]: kernel trace + stats per tools/vrun build
+      local tag=$1 vs=$2; shift 2
+      for v in $vs; do
+        ( export CWQ_LIB_PATH=$PWD/tools/vrun/libcwq_$v.so; run_one trace ${tag}_$v "$@" ) || return 1
+        python3 tools/kstats.py $v gpurun_out/prof_${tag}_${v}_trace/run_kernel_stats.csv \
+          ${KSUBS:-k_small k_encode k_imp_eval k_csr} || return 1
+      done ;;
     stress)
       local n=${1:-400}
       timeout -k 10 300 python -u tools/stress_csr.py $n ${STRESS_SEED:-20000} 200 \
