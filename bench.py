@@ -91,8 +91,11 @@ HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=3)
-    ap.add_argument("--warmup", type=int, default=1)
+    # defaults per config (None): the block configs 3 steps after 1 warmup (C4: ~0.3 s a
+    # step); the grouped, importance and PLN configs 20 after 3 (a step is 0.5-55 ms, and
+    # their first steps grow torch's pinned-memory cache for the results they return)
+    ap.add_argument("--steps", type=int, default=None)
+    ap.add_argument("--warmup", type=int, default=None)
     ap.add_argument("--config", default="c4",
                     choices=sorted(CONFIGS) + sorted(GROUPED) + sorted(IMPORTANCE) + sorted(PLN))
     ap.add_argument("--blocks", type=int, default=0, help="override the config's block count (the whole job under strong scaling, "
@@ -112,7 +115,13 @@ def parse():
                          "split over the ranks) or weak (that many blocks per rank)")
     ap.add_argument("--check-blocks", type=int, default=16,
                     help="N > 1: blocks per rank checked against the CPU oracle")
-    return ap.parse_args()
+    args = ap.parse_args()
+    block = args.config in CONFIGS
+    if args.steps is None:
+        args.steps = 3 if block else 20
+    if args.warmup is None:
+        args.warmup = 1 if block else 3
+    return args
 
 
 def grouped_main(args):

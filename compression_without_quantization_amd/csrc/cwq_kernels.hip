@@ -1996,7 +1996,13 @@ __global__ void __launch_bounds__(256) k_small_survivors(
 #define CWQ_FUSED_WAVES 8
 #endif
 #ifndef CWQ_SMALL_RARE
-#define CWQ_SMALL_RARE 1  // k_small_one leaves blocks needing exact values to k_small_rare
+#define CWQ_SMALL_RARE 0  // 1: k_small_one leaves blocks needing exact values to k_small_rare
+#endif
+#ifndef CWQ_SMALL_PAIR
+#define CWQ_SMALL_PAIR 0  // k_small_pair: two blocks per wave (half-waves)
+#endif
+#ifndef CWQ_PAIR_WAVES
+#define CWQ_PAIR_WAVES 8
 #endif
 #ifndef CWQ_RARE_GRID
 #define CWQ_RARE_GRID 1024  // k_small_rare's waves
@@ -2318,6 +2324,10 @@ __device__ __forceinline__ void small_block(
     const int64_t off = (int64_t)(((uint64_t)ufirst(q0.y) << 32) | ufirst(q0.x));
     const int db = (int)ufirst(q0.z);
     uint32_t state = ufirst(q0.w);
+#ifdef CWQ_QUAD_FINE  // the record has arrived (phases a block skips take zero time)
+    if (kTimes && lane == 0u && g < kQuadTimes)
+      g_quad_t[g][1] = g_quad_t[g][2] = g_quad_t[g][3] = __builtin_amdgcn_s_memrealtime();
+#endif
     PhiloxStream sb;
     sb.k0 = ufirst(q1.x);
     sb.k1 = ufirst(q1.y);
@@ -2337,6 +2347,9 @@ __device__ __forceinline__ void small_block(
         for (int r = 0; r < 4; ++r) ax[r * db + (int)lane] = e;
       }
       wave_lds_sync();
+#ifdef CWQ_QUAD_FINE  // the block's constants are in LDS
+      if (kTimes && lane == 0u && g < kQuadTimes) g_quad_t[g][2] = __builtin_amdgcn_s_memrealtime();
+#endif
       const PhiloxLo K = philox_lo_key(sb);  // n_cand * d / 4 < 2^32 (d <= 64, < 4096 rows)
       float tau = -__builtin_inff();
       bool over = false;
@@ -2422,6 +2435,9 @@ __device__ __forceinline__ void small_block(
         used = at;
         wave_lds_sync();
       }
+#ifdef CWQ_QUAD_FINE  // the screen's loop is done
+      if (kTimes && lane == 0u && g < kQuadTimes) g_quad_t[g][3] = __builtin_amdgcn_s_memrealtime();
+#endif
       if (over) {
         state = kQuadExact;
         used = 0;
@@ -2445,7 +2461,11 @@ __device__ __forceinline__ void small_block(
     }
 #ifdef CWQ_QUAD_TIMES
     if (kTimes && lane == 0u && g < kQuadTimes) {
+#ifdef CWQ_QUAD_FINE
+      g_quad_t[g][4] = __builtin_amdgcn_s_memrealtime();
+#else
       g_quad_t[g][1] = __builtin_amdgcn_s_memrealtime();
+#endif
       g_quad_info[g][0] = (uint32_t)__builtin_amdgcn_s_getreg((4) | (0 << 6) | ((32 - 1) << 11));
       g_quad_info[g][1] = (uint32_t)__builtin_amdgcn_s_getreg((20) | (0 << 6) | ((4 - 1) << 11));
       g_quad_info[g][2] = used;
@@ -2488,7 +2508,12 @@ __device__ __forceinline__ void small_block(
       }
     }
     if (lane == 0) out_idx[g * n_steps + step] = (int32_t)idx;
-#ifdef CWQ_QUAD_TIMES
+#if defined(CWQ_QUAD_TIMES) && defined(CWQ_QUAD_FINE)
+    if (kTimes && lane == 0u && g < kQuadTimes) {
+      const unsigned long long t = __builtin_amdgcn_s_memrealtime();
+      g_quad_t[g][5] = t;
+    }
+#elif defined(CWQ_QUAD_TIMES)
     if (kTimes && lane == 0u && g < kQuadTimes)
       g_quad_t[g][2] = g_quad_t[g][3] = g_quad_t[g][4] = g_quad_t[g][5] =
           __builtin_amdgcn_s_memrealtime();
@@ -2543,7 +2568,7 @@ __global__ void __launch_bounds__(64 * CWQ_ONE_WPG, CWQ_FUSED_WAVES) k_small_one
 // wave per listed block; the grid's waves stride the list, whose length only
 // the device knows.
 template <bool STEP0>
-__global__ void __launch_bounds__(64) k_small_rare(
+__global__ void __launch_bounds__(64, CWQ_FUSED_WAVES) k_small_rare(
     const float* __restrict__ t_loc, const float* __restrict__ t_scale,
     const float* __restrict__ loc_s, const float* __restrict__ scale_s,
     const float* __restrict__ lognorm, const float* __restrict__ best,
@@ -2563,6 +2588,193 @@ __global__ void __launch_bounds__(64) k_small_rare(
     small_block<STEP0, true>((int64_t)rare[1 + i], t_loc, t_scale, loc_s, scale_s, lognorm, best,
                              rec, pre_ab, n_cand, step, n_steps, out_idx, rare, logtab, abx, ln,
                              lu, lpv, kmax);
+}
+
+// Max over the 32 lanes of each half-wave (DPP rows 0-1 and 2-3); full exec
+// mask.  Four row steps leave every lane with its row's max, row_bcast:15
+// folds row 0 into row 1 and row 2 into row 3.
+__device__ __forceinline__ float half_max_f32(float v, uint32_t h) {
+#if CWQ_WAVE_MAX_ASM
+  CWQ_DPP_MAX_STEP(v, "quad_perm:[1,0,3,2]", "0xf");
+  CWQ_DPP_MAX_STEP(v, "quad_perm:[2,3,0,1]", "0xf");
+  CWQ_DPP_MAX_STEP(v, "row_half_mirror", "0xf");
+  CWQ_DPP_MAX_STEP(v, "row_mirror", "0xf");
+  CWQ_DPP_MAX_STEP(v, "row_bcast:15", "0xa");
+  asm volatile("s_nop 1" : "+v"(v));
+#else
+  v = dpp_max_step<0xb1, 0xf>(v);
+  v = dpp_max_step<0x4e, 0xf>(v);
+  v = dpp_max_step<0x141, 0xf>(v);
+  v = dpp_max_step<0x140, 0xf>(v);
+  v = dpp_max_step<0x142, 0xa>(v);
+#endif
+  const float a = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 31));
+  const float b = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 63));
+  return h ? b : a;
+}
+__device__ __forceinline__ uint32_t half_bits(uint64_t m, uint32_t h) {
+  return (uint32_t)(m >> (32u * h));
+}
+
+// k_small_one for two blocks per wave: half-wave h (lanes 32 h .. 32 h + 31)
+// screens block 2 w + h, each lane taking 4-row spans of rows 4 (lane + 32 m).
+// The same spans, bounds and lists as small_block<STEP0, false>: the final τ
+// is the max over the same spans' lower bounds, so the rows kept at the end
+// are the same; a block whose longer list (rows 0..127 were listed against a
+// lower τ) overflows goes to the rare list, which scores it in full as
+// k_small_one would.  Halves a launch's waves: k_small_one is bound by the
+// rate at which waves start (§5e of DESIGN.md), not by their work.
+template <bool STEP0>
+__global__ void __launch_bounds__(64, CWQ_PAIR_WAVES) k_small_pair(
+    const SmallRec* __restrict__ rec, const float2* __restrict__ pre_ab, int64_t nb, int64_t u0,
+    int64_t n_cand, int32_t step, int n_steps, int32_t* __restrict__ out_idx,
+    uint32_t* __restrict__ rare) {
+  __shared__ float4 abx[2][2 * CWQ_FUSED_DMAX];
+  __shared__ uint32_t ln[2][CWQ_FUSED_LIST];
+  __shared__ float lu[2][CWQ_FUSED_LIST];
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t h = lane >> 5, hl = lane & 31u;
+  const int64_t g = u0 + 2 * (int64_t)blockIdx.x + h;
+  const bool live = g < nb;
+  const int64_t gs = live ? g : nb - 1;  // a half past the end reads a valid record
+  const uint4 q0 = rec[gs].q0, q1 = rec[gs].q1, q2 = rec[gs].q2;
+  const uint32_t q3x = rec[gs].q3.x;
+  const int64_t off = (int64_t)(((uint64_t)q0.y << 32) | q0.x);
+  const int db = (int)q0.z;
+  uint32_t state = live ? q0.w : kQuadKnown;
+  bool scr = state == kQuadListed;  // this half still screening
+  uint32_t idx = 0u;
+  float4* ab = abx[h];
+  if (scr) {
+    float2* ax = (float2*)ab;
+    for (int j = (int)hl; j < db; j += 32) {  // d <= 64 (launch_small)
+      const float2 e = pre_ab[off + j];
+      for (int r = 0; r < 4; ++r) ax[r * db + j] = e;
+    }
+  }
+  wave_lds_sync();
+  const float bfb = u2f(q2.x), c1b = u2f(q2.y), c2b = u2f(q2.z), asb = u2f(q2.w), pqb = u2f(q3x);
+  // philox_lo_key with per-half (vector) stream words
+  const uint32_t sk0 = q1.x, sk1 = q1.y, sc2 = q1.z, sc3 = q1.w;
+  PhiloxLo K;
+  {
+    const uint64_t p1 = (uint64_t)kPhiloxM1 * sc2;
+    const uint32_t n0 = (uint32_t)(p1 >> 32) ^ sk0;
+    const uint64_t qq0 = (uint64_t)kPhiloxM0 * n0;
+    K.A = sc3 ^ sk1;
+    K.B = (uint32_t)p1 ^ (sk0 + kPhiloxW0);
+    K.C = (uint32_t)(qq0 >> 32) ^ (sk1 + kPhiloxW1);
+    K.D = (uint32_t)qq0 ^ (sk1 + 2u * kPhiloxW1);
+  }
+  const int dl = scr ? db : 0;
+  const int dmax = max(__builtin_amdgcn_readlane(dl, 0), __builtin_amdgcn_readlane(dl, 32));
+  float tau = -__builtin_inff();
+  uint32_t used = 0;
+  for (int64_t m0 = 0; 128 * m0 < n_cand; ++m0) {
+    const int64_t ns = 4 * ((int64_t)hl + 32 * m0);
+    const uint32_t b0 = (uint32_t)((uint64_t)ns * (uint64_t)db / 4u);
+    float rs[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+    float cur = 0.0f;
+    int j = 0, qd = 0;
+    for (int b = 0; b < dmax; ++b) {
+      if (b < dl) {
+        const float4 e01 = ab[2 * b], e23 = ab[2 * b + 1];
+        const U4 x = philox10_lo(b0 + (uint32_t)b, K, sk0, sk1);
+        float z[4];
+        box_muller_screen(x.x, x.y, z[0], z[1]);
+        box_muller_screen(x.z, x.w, z[2], z[3]);
+        const float2 ev[4] = {float2{e01.x, e01.y}, float2{e01.z, e01.w},
+                              float2{e23.x, e23.y}, float2{e23.z, e23.w}};
+#pragma unroll
+        for (int tt = 0; tt < 4; ++tt) {
+          const float2 e = ev[tt];
+          const float a = __builtin_fmaf(e.x, z[tt], e.y);
+          cur = __builtin_fmaf(-a, a, cur);
+          if (++j == db) {
+            if (qd == 0) rs[0] = cur;
+            else if (qd == 1) rs[1] = cur;
+            else if (qd == 2) rs[2] = cur;
+            else rs[3] = cur;
+            cur = 0.0f;
+            j = 0;
+            ++qd;
+          }
+        }
+      }
+    }
+    float smax = -__builtin_inff();
+    bool any = false;
+#pragma unroll
+    for (int qq = 0; qq < 4; ++qq)
+      if (ns + qq < n_cand) {
+        smax = fmaxf(smax, rs[qq]);
+        any = true;
+      }
+    const float lower = (scr && any) ? __builtin_fmaf(smax, c2b, asb) -
+                                           pqb * __builtin_amdgcn_sqrtf(-smax)
+                                     : -__builtin_inff();
+    tau = fmaxf(tau, half_max_f32(lower, h));
+    uint64_t m[4];
+    uint32_t cnt = 0;
+#pragma unroll
+    for (int qq = 0; qq < 4; ++qq) {
+      m[qq] = __ballot(scr && ns + qq < n_cand && __builtin_fmaf(rs[qq], c1b, bfb) >= tau);
+      cnt += (uint32_t)__builtin_popcount(half_bits(m[qq], h));
+    }
+    const bool full = scr && used + cnt > CWQ_FUSED_LIST;
+    if (__ballot(full)) {  // drop the rows the raised τ excludes (two entries per lane)
+      const bool h0 = full && hl < used, h1 = full && hl + 32 < used;
+      const uint32_t n0 = ln[h][hl], n1 = ln[h][hl + 32];
+      const float v0 = lu[h][hl], v1 = lu[h][hl + 32];
+      const uint64_t k0 = __ballot(h0 && v0 >= tau), k1 = __ballot(h1 && v1 >= tau);
+      const uint32_t c0 = (uint32_t)__builtin_popcount(half_bits(k0, h));
+      wave_lds_sync();
+      const uint32_t r0 = lane_rank(k0) - (h ? (uint32_t)__builtin_popcount((uint32_t)k0) : 0u);
+      const uint32_t r1 = lane_rank(k1) - (h ? (uint32_t)__builtin_popcount((uint32_t)k1) : 0u);
+      if ((k0 >> lane) & 1ull) {
+        ln[h][r0] = n0;
+        lu[h][r0] = v0;
+      }
+      if ((k1 >> lane) & 1ull) {
+        ln[h][c0 + r1] = n1;
+        lu[h][c0 + r1] = v1;
+      }
+      if (full) used = c0 + (uint32_t)__builtin_popcount(half_bits(k1, h));
+      wave_lds_sync();
+    }
+    if (scr && used + cnt > CWQ_FUSED_LIST) {  // still full (near-ties): the rare path
+      state = kQuadExact;
+      scr = false;
+    }
+    uint32_t at = used;
+#pragma unroll
+    for (int qq = 0; qq < 4; ++qq) {
+      const uint32_t mq = scr ? half_bits(m[qq], h) : 0u;
+      if ((mq >> hl) & 1u) {
+        const uint32_t slot_i = at + (uint32_t)__builtin_popcount(mq & ((1u << hl) - 1u));
+        ln[h][slot_i] = (uint32_t)(ns + qq);
+        lu[h][slot_i] = __builtin_fmaf(rs[qq], c1b, bfb);
+      }
+      at += (uint32_t)__builtin_popcount(mq);
+    }
+    if (scr) used = at;
+    wave_lds_sync();
+  }
+  if (scr) {  // the rows whose upper bound reaches the final τ
+    const bool h0 = hl < used, h1 = hl + 32 < used;
+    const uint64_t k0 = __ballot(scr && h0 && lu[h][h0 ? hl : 0] >= tau);
+    const uint64_t k1 = __ballot(scr && h1 && lu[h][h1 ? hl + 32 : 0] >= tau);
+    const uint32_t a0 = half_bits(k0, h), a1 = half_bits(k1, h);
+    const uint32_t nk = (uint32_t)(__builtin_popcount(a0) + __builtin_popcount(a1));
+    if (nk == 1u) {  // the single listed row is the argmax
+      idx = ln[h][a0 ? (uint32_t)__builtin_ctz(a0) : 32u + (uint32_t)__builtin_ctz(a1)];
+      state = kQuadKnown;
+    }  // else (two or more, or never none): the rare path
+  }
+  if (live && hl == 0u) {
+    if (state == kQuadKnown) out_idx[g * n_steps + step] = (int32_t)idx;
+    else rare[1 + atomicAdd(rare, 1u)] = (uint32_t)g;
+  }
 }
 
 // A thread per dim of [d0, d0 + n): best += the winning row of its block (:63)
@@ -3381,6 +3593,14 @@ static bool launch_small(const EncodeArgs& a, int step, hipStream_t stream) {
                          a.lognorm, a.out_sample, a.block_off, a.ud, a.nb, seeds_of(a), step,
                          pab, rec, a.sdmap, a.ordu);
     const int64_t nu = a.nb;
+    if (CWQ_SMALL_PAIR && CWQ_SMALL_RARE) {
+      for (int64_t u0 = 0; u0 < nu; u0 += (int64_t)1 << 30) {
+        const int64_t nc = nu - u0 < (1LL << 30) ? nu - u0 : (1LL << 30);
+        hipLaunchKernelGGL((k_small_pair<STEP0>), dim3((unsigned)((nc + 1) / 2)), dim3(64), 0,
+                           stream, rec, a.pre_ab, a.nb, u0, a.n_cand, step, a.n_steps, a.out_idx,
+                           a.ordu);
+      }
+    } else
     for (int64_t u0 = 0; u0 < nu; u0 += (int64_t)1 << 30) {
       int64_t nw = ((nu - u0 < (1LL << 30) ? nu - u0 : (1LL << 30)) + CWQ_ONE_WPG - 1) /
                    CWQ_ONE_WPG;
@@ -3469,9 +3689,11 @@ static hipError_t encode_steps(const EncodeArgs& a, hipStream_t stream, bool eve
   const unsigned fgrid_dims =
       grid_for(a.total_dims > a.nb ? a.total_dims : a.nb, 256, CWQ_FIN_MAX_WGS);
   for (int s = 0; s < a.n_steps; ++s) {
-    // step 0's keys were zeroed by k_prep_dims (launch_encode)
-    if (s > 0 && (e = hipMemsetAsync(a.keys, 0, (size_t)a.nb * sizeof(unsigned long long),
-                                     stream)) != hipSuccess)
+    // step 0's keys were zeroed by k_prep_dims (launch_encode); the small
+    // pipeline keeps its argmax in registers and LDS and never reads keys
+    if (s > 0 && !takes_small_pipe(a) &&
+        (e = hipMemsetAsync(a.keys, 0, (size_t)a.nb * sizeof(unsigned long long), stream)) !=
+            hipSuccess)
       return e;
     if (events && s == 0 && a.ev_start) {
       e = hipEventRecord((hipEvent_t)a.ev_start, stream);

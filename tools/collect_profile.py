@@ -20,6 +20,7 @@ counter_collection.csv row), tools/pmc_frac.py:
 Everything in traffic_CONFIG.json can be recomputed from the CSVs it lists.
 """
 import glob
+import gzip
 import json
 import os
 import shutil
@@ -52,14 +53,20 @@ def main():
         f = one(os.path.join(src, pat))
         if f:
             files[what] = os.path.join("profiles", f"{tag}_{what}.csv")
-            shutil.copy(f, os.path.join(ROOT, files[what]))
+            if what == "kernel_trace":  # one row per dispatch: kept gzipped
+                files[what] += ".gz"
+                with open(f, "rb") as fi, gzip.open(os.path.join(ROOT, files[what]), "wb") as fo:
+                    shutil.copyfileobj(fi, fo)
+            else:
+                shutil.copy(f, os.path.join(ROOT, files[what]))
     csvs = []
     for p in PASSES:
         f = one(os.path.join(src, f"prof_{tag}_{p}/**/*counter_collection.csv"))
         if not f:
             continue
-        rel = os.path.join("profiles", f"{tag}_pmc_{p}.csv")
-        shutil.copy(f, os.path.join(ROOT, rel))
+        rel = os.path.join("profiles", f"{tag}_pmc_{p}.csv.gz")  # gzipped (pmc_frac reads it)
+        with open(f, "rb") as fi, gzip.open(os.path.join(ROOT, rel), "wb") as fo:
+            shutil.copyfileobj(fi, fo)
         csvs.append(rel)
     absf = [os.path.join(ROOT, c) for c in csvs]
     d = pmc_frac.summarize(dom, absf)
