@@ -24,11 +24,12 @@
 //                 by their stored ex of the entry), then the walk's nodes in
 //                 the chunk marked by pointer jumping in LDS, counted and
 //                 compacted;
-//   k_part_emit   per chunk: the global rank of its first node (the earlier
-//                 superchunks' sums, which k_part_mark adds its count to, plus
-//                 the earlier chunks of its own superchunk of kPartSuper: per
-//                 chunk O(nch / kPartSuper + kPartSuper) loads, not O(nch)),
-//                 the walk's nodes in rank order (one
+//   k_part_emit   per chunk: the global rank of its first node (the sum of
+//                 the earlier chunks' counts; past kPartDirect chunks the
+//                 earlier superchunks' sums from k_part_sup plus the earlier
+//                 chunks of its own superchunk of kPartSuper, so the total
+//                 work stays linear in the chunk count), the walk's nodes in
+//                 rank order (one
 //                 item: straight into its start list, with its largest group,
 //                 and the two launches below are skipped);
 //   k_part_ihdr / k_part_ibody  per item: its nodes (a rank range found by
@@ -53,7 +54,11 @@ constexpr int kPartMaxJump = 512;   // longest group the device path takes
 constexpr int kPartRun = 8;         // non-converged chunks a walk may cross
 constexpr int kPartThreads = 256;
 constexpr int kPartLdsItems = 1024;  // batches up to this many items search offsets in LDS
-constexpr int kPartSuper = 256;      // chunks per superchunk (k_part_mark's sums)
+constexpr int kPartSuper = 256;      // chunks per superchunk (k_part_sup's sums)
+// up to this many chunks k_part_emit sums the earlier counts directly (at most
+// 64 loads per thread; C3's 4,660 chunks: 18): an atomic per chunk into the
+// superchunk sums instead cost C3's k_part_mark 33 us (37 -> 70 us)
+constexpr int64_t kPartDirect = 16384;
 
 // info[0] nodes on the walk, info[2] fallback flag, info[4] a jump nxt(i) - i
 // above kPartMaxJump (the fallback; 0 when there is none).  Per item k: iinfo[2k] its starts (G + 1),
@@ -77,8 +82,7 @@ __global__ void __launch_bounds__(256) k_part_next(const float* __restrict__ kl,
                                                    const int64_t* __restrict__ item_off,
                                                    int64_t n_items, int64_t T, float thr,
                                                    int32_t* __restrict__ nxt,
-                                                   unsigned long long* __restrict__ info,
-                                                   int32_t* __restrict__ sup, int64_t nsup) {
+                                                   unsigned long long* __restrict__ info) {
   __shared__ int32_t red[256];
   // the workgroup's 256 dims and the kPartMaxJump after them, staged in LDS
   // (coalesced): each thread's scan then reads LDS instead of a chain of
@@ -87,7 +91,6 @@ __global__ void __launch_bounds__(256) k_part_next(const float* __restrict__ kl,
   __shared__ int64_t soff[kPartLdsItems + 1];
   const int64_t b = (int64_t)blockIdx.x * blockDim.x;
   const int64_t i = b + threadIdx.x;
-  if (i < nsup) sup[i] = 0;  // k_part_mark's superchunk sums (D >= nsup threads)
   for (int t = threadIdx.x; t < 256 + kPartMaxJump + 1; t += 256)
     skl[t] = b + t < D ? kl[b + t] : 0.0f;
   // a batch's item offsets in LDS too (the binary search per dim is a chain of
@@ -193,8 +196,7 @@ __global__ void __launch_bounds__(256) k_part_mark(const int32_t* __restrict__ n
                                                    const int32_t* __restrict__ conv,
                                                    int32_t* __restrict__ node,
                                                    int32_t* __restrict__ cnt,
-                                                   unsigned long long* __restrict__ info,
-                                                   int32_t* __restrict__ sup) {
+                                                   unsigned long long* __restrict__ info) {
   __shared__ int32_t ja[kPartW], jb[kPartW];
   __shared__ uint8_t mark[kPartW];
   __shared__ int32_t red[kPartThreads];
@@ -275,10 +277,26 @@ __global__ void __launch_bounds__(256) k_part_mark(const int32_t* __restrict__ n
     const int l = threadIdx.x * kPer + q;
     if (l < n && mark[l]) node[b + at++] = (int32_t)(b + l);
   }
-  if (threadIdx.x == kPartThreads - 1) {
-    cnt[c] = red[threadIdx.x];
-    if (red[threadIdx.x]) atomicAdd(&sup[c / kPartSuper], red[threadIdx.x]);
+  if (threadIdx.x == kPartThreads - 1) cnt[c] = red[threadIdx.x];
+}
+
+// Superchunk sums of the chunk counts (launched past kPartDirect chunks): a
+// workgroup per kPartSuper chunks
+__global__ void __launch_bounds__(256) k_part_sup(const int32_t* __restrict__ cnt, int64_t nch,
+                                                  int32_t* __restrict__ sup,
+                                                  const unsigned long long* __restrict__ info) {
+  __shared__ int64_t red[kPartThreads];
+  if (info[4] > (unsigned long long)kPartMaxJump || info[2]) return;
+  const int64_t k0 = (int64_t)blockIdx.x * kPartSuper;
+  int64_t v = 0;
+  for (int64_t k = k0 + threadIdx.x; k < k0 + kPartSuper && k < nch; k += kPartThreads) v += cnt[k];
+  red[threadIdx.x] = v;
+  __syncthreads();
+  for (int w = kPartThreads / 2; w > 0; w >>= 1) {
+    if ((int)threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+    __syncthreads();
   }
+  if (threadIdx.x == 0) sup[blockIdx.x] = (int32_t)red[0];
 }
 
 // SINGLE (one item, no item_off): the chunk's nodes go straight to the start
@@ -301,11 +319,13 @@ __global__ void __launch_bounds__(256) k_part_emit(int64_t nchunks,
   if (info[4] > (unsigned long long)kPartMaxJump || info[2]) return;
   const int64_t c = blockIdx.x;
   const int64_t b = c * kPartW;
-  // rank of the chunk's first node: the earlier superchunks' sums, then the
-  // earlier chunks of its own superchunk
-  const int64_t c0 = c - c % kPartSuper;
+  // rank of the chunk's first node: the earlier chunks' counts (past
+  // kPartDirect chunks: the earlier superchunks' sums, then the earlier chunks
+  // of its own superchunk)
+  const int64_t c0 = nchunks > kPartDirect ? c - c % kPartSuper : 0;
   int64_t s = 0;
-  for (int64_t k = threadIdx.x; k < c / kPartSuper; k += kPartThreads) s += sup[k];
+  if (nchunks > kPartDirect)
+    for (int64_t k = threadIdx.x; k < c / kPartSuper; k += kPartThreads) s += sup[k];
   for (int64_t k = c0 + threadIdx.x; k < c; k += kPartThreads) s += cnt[k];
   red[threadIdx.x] = s;
   __syncthreads();
@@ -509,11 +529,14 @@ hipError_t launch_partition(const float* kl, int64_t D, const int64_t* item_off,
     if (e != hipSuccess) return e;
   }
   hipLaunchKernelGGL(k_part_next, dim3((unsigned)((D + 255) / 256)), dim3(256), 0, stream, kl, D,
-                     item_off, n_items, size_threshold, thr, nxt, info, sup, nsup);
+                     item_off, n_items, size_threshold, thr, nxt, info);
   hipLaunchKernelGGL(k_part_exit, dim3((unsigned)nch), dim3(kPartThreads), 0, stream, nxt, D, exg,
                      conv, info);
   hipLaunchKernelGGL(k_part_mark, dim3((unsigned)nch), dim3(kPartThreads), 0, stream, nxt, D, exg,
-                     conv, node, cnt, info, sup);
+                     conv, node, cnt, info);
+  if (nch > kPartDirect)
+    hipLaunchKernelGGL(k_part_sup, dim3((unsigned)nsup), dim3(kPartThreads), 0, stream, cnt, nch,
+                       sup, info);
   if (single) {
     hipLaunchKernelGGL(k_part_emit<true>, dim3((unsigned)nch), dim3(kPartThreads), 0, stream, nch,
                        node, cnt, sup, gnode, info, kl, D, size_threshold, thr, nxt, starts, iinfo);

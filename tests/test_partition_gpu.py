@@ -58,9 +58,10 @@ def _check(kl, bits=8, mgsb=12, expect_device=None):
 
 def test_partition_random_sizes():
     rng = np.random.default_rng(5)
-    # 262,144 dims and up: several superchunks of 256 chunks (k_part_emit's ranks)
+    # 262,144 dims and up: several superchunks of 256 chunks; past 16,384 chunks
+    # (16.8M dims) k_part_emit's ranks come from k_part_sup's superchunk sums
     for D in (2, 3, 4, 5, 7, 63, 100, 1023, 1024, 1025, 2047, 2048, 2049, 5000, 65536,
-              262144, 262145, 600001):
+              262144, 262145, 600001, 16384 * 1024 + 12345):
         kl = rng.exponential(0.8, D)
         _check(kl, expect_device=True)
 

@@ -15,6 +15,7 @@
 #   tools/gpu_task.sh py TAG SCRIPT [args]               a tools/ script -> gpurun_out/py_TAG.log
 #   tools/gpu_task.sh timeline TAG [bench args]          kernel + copy trace -> tools/timeline.py
 #   tools/gpu_task.sh vtrace TAG "V1 V2" [bench args]    kernel trace + stats per tools/vrun build
+#   tools/gpu_task.sh ktimeline TAG WINDOW_MS SCRIPT [args]  kernel-trace timeline of a script
 # Several tasks can be chained: tools/gpu_task.sh tests -- pmc c2 wait --config c2
 set -o pipefail
 cd "$(dirname "$0")/.."
@@ -103,6 +104,12 @@ run_one() {
       BARGS="$* --steps 3 --warmup 1" prof prof_${tag}_tl --kernel-trace --memory-copy-trace --stats && \
         python3 tools/timeline.py gpurun_out/prof_${tag}_tl ${TL_MS:-12} > gpurun_out/tl_$tag.txt && \
         tail -3 gpurun_out/tl_$tag.txt ;;
+    ktimeline)  # ktimeline TAG WINDOW_MS SCRIPT [args]: kernel trace of a tools/ script + timeline.py
+      local tag=$1 win=$2; shift 2
+      timeout -s KILL 180 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_${tag}_kt -o run \
+        --output-format csv -- python3 "$@" > gpurun_out/prof_${tag}_kt.log 2>&1 && \
+        python3 tools/timeline.py gpurun_out/prof_${tag}_kt $win > gpurun_out/tl_$tag.txt && \
+        tail -n 1 gpurun_out/prof_${tag}_kt.log && tail -n 1 gpurun_out/tl_$tag.txt ;;
     *) echo "unknown task $task"; return 2 ;;
   esac
 }
