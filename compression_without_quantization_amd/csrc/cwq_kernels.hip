@@ -2007,6 +2007,9 @@ __global__ void __launch_bounds__(256) k_small_survivors(
 #ifndef CWQ_RARE_GRID
 #define CWQ_RARE_GRID 1024  // k_small_rare's waves
 #endif
+#ifndef CWQ_ONE_FIN
+#define CWQ_ONE_FIN 0  // 1: k_small_one also does k_small_finalize's work (one launch fewer)
+#endif
 #ifndef CWQ_ONE_GRID
 #define CWQ_ONE_GRID 0  // k_small_one workgroups, each striding the blocks (0: one per block)
 #endif
@@ -2311,7 +2314,9 @@ __device__ __forceinline__ void small_block(
     const SmallRec* __restrict__ rec, const float2* __restrict__ pre_ab, int64_t n_cand,
     int32_t step, int n_steps, int32_t* __restrict__ out_idx, uint32_t* __restrict__ rare,
     double* logtab, float4* abx, uint32_t* ln, float* lu, float* lpv,
-    unsigned long long& kmax) {
+    unsigned long long& kmax, float* __restrict__ fbest = nullptr,
+    float* __restrict__ ds_out = nullptr, const float* __restrict__ ds_loc = nullptr,
+    const float* __restrict__ ds_scale = nullptr) {
   const uint32_t lane = threadIdx.x & 63u;
   auto ufirst = [](uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); };
   auto ffirst = [&](uint32_t v) { return u2f(ufirst(v)); };
@@ -2508,6 +2513,20 @@ __device__ __forceinline__ void small_block(
       }
     }
     if (lane == 0) out_idx[g * n_steps + step] = (int32_t)idx;
+#if CWQ_ONE_FIN
+    if (FULL && fbest && (int)lane < db) {  // k_small_finalize's work for this block (:63, :292)
+      const int64_t i = off + (int64_t)lane;
+      const float zz = exact_normal(sb, (uint64_t)idx * (uint64_t)db + lane, logtab);
+      float sv = scale_s[i] * zz;  // misc.py:14
+      sv = loc_s[i] + sv;          // misc.py:15
+      const float b = (STEP0 ? 0.0f : fbest[i]) + sv;
+      fbest[i] = b;
+      if (ds_out) {
+        const float m = ds_scale[i] * b;
+        ds_out[i] = m + ds_loc[i];
+      }
+    }
+#endif
 #if defined(CWQ_QUAD_TIMES) && defined(CWQ_QUAD_FINE)
     if (kTimes && lane == 0u && g < kQuadTimes) {
       const unsigned long long t = __builtin_amdgcn_s_memrealtime();
@@ -2529,7 +2548,8 @@ __global__ void __launch_bounds__(64 * CWQ_ONE_WPG, CWQ_FUSED_WAVES) k_small_one
     const float* __restrict__ lognorm, const float* __restrict__ best,
     const SmallRec* __restrict__ rec, const float2* __restrict__ pre_ab, int64_t nb, int64_t u0,
     int64_t n_cand, int32_t step, int n_steps, int32_t* __restrict__ out_idx,
-    uint32_t* __restrict__ rare) {
+    uint32_t* __restrict__ rare, float* __restrict__ fbest, float* __restrict__ ds_out,
+    const float* __restrict__ ds_loc, const float* __restrict__ ds_scale) {
   // every wave of the workgroup its own block and its own LDS (no barrier
   // between the waves: a wave whose block is past nb just ends)
   constexpr int W = CWQ_ONE_WPG;
@@ -2559,7 +2579,7 @@ __global__ void __launch_bounds__(64 * CWQ_ONE_WPG, CWQ_FUSED_WAVES) k_small_one
   small_block<STEP0, !CWQ_SMALL_RARE>(g, t_loc, t_scale, loc_s, scale_s, lognorm, best, rec,
                                       pre_ab, n_cand, step, n_steps, out_idx, rare,
                                       logtab_w[wv], abx_w[wv], ln_w[wv], lu_w[wv], lpv_w[wv],
-                                      kmax_w[wv]);
+                                      kmax_w[wv], fbest, ds_out, ds_loc, ds_scale);
 #endif
 }
 
@@ -3608,7 +3628,8 @@ static bool launch_small(const EncodeArgs& a, int step, hipStream_t stream) {
       hipLaunchKernelGGL((k_small_one<STEP0>), dim3((unsigned)nw),
                          dim3(64 * CWQ_ONE_WPG), 0, stream, a.t_loc, a.t_scale, a.loc_s, a.scale_s, a.lognorm,
                          a.out_sample, rec, a.pre_ab, a.nb, u0, a.n_cand, step, a.n_steps,
-                         a.out_idx, a.ordu);
+                         a.out_idx, a.ordu, a.out_sample,
+                         step == a.n_steps - 1 ? a.ds_out : nullptr, a.ds_loc, a.ds_scale);
     }
     // the rare list (a.ordu: the pipeline leaves that scratch unused; a forked
     // part's view is its own)
@@ -3619,6 +3640,7 @@ static bool launch_small(const EncodeArgs& a, int step, hipStream_t stream) {
                          a.out_sample, rec, a.pre_ab, a.n_cand, step, a.n_steps, a.out_idx,
                          a.ordu);
     const unsigned dgrid = grid_for(a.total_dims > a.nb ? a.total_dims : a.nb, 256, 16384);
+    if (!(CWQ_ONE_FIN && !CWQ_SMALL_RARE && !CWQ_SMALL_PAIR))  // else k_small_one finalizes
     hipLaunchKernelGGL((k_small_finalize<STEP0>), dim3(dgrid), dim3(256), 0, stream, a.loc_s,
                        a.scale_s, rec, a.sdmap, a.out_idx, step, a.n_steps, a.block_off, a.ud,
                        a.nb, a.out_sample, step == a.n_steps - 1 ? a.ds_out : nullptr, a.ds_loc,
