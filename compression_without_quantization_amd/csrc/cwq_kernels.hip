@@ -1995,29 +1995,6 @@ __global__ void __launch_bounds__(256) k_small_survivors(
 #ifndef CWQ_FUSED_WAVES
 #define CWQ_FUSED_WAVES 8
 #endif
-#ifndef CWQ_SMALL_RARE
-#define CWQ_SMALL_RARE 0  // 1: k_small_one leaves blocks needing exact values to k_small_rare
-#endif
-#ifndef CWQ_SMALL_PAIR
-#define CWQ_SMALL_PAIR 0  // k_small_pair: two blocks per wave (half-waves)
-#endif
-#ifndef CWQ_PAIR_WAVES
-#define CWQ_PAIR_WAVES 8
-#endif
-#ifndef CWQ_RARE_GRID
-#define CWQ_RARE_GRID 1024  // k_small_rare's waves
-#endif
-#ifndef CWQ_ONE_FIN
-#define CWQ_ONE_FIN 0  // 1: k_small_one also does k_small_finalize's work (one launch fewer)
-#endif
-#ifndef CWQ_ONE_GRID
-#define CWQ_ONE_GRID 0  // k_small_one workgroups, each striding the blocks (0: one per block)
-#endif
-#ifndef CWQ_ONE_WPG
-#define CWQ_ONE_WPG 1  // waves (blocks) per k_small_one workgroup
-#endif
-static_assert(CWQ_ONE_WPG >= 1 && (CWQ_ONE_WPG & (CWQ_ONE_WPG - 1)) == 0 && CWQ_ONE_WPG <= 16,
-              "k_small_one: a power-of-two number of waves per workgroup (launch_small's chunks)");
 static_assert(CWQ_FUSED_STAGE >= CWQ_FUSED_DMAX, "an exact batch holds at least one row");
 static_assert(CWQ_FUSED_LIST <= 64, "one listed row per lane");
 
@@ -2121,8 +2098,10 @@ __device__ unsigned int g_quad_info[kQuadTimes][4];
 //                     (csr_dim), summed per block in LDS; then a thread per
 //                     block: bounds, stream key -> a 64-byte record; the
 //                     dim -> block map
-//   k_small_one       a wave per block (CWQ_ONE_WPG waves per workgroup):
-//                     screen, exact survivors -> index
+//   k_small_one       a wave per block: screen, exact survivors -> index
+//                     (variants measured in DESIGN.md 5e: more blocks per
+//                     wave or per workgroup, a striding grid, a second kernel
+//                     for the exact paths, the finalize fused in: all slower)
 //   k_small_finalize  a thread per dim: best += the winning row (:63), and
 //                     at the last step the destandardised sample (:292)
 // ---------------------------------------------------------------------------
@@ -2161,7 +2140,7 @@ __global__ void __launch_bounds__(CWQ_PREP1_THREADS) k_small_prep1(
     float rho, float* __restrict__ loc_s, float* __restrict__ scale_s,
     float* __restrict__ lognorm, float* __restrict__ best, const int64_t* __restrict__ block_off,
     int64_t ud, int64_t nb, SeedSpec sd, int32_t step, float2* __restrict__ pre_ab,
-    SmallRec* __restrict__ rec, uint32_t* __restrict__ dmap, uint32_t* __restrict__ rare) {
+    SmallRec* __restrict__ rec, uint32_t* __restrict__ dmap) {
   constexpr int B = kSmallPrepBlocks;
   constexpr int T = CWQ_PREP1_THREADS;
   __shared__ int64_t boff[B + 1];
@@ -2170,7 +2149,6 @@ __global__ void __launch_bounds__(CWQ_PREP1_THREADS) k_small_prep1(
   const int t = threadIdx.x;
   const int64_t g0 = (int64_t)blockIdx.x * B;
   const int n = (int)(nb - g0 < B ? nb - g0 : B);
-  if (blockIdx.x == 0 && t == 0) rare[0] = 0u;  // k_small_one's rare list, empty
   for (int k = t; k <= n; k += T) boff[k] = block_off ? block_off[g0 + k] : (g0 + k) * ud;
   if (t < B) {
     for (int k = 0; k < 5; ++k) acc[k][t] = 0.0;
@@ -2300,39 +2278,35 @@ CWQ_RARE unsigned long long small_listed_exact(
 // C3 (C3's scoring 1.11-1.20 ms per step in all five);
 // longest blocks first (a counting sort by d), 41 us against 47 but the sort
 // cost a launch and a histogram that needed zeroing.
-// One block of the screen (a wave): FULL scores the listed rows / the whole
-// block exactly where the screen leaves more than one candidate (the two
-// out-of-line paths); otherwise such a block goes on the rare list (rare[0]
-// the count, rare[1..] block numbers) for k_small_rare, so k_small_one makes
-// no calls: without them it needs 32 VGPRs and no scratch (the calls' ABI took
-// 64 and 496 B/lane of scratch)
-template <bool STEP0, bool FULL>
-__device__ __forceinline__ void small_block(
-    const int64_t g, const float* __restrict__ t_loc, const float* __restrict__ t_scale,
+template <bool STEP0>
+__global__ void __launch_bounds__(64, CWQ_FUSED_WAVES) k_small_one(
+    const float* __restrict__ t_loc, const float* __restrict__ t_scale,
     const float* __restrict__ loc_s, const float* __restrict__ scale_s,
     const float* __restrict__ lognorm, const float* __restrict__ best,
-    const SmallRec* __restrict__ rec, const float2* __restrict__ pre_ab, int64_t n_cand,
-    int32_t step, int n_steps, int32_t* __restrict__ out_idx, uint32_t* __restrict__ rare,
-    double* logtab, float4* abx, uint32_t* ln, float* lu, float* lpv,
-    unsigned long long& kmax, float* __restrict__ fbest = nullptr,
-    float* __restrict__ ds_out = nullptr, const float* __restrict__ ds_loc = nullptr,
-    const float* __restrict__ ds_scale = nullptr) {
+    const SmallRec* __restrict__ rec, const float2* __restrict__ pre_ab, int64_t nb, int64_t u0,
+    int64_t n_cand, int32_t step, int n_steps, int32_t* __restrict__ out_idx) {
+  __shared__ double logtab[32];
+  // the block's (sA, sB) repeated 4 times: a lane's span of 4 rows is 4 d
+  // normals, so Philox block b covers abx[4 b .. 4 b + 3] (two b128 reads,
+  // issued ahead of the Philox rounds that hide their latency)
+  __shared__ float4 abx[2 * CWQ_FUSED_DMAX];
+  __shared__ uint32_t ln[CWQ_FUSED_LIST];
+  __shared__ float lu[CWQ_FUSED_LIST];
+  __shared__ float lpv[CWQ_FUSED_STAGE];
+  __shared__ unsigned long long kmax;
   const uint32_t lane = threadIdx.x & 63u;
+  if (lane < 32) logtab[lane] = kLogTabConst[lane];
   auto ufirst = [](uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); };
   auto ffirst = [&](uint32_t v) { return u2f(ufirst(v)); };
+  const int64_t g = u0 + blockIdx.x;
   {
 #ifdef CWQ_QUAD_TIMES  // tools/quad_times.py --one: per block start, after the screen, end
-    constexpr bool kTimes = !(FULL && CWQ_SMALL_RARE);  // k_small_one's launch only
-    if (kTimes && lane == 0u && g < kQuadTimes) g_quad_t[g][0] = __builtin_amdgcn_s_memrealtime();
+    if (lane == 0u && g < kQuadTimes) g_quad_t[g][0] = __builtin_amdgcn_s_memrealtime();
 #endif
     const uint4 q0 = rec[g].q0, q1 = rec[g].q1;
     const int64_t off = (int64_t)(((uint64_t)ufirst(q0.y) << 32) | ufirst(q0.x));
     const int db = (int)ufirst(q0.z);
     uint32_t state = ufirst(q0.w);
-#ifdef CWQ_QUAD_FINE  // the record has arrived (phases a block skips take zero time)
-    if (kTimes && lane == 0u && g < kQuadTimes)
-      g_quad_t[g][1] = g_quad_t[g][2] = g_quad_t[g][3] = __builtin_amdgcn_s_memrealtime();
-#endif
     PhiloxStream sb;
     sb.k0 = ufirst(q1.x);
     sb.k1 = ufirst(q1.y);
@@ -2352,9 +2326,6 @@ __device__ __forceinline__ void small_block(
         for (int r = 0; r < 4; ++r) ax[r * db + (int)lane] = e;
       }
       wave_lds_sync();
-#ifdef CWQ_QUAD_FINE  // the block's constants are in LDS
-      if (kTimes && lane == 0u && g < kQuadTimes) g_quad_t[g][2] = __builtin_amdgcn_s_memrealtime();
-#endif
       const PhiloxLo K = philox_lo_key(sb);  // n_cand * d / 4 < 2^32 (d <= 64, < 4096 rows)
       float tau = -__builtin_inff();
       bool over = false;
@@ -2440,9 +2411,6 @@ __device__ __forceinline__ void small_block(
         used = at;
         wave_lds_sync();
       }
-#ifdef CWQ_QUAD_FINE  // the screen's loop is done
-      if (kTimes && lane == 0u && g < kQuadTimes) g_quad_t[g][3] = __builtin_amdgcn_s_memrealtime();
-#endif
       if (over) {
         state = kQuadExact;
         used = 0;
@@ -2465,335 +2433,43 @@ __device__ __forceinline__ void small_block(
       }
     }
 #ifdef CWQ_QUAD_TIMES
-    if (kTimes && lane == 0u && g < kQuadTimes) {
-#ifdef CWQ_QUAD_FINE
-      g_quad_t[g][4] = __builtin_amdgcn_s_memrealtime();
-#else
+    if (lane == 0u && g < kQuadTimes) {
       g_quad_t[g][1] = __builtin_amdgcn_s_memrealtime();
-#endif
       g_quad_info[g][0] = (uint32_t)__builtin_amdgcn_s_getreg((4) | (0 << 6) | ((32 - 1) << 11));
       g_quad_info[g][1] = (uint32_t)__builtin_amdgcn_s_getreg((20) | (0 << 6) | ((4 - 1) << 11));
       g_quad_info[g][2] = used;
       g_quad_info[g][3] = (state == kQuadExact ? 1u : 0u) | ((uint32_t)db << 8);
     }
 #endif
-    if (!FULL) {
-      if (state != kQuadKnown) {  // exact values needed: k_small_rare's (C2: 0.2% of the blocks)
-        if (lane == 0) rare[1 + atomicAdd(rare, 1u)] = (uint32_t)g;
-#ifdef CWQ_QUAD_TIMES
-        if (lane == 0u && g < kQuadTimes)
-          g_quad_t[g][2] = g_quad_t[g][3] = g_quad_t[g][4] = g_quad_t[g][5] =
-              __builtin_amdgcn_s_memrealtime();
-#endif
-        return;
-      }
-    } else {
-      if (state == kQuadListed && used > 0) {  // the listed rows' exact values
-        const unsigned long long bk = small_listed_exact<STEP0>(
-            off, db, sb, used, ln, lpv, logtab, t_loc, t_scale, loc_s, scale_s, lognorm, best);
-        if (lane == 0) kmax = bk;
-        wave_lds_sync();
-      }
-      if (state == kQuadExact) {  // every candidate exactly (constants outside the gate, list full)
-        QuadBlk r;
-        r.off = off;
-        r.d = (uint32_t)db;
-        r.k0 = sb.k0;
-        r.k1 = sb.k1;
-        r.c2 = sb.c2;
-        r.c3 = sb.c3;
-        const unsigned long long bk = quad_exact_block<STEP0>(r, t_loc, t_scale, loc_s, scale_s,
-                                                               lognorm, best, n_cand, logtab);
-        if (lane == 0) kmax = bk;
-        wave_lds_sync();
-      }
-      if (state != kQuadKnown) {  // ArgMaxTupleReducer: a key at the clamp level is index 0
-        const unsigned long long kb = kmax;
-        idx = (kb >> 32) > kArgmaxClampOrd ? argmax_key_index(kb) : 0u;
-      }
+    if (state == kQuadListed && used > 0) {  // rare (C2: 0.6% of the blocks): out of line
+      const unsigned long long bk = small_listed_exact<STEP0>(
+          off, db, sb, used, ln, lpv, logtab, t_loc, t_scale, loc_s, scale_s, lognorm, best);
+      if (lane == 0) kmax = bk;
+      wave_lds_sync();
+    }
+    if (state == kQuadExact) {  // every candidate exactly (constants outside the gate, list full)
+      QuadBlk r;
+      r.off = off;
+      r.d = (uint32_t)db;
+      r.k0 = sb.k0;
+      r.k1 = sb.k1;
+      r.c2 = sb.c2;
+      r.c3 = sb.c3;
+      const unsigned long long bk = quad_exact_block<STEP0>(r, t_loc, t_scale, loc_s, scale_s,
+                                                             lognorm, best, n_cand, logtab);
+      if (lane == 0) kmax = bk;
+      wave_lds_sync();
+    }
+    if (state != kQuadKnown) {  // ArgMaxTupleReducer: a key at the clamp level is index 0
+      const unsigned long long kb = kmax;
+      idx = (kb >> 32) > kArgmaxClampOrd ? argmax_key_index(kb) : 0u;
     }
     if (lane == 0) out_idx[g * n_steps + step] = (int32_t)idx;
-#if CWQ_ONE_FIN
-    if (FULL && fbest && (int)lane < db) {  // k_small_finalize's work for this block (:63, :292)
-      const int64_t i = off + (int64_t)lane;
-      const float zz = exact_normal(sb, (uint64_t)idx * (uint64_t)db + lane, logtab);
-      float sv = scale_s[i] * zz;  // misc.py:14
-      sv = loc_s[i] + sv;          // misc.py:15
-      const float b = (STEP0 ? 0.0f : fbest[i]) + sv;
-      fbest[i] = b;
-      if (ds_out) {
-        const float m = ds_scale[i] * b;
-        ds_out[i] = m + ds_loc[i];
-      }
-    }
-#endif
-#if defined(CWQ_QUAD_TIMES) && defined(CWQ_QUAD_FINE)
-    if (kTimes && lane == 0u && g < kQuadTimes) {
-      const unsigned long long t = __builtin_amdgcn_s_memrealtime();
-      g_quad_t[g][5] = t;
-    }
-#elif defined(CWQ_QUAD_TIMES)
-    if (kTimes && lane == 0u && g < kQuadTimes)
+#ifdef CWQ_QUAD_TIMES
+    if (lane == 0u && g < kQuadTimes)
       g_quad_t[g][2] = g_quad_t[g][3] = g_quad_t[g][4] = g_quad_t[g][5] =
           __builtin_amdgcn_s_memrealtime();
 #endif
-  }
-}
-
-
-template <bool STEP0>
-__global__ void __launch_bounds__(64 * CWQ_ONE_WPG, CWQ_FUSED_WAVES) k_small_one(
-    const float* __restrict__ t_loc, const float* __restrict__ t_scale,
-    const float* __restrict__ loc_s, const float* __restrict__ scale_s,
-    const float* __restrict__ lognorm, const float* __restrict__ best,
-    const SmallRec* __restrict__ rec, const float2* __restrict__ pre_ab, int64_t nb, int64_t u0,
-    int64_t n_cand, int32_t step, int n_steps, int32_t* __restrict__ out_idx,
-    uint32_t* __restrict__ rare, float* __restrict__ fbest, float* __restrict__ ds_out,
-    const float* __restrict__ ds_loc, const float* __restrict__ ds_scale) {
-  // every wave of the workgroup its own block and its own LDS (no barrier
-  // between the waves: a wave whose block is past nb just ends)
-  constexpr int W = CWQ_ONE_WPG;
-  __shared__ double logtab_w[W][32];
-  // the block's (sA, sB) repeated 4 times: a lane's span of 4 rows is 4 d
-  // normals, so Philox block b covers abx[4 b .. 4 b + 3] (two b128 reads,
-  // issued ahead of the Philox rounds that hide their latency)
-  __shared__ float4 abx_w[W][2 * CWQ_FUSED_DMAX];
-  __shared__ uint32_t ln_w[W][CWQ_FUSED_LIST];
-  __shared__ float lu_w[W][CWQ_FUSED_LIST];
-  __shared__ float lpv_w[W][CWQ_SMALL_RARE ? 1 : CWQ_FUSED_STAGE];
-  __shared__ unsigned long long kmax_w[W];
-  const int wv = W == 1 ? 0 : (int)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-  const uint32_t lane = threadIdx.x & 63u;
-  const int64_t g = u0 + (int64_t)blockIdx.x * W + wv;
-  if (W > 1 && g >= nb) return;
-  if (lane < 32) logtab_w[wv][lane] = kLogTabConst[lane];
-#if CWQ_ONE_GRID
-  // a fixed grid, each wave striding the chunk's blocks
-  const int64_t u1 = nb - u0 < (1LL << 30) ? nb : u0 + (1LL << 30);
-  for (int64_t gg = g; gg < u1; gg += (int64_t)gridDim.x * W)
-    small_block<STEP0, !CWQ_SMALL_RARE>(gg, t_loc, t_scale, loc_s, scale_s, lognorm, best, rec,
-                                        pre_ab, n_cand, step, n_steps, out_idx, rare,
-                                        logtab_w[wv], abx_w[wv], ln_w[wv], lu_w[wv], lpv_w[wv],
-                                        kmax_w[wv]);
-#else
-  small_block<STEP0, !CWQ_SMALL_RARE>(g, t_loc, t_scale, loc_s, scale_s, lognorm, best, rec,
-                                      pre_ab, n_cand, step, n_steps, out_idx, rare,
-                                      logtab_w[wv], abx_w[wv], ln_w[wv], lu_w[wv], lpv_w[wv],
-                                      kmax_w[wv], fbest, ds_out, ds_loc, ds_scale);
-#endif
-}
-
-// The blocks k_small_one put on the rare list: the same screen again (the same
-// list), then the exact scoring of the listed rows or of the whole block.  A
-// wave per listed block; the grid's waves stride the list, whose length only
-// the device knows.
-template <bool STEP0>
-__global__ void __launch_bounds__(64, CWQ_FUSED_WAVES) k_small_rare(
-    const float* __restrict__ t_loc, const float* __restrict__ t_scale,
-    const float* __restrict__ loc_s, const float* __restrict__ scale_s,
-    const float* __restrict__ lognorm, const float* __restrict__ best,
-    const SmallRec* __restrict__ rec, const float2* __restrict__ pre_ab, int64_t n_cand,
-    int32_t step, int n_steps, int32_t* __restrict__ out_idx, uint32_t* __restrict__ rare) {
-  __shared__ double logtab[32];
-  __shared__ float4 abx[2 * CWQ_FUSED_DMAX];
-  __shared__ uint32_t ln[CWQ_FUSED_LIST];
-  __shared__ float lu[CWQ_FUSED_LIST];
-  __shared__ float lpv[CWQ_FUSED_STAGE];
-  __shared__ unsigned long long kmax;
-  const uint32_t lane = threadIdx.x & 63u;
-  const uint32_t n = rare[0];
-  if (blockIdx.x >= n) return;
-  if (lane < 32) logtab[lane] = kLogTabConst[lane];
-  for (uint32_t i = blockIdx.x; i < n; i += gridDim.x)
-    small_block<STEP0, true>((int64_t)rare[1 + i], t_loc, t_scale, loc_s, scale_s, lognorm, best,
-                             rec, pre_ab, n_cand, step, n_steps, out_idx, rare, logtab, abx, ln,
-                             lu, lpv, kmax);
-}
-
-// Max over the 32 lanes of each half-wave (DPP rows 0-1 and 2-3); full exec
-// mask.  Four row steps leave every lane with its row's max, row_bcast:15
-// folds row 0 into row 1 and row 2 into row 3.
-__device__ __forceinline__ float half_max_f32(float v, uint32_t h) {
-#if CWQ_WAVE_MAX_ASM
-  CWQ_DPP_MAX_STEP(v, "quad_perm:[1,0,3,2]", "0xf");
-  CWQ_DPP_MAX_STEP(v, "quad_perm:[2,3,0,1]", "0xf");
-  CWQ_DPP_MAX_STEP(v, "row_half_mirror", "0xf");
-  CWQ_DPP_MAX_STEP(v, "row_mirror", "0xf");
-  CWQ_DPP_MAX_STEP(v, "row_bcast:15", "0xa");
-  asm volatile("s_nop 1" : "+v"(v));
-#else
-  v = dpp_max_step<0xb1, 0xf>(v);
-  v = dpp_max_step<0x4e, 0xf>(v);
-  v = dpp_max_step<0x141, 0xf>(v);
-  v = dpp_max_step<0x140, 0xf>(v);
-  v = dpp_max_step<0x142, 0xa>(v);
-#endif
-  const float a = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 31));
-  const float b = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 63));
-  return h ? b : a;
-}
-__device__ __forceinline__ uint32_t half_bits(uint64_t m, uint32_t h) {
-  return (uint32_t)(m >> (32u * h));
-}
-
-// k_small_one for two blocks per wave: half-wave h (lanes 32 h .. 32 h + 31)
-// screens block 2 w + h, each lane taking 4-row spans of rows 4 (lane + 32 m).
-// The same spans, bounds and lists as small_block<STEP0, false>: the final τ
-// is the max over the same spans' lower bounds, so the rows kept at the end
-// are the same; a block whose longer list (rows 0..127 were listed against a
-// lower τ) overflows goes to the rare list, which scores it in full as
-// k_small_one would.  Halves a launch's waves: k_small_one is bound by the
-// rate at which waves start (§5e of DESIGN.md), not by their work.
-template <bool STEP0>
-__global__ void __launch_bounds__(64, CWQ_PAIR_WAVES) k_small_pair(
-    const SmallRec* __restrict__ rec, const float2* __restrict__ pre_ab, int64_t nb, int64_t u0,
-    int64_t n_cand, int32_t step, int n_steps, int32_t* __restrict__ out_idx,
-    uint32_t* __restrict__ rare) {
-  __shared__ float4 abx[2][2 * CWQ_FUSED_DMAX];
-  __shared__ uint32_t ln[2][CWQ_FUSED_LIST];
-  __shared__ float lu[2][CWQ_FUSED_LIST];
-  const uint32_t lane = threadIdx.x & 63u;
-  const uint32_t h = lane >> 5, hl = lane & 31u;
-  const int64_t g = u0 + 2 * (int64_t)blockIdx.x + h;
-  const bool live = g < nb;
-  const int64_t gs = live ? g : nb - 1;  // a half past the end reads a valid record
-  const uint4 q0 = rec[gs].q0, q1 = rec[gs].q1, q2 = rec[gs].q2;
-  const uint32_t q3x = rec[gs].q3.x;
-  const int64_t off = (int64_t)(((uint64_t)q0.y << 32) | q0.x);
-  const int db = (int)q0.z;
-  uint32_t state = live ? q0.w : kQuadKnown;
-  bool scr = state == kQuadListed;  // this half still screening
-  uint32_t idx = 0u;
-  float4* ab = abx[h];
-  if (scr) {
-    float2* ax = (float2*)ab;
-    for (int j = (int)hl; j < db; j += 32) {  // d <= 64 (launch_small)
-      const float2 e = pre_ab[off + j];
-      for (int r = 0; r < 4; ++r) ax[r * db + j] = e;
-    }
-  }
-  wave_lds_sync();
-  const float bfb = u2f(q2.x), c1b = u2f(q2.y), c2b = u2f(q2.z), asb = u2f(q2.w), pqb = u2f(q3x);
-  // philox_lo_key with per-half (vector) stream words
-  const uint32_t sk0 = q1.x, sk1 = q1.y, sc2 = q1.z, sc3 = q1.w;
-  PhiloxLo K;
-  {
-    const uint64_t p1 = (uint64_t)kPhiloxM1 * sc2;
-    const uint32_t n0 = (uint32_t)(p1 >> 32) ^ sk0;
-    const uint64_t qq0 = (uint64_t)kPhiloxM0 * n0;
-    K.A = sc3 ^ sk1;
-    K.B = (uint32_t)p1 ^ (sk0 + kPhiloxW0);
-    K.C = (uint32_t)(qq0 >> 32) ^ (sk1 + kPhiloxW1);
-    K.D = (uint32_t)qq0 ^ (sk1 + 2u * kPhiloxW1);
-  }
-  const int dl = scr ? db : 0;
-  const int dmax = max(__builtin_amdgcn_readlane(dl, 0), __builtin_amdgcn_readlane(dl, 32));
-  float tau = -__builtin_inff();
-  uint32_t used = 0;
-  for (int64_t m0 = 0; 128 * m0 < n_cand; ++m0) {
-    const int64_t ns = 4 * ((int64_t)hl + 32 * m0);
-    const uint32_t b0 = (uint32_t)((uint64_t)ns * (uint64_t)db / 4u);
-    float rs[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-    float cur = 0.0f;
-    int j = 0, qd = 0;
-    for (int b = 0; b < dmax; ++b) {
-      if (b < dl) {
-        const float4 e01 = ab[2 * b], e23 = ab[2 * b + 1];
-        const U4 x = philox10_lo(b0 + (uint32_t)b, K, sk0, sk1);
-        float z[4];
-        box_muller_screen(x.x, x.y, z[0], z[1]);
-        box_muller_screen(x.z, x.w, z[2], z[3]);
-        const float2 ev[4] = {float2{e01.x, e01.y}, float2{e01.z, e01.w},
-                              float2{e23.x, e23.y}, float2{e23.z, e23.w}};
-#pragma unroll
-        for (int tt = 0; tt < 4; ++tt) {
-          const float2 e = ev[tt];
-          const float a = __builtin_fmaf(e.x, z[tt], e.y);
-          cur = __builtin_fmaf(-a, a, cur);
-          if (++j == db) {
-            if (qd == 0) rs[0] = cur;
-            else if (qd == 1) rs[1] = cur;
-            else if (qd == 2) rs[2] = cur;
-            else rs[3] = cur;
-            cur = 0.0f;
-            j = 0;
-            ++qd;
-          }
-        }
-      }
-    }
-    float smax = -__builtin_inff();
-    bool any = false;
-#pragma unroll
-    for (int qq = 0; qq < 4; ++qq)
-      if (ns + qq < n_cand) {
-        smax = fmaxf(smax, rs[qq]);
-        any = true;
-      }
-    const float lower = (scr && any) ? __builtin_fmaf(smax, c2b, asb) -
-                                           pqb * __builtin_amdgcn_sqrtf(-smax)
-                                     : -__builtin_inff();
-    tau = fmaxf(tau, half_max_f32(lower, h));
-    uint64_t m[4];
-    uint32_t cnt = 0;
-#pragma unroll
-    for (int qq = 0; qq < 4; ++qq) {
-      m[qq] = __ballot(scr && ns + qq < n_cand && __builtin_fmaf(rs[qq], c1b, bfb) >= tau);
-      cnt += (uint32_t)__builtin_popcount(half_bits(m[qq], h));
-    }
-    const bool full = scr && used + cnt > CWQ_FUSED_LIST;
-    if (__ballot(full)) {  // drop the rows the raised τ excludes (two entries per lane)
-      const bool h0 = full && hl < used, h1 = full && hl + 32 < used;
-      const uint32_t n0 = ln[h][hl], n1 = ln[h][hl + 32];
-      const float v0 = lu[h][hl], v1 = lu[h][hl + 32];
-      const uint64_t k0 = __ballot(h0 && v0 >= tau), k1 = __ballot(h1 && v1 >= tau);
-      const uint32_t c0 = (uint32_t)__builtin_popcount(half_bits(k0, h));
-      wave_lds_sync();
-      const uint32_t r0 = lane_rank(k0) - (h ? (uint32_t)__builtin_popcount((uint32_t)k0) : 0u);
-      const uint32_t r1 = lane_rank(k1) - (h ? (uint32_t)__builtin_popcount((uint32_t)k1) : 0u);
-      if ((k0 >> lane) & 1ull) {
-        ln[h][r0] = n0;
-        lu[h][r0] = v0;
-      }
-      if ((k1 >> lane) & 1ull) {
-        ln[h][c0 + r1] = n1;
-        lu[h][c0 + r1] = v1;
-      }
-      if (full) used = c0 + (uint32_t)__builtin_popcount(half_bits(k1, h));
-      wave_lds_sync();
-    }
-    if (scr && used + cnt > CWQ_FUSED_LIST) {  // still full (near-ties): the rare path
-      state = kQuadExact;
-      scr = false;
-    }
-    uint32_t at = used;
-#pragma unroll
-    for (int qq = 0; qq < 4; ++qq) {
-      const uint32_t mq = scr ? half_bits(m[qq], h) : 0u;
-      if ((mq >> hl) & 1u) {
-        const uint32_t slot_i = at + (uint32_t)__builtin_popcount(mq & ((1u << hl) - 1u));
-        ln[h][slot_i] = (uint32_t)(ns + qq);
-        lu[h][slot_i] = __builtin_fmaf(rs[qq], c1b, bfb);
-      }
-      at += (uint32_t)__builtin_popcount(mq);
-    }
-    if (scr) used = at;
-    wave_lds_sync();
-  }
-  if (scr) {  // the rows whose upper bound reaches the final τ
-    const bool h0 = hl < used, h1 = hl + 32 < used;
-    const uint64_t k0 = __ballot(scr && h0 && lu[h][h0 ? hl : 0] >= tau);
-    const uint64_t k1 = __ballot(scr && h1 && lu[h][h1 ? hl + 32 : 0] >= tau);
-    const uint32_t a0 = half_bits(k0, h), a1 = half_bits(k1, h);
-    const uint32_t nk = (uint32_t)(__builtin_popcount(a0) + __builtin_popcount(a1));
-    if (nk == 1u) {  // the single listed row is the argmax
-      idx = ln[h][a0 ? (uint32_t)__builtin_ctz(a0) : 32u + (uint32_t)__builtin_ctz(a1)];
-      state = kQuadKnown;
-    }  // else (two or more, or never none): the rare path
-  }
-  if (live && hl == 0u) {
-    if (state == kQuadKnown) out_idx[g * n_steps + step] = (int32_t)idx;
-    else rare[1 + atomicAdd(rare, 1u)] = (uint32_t)g;
   }
 }
 
@@ -3586,7 +3262,7 @@ static bool takes_small_path(const EncodeArgs& a) {  // launch_small's d <= 64 s
          a.max_d <= CWQ_FUSED_DMAX && a.n_cand < 4096;
 }
 static bool small_pipe_ok(const EncodeArgs& a) {  // ... and the pipeline's arrays are there
-  return a.sdmap && a.sab && a.slist && a.ordu && a.nb < (1LL << 32);
+  return a.sdmap && a.sab && a.slist && a.nb < (1LL << 32);
 }
 static bool takes_small_pipe(const EncodeArgs& a) {
   return CWQ_SMALL_PIPE && takes_small_path(a) && small_pipe_ok(a);
@@ -3606,41 +3282,20 @@ static bool launch_small(const EncodeArgs& a, int step, hipStream_t stream) {
       hipLaunchKernelGGL(k_small_prep1<true>, dim3(pgrid), dim3(CWQ_PREP1_THREADS), 0, stream, a.t_loc,
                          a.t_scale, a.p_loc, a.p_scale, nst, sdiv, a.rho, a.loc_s, a.scale_s,
                          a.lognorm, a.out_sample, a.block_off, a.ud, a.nb, seeds_of(a), step,
-                         pab, rec, a.sdmap, a.ordu);
+                         pab, rec, a.sdmap);
     else
       hipLaunchKernelGGL(k_small_prep1<false>, dim3(pgrid), dim3(CWQ_PREP1_THREADS), 0, stream, a.t_loc,
                          a.t_scale, a.p_loc, a.p_scale, nst, sdiv, a.rho, a.loc_s, a.scale_s,
                          a.lognorm, a.out_sample, a.block_off, a.ud, a.nb, seeds_of(a), step,
-                         pab, rec, a.sdmap, a.ordu);
+                         pab, rec, a.sdmap);
     const int64_t nu = a.nb;
-    if (CWQ_SMALL_PAIR && CWQ_SMALL_RARE) {
-      for (int64_t u0 = 0; u0 < nu; u0 += (int64_t)1 << 30) {
-        const int64_t nc = nu - u0 < (1LL << 30) ? nu - u0 : (1LL << 30);
-        hipLaunchKernelGGL((k_small_pair<STEP0>), dim3((unsigned)((nc + 1) / 2)), dim3(64), 0,
-                           stream, rec, a.pre_ab, a.nb, u0, a.n_cand, step, a.n_steps, a.out_idx,
-                           a.ordu);
-      }
-    } else
-    for (int64_t u0 = 0; u0 < nu; u0 += (int64_t)1 << 30) {
-      int64_t nw = ((nu - u0 < (1LL << 30) ? nu - u0 : (1LL << 30)) + CWQ_ONE_WPG - 1) /
-                   CWQ_ONE_WPG;
-      if (CWQ_ONE_GRID && nw > CWQ_ONE_GRID) nw = CWQ_ONE_GRID;
-      hipLaunchKernelGGL((k_small_one<STEP0>), dim3((unsigned)nw),
-                         dim3(64 * CWQ_ONE_WPG), 0, stream, a.t_loc, a.t_scale, a.loc_s, a.scale_s, a.lognorm,
+    for (int64_t u0 = 0; u0 < nu; u0 += (int64_t)1 << 30)
+      hipLaunchKernelGGL((k_small_one<STEP0>),
+                         dim3((unsigned)(nu - u0 < (1LL << 30) ? nu - u0 : (1LL << 30))),
+                         dim3(64), 0, stream, a.t_loc, a.t_scale, a.loc_s, a.scale_s, a.lognorm,
                          a.out_sample, rec, a.pre_ab, a.nb, u0, a.n_cand, step, a.n_steps,
-                         a.out_idx, a.ordu, a.out_sample,
-                         step == a.n_steps - 1 ? a.ds_out : nullptr, a.ds_loc, a.ds_scale);
-    }
-    // the rare list (a.ordu: the pipeline leaves that scratch unused; a forked
-    // part's view is its own)
-    if (CWQ_SMALL_RARE)
-      hipLaunchKernelGGL((k_small_rare<STEP0>),
-                         dim3((unsigned)(a.nb < CWQ_RARE_GRID ? a.nb : CWQ_RARE_GRID)), dim3(64),
-                         0, stream, a.t_loc, a.t_scale, a.loc_s, a.scale_s, a.lognorm,
-                         a.out_sample, rec, a.pre_ab, a.n_cand, step, a.n_steps, a.out_idx,
-                         a.ordu);
+                         a.out_idx);
     const unsigned dgrid = grid_for(a.total_dims > a.nb ? a.total_dims : a.nb, 256, 16384);
-    if (!(CWQ_ONE_FIN && !CWQ_SMALL_RARE && !CWQ_SMALL_PAIR))  // else k_small_one finalizes
     hipLaunchKernelGGL((k_small_finalize<STEP0>), dim3(dgrid), dim3(256), 0, stream, a.loc_s,
                        a.scale_s, rec, a.sdmap, a.out_idx, step, a.n_steps, a.block_off, a.ud,
                        a.nb, a.out_sample, step == a.n_steps - 1 ? a.ds_out : nullptr, a.ds_loc,

@@ -1,6 +1,6 @@
 """Per-quad timeline of one k_small_fused launch (C2-shaped grouped encode; run
 on the GPU box with a -DCWQ_QUAD_TIMES build selected through CWQ_LIB_PATH).
-Usage: CWQ_LIB_PATH=tools/vrun/libcwq_qt.so python tools/quad_times.py [BITS] [D] [--one | --fine]
+Usage: CWQ_LIB_PATH=tools/vrun/libcwq_qt.so python tools/quad_times.py [BITS] [D] [--one]
 --one: the small pipeline's k_small_one (a wave per block; records per block:
 start, after the screen, end).
 Prints the launch span, the quad start times (how many resident rounds the
@@ -19,9 +19,8 @@ import compression_without_quantization_amd as C  # noqa: E402
 from compression_without_quantization_amd import _lib  # noqa: E402
 from compression_without_quantization_amd.synthetic import make_latents  # noqa: E402
 
-ONE = "--one" in sys.argv or "--fine" in sys.argv
-FINE = "--fine" in sys.argv  # a -DCWQ_QUAD_FINE build: record, LDS constants, screen, keep, end
-argv = [a for a in sys.argv if a not in ("--one", "--fine")]
+ONE = "--one" in sys.argv
+argv = [a for a in sys.argv if a != "--one"]
 bits = int(argv[1]) if len(argv) > 1 else 8
 D = int(argv[2]) if len(argv) > 2 else 32 * 48 * 128
 lib = _lib.load()
@@ -50,8 +49,7 @@ ph = np.diff(us, axis=1)  # constants, screen, exact rows, exact blocks, finaliz
 print(f"{G} groups, {nq} {'blocks' if ONE else 'quads'} (waves), span {span:.1f} us")
 print(f"quad duration us: mean {dur.mean():.2f} med {np.median(dur):.2f} p10 "
       f"{np.percentile(dur, 10):.2f} p90 {np.percentile(dur, 90):.2f} max {dur.max():.2f}")
-names = (("record load", "constants to LDS", "screen loop", "list / keep", "exact + index")
-         if FINE else ("screen", "exact", "-", "-", "-") if ONE else
+names = (("screen", "exact", "-", "-", "-") if ONE else
          ("constants", "screen", "exact rows", "exact blocks", "finalize"))
 for i, nm in enumerate(names):
     print(f"  {nm:13s}: mean {ph[:, i].mean():6.2f} us ({ph[:, i].sum() / dur.sum():.1%})")
