@@ -30,8 +30,13 @@ for _ in range(5):
     res = C.code_grouped_greedy_sample_batch(None, T, P, 1, 8, 42)
 torch.cuda.synchronize()
 t0 = time.perf_counter()
+per = []
 for _ in range(n):
     res = C.code_grouped_greedy_sample_batch(None, T, P, 1, 8, 42)
+    per.append(time.perf_counter())
 torch.cuda.synchronize()
 el = time.perf_counter() - t0
+if os.environ.get("CWQ_BENCH_STEP_TIMES"):
+    print("step ms:", " ".join(f"{(b - a) * 1e3:.2f}" for a, b in zip([t0] + per, per)),
+          flush=True)
 print(f"{n} calls, {el / n * 1e3:.3f} ms per call, {24 * n / el:.0f} images/s", flush=True)
