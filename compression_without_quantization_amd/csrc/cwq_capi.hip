@@ -16,8 +16,10 @@
 #include <atomic>
 #include <memory>
 #include <condition_variable>
+#include <functional>
 #include <mutex>
 #include <sched.h>
+#include <unistd.h>
 #include <stdlib.h>
 #include <thread>
 #include <vector>
@@ -1066,6 +1068,72 @@ int64_t host_threads() {
   }();
   return n;
 }
+// A process-wide pool of host worker threads for the batch call's per-item
+// work (C3: 48 bitcodes), created on first use and kept: creating and joining
+// seven threads per call sat on the call's critical path.  The pool object is
+// never destroyed (its threads sleep on a condition variable through process
+// exit).  run() executes f on up to n pool threads and the calling thread and
+// returns once every one of them has returned; concurrent run()s queue.
+class HostPool {
+ public:
+  static HostPool& get() {
+    static HostPool* p = new HostPool();
+    return *p;
+  }
+  void run(int64_t n, const std::function<void()>& f) {
+    std::lock_guard<std::mutex> one(run_m_);  // one job at a time
+    int64_t started = 0;
+    {
+      std::unique_lock<std::mutex> lk(m_);
+      if (pid_ != getpid()) {  // a forked child has none of the parent's threads
+        pid_ = getpid();
+        threads_ = 0;
+      }
+      while ((int64_t)threads_ < n) {
+        try {
+          std::thread(&HostPool::loop, this, threads_).detach();
+        } catch (...) {
+          break;  // no more threads (pids cgroup): fewer helpers
+        }
+        ++threads_;
+      }
+      started = std::min<int64_t>(n, (int64_t)threads_);
+      job_ = &f;
+      active_ = started;
+      left_ = started;
+      ++gen_;
+    }
+    cv_.notify_all();
+    f();
+    std::unique_lock<std::mutex> lk(m_);
+    done_.wait(lk, [&] { return left_ == 0; });
+    job_ = nullptr;
+  }
+
+ private:
+  void loop(int64_t id) {
+    uint64_t seen = 0;
+    for (;;) {
+      const std::function<void()>* f = nullptr;
+      {
+        std::unique_lock<std::mutex> lk(m_);
+        cv_.wait(lk, [&] { return gen_ != seen; });
+        seen = gen_;
+        if (id >= active_) continue;
+        f = job_;
+      }
+      (*f)();
+      std::lock_guard<std::mutex> lk(m_);
+      if (--left_ == 0) done_.notify_all();
+    }
+  }
+  std::mutex run_m_, m_;
+  std::condition_variable cv_, done_;
+  const std::function<void()>* job_ = nullptr;
+  pid_t pid_ = getpid();
+  uint64_t gen_ = 0;
+  int64_t threads_ = 0, active_ = 0, left_ = 0;
+};
 // Chunks a batch is pipelined in (CWQ_BATCH_CHUNKS, default below): the host
 // phases of one chunk run while the device codes another.
 #ifndef CWQ_BATCH_CHUNKS
@@ -1302,16 +1370,10 @@ int64_t batch_device_path(int64_t n_items, const int64_t* item_off, int64_t D, i
       if (o.item_ready) __atomic_store_n(o.item_ready + i, 1, __ATOMIC_RELEASE);
     }
   };
-  std::vector<std::thread> pool;
   if (rc == CWQ_OK) {
     const int64_t nw = std::min<int64_t>(host_threads() - 1, n_items - 1);
-    try {
-      for (int64_t t = 0; t < nw; ++t) pool.emplace_back(bits_worker);
-    } catch (...) {
-    }
-    bits_worker();
+    HostPool::get().run(nw > 0 ? nw : 0, bits_worker);
   }
-  for (auto& th : pool) th.join();
   lap("bits written");
   drain();
   lap("drained");
