@@ -1487,10 +1487,14 @@ int64_t cwq_code_grouped_greedy_batch(
   std::vector<int64_t> ci;  // chunk c = items [ci[c], ci[c + 1])
   {
     const int64_t K = D < (1 << 16) ? 1 : std::min<int64_t>(batch_chunks(), n_items);
+    // the first and the last chunk a quarter share each: the device starts
+    // early, and what follows its last launch (the last chunk's result copies,
+    // bitcodes and Python strings) is short.  Boundary c (1 <= c < K) at
+    // D (c - 3/4) / (K - 3/2); one chunk when K == 1
     ci.push_back(0);
-    for (int64_t i = 1; i < n_items; ++i) {
-      const int64_t c = (int64_t)ci.size();  // boundary c at D (c - 3/4) / (K - 3/4)
-      if (c < K && item_off[i] * (4 * K - 3) >= D * (4 * c - 3) &&
+    for (int64_t i = 1; i < n_items && K > 1; ++i) {
+      const int64_t c = (int64_t)ci.size();
+      if (c < K && item_off[i] * (4 * K - 6) >= D * (4 * c - 3) &&
           item_off[i] > item_off[ci.back()])
         ci.push_back(i);
     }
