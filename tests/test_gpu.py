@@ -691,15 +691,15 @@ def test_csr_pruned_adversarial(cwq, cwqlib, oracle, kind):
                                   "posterior_is_prior", "inf_scale", "zero_scale", "nan_scale",
                                   "nan_loc_one_dim"])
 @pytest.mark.parametrize("bits,n_steps", [(6, 1), (8, 2), (11, 1)])
-@pytest.mark.parametrize("path", ["fused", "three_kernel"])
+@pytest.mark.parametrize("path", ["pipeline", "three_kernel"])
 def test_small_path_adversarial(cwq, cwqlib, oracle, kind, bits, n_steps, path):
     """The screened small-candidate paths (64 <= 2^b < 4096) on
     ragged groups (an empty one included): near-ties everywhere overflow the
     survivor list (exact fallback), non-finite or out-of-range constants fail
-    the gate (exact fallback); every mode equals the oracle.  "fused": every
-    block <= 64 dims, so k_small_fused takes the launch (its step-0 constants
-    from the prep launch, later steps computed in the kernel); "three_kernel":
-    a 130-dim block sends it to k_small_prep/screen/survivors."""
+    the gate (exact fallback); every mode equals the oracle.  "pipeline": every
+    block <= 64 dims, so the small pipeline takes the launch (k_small_prep1,
+    k_small_one, k_small_finalize); "three_kernel": a 130-dim block sends it to
+    k_small_prep/screen/survivors."""
     rng = np.random.default_rng(sum(map(ord, kind)) + bits)
     sizes = [3, 20, 1, 45, 0, 7, 64, 130] if path == "three_kernel" else \
         [3, 20, 1, 45, 0, 7, 64, 33, 64, 2, 0, 0, 5]

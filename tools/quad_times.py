@@ -1,12 +1,11 @@
-"""Per-quad timeline of one k_small_fused launch (C2-shaped grouped encode; run
+"""Per-block timeline of one k_small_one launch (C2-shaped grouped encode; run
 on the GPU box with a -DCWQ_QUAD_TIMES build selected through CWQ_LIB_PATH).
 Usage: CWQ_LIB_PATH=tools/vrun/libcwq_qt.so python tools/quad_times.py [BITS] [D] [--one]
---one: the small pipeline's k_small_one (a wave per block; records per block:
-start, after the screen, end).
-Prints the launch span, the quad start times (how many resident rounds the
-grid makes), per-phase durations (constants, screen, exact rows, exact
-blocks, finalize), how many quads run at once over time, and per-XCD /
-per-SIMD spread."""
+Each wave (block) records its start, the end of its screen and its end
+(s_memrealtime).  Prints the launch span, the start-time percentiles, how many
+waves run at once over time, per-XCD / per-SIMD spread and durations by block
+length.  (--one is the only layout since round 5; round 4's four-block
+k_small_fused quads are gone, and the flag is kept for old command lines.)"""
 import ctypes
 import os
 import sys
@@ -19,7 +18,7 @@ import compression_without_quantization_amd as C  # noqa: E402
 from compression_without_quantization_amd import _lib  # noqa: E402
 from compression_without_quantization_amd.synthetic import make_latents  # noqa: E402
 
-ONE = "--one" in sys.argv
+ONE = True  # a wave per block (k_small_one)
 argv = [a for a in sys.argv if a != "--one"]
 bits = int(argv[1]) if len(argv) > 1 else 8
 D = int(argv[2]) if len(argv) > 2 else 32 * 48 * 128

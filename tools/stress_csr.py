@@ -46,7 +46,8 @@ VERBOSE = bool(os.environ.get("STRESS_VERBOSE"))
 # kernel (>= 4096 candidates); STRESS_BITS=6,11 the screened small-candidate path
 BITS_LO, BITS_HI = (int(v) for v in os.environ.get("STRESS_BITS", "12,16").split(","))
 # STRESS_SMALL=1: short groups only (d <= 128; all <= 64 in a third of the trials:
-# k_small_fused with STRESS_BITS=6,11)
+# the small pipeline k_small_prep1 / k_small_one / k_small_finalize with
+# STRESS_BITS=6,11)
 SMALL = bool(os.environ.get("STRESS_SMALL"))
 
 
