@@ -253,11 +253,16 @@ int64_t cwq_code_grouped_greedy_end(const int32_t* idx_host, int64_t G, int n_st
  * == 0) and is coded exactly as cwq_code_grouped_greedy on that slice with seed
  * seeds[i] (HOST int32 [n_items]): its own partition (:207-252), its groups
  * numbered from 0 and coded with seeds[i] + g (:273-284).  One standardisation
- * and KL launch serve all items; the items are then pipelined in chunks of
- * consecutive items (CWQ_BATCH_CHUNKS, about D_total / 6 dims each): chunk
- * c's KL arrives on the host, host threads partition it and lay out its groups
- * while the device codes chunk c - 1 (one encode launch sequence per chunk,
- * per-block seeds), and chunk c - 1's bitcodes are written while chunk c codes.
+ * and KL launch serve all items, and one device partition (cwq_partition.hip)
+ * finds every item's groups (when the device scheme does not cover an input,
+ * the host loop partitions chunk by chunk instead, with identical results).
+ * The items are then pipelined in chunks of consecutive items
+ * (CWQ_BATCH_CHUNKS, default 6; the first and the last a quarter share): one
+ * encode launch sequence per chunk with per-block seeds, chunk c's results
+ * copied to the host while chunk c + 1 codes, and each item's bitcode written
+ * as soon as its chunk's indices arrive, on a pool of host threads (up to
+ * CWQ_HOST_THREADS - 1, default min(8, CPUs) - 1) that the library creates on
+ * the first batch call and keeps for the life of the process.
  * HOST outputs: sample_host [D_total]; item i's bitcode at
  * bits_host[bits_off[i], bits_off[i+1]) (bits_off: HOST int64 [n_items + 1],
  * written); item i's group_start_indices (local, incl. its trailing D_i):
