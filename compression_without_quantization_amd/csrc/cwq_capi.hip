@@ -1854,9 +1854,8 @@ GroupedImpWs grouped_imp_ws(int64_t D) {
   l.total = o;
   return l;
 }
-thread_local std::vector<float> g_imp_kl, g_imp_ts, g_imp_out;
-thread_local std::vector<uint8_t> g_imp_keep;
-thread_local std::vector<int64_t> g_imp_ns;
+thread_local PinnedTl tl_imp_pin;             // cwq_code_grouped_importance's host staging
+thread_local std::vector<char> tl_imp_pageable;  // ... when page-locked memory is unavailable
 }  // namespace
 
 size_t cwq_code_grouped_importance_workspace_size(int64_t D) {
@@ -1926,43 +1925,67 @@ int64_t cwq_code_grouped_importance(const float* q_loc, const float* q_scale,
   if ((e = hipMemsetD32Async((hipDeviceptr_t)ones, 0x3f800000u, (size_t)D, s)) != hipSuccess)
     return hip_fail(e, "memset");
   if ((rc = cwq_kl_normal_normal(t_loc, t_scale, zeros, ones, D, kl2, stream)) < 0) return rc;
-  g_imp_kl.resize((size_t)D);
-  g_imp_keep.resize((size_t)D);
-  g_imp_ts.resize((size_t)D);
-  if ((e = hipMemcpyAsync(g_imp_kl.data(), kl2, (size_t)D * 4, hipMemcpyDeviceToHost, s)) !=
-          hipSuccess ||
-      (e = hipMemcpyAsync(g_imp_keep.data(), keep, (size_t)D, hipMemcpyDeviceToHost, s)) !=
-          hipSuccess ||
-      (e = hipMemcpyAsync(g_imp_ts.data(), tsamp, (size_t)D * 4, hipMemcpyDeviceToHost, s)) !=
-          hipSuccess)
+  // the host side's arrays in this thread's page-locked staging (pageable
+  // memory is staged by the runtime: I1's 2.9 MB of copies took ~0.5 ms more),
+  // waits polled on events (a blocking wait's wake-up cost I2's small calls
+  // ~0.1 ms each)
+  const size_t Dz = (size_t)D;
+  size_t ho = 0;
+  auto htake = [&](size_t b) {
+    const size_t at = ho;
+    ho = align_up(ho + b, 256);
+    return at;
+  };
+  const size_t o_kl = htake(Dz * 4), o_ts = htake(Dz * 4), o_out = htake(Dz * 4),
+               o_keep = htake(Dz), o_idx = htake((Dz + 1) * 8), o_offs = htake((Dz + 2) * 8),
+               o_ns = htake((Dz + 1) * 8);
+  char* hp = (char*)tl_imp_pin.get(ho, ho + ho / 4);
+  if (!hp) {  // no page-locked memory: pageable staging (slower copies)
+    tl_imp_pageable.resize(ho);
+    hp = tl_imp_pageable.data();
+  }
+  float* kl_h = (float*)(hp + o_kl);
+  float* ts_h = (float*)(hp + o_ts);
+  float* out_h = (float*)(hp + o_out);
+  uint8_t* keep_h = (uint8_t*)(hp + o_keep);
+  int64_t* idx_h = (int64_t*)(hp + o_idx);
+  int64_t* offs_h = (int64_t*)(hp + o_offs);
+  int64_t* ns_h = (int64_t*)(hp + o_ns);
+  CallEvents hev;
+  if (!hev.made(2, s, hipEventDisableTiming))
+    return fail(CWQ_ERR_HIP, "cwq_code_grouped_importance: event creation failed");
+  if ((e = hipMemcpyAsync(kl_h, kl2, Dz * 4, hipMemcpyDeviceToHost, s)) != hipSuccess ||
+      (e = hipMemcpyAsync(keep_h, keep, Dz, hipMemcpyDeviceToHost, s)) != hipSuccess ||
+      (e = hipMemcpyAsync(ts_h, tsamp, Dz * 4, hipMemcpyDeviceToHost, s)) != hipSuccess ||
+      (e = hipEventRecord(hev.ev[0], s)) != hipSuccess) {
+    (void)hipStreamSynchronize(s);
     return hip_fail(e, "to host");
-  if ((e = hipStreamSynchronize(s)) != hipSuccess) return hip_fail(e, "sync");
+  }
+  if ((e = wait_event(hev.ev[0])) != hipSuccess) return hip_fail(e, "sync");
   int64_t no = 0;
   for (int64_t j = 0; j < D; ++j)
-    if (!g_imp_keep[(size_t)j]) {
+    if (!keep_h[j]) {
       outlier_idx_host[no] = j;
-      outlier_val_host[no] = g_imp_ts[(size_t)j];
+      outlier_val_host[no] = ts_h[j];
       ++no;
     }
   *n_outliers = no;
   if (kl_sum_out) {  // log line only
     double t = 0.0;
-    for (int64_t j = 0; j < D; ++j) t += (double)g_imp_kl[(size_t)j];
+    for (int64_t j = 0; j < D; ++j) t += (double)kl_h[j];
     *kl_sum_out = t;
   }
   // :164-203 the sequential partition (strict >), :48-51 ceil(exp(sum KL)) per group
-  const int64_t n = group_starts_impl(g_imp_kl.data(), D, size_threshold, n_nats, starts_host,
-                                      starts_cap, true);
+  const int64_t n = group_starts_impl(kl_h, D, size_threshold, n_nats, starts_host, starts_cap,
+                                      true);
   if (n < 0) return n;
   const int64_t G = n - 1;
-  g_imp_ns.resize((size_t)(G > 0 ? G : 1));
-  if ((rc = cwq_importance_plan(g_imp_kl.data(), starts_host, G, g_imp_ns.data())) < 0)
-    return rc;
+  if ((rc = cwq_importance_plan(kl_h, starts_host, G, ns_h)) < 0) return rc;
   if (G > 0) {
-    if ((e = hipMemcpyAsync(offs, starts_host, (size_t)(G + 1) * 8, hipMemcpyHostToDevice, s)) !=
+    memcpy(offs_h, starts_host, (size_t)(G + 1) * 8);
+    if ((e = hipMemcpyAsync(offs, offs_h, (size_t)(G + 1) * 8, hipMemcpyHostToDevice, s)) !=
             hipSuccess ||
-        (e = hipMemcpyAsync(nsamp, g_imp_ns.data(), (size_t)G * 8, hipMemcpyHostToDevice, s)) !=
-            hipSuccess)
+        (e = hipMemcpyAsync(nsamp, ns_h, (size_t)G * 8, hipMemcpyHostToDevice, s)) != hipSuccess)
       return hip_fail(e, "plan to device");
     // :212-245 every group's importance coder, seed + g; eval_ms_out: its
     // launches timed with events of this call (the call synchronises anyway)
@@ -1989,15 +2012,16 @@ int64_t cwq_code_grouped_importance(const float* q_loc, const float* q_scale,
   }
   // :265 rescale, :267 outliers keep their target draw
   if ((rc = cwq_destandardise(sample, p_loc, p_scale, D, out, stream)) < 0) return rc;
-  g_imp_out.resize((size_t)D);
-  if ((G > 0 && (e = hipMemcpyAsync(index_host, idx, (size_t)G * 8, hipMemcpyDeviceToHost, s)) !=
+  if ((G > 0 && (e = hipMemcpyAsync(idx_h, idx, (size_t)G * 8, hipMemcpyDeviceToHost, s)) !=
                     hipSuccess) ||
-      (e = hipMemcpyAsync(g_imp_out.data(), out, (size_t)D * 4, hipMemcpyDeviceToHost, s)) !=
-          hipSuccess)
+      (e = hipMemcpyAsync(out_h, out, Dz * 4, hipMemcpyDeviceToHost, s)) != hipSuccess ||
+      (e = hipEventRecord(hev.ev[1], s)) != hipSuccess) {
+    (void)hipStreamSynchronize(s);
     return hip_fail(e, "to host");
-  if ((e = hipStreamSynchronize(s)) != hipSuccess) return hip_fail(e, "sync");
-  for (int64_t j = 0; j < D; ++j)
-    sample_host[j] = g_imp_keep[(size_t)j] ? g_imp_out[(size_t)j] : g_imp_ts[(size_t)j];
+  }
+  if ((e = wait_event(hev.ev[1])) != hipSuccess) return hip_fail(e, "sync");
+  if (G > 0) memcpy(index_host, idx_h, (size_t)G * 8);
+  for (int64_t j = 0; j < D; ++j) sample_host[j] = keep_h[j] ? out_h[j] : ts_h[j];
   cwq::set_error(CWQ_OK, "");
   return G;
 }
