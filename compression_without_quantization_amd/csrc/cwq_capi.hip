@@ -1910,21 +1910,15 @@ int64_t cwq_code_grouped_importance(const float* q_loc, const float* q_scale,
     starts_host[0] = 0;
     return ok();
   }
-  // :137-138 standardise; :142 KL(target || proposal); :144-148 outliers
-  if ((rc = cwq_standardise(q_loc, q_scale, p_loc, p_scale, D, t_loc, t_scale, stream)) < 0)
-    return rc;
-  if ((rc = cwq_kl_normal_normal(q_loc, q_scale, p_loc, p_scale, D, kl, stream)) < 0) return rc;
-  if ((e = cwq::launch_imp_outliers(kl, D, dim_kl_bit_limit, t_loc, t_scale, keep, s)) !=
-      hipSuccess)
-    return hip_fail(e, "outliers");
+  // :137-138 standardise; :142 KL(target || proposal); :144-148 outliers;
+  // :160-163 KL of the standardised target against N(0, 1): one launch
+  (void)kl;
+  if ((e = cwq::launch_imp_grouped_prep(q_loc, q_scale, p_loc, p_scale, D, dim_kl_bit_limit,
+                                        t_loc, t_scale, keep, zeros, ones, kl2, s)) != hipSuccess)
+    return hip_fail(e, "standardise / KL / outliers");
   // :150 the outlier dims' target draw, seeded [seed - 1, 42]
   const int32_t s1 = (int32_t)((uint32_t)seed - 1u);
   if ((rc = cwq_stateless_normal_sample(q_loc, q_scale, D, 1, s1, tsamp, stream)) < 0) return rc;
-  // :160-163 KL of the standardised target against N(0, 1)
-  if ((e = hipMemsetAsync(zeros, 0, (size_t)D * 4, s)) != hipSuccess) return hip_fail(e, "memset");
-  if ((e = hipMemsetD32Async((hipDeviceptr_t)ones, 0x3f800000u, (size_t)D, s)) != hipSuccess)
-    return hip_fail(e, "memset");
-  if ((rc = cwq_kl_normal_normal(t_loc, t_scale, zeros, ones, D, kl2, stream)) < 0) return rc;
   // the host side's arrays in this thread's page-locked staging (pageable
   // memory is staged by the runtime: I1's 2.9 MB of copies took ~0.5 ms more),
   // waits polled on events (a blocking wait's wake-up cost I2's small calls

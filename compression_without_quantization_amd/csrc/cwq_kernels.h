@@ -114,6 +114,12 @@ hipError_t launch_destandardise(const float* sample, const float* p_loc, const f
                                 int64_t n, float* out, hipStream_t stream);
 // standardise + KL + the standard prior's zeros/ones + nz zeroed u64 at zinfo
 // (nz <= 256), one launch (the grouped coder's first step)
+// the grouped importance coder's standardise + KL + outliers + standard prior
+// + KL against N(0, 1), one launch (cwq_code_grouped_importance)
+hipError_t launch_imp_grouped_prep(const float* q_loc, const float* q_scale, const float* p_loc,
+                                   const float* p_scale, int64_t n, float limit, float* t_loc,
+                                   float* t_scale, uint8_t* keep, float* zeros, float* ones,
+                                   float* kl2, hipStream_t stream);
 hipError_t launch_grouped_prep(const float* q_loc, const float* q_scale, const float* p_loc,
                                const float* p_scale, int64_t n, float* t_loc, float* t_scale,
                                float* kl, float* zeros, float* ones, unsigned long long* zinfo,

@@ -2978,6 +2978,40 @@ __global__ void __launch_bounds__(256) k_grouped_prep(
   }
 }
 
+// The grouped importance coder's first launch (coded_importance_sampler.py:
+// 137-148, 160-163) in one pass: the standardised target (k_standardise's
+// expressions), the per-dim KL (k_kl_normal_normal's) and the outlier test
+// (k_imp_outliers': bits = kl / np.float32(log 2) <= limit, NaN an outlier,
+// outliers standardised to N(0, 1)), the standard prior's zeros and ones, and
+// the KL of the (masked) standardised target against N(0, 1), which is what
+// the partition and the plan read.
+__global__ void __launch_bounds__(256) k_imp_grouped_prep(
+    const float* __restrict__ q_loc, const float* __restrict__ q_scale,
+    const float* __restrict__ p_loc, const float* __restrict__ p_scale, int64_t n, float limit,
+    float* __restrict__ t_loc, float* __restrict__ t_scale, uint8_t* __restrict__ keep,
+    float* __restrict__ zeros, float* __restrict__ ones, float* __restrict__ kl2) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const float ql = q_loc[i], qs = q_scale[i], pl = p_loc[i], ps = p_scale[i];
+    const float dl = ql - pl;
+    float tl = dl / ps;
+    float ts = qs / ps;
+    const float kl = kl_normal_normal_1(ql, qs, pl, ps);
+    const float bits = kl / 0.6931472f;
+    const bool k = bits <= limit;
+    if (!k) {
+      tl = 0.0f;
+      ts = 1.0f;
+    }
+    t_loc[i] = tl;
+    t_scale[i] = ts;
+    keep[i] = k ? 1 : 0;
+    zeros[i] = 0.0f;
+    ones[i] = 1.0f;
+    kl2[i] = kl_normal_normal_1(tl, ts, 0.0f, 1.0f);
+  }
+}
+
 __global__ void __launch_bounds__(256) k_destandardise(const float* sample,
                                                        const float* __restrict__ p_loc,
                                                        const float* __restrict__ p_scale,
@@ -3618,6 +3652,17 @@ hipError_t launch_grouped_prep(const float* q_loc, const float* q_scale, const f
   hipLaunchKernelGGL(k_grouped_prep, dim3(n > 0 ? grid_for(n, 256, 65536) : 1u), dim3(256), 0,
                      stream, q_loc, q_scale, p_loc, p_scale, n, t_loc, t_scale, kl, zeros, ones,
                      zinfo, nz);
+  return hipGetLastError();
+}
+
+hipError_t launch_imp_grouped_prep(const float* q_loc, const float* q_scale, const float* p_loc,
+                                   const float* p_scale, int64_t n, float limit, float* t_loc,
+                                   float* t_scale, uint8_t* keep, float* zeros, float* ones,
+                                   float* kl2, hipStream_t stream) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_imp_grouped_prep, dim3(grid_for(n, 256, 65536)), dim3(256), 0, stream,
+                     q_loc, q_scale, p_loc, p_scale, n, limit, t_loc, t_scale, keep, zeros, ones,
+                     kl2);
   return hipGetLastError();
 }
 
