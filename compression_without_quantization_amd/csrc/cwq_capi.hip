@@ -1187,9 +1187,11 @@ int64_t batch_device_path(int64_t n_items, const int64_t* item_off, int64_t D, i
   auto lap = [&](const char* what) {
     struct timespec t;
     clock_gettime(CLOCK_MONOTONIC, &t);
-    fprintf(stderr, "[cwq batch dev] %-14s at %8.1f us\n", what,
-            (t.tv_sec - ts_start.tv_sec) * 1e6 + (t.tv_nsec - ts_start.tv_nsec) * 1e-3);
+    fprintf(stderr, "[cwq batch dev] %-14s at %8.1f us (monotonic %.1f us)\n", what,
+            (t.tv_sec - ts_start.tv_sec) * 1e6 + (t.tv_nsec - ts_start.tv_nsec) * 1e-3,
+            t.tv_sec * 1e6 + t.tv_nsec * 1e-3);
   };
+  lap("entry");
 #else
   auto lap = [](const char*) {};
 #endif
@@ -1455,9 +1457,12 @@ int64_t cwq_code_grouped_greedy_batch(
   auto lap = [&](const char* what, int64_t c) {
     struct timespec t;
     clock_gettime(CLOCK_MONOTONIC, &t);
-    fprintf(stderr, "[cwq batch] %-12s chunk %2lld at %8.1f us\n", what, (long long)c,
-            (t.tv_sec - ts_start.tv_sec) * 1e6 + (t.tv_nsec - ts_start.tv_nsec) * 1e-3);
+    fprintf(stderr, "[cwq batch] %-12s chunk %2lld at %8.1f us (monotonic %.1f us)\n", what,
+            (long long)c,
+            (t.tv_sec - ts_start.tv_sec) * 1e6 + (t.tv_nsec - ts_start.tv_nsec) * 1e-3,
+            t.tv_sec * 1e6 + t.tv_nsec * 1e-3);
   };
+  lap("entry", 0);
 #else
   auto lap = [](const char*, int64_t) {};
 #endif
@@ -1543,6 +1548,7 @@ int64_t cwq_code_grouped_greedy_batch(
     // over the batch, bit-identical to the host loop), then the chunks' group
     // layouts on the device too: the host only sequences launches and writes the
     // bitcode.  Falls through to the host path when the device one does not apply.
+    lap("to device", 0);
     const int64_t r = batch_device_path(
         n_items, item_off, D, n_steps, n_bits_per_step, seeds, rho, size_threshold, n_nats,
         sample_host, bits_host, bits_cap, bits_off, starts_host, n_starts, w, workspace_bytes, bl,

@@ -30,10 +30,16 @@ for _ in range(int(os.environ.get("C3_WARMUP", "5"))):  # host clocks ramp over 
     res = C.code_grouped_greedy_sample_batch(None, T, P, 1, 8, 42)
 torch.cuda.synchronize()
 t0 = time.perf_counter()
-per = []
+per, marks = [], []
 for _ in range(n):
+    m0 = time.monotonic()
     res = C.code_grouped_greedy_sample_batch(None, T, P, 1, 8, 42)
     per.append(time.perf_counter())
+    marks.append((m0, time.monotonic()))
+if os.environ.get("C3_TSTAMPS"):  # with a CWQ_PHASE_TIMES build: the Python side's
+    for m0, m1 in marks[-4:]:     # entry / return on the native laps' clock
+        print(f"[py] call entry {m0 * 1e6:.1f} return {m1 * 1e6:.1f} us (monotonic)",
+              file=sys.stderr)
 torch.cuda.synchronize()
 el = time.perf_counter() - t0
 if os.environ.get("CWQ_BENCH_STEP_TIMES"):

@@ -54,4 +54,17 @@ res["pinned_out"], _ = tm(lambda: torch.empty(Dt * 4 + n_out * 8, dtype=torch.ui
                                               pin_memory=True).numpy())
 res["ws_size_calls"], _ = tm(lambda: (lib.cwq_code_grouped_greedy_batch_workspace_size(Dt, 48, 1),
                                       lib.cwq_code_grouped_greedy_batch_host_workspace_size(Dt, 48, 1)))
+res["seeds_obj"], _ = tm(lambda: (np.full(48, 42, dtype=object) & 0xFFFFFFFF).astype(np.uint64)
+                         .astype(np.uint32).view(np.int32))
+res["list_args"], _ = tm(lambda: (list(T), list(P)))
+res["thread_roundtrip"], _ = tm(lambda: S._batch_thread().submit(lambda: None).result())
+res["current_stream"], _ = tm(lambda: torch.cuda.current_stream(dev).cuda_stream)
+
+
+def _device_ctx():
+    with torch.cuda.device(dev):
+        pass
+
+
+res["device_ctx"], _ = tm(_device_ctx)
 print(" ".join(f"{k} {v:.3f}" for k, v in res.items()), "ms", flush=True)
