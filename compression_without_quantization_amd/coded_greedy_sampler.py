@@ -403,7 +403,7 @@ def code_grouped_greedy_sample(sess, target, proposal, n_steps, n_bits_per_step,
 def code_grouped_greedy_sample_batch(sess, targets, proposals, n_steps, n_bits_per_step, seeds,
                                      max_group_size_bits=12, adaptive=True, backfitting_steps=0,
                                      use_log_prob=False, rho=1., *, prune_mode=None,
-                                     eval_events=None, eval_ms_out=None):
+                                     eval_events=None, eval_ms_out=None, defer=False):
     """code_grouped_greedy_sample (coded_greedy_sampler.py:170-296) for a batch
     of independent items (the images of a dataset, the ladder levels of several
     images) in one native call (cwq_code_grouped_greedy_batch).
@@ -417,6 +417,13 @@ def code_grouped_greedy_sample_batch(sess, targets, proposals, n_steps, n_bits_p
     image's ~41k starts costs ~0.5 ms, as much as coding it).  Not in the
     reference (an extension for throughput: one encode launch over every item's
     groups).
+
+    ``defer=True`` (keyword only): return at once a handle whose ``result()``
+    gives that list.  The call is queued behind the ones before it (one host
+    thread runs them in order on the current stream), so a caller that queues
+    batch k + 1 before collecting batch k overlaps k + 1's argument pass and
+    k's bitcode strings with the device work instead of leaving the device idle
+    between calls.  The results are the same either way.
     """
     lib = _lib.load()
     targets, proposals = list(targets), list(proposals)
@@ -424,7 +431,7 @@ def code_grouped_greedy_sample_batch(sess, targets, proposals, n_steps, n_bits_p
         raise ValueError("targets and proposals must have the same length")
     n_items = len(targets)
     if n_items == 0:
-        return []
+        return _Done([]) if defer else []
     if np.ndim(seeds) == 0:
         seeds64 = np.full(n_items, int(seeds), dtype=object)
     else:
@@ -492,7 +499,8 @@ def code_grouped_greedy_sample_batch(sess, targets, proposals, n_steps, n_bits_p
     starts_h = out_np[:n_out * 8].view(np.int64)
     sample_h = out_np[n_out * 8:].view(np.float32)
     bits_cap = (D + n_items) * n_bits_per_group
-    bits_h = _scratch_bytes(bits_cap)  # consumed into str below: reusable
+    # consumed into str below: reusable (a deferred call's until its result())
+    bits_h = _bits_take(bits_cap) if defer else _scratch_bytes(bits_cap)
     bits_off = np.empty(n_items + 1, dtype=np.int64)
     n_starts = np.empty(n_items, dtype=np.int64)
     n_nats = n_bits_per_group * np.log(2) - 1
@@ -500,7 +508,7 @@ def code_grouped_greedy_sample_batch(sess, targets, proposals, n_steps, n_bits_p
     # With several items the call runs on a helper thread (ctypes releases the
     # GIL) and raises item i's flag once its outputs are final: this thread
     # turns the finished items' bitcodes into str while later chunks code.
-    ready = np.zeros(n_items, dtype=np.int32) if n_items > 1 else None
+    ready = np.zeros(n_items, dtype=np.int32) if n_items > 1 or defer else None
 
     def call():
         with torch.cuda.device(dev):
@@ -522,25 +530,86 @@ def code_grouped_greedy_sample_batch(sess, targets, proposals, n_steps, n_bits_p
         s0 = a + 2 * i  # item i's starts region (cwq_code_grouped_greedy_batch)
         return sample_h[a:b], bitcode, starts_h[s0:s0 + n_starts[i]]
 
-    out = []
     if ready is None:
         call()
-    else:
-        fut = _batch_thread().submit(call)
-        for i in range(n_items):
-            spins = 0
-            while not ready[i] and not fut.done():
-                # yield the GIL (the call needs it only to return); after a
-                # short spin back off, so this thread does not hold a whole
-                # CPU of the quota the native host threads partition on
-                spins += 1
-                time.sleep(0 if spins < 32 else 5e-5)
-            if not ready[i]:
-                break  # the call ended early: its error is raised below
-            out.append(item(i))
-        fut.result()
-    out.extend(item(i) for i in range(len(out), n_items))
-    return out
+        return [item(i) for i in range(n_items)]
+    fut = _batch_thread().submit(call)
+
+    def finish():
+        out = []
+        try:
+            for i in range(n_items):
+                spins = 0
+                while not ready[i] and not fut.done():
+                    # yield the GIL (the call needs it only to return); after a
+                    # short spin back off, so this thread does not hold a whole
+                    # CPU of the quota the native host threads partition on
+                    spins += 1
+                    time.sleep(0 if spins < 32 else 5e-5)
+                if not ready[i]:
+                    break  # the call ended early: its error is raised below
+                out.append(item(i))
+            fut.result()
+            out.extend(item(i) for i in range(len(out), n_items))
+        finally:
+            if defer:
+                fut.exception()  # (waits) the buffer is free once the call has ended
+                _bits_give(bits_h)
+        return out
+
+    return _Deferred(finish) if defer else finish()
+
+
+class _Done:
+    """A deferred batch call's handle whose result is already known."""
+
+    def __init__(self, value):
+        self._value = value
+
+    def result(self):
+        return self._value
+
+
+class _Deferred:
+    """code_grouped_greedy_sample_batch(..., defer=True)'s handle: result()
+    waits for the call, builds the per-item results once and returns them."""
+
+    def __init__(self, finish):
+        self._finish = finish
+        self._value = self._error = None
+        self._lock = threading.Lock()
+
+    def result(self):
+        with self._lock:
+            if self._finish is not None:
+                f, self._finish = self._finish, None
+                try:
+                    self._value = f()
+                except BaseException as e:  # raised again by every later result()
+                    self._error = e
+            if self._error is not None:
+                raise self._error
+            return self._value
+
+
+_bits_free = []
+_bits_lock = threading.Lock()
+
+
+def _bits_take(n):
+    """A bitcode buffer of at least n bytes for a deferred batch call (its
+    pages stay mapped between calls: a fresh one costs its page faults)."""
+    with _bits_lock:
+        for k, b in enumerate(_bits_free):
+            if b.size >= n:
+                return _bits_free.pop(k)
+    return np.empty(max(int(n), 1), dtype=np.uint8)
+
+
+def _bits_give(b):
+    with _bits_lock:
+        if len(_bits_free) < 4:
+            _bits_free.append(b)
 
 
 _batch_pool = None

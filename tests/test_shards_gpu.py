@@ -235,6 +235,46 @@ def test_grouped_batch_equals_single_calls(cwq, sizes, seeds, bits, n_steps):
         assert np.array_equal(_u32(bs), _u32(sample)), k
 
 
+def test_grouped_batch_deferred_overlapping_calls(cwq):
+    """defer=True: three batches queued before any is collected (different
+    items, seeds and sizes; the large one takes the pipelined path), collected
+    out of order and twice, each equal to the synchronous call; an invalid
+    batch raises from result(), and again on a second result()."""
+    cwq.coded_greedy_sampler.VERBOSE = False
+    rng = np.random.default_rng(77)
+
+    def batch(sizes):
+        tg, pr = [], []
+        for D in sizes:
+            pl = (0.1 * rng.standard_normal(D)).astype(np.float32)
+            ps = rng.uniform(0.8, 1.2, D).astype(np.float32)
+            ql = (pl + ps * rng.standard_normal(D) * 0.7).astype(np.float32)
+            qs = (ps * rng.uniform(0.3, 1.0, D)).astype(np.float32)
+            tg.append(cwq.Normal(torch.from_numpy(ql).cuda(), torch.from_numpy(qs).cuda()))
+            pr.append(cwq.Normal(torch.from_numpy(pl).cuda(), torch.from_numpy(ps).cuda()))
+        return tg, pr
+
+    jobs = [(batch([3000, 1, 500, 0, 70000, 9000]), [5, -7, 2 ** 31 - 1, 0, 11, 12]),
+            (batch([4000, 4000]), 42),
+            (batch([123]), 9)]
+    handles = [cwq.code_grouped_greedy_sample_batch(None, tg, pr, 1, 8, sd, defer=True)
+               for (tg, pr), sd in jobs]
+    assert cwq.code_grouped_greedy_sample_batch(None, [], [], 1, 8, 0, defer=True).result() == []
+    for k in (2, 0, 1, 0):  # out of order, and one handle twice
+        got = handles[k].result()
+        (tg, pr), sd = jobs[k]
+        want = cwq.code_grouped_greedy_sample_batch(None, tg, pr, 1, 8, sd)
+        assert len(got) == len(want)
+        for (gs, gb, gst), (ws, wb, wst) in zip(got, want):
+            assert gb == wb and gst.tolist() == wst.tolist()
+            assert np.array_equal(_u32(gs), _u32(ws))
+    (tg, pr), _ = jobs[1]
+    bad = cwq.code_grouped_greedy_sample_batch(None, tg, pr, 1, 40, 0, defer=True)
+    for _ in range(2):
+        with pytest.raises(Exception):
+            bad.result()
+
+
 def test_grouped_batch_many_items(cwq):
     """More items than the device partition keeps in LDS (1,024): 1,300 items
     of 0..200 dims (empty and 1-dim ones among them, ~130k dims: the pipelined
