@@ -257,7 +257,7 @@ int64_t cwq_code_grouped_greedy_end(const int32_t* idx_host, int64_t G, int n_st
  * finds every item's groups (when the device scheme does not cover an input,
  * the host loop partitions chunk by chunk instead, with identical results).
  * The items are then pipelined in chunks of consecutive items
- * (CWQ_BATCH_CHUNKS, default 6; the first and the last a quarter share): one
+ * (CWQ_BATCH_CHUNKS, default 6; the first a quarter share, the last a half): one
  * encode launch sequence per chunk with per-block seeds, chunk c's results
  * copied to the host while chunk c + 1 codes, and each item's bitcode written
  * as soon as its chunk's indices arrive, on a pool of host threads (up to
