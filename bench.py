@@ -414,7 +414,7 @@ def importance_main(args):
                     C.Normal(torch.from_numpy(p_loc).to(dev), torch.from_numpy(p_scale).to(dev))))
     evq = []
 
-    def step(timed=False):
+    def step_single(timed=False):  # one code_grouped_importance_sample call per image
         out = []
         for t, p in lat:
             v = ctypes.c_float(0.0) if timed else None
@@ -424,16 +424,53 @@ def importance_main(args):
             if v is not None:
                 evq.append(v)
         return out
-    for _ in range(args.warmup):
-        res = step()
-    torch.cuda.synchronize()
-    evq.clear()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        res = step(True)
-    torch.cuda.synchronize()
-    el = time.perf_counter() - t0
-    kernel_ms = sum(v.value for v in evq) / max(args.steps, 1)
+
+    def step_batch(timed=False):  # every image of the step in one batched call
+        v = ctypes.c_float(0.0) if timed else None
+        out = I.code_grouped_importance_sample_batch(None, [t for t, _ in lat],
+                                                     [p for _, p in lat], 42, nbits,
+                                                     max_group_size_bits=gbits,
+                                                     dim_kl_bit_limit=kl_lim, eval_ms_out=v)
+        if v is not None:
+            evq.append(v)
+        return out
+
+    def timed(step):
+        """(seconds for args.steps steps, results, scoring ms per step): the
+        steps timed with the scoring timers on (each call synchronises anyway)."""
+        res = None
+        for _ in range(args.warmup):
+            res = step()
+        torch.cuda.synchronize()
+        evq.clear()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            res = step(True)
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t0
+        return el, res, sum(v.value for v in evq) / max(args.steps, 1)
+
+    batch = n_img > 1 and not args.per_image
+    batched = None
+    if batch and args.batch_only:
+        el, res, kernel_ms = timed(step_batch)
+        batched = {"images_per_call": n_img, "equal_to_single_calls": None,
+                   "single_call_images_per_s": None}
+    else:
+        el, res, kernel_ms = timed(step_single)
+        if batch:
+            el_s, kms_s, res_s = el, kernel_ms, res
+            el, res, kernel_ms = timed(step_batch)
+            same = all(a[1] == b[1] and np.array_equal(np.asarray(a[2]), np.asarray(b[2])) and
+                       np.array_equal(np.asarray(a[0]).view(np.uint32),
+                                      np.asarray(b[0]).view(np.uint32)) and
+                       np.array_equal(a[3][0], b[3][0]) and np.array_equal(a[3][1], b[3][1])
+                       for a, b in zip(res_s, res))
+            if not same:
+                raise SystemExit("bench.py: batched importance results differ from the single calls")
+            batched = {"images_per_call": n_img, "equal_to_single_calls": bool(same),
+                       "single_call_images_per_s": n_img * args.steps / el_s,
+                       "single_call_scoring_kernel_ms": round(kms_s, 4)}
     # work: sum over groups of N_g * d_g candidate-dims (the plan the coder used)
     cand_dims = 0
     for (t, p), r in zip(lat, res):
@@ -446,8 +483,8 @@ def importance_main(args):
     roofline = scoring_roofline(args.config, groups, alg, kernel_ms, cand_dims,
                                 "k_imp_prep + k_imp_tiles + k_imp_eval + k_imp_rows "
                                 "(DESIGN.md 8)", "cwq_options.eval_ms_out of each "
-                                "code_grouped_importance_sample call (HIP events around its "
-                                "candidate-scoring launches), summed over the step's calls")
+                                "code_grouped_importance_sample[_batch] call (HIP events around "
+                                "its candidate-scoring launches), summed over the step's calls")
     cpu = parity = None
     if not args.no_cpu:
         cpu, parity = importance_cpu_baseline(args, lat_np[0], res[0], nbits, gbits, kl_lim)
@@ -459,7 +496,11 @@ def importance_main(args):
             "config": {"workload": desc, "groups_per_step": groups, "bits_per_step": bitlen,
                        "groups_per_s": groups * args.steps / el,
                        "candidate_dims_per_step": cand_dims,
-                       "candidate_dims_per_s": cand_dims * args.steps / el},
+                       "candidate_dims_per_s": cand_dims * args.steps / el,
+                       "mode": ("code_grouped_importance_sample_batch: every image of a step in "
+                                "one call" if batched else
+                                "one code_grouped_importance_sample call per image"),
+                       "batched": batched},
             "roofline": roofline, "cpu_baseline": cpu, "parity": parity}
     print(json.dumps(line), flush=True)
 

@@ -15,6 +15,7 @@ from .coded_greedy_sampler import (Normal, code_greedy_sample, code_grouped_gree
                                    decode_grouped_greedy_sample, encode, encode_blocks,
                                    encode_workspace_bytes, group_size_threshold, group_starts)
 from .coded_importance_sampler import (code_grouped_importance_sample,
+                                       code_grouped_importance_sample_batch,
                                        code_importance_sample,
                                        decode_grouped_importance_sample,
                                        decode_importance_sample, importance_decode_blocks,
@@ -33,6 +34,7 @@ __all__ = [
     "elias_delta_decode", "elias_delta_code_many", "elias_delta_decode_many",
     "code_importance_sample", "decode_importance_sample",
     "code_grouped_importance_sample", "decode_grouped_importance_sample",
+    "code_grouped_importance_sample_batch",
     "importance_encode_blocks", "importance_decode_blocks", "ArithmeticCoder",
     "write_bin_code", "read_bin_code", "ProbabilisticLadderNetwork", "build_empirical_dists",
     "encode_blocks_host", "code_grouped_greedy_sample_batch",

@@ -95,6 +95,11 @@ SIGNATURES = {
     "cwq_code_grouped_importance": (c_i64, [c_vp, c_vp, c_vp, c_vp, c_i64, c_i32, c_f32, c_i64,
                                             c_f64, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp,
                                             c_vp, c_vp, c_size, c_opts, c_vp]),
+    "cwq_code_grouped_importance_batch_workspace_size": (c_size, [c_i64, c_i64]),
+    "cwq_code_grouped_importance_batch": (c_i64, [c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
+                                                  c_f32, c_i64, c_f64, c_vp, c_vp, c_vp, c_i64,
+                                                  c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_size,
+                                                  c_opts, c_vp]),
     "cwq_ac_encode": (c_i64, [c_vp, c_i64, c_int, c_vp, c_i64, c_vp, c_i64]),
     "cwq_ac_decode": (c_i64, [c_vp, c_i64, c_int, c_vp, c_i64, c_vp, c_i64]),
     "cwq_elias_delta_encode": (c_i64, [c_vp, c_i64, c_vp, c_i64]),
@@ -122,7 +127,7 @@ TOOL_SIGNATURES = {
 
 # CWQ_ABI_VERSION of the include/cwq.h these signatures mirror: a library
 # reporting another version has other argument lists and is refused.
-ABI_VERSION = (0 << 16) | 5
+ABI_VERSION = (0 << 16) | 6
 
 _lib = None
 

@@ -171,12 +171,19 @@ def decode_importance_sample(sample_index, p_loc, p_scale, seed, use_index=False
 
 def quantize_quint16(x, mn=QUANT_MIN, mx=QUANT_MAX):
     """tf.quantization.quantize(x, mn, mx, tf.quint16) (MIN_COMBINED, float32):
-    uint16((clamp(x) - mn) * float32(65535 / (mx - mn)) + 0.5f)."""
+    uint16((clamp(x) - mn) * float32(65535 / (mx - mn)) + 0.5f).
+
+    NaN (a NaN outlier draw) is coded as 0, the code of ``mn``: the value an
+    x86 truncating conversion gives (cvttss2si returns the integer-indefinite
+    0x80000000, whose low 16 bits are 0).  The reference's float -> quint16
+    cast of NaN (:156) is unspecified; this build fixes it instead of leaving
+    it to NumPy's undefined cast."""
     x = np.asarray(x, dtype=np.float32)
     scale = np.float32((65535.0 - 0.0) / (float(mx) - float(mn)))
     v = np.maximum(np.minimum(x, np.float32(mx)), np.float32(mn))
     t = (v - np.float32(mn)) * scale
     t = t + np.float32(0.5)
+    t = np.where(np.isnan(t), np.float32(0.0), t)
     return t.astype(np.uint16)
 
 
@@ -225,7 +232,7 @@ def _code_grouped_importance_on(dev, target, proposal, seed, n_bits_per_group,
     p_loc, p_scale = _f32(proposal.loc, dev, "proposal.loc"), _f32(proposal.scale, dev,
                                                                    "proposal.scale")
     D = p_loc.numel()
-    if USE_FUSED and D > 0 and not (return_group_indices_only or return_indices_only):
+    if USE_FUSED and not (return_group_indices_only or return_indices_only):
         return _code_grouped_fused(lib, dev, q_loc, q_scale, p_loc, p_scale, D, seed,
                                    n_bits_per_group, max_group_size_bits, dim_kl_bit_limit,
                                    return_indices, prune_mode, eval_ms_out)
@@ -315,6 +322,91 @@ def _code_grouped_fused(lib, dev, q_loc, q_scale, p_loc, p_scale, D, seed, n_bit
     if return_indices:
         return sample_h, indices, group_start_indices, outlier_extras
     return sample_h, elias_delta_code_many(indices), group_start_indices, outlier_extras
+
+
+def code_grouped_importance_sample_batch(sess, targets, proposals, seeds, n_bits_per_group,
+                                         max_group_size_bits=4, dim_kl_bit_limit=12,
+                                         return_indices=False, *, prune_mode=None,
+                                         eval_ms_out=None):
+    """code_grouped_importance_sample (coded_importance_sampler.py:112-274) for a
+    batch of independent items (the level-2 latents of a dataset's images,
+    pln.py:350-359) in one native call (cwq_code_grouped_importance_batch): one
+    preparation launch and one encode launch over every item's groups.
+
+    ``targets`` / ``proposals``: sequences of distributions (``.loc`` /
+    ``.scale``), item i coded with seed ``seeds[i]`` (an int: the same seed for
+    every item).  Returns a list with one (sample, bitcode | indices,
+    group_start_indices, outlier_extras) per item, each equal to
+    code_grouped_importance_sample on that item alone.  Not in the reference
+    (an extension for throughput)."""
+    lib = _lib.load()
+    targets, proposals = list(targets), list(proposals)
+    if len(targets) != len(proposals):
+        raise ValueError("targets and proposals must have the same length")
+    n_items = len(targets)
+    if n_items == 0:
+        return []
+    if np.ndim(seeds) == 0:
+        seeds = [int(seeds)] * n_items
+    seeds = [int(x) for x in seeds]
+    if len(seeds) != n_items:
+        raise ValueError("one seed per item")
+    seeds32 = np.array([int(np.int32(np.uint32(s & 0xFFFFFFFF))) for s in seeds], dtype=np.int32)
+    for t, p in zip(targets, proposals):
+        if not _is_float32(t.loc) or not _is_float32(t.scale):
+            raise Exception("Target datatype must be float32!")   # :126-129
+        if not _is_float32(p.loc) or not _is_float32(p.scale):
+            raise Exception("Proposal datatype must be float32!")
+    dev = _device_of(*[a for t, p in zip(targets, proposals)
+                       for a in (t.loc, t.scale, p.loc, p.scale)])
+    with torch.cuda.device(dev):
+        cols = [[_f32(getattr(d, k), dev, n).reshape(-1) for d in ds]
+                for ds, k, n in ((targets, "loc", "target.loc"), (targets, "scale", "target.scale"),
+                                 (proposals, "loc", "proposal.loc"),
+                                 (proposals, "scale", "proposal.scale"))]
+        sizes = np.array([a.numel() for a in cols[0]], dtype=np.int64)
+        if any([a.numel() for a in c] != sizes.tolist() for c in cols[1:]):
+            raise ValueError("target and proposal of an item must have the same size")
+        cat = [torch.cat(c) for c in cols]
+        item_off = np.concatenate([[0], np.cumsum(sizes)]).astype(np.int64)
+        D = int(item_off[-1])
+        need = int(lib.cwq_code_grouped_importance_batch_workspace_size(D, n_items))
+        ws = torch.empty(max(need, 1), dtype=torch.uint8, device=dev)
+        sample_h = np.empty(max(D, 1), dtype=np.float32)
+        index_h = np.empty(D + n_items, dtype=np.int64)
+        starts_h = np.empty(D + 2 * n_items, dtype=np.int64)
+        n_starts = np.zeros(n_items, dtype=np.int64)
+        out_i = np.empty(max(D, 1), dtype=np.int64)
+        out_v = np.empty(max(D, 1), dtype=np.float32)
+        n_out = np.zeros(n_items, dtype=np.int64)
+        kl_sum = np.zeros(n_items, dtype=np.float64)
+        _lib.check(lib.cwq_code_grouped_importance_batch(
+            n_items, item_off.ctypes.data, _ptr(cat[0]), _ptr(cat[1]), _ptr(cat[2]), _ptr(cat[3]),
+            seeds32.ctypes.data, float(np.float32(dim_kl_bit_limit)),
+            importance_group_size_threshold(max_group_size_bits),
+            float(n_bits_per_group * np.log(2) - 1), sample_h.ctypes.data, index_h.ctypes.data,
+            starts_h.ctypes.data, starts_h.size, n_starts.ctypes.data, out_i.ctypes.data,
+            out_v.ctypes.data, n_out.ctypes.data, kl_sum.ctypes.data, ws.data_ptr(), ws.numel(),
+            _lib.options(prune_mode, eval_ms_out=eval_ms_out), _stream(dev)),
+            "cwq_code_grouped_importance_batch")
+    res = []
+    for i in range(n_items):
+        a, b = int(item_off[i]), int(item_off[i + 1])
+        if VERBOSE and b > a:
+            total_kl_bits = kl_sum[i] / np.log(2)
+            print("Total KL to split up: {:.2f} bits, "
+                  "maximum bits per group: {}, "
+                  "estimated number of groups: {},"
+                  "coding {} dimensions".format(total_kl_bits, n_bits_per_group,
+                                                total_kl_bits // n_bits_per_group + 1, b - a))
+        ns, no = int(n_starts[i]), int(n_out[i])
+        gs = starts_h[a + 2 * i:a + 2 * i + ns].copy()
+        indices = tuple((index_h[a + i:a + i + ns - 1] + 1).tolist())
+        extras = (out_i[a:a + no].copy(), quantize_quint16(out_v[a:a + no]))
+        smp = sample_h[a:b].copy()
+        code = indices if return_indices else elias_delta_code_many(indices)
+        res.append((smp, code, gs, extras))
+    return res
 
 
 def _group_kls(kl_divs, starts):

@@ -1829,18 +1829,22 @@ int64_t cwq_code_grouped_greedy_batch(
 }
 
 // ---------------------------------------------------------------------------
-// code_grouped_importance_sample (coded_importance_sampler.py:112-274) in one
-// call: device standardisation, KL and outlier masking, the seeded outlier
-// target draw, host partition and sample-count plan, one CSR encode launch,
-// device destandardisation.  Elias-delta strings and quint16 packing stay with
-// the caller (host, cheap).
+// code_grouped_importance_sample (coded_importance_sampler.py:112-274) for one
+// item or a batch of items in one call: device standardisation, KL, outlier
+// masking and the outliers' seeded target draw (one launch), the host
+// partition and sample-count plan of every item, one encode launch over every
+// item's groups (item i's group g seeded seeds[i] + g), device
+// destandardisation.  Elias-delta strings and quint16 packing stay with the
+// caller (host, cheap).
 // ---------------------------------------------------------------------------
 namespace {
 struct GroupedImpWs {
-  size_t t_loc, t_scale, kl, kl2, zeros, ones, tsamp, sample, out, keep, offs, nsamp, idx, enc,
-      total;
+  size_t t_loc, t_scale, kl2, zeros, ones, tsamp, sample, out, keep, offs, nsamp, idx, gseed,
+      items, seed1, enc, total;
 };
-GroupedImpWs grouped_imp_ws(int64_t D) {
+// D dims in I items: at most D + I groups (an item's partition has at most
+// D_i + 1 groups)
+GroupedImpWs grouped_imp_ws(int64_t D, int64_t I) {
   GroupedImpWs l;
   size_t o = 0;
   auto take = [&](size_t bytes) {
@@ -1848,10 +1852,9 @@ GroupedImpWs grouped_imp_ws(int64_t D) {
     o = align_up(o + bytes, 256);
     return at;
   };
-  const size_t n = (size_t)(D > 0 ? D : 0);
+  const size_t n = (size_t)(D > 0 ? D : 0), ni = (size_t)(I > 0 ? I : 0), g = n + ni;
   l.t_loc = take(n * 4);
   l.t_scale = take(n * 4);
-  l.kl = take(n * 4);
   l.kl2 = take(n * 4);
   l.zeros = take(n * 4);
   l.ones = take(n * 4);
@@ -1859,52 +1862,59 @@ GroupedImpWs grouped_imp_ws(int64_t D) {
   l.sample = take(n * 4);
   l.out = take(n * 4);
   l.keep = take(n);
-  l.offs = take((n + 2) * 8);
-  l.nsamp = take((n + 1) * 8);
-  l.idx = take((n + 1) * 8);
-  l.enc = take(cwq::importance_workspace_size(D + 1, D));
+  l.offs = take((g + 1) * 8);
+  l.nsamp = take(g * 8);
+  l.idx = take(g * 8);
+  l.gseed = take(g * 4);
+  l.items = take((ni + 1) * 8);
+  l.seed1 = take(ni * 4);
+  l.enc = take(cwq::importance_workspace_size((int64_t)g, (int64_t)n));
   l.total = o;
   return l;
 }
-thread_local PinnedTl tl_imp_pin;             // cwq_code_grouped_importance's host staging
+thread_local PinnedTl tl_imp_pin;             // the grouped importance calls' host staging
 thread_local std::vector<char> tl_imp_pageable;  // ... when page-locked memory is unavailable
-}  // namespace
 
-size_t cwq_code_grouped_importance_workspace_size(int64_t D) {
-  if (D < 0) return 0;
-  return grouped_imp_ws(D).total;
-}
-
-int64_t cwq_code_grouped_importance(const float* q_loc, const float* q_scale,
-                                    const float* p_loc, const float* p_scale, int64_t D,
-                                    int32_t seed, float dim_kl_bit_limit, int64_t size_threshold,
-                                    double n_nats, float* sample_host, int64_t* index_host,
-                                    int64_t* starts_host, int64_t starts_cap,
-                                    int64_t* outlier_idx_host, float* outlier_val_host,
-                                    int64_t* n_outliers, double* kl_sum_out, void* workspace,
-                                    size_t workspace_bytes, const cwq_options* opts,
-                                    void* stream) {
+int64_t grouped_importance_impl(int64_t I, const int64_t* item_off, const float* q_loc,
+                                const float* q_scale, const float* p_loc, const float* p_scale,
+                                const int32_t* seeds, float dim_kl_bit_limit,
+                                int64_t size_threshold, double n_nats, float* sample_host,
+                                int64_t* index_host, int64_t* starts_host, int64_t starts_cap,
+                                int64_t* n_starts, int64_t* outlier_idx_host,
+                                float* outlier_val_host, int64_t* n_outliers,
+                                double* kl_sum_out, void* workspace, size_t workspace_bytes,
+                                const cwq_options* opts, void* stream, const char* who) {
+  cwq_options oi;
   {
-    cwq_options o;
-    const int rc0 = read_options(opts, &o);
+    const int rc0 = read_options(opts, &oi);
     if (rc0) return rc0;
   }
-  if (D < 0) return fail(CWQ_ERR_INVALID, "cwq_code_grouped_importance: negative size");
+  if (I < 1 || !item_off || !seeds || !n_starts || !n_outliers)
+    return fail(CWQ_ERR_INVALID, "%s: bad arguments", who);
+  if (item_off[0] != 0) return fail(CWQ_ERR_INVALID, "%s: item_off[0] must be 0", who);
+  for (int64_t i = 0; i < I; ++i)
+    if (item_off[i + 1] < item_off[i]) return fail(CWQ_ERR_INVALID, "%s: item_off not sorted", who);
+  const int64_t D = item_off[I];
   if (D > 0 && (!q_loc || !q_scale || !p_loc || !p_scale || !sample_host || !index_host ||
                 !outlier_idx_host || !outlier_val_host))
-    return fail(CWQ_ERR_INVALID, "cwq_code_grouped_importance: null pointer");
-  if (!n_outliers) return fail(CWQ_ERR_INVALID, "cwq_code_grouped_importance: null pointer");
-  if (!starts_host || starts_cap < D + 2)
-    return fail(CWQ_ERR_CAPACITY, "cwq_code_grouped_importance: starts_cap must be >= D + 2");
-  const GroupedImpWs l = grouped_imp_ws(D);
+    return fail(CWQ_ERR_INVALID, "%s: null pointer", who);
+  if (!starts_host || starts_cap < D + 2 * I)
+    return fail(CWQ_ERR_CAPACITY, "%s: starts_cap must be >= D + 2 n_items", who);
+  const GroupedImpWs l = grouped_imp_ws(D, I);
   if (workspace_bytes < l.total || !workspace)
-    return fail(CWQ_ERR_WORKSPACE, "workspace %zu bytes < required %zu", workspace_bytes,
-                l.total);
+    return fail(CWQ_ERR_WORKSPACE, "workspace %zu bytes < required %zu", workspace_bytes, l.total);
+  for (int64_t i = 0; i < I; ++i) {
+    n_outliers[i] = 0;
+    n_starts[i] = 1;
+    starts_host[item_off[i] + 2 * i] = 0;
+    if (kl_sum_out) kl_sum_out[i] = 0.0;
+  }
+  if (oi.eval_ms_out) *oi.eval_ms_out = 0.0f;
+  if (D == 0) return ok();
   hipStream_t s = (hipStream_t)stream;
   char* w = (char*)workspace;
   float* t_loc = (float*)(w + l.t_loc);
   float* t_scale = (float*)(w + l.t_scale);
-  float* kl = (float*)(w + l.kl);
   float* kl2 = (float*)(w + l.kl2);
   float* zeros = (float*)(w + l.zeros);
   float* ones = (float*)(w + l.ones);
@@ -1915,27 +1925,14 @@ int64_t cwq_code_grouped_importance(const float* q_loc, const float* q_scale,
   int64_t* offs = (int64_t*)(w + l.offs);
   int64_t* nsamp = (int64_t*)(w + l.nsamp);
   int64_t* idx = (int64_t*)(w + l.idx);
-  hipError_t e = hipSuccess;
-  int rc;
-  *n_outliers = 0;
-  if (D == 0) {
-    starts_host[0] = 0;
-    return ok();
-  }
-  // :137-138 standardise; :142 KL(target || proposal); :144-148 outliers;
-  // :160-163 KL of the standardised target against N(0, 1): one launch
-  (void)kl;
-  if ((e = cwq::launch_imp_grouped_prep(q_loc, q_scale, p_loc, p_scale, D, dim_kl_bit_limit,
-                                        t_loc, t_scale, keep, zeros, ones, kl2, s)) != hipSuccess)
-    return hip_fail(e, "standardise / KL / outliers");
-  // :150 the outlier dims' target draw, seeded [seed - 1, 42]
-  const int32_t s1 = (int32_t)((uint32_t)seed - 1u);
-  if ((rc = cwq_stateless_normal_sample(q_loc, q_scale, D, 1, s1, tsamp, stream)) < 0) return rc;
+  int32_t* gseed = (int32_t*)(w + l.gseed);
+  int64_t* items_d = (int64_t*)(w + l.items);
+  int32_t* seed1_d = (int32_t*)(w + l.seed1);
   // the host side's arrays in this thread's page-locked staging (pageable
   // memory is staged by the runtime: I1's 2.9 MB of copies took ~0.5 ms more),
   // waits polled on events (a blocking wait's wake-up cost I2's small calls
   // ~0.1 ms each)
-  const size_t Dz = (size_t)D;
+  const size_t Dz = (size_t)D, Gz = (size_t)(D + I), Iz = (size_t)I;
   size_t ho = 0;
   auto htake = [&](size_t b) {
     const size_t at = ho;
@@ -1943,8 +1940,9 @@ int64_t cwq_code_grouped_importance(const float* q_loc, const float* q_scale,
     return at;
   };
   const size_t o_kl = htake(Dz * 4), o_ts = htake(Dz * 4), o_out = htake(Dz * 4),
-               o_keep = htake(Dz), o_idx = htake((Dz + 1) * 8), o_offs = htake((Dz + 2) * 8),
-               o_ns = htake((Dz + 1) * 8);
+               o_keep = htake(Dz), o_idx = htake(Gz * 8), o_offs = htake((Gz + 1) * 8),
+               o_ns = htake(Gz * 8), o_gs = htake(Gz * 4), o_items = htake((Iz + 1) * 8),
+               o_s1 = htake(Iz * 4);
   char* hp = (char*)tl_imp_pin.get(ho, ho + ho / 4);
   if (!hp) {  // no page-locked memory: pageable staging (slower copies)
     tl_imp_pageable.resize(ho);
@@ -1957,79 +1955,175 @@ int64_t cwq_code_grouped_importance(const float* q_loc, const float* q_scale,
   int64_t* idx_h = (int64_t*)(hp + o_idx);
   int64_t* offs_h = (int64_t*)(hp + o_offs);
   int64_t* ns_h = (int64_t*)(hp + o_ns);
+  int32_t* gs_h = (int32_t*)(hp + o_gs);
+  int64_t* items_h = (int64_t*)(hp + o_items);
+  int32_t* s1_h = (int32_t*)(hp + o_s1);
+  hipError_t e = hipSuccess;
+  int rc;
+  // every failure after the first copy or launch drains the stream first: the
+  // staging buffer may be reused (or reallocated) by this thread's next call
+  auto drain_fail = [&](hipError_t err, const char* where) -> int64_t {
+    (void)hipStreamSynchronize(s);
+    return hip_fail(err, where);
+  };
+  auto drain_rc = [&](int64_t r) -> int64_t {
+    (void)hipStreamSynchronize(s);
+    return r;
+  };
   CallEvents hev;
   if (!hev.made(2, s, hipEventDisableTiming))
-    return fail(CWQ_ERR_HIP, "cwq_code_grouped_importance: event creation failed");
+    return fail(CWQ_ERR_HIP, "%s: event creation failed", who);
+  // :137-138 standardise; :142 KL(target || proposal); :144-148 outliers; :150
+  // the outlier dims' target draw, seeded [seed - 1, 42];
+  // :160-163 KL of the standardised target against N(0, 1): one launch
+  const int64_t* items_arg = nullptr;
+  const int32_t* seed1_arg = nullptr;
+  if (I > 1) {
+    memcpy(items_h, item_off, (Iz + 1) * 8);
+    for (int64_t i = 0; i < I; ++i) s1_h[i] = (int32_t)((uint32_t)seeds[i] - 1u);
+    if ((e = hipMemcpyAsync(items_d, items_h, (Iz + 1) * 8, hipMemcpyHostToDevice, s)) !=
+            hipSuccess ||
+        (e = hipMemcpyAsync(seed1_d, s1_h, Iz * 4, hipMemcpyHostToDevice, s)) != hipSuccess)
+      return drain_fail(e, "items to device");
+    items_arg = items_d;
+    seed1_arg = seed1_d;
+  }
+  if ((e = cwq::launch_imp_grouped_prep(q_loc, q_scale, p_loc, p_scale, D, dim_kl_bit_limit,
+                                        items_arg, seed1_arg, I,
+                                        (int32_t)((uint32_t)seeds[0] - 1u), t_loc, t_scale, keep,
+                                        zeros, ones, kl2, tsamp, s)) != hipSuccess)
+    return drain_fail(e, "standardise / KL / outliers");
   if ((e = hipMemcpyAsync(kl_h, kl2, Dz * 4, hipMemcpyDeviceToHost, s)) != hipSuccess ||
       (e = hipMemcpyAsync(keep_h, keep, Dz, hipMemcpyDeviceToHost, s)) != hipSuccess ||
       (e = hipMemcpyAsync(ts_h, tsamp, Dz * 4, hipMemcpyDeviceToHost, s)) != hipSuccess ||
-      (e = hipEventRecord(hev.ev[0], s)) != hipSuccess) {
-    (void)hipStreamSynchronize(s);
-    return hip_fail(e, "to host");
-  }
-  if ((e = wait_event(hev.ev[0])) != hipSuccess) return hip_fail(e, "sync");
-  int64_t no = 0;
-  for (int64_t j = 0; j < D; ++j)
-    if (!keep_h[j]) {
-      outlier_idx_host[no] = j;
-      outlier_val_host[no] = ts_h[j];
-      ++no;
+      (e = hipEventRecord(hev.ev[0], s)) != hipSuccess)
+    return drain_fail(e, "to host");
+  if ((e = wait_event(hev.ev[0])) != hipSuccess) return drain_fail(e, "sync");
+  // per item: outliers, :164-203 the sequential partition (strict >), :48-51
+  // ceil(exp(sum KL)) per group, and its groups' global offsets and seeds
+  int64_t Gtot = 0;
+  for (int64_t i = 0; i < I; ++i) {
+    const int64_t a = item_off[i], Di = item_off[i + 1] - a;
+    int64_t no = 0;
+    for (int64_t j = 0; j < Di; ++j)
+      if (!keep_h[a + j]) {
+        outlier_idx_host[a + no] = j;
+        outlier_val_host[a + no] = ts_h[a + j];
+        ++no;
+      }
+    n_outliers[i] = no;
+    if (kl_sum_out) {  // log line only
+      double t = 0.0;
+      for (int64_t j = 0; j < Di; ++j) t += (double)kl_h[a + j];
+      kl_sum_out[i] = t;
     }
-  *n_outliers = no;
-  if (kl_sum_out) {  // log line only
-    double t = 0.0;
-    for (int64_t j = 0; j < D; ++j) t += (double)kl_h[j];
-    *kl_sum_out = t;
+    if (Di == 0) continue;
+    int64_t* st = starts_host + a + 2 * i;
+    const int64_t n = group_starts_impl(kl_h + a, Di, size_threshold, n_nats, st, Di + 2, true);
+    if (n < 0) return drain_rc(n);
+    const int64_t G = n - 1;
+    n_starts[i] = n;
+    if ((rc = cwq_importance_plan(kl_h + a, st, G, ns_h + Gtot)) < 0) return drain_rc(rc);
+    for (int64_t g = 0; g < G; ++g) {
+      offs_h[Gtot + g] = a + st[g];
+      gs_h[Gtot + g] = (int32_t)((uint32_t)seeds[i] + (uint32_t)g);  // :243 seed + g
+    }
+    Gtot += G;
   }
-  // :164-203 the sequential partition (strict >), :48-51 ceil(exp(sum KL)) per group
-  const int64_t n = group_starts_impl(kl_h, D, size_threshold, n_nats, starts_host, starts_cap,
-                                      true);
-  if (n < 0) return n;
-  const int64_t G = n - 1;
-  if ((rc = cwq_importance_plan(kl_h, starts_host, G, ns_h)) < 0) return rc;
-  if (G > 0) {
-    memcpy(offs_h, starts_host, (size_t)(G + 1) * 8);
-    if ((e = hipMemcpyAsync(offs, offs_h, (size_t)(G + 1) * 8, hipMemcpyHostToDevice, s)) !=
+  offs_h[Gtot] = D;
+  int64_t tcand = 0;  // the launch's candidates (selects the encoder's instantiation)
+  for (int64_t g = 0; g < Gtot; ++g) tcand += ns_h[g] > 1 ? ns_h[g] : 1;
+  if (Gtot > 0) {
+    if ((e = hipMemcpyAsync(offs, offs_h, (size_t)(Gtot + 1) * 8, hipMemcpyHostToDevice, s)) !=
             hipSuccess ||
-        (e = hipMemcpyAsync(nsamp, ns_h, (size_t)G * 8, hipMemcpyHostToDevice, s)) != hipSuccess)
-      return hip_fail(e, "plan to device");
-    // :212-245 every group's importance coder, seed + g; eval_ms_out: its
-    // launches timed with events of this call (the call synchronises anyway)
-    cwq_options oi;
-    if ((rc = read_options(opts, &oi)) != 0) return rc;
+        (e = hipMemcpyAsync(nsamp, ns_h, (size_t)Gtot * 8, hipMemcpyHostToDevice, s)) !=
+            hipSuccess ||
+        (I > 1 && (e = hipMemcpyAsync(gseed, gs_h, (size_t)Gtot * 4, hipMemcpyHostToDevice, s)) !=
+                      hipSuccess))
+      return drain_fail(e, "plan to device");
+    // :212-245 every group's importance coder; eval_ms_out: its launches timed
+    // with events of this call (the call synchronises anyway)
     CallEvents tev;
-    if (oi.eval_ms_out) {
-      if (!tev.made(2, s, hipEventDefault))
-        return fail(CWQ_ERR_HIP, "cwq_code_grouped_importance: event creation failed");
-      oi.eval_start_event = tev.ev[0];
-      oi.eval_stop_event = tev.ev[1];
-    }
-    if ((rc = cwq_importance_encode(t_loc, t_scale, zeros, ones, offs, nsamp, G, D, seed, 0, idx,
-                                    sample, w + l.enc, workspace_bytes - l.enc, &oi, stream)) < 0)
-      return rc;
+    if (oi.eval_ms_out && !tev.made(2, s, hipEventDefault))
+      return drain_rc(fail(CWQ_ERR_HIP, "%s: event creation failed", who));
+    if ((oi.eval_ms_out && (e = hipEventRecord(tev.ev[0], s)) != hipSuccess) ||
+        (e = cwq::launch_importance_encode(t_loc, t_scale, zeros, ones, offs, nsamp, Gtot, D,
+                                           seeds[0], 0, I > 1 ? gseed : nullptr,
+                                           oi.prune_mode >= 2 ? 1 : 0, idx, sample, w + l.enc,
+                                           s, tcand)) != hipSuccess ||
+        (oi.eval_ms_out && (e = hipEventRecord(tev.ev[1], s)) != hipSuccess))
+      return drain_fail(e, "importance encode");
     if (oi.eval_ms_out) {
       if ((e = hipEventSynchronize(tev.ev[1])) != hipSuccess ||
           (e = hipEventElapsedTime(oi.eval_ms_out, tev.ev[0], tev.ev[1])) != hipSuccess)
-        return hip_fail(e, "event time");
+        return drain_fail(e, "event time");
     }
   } else {
-    if ((e = hipMemsetAsync(sample, 0, (size_t)D * 4, s)) != hipSuccess)
-      return hip_fail(e, "memset");
+    if ((e = hipMemsetAsync(sample, 0, Dz * 4, s)) != hipSuccess) return drain_fail(e, "memset");
   }
   // :265 rescale, :267 outliers keep their target draw
-  if ((rc = cwq_destandardise(sample, p_loc, p_scale, D, out, stream)) < 0) return rc;
-  if ((G > 0 && (e = hipMemcpyAsync(idx_h, idx, (size_t)G * 8, hipMemcpyDeviceToHost, s)) !=
-                    hipSuccess) ||
+  if ((e = cwq::launch_destandardise(sample, p_loc, p_scale, D, out, s)) != hipSuccess)
+    return drain_fail(e, "destandardise");
+  if ((Gtot > 0 && (e = hipMemcpyAsync(idx_h, idx, (size_t)Gtot * 8, hipMemcpyDeviceToHost, s)) !=
+                       hipSuccess) ||
       (e = hipMemcpyAsync(out_h, out, Dz * 4, hipMemcpyDeviceToHost, s)) != hipSuccess ||
-      (e = hipEventRecord(hev.ev[1], s)) != hipSuccess) {
-    (void)hipStreamSynchronize(s);
-    return hip_fail(e, "to host");
+      (e = hipEventRecord(hev.ev[1], s)) != hipSuccess)
+    return drain_fail(e, "to host");
+  if ((e = wait_event(hev.ev[1])) != hipSuccess) return drain_fail(e, "sync");
+  int64_t gb = 0;
+  for (int64_t i = 0; i < I; ++i) {
+    const int64_t G = n_starts[i] - 1;
+    if (G > 0) memcpy(index_host + item_off[i] + i, idx_h + gb, (size_t)G * 8);
+    gb += G;
   }
-  if ((e = wait_event(hev.ev[1])) != hipSuccess) return hip_fail(e, "sync");
-  if (G > 0) memcpy(index_host, idx_h, (size_t)G * 8);
   for (int64_t j = 0; j < D; ++j) sample_host[j] = keep_h[j] ? out_h[j] : ts_h[j];
   cwq::set_error(CWQ_OK, "");
-  return G;
+  return Gtot;
+}
+}  // namespace
+
+size_t cwq_code_grouped_importance_workspace_size(int64_t D) {
+  if (D < 0) return 0;
+  return grouped_imp_ws(D, 1).total;
+}
+
+int64_t cwq_code_grouped_importance(const float* q_loc, const float* q_scale,
+                                    const float* p_loc, const float* p_scale, int64_t D,
+                                    int32_t seed, float dim_kl_bit_limit, int64_t size_threshold,
+                                    double n_nats, float* sample_host, int64_t* index_host,
+                                    int64_t* starts_host, int64_t starts_cap,
+                                    int64_t* outlier_idx_host, float* outlier_val_host,
+                                    int64_t* n_outliers, double* kl_sum_out, void* workspace,
+                                    size_t workspace_bytes, const cwq_options* opts,
+                                    void* stream) {
+  if (D < 0) return fail(CWQ_ERR_INVALID, "cwq_code_grouped_importance: negative size");
+  const int64_t item_off[2] = {0, D};
+  int64_t n_starts = 0;
+  return grouped_importance_impl(1, item_off, q_loc, q_scale, p_loc, p_scale, &seed,
+                                 dim_kl_bit_limit, size_threshold, n_nats, sample_host,
+                                 index_host, starts_host, starts_cap, &n_starts, outlier_idx_host,
+                                 outlier_val_host, n_outliers, kl_sum_out, workspace,
+                                 workspace_bytes, opts, stream, "cwq_code_grouped_importance");
+}
+
+size_t cwq_code_grouped_importance_batch_workspace_size(int64_t D_total, int64_t n_items) {
+  if (D_total < 0 || n_items < 1) return 0;
+  return grouped_imp_ws(D_total, n_items).total;
+}
+
+int64_t cwq_code_grouped_importance_batch(
+    int64_t n_items, const int64_t* item_off, const float* q_loc, const float* q_scale,
+    const float* p_loc, const float* p_scale, const int32_t* seeds, float dim_kl_bit_limit,
+    int64_t size_threshold, double n_nats, float* sample_host, int64_t* index_host,
+    int64_t* starts_host, int64_t starts_cap, int64_t* n_starts, int64_t* outlier_idx_host,
+    float* outlier_val_host, int64_t* n_outliers, double* kl_sum_out, void* workspace,
+    size_t workspace_bytes, const cwq_options* opts, void* stream) {
+  return grouped_importance_impl(n_items, item_off, q_loc, q_scale, p_loc, p_scale, seeds,
+                                 dim_kl_bit_limit, size_threshold, n_nats, sample_host,
+                                 index_host, starts_host, starts_cap, n_starts, outlier_idx_host,
+                                 outlier_val_host, n_outliers, kl_sum_out, workspace,
+                                 workspace_bytes, opts, stream,
+                                 "cwq_code_grouped_importance_batch");
 }
 
 int64_t cwq_group_starts(const float* kl, int64_t D, int64_t size_threshold, double n_nats,
@@ -2082,7 +2176,8 @@ int cwq_importance_encode(const float* t_loc, const float* t_scale, const float*
     e = hipEventRecord((hipEvent_t)o.eval_start_event, (hipStream_t)stream);
   if (e == hipSuccess)
     e = cwq::launch_importance_encode(t_loc, t_scale, p_loc, p_scale, block_off, n_samples, nb,
-                                      total_dims, seed, block_id_base, o.prune_mode >= 2 ? 1 : 0,
+                                      total_dims, seed, block_id_base, nullptr,
+                                      o.prune_mode >= 2 ? 1 : 0,
                                       out_index, out_sample, workspace, (hipStream_t)stream);
   if (e == hipSuccess && o.eval_stop_event)
     e = hipEventRecord((hipEvent_t)o.eval_stop_event, (hipStream_t)stream);

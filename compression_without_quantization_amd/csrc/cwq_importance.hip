@@ -36,41 +36,90 @@ __global__ void __launch_bounds__(256) k_imp_prep(const float* __restrict__ t_sc
   }
 }
 
+// Tile size: the launch's candidates cut into about kImpTargetTiles tiles (a
+// few per CU, so one image's ~600 groups do not leave most of a fixed grid
+// idle), a power of two in [kImpMinCandPerTile, kImpCandPerTile].
+#ifndef CWQ_IMP_TARGET_TILES
+#define CWQ_IMP_TARGET_TILES 2048
+#endif
+#ifndef CWQ_IMP_MIN_CPT
+#define CWQ_IMP_MIN_CPT 1024
+#endif
+constexpr int64_t kImpMinCandPerTile = CWQ_IMP_MIN_CPT;
+constexpr int64_t kImpEvalGrid = 256 * 16;  // persistent k_imp_eval workgroups
+
+// The tile-size rule (k_imp_tiles on the device; the launcher on the host
+// when it knows the launch's candidate count T = sum max(N_g, 1)).
+__host__ __device__ inline int64_t imp_cand_per_tile(int64_t T) {
+  int64_t cpt = kImpMinCandPerTile;
+  while (cpt < kImpCandPerTile && cpt * CWQ_IMP_TARGET_TILES < T) cpt <<= 1;
+  return cpt;
+}
+
+// Exclusive prefix over the 1024 threads of the workgroup (inclusive wave scans
+// by shuffles, then the 16 wave totals).  Returns the prefix and
+// sets *total.
+__device__ __forceinline__ int64_t block_exclusive_scan_1024(int64_t v, int64_t* wsum,
+                                                            int64_t* total) {
+  const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+  int64_t inc = v;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const int64_t o = __shfl_up(inc, off, 64);
+    if ((int)lane >= off) inc += o;
+  }
+  if (lane == 63u) wsum[wv] = inc;
+  __syncthreads();
+  int64_t base = 0, all = 0;
+  for (uint32_t w = 0; w < 16u; ++w) {
+    const int64_t t = wsum[w];
+    base += w < wv ? t : 0;
+    all += t;
+  }
+  __syncthreads();
+  *total = all;
+  return base + inc - v;
+}
+
+// Chooses the launch's candidates per tile (*cpt_out), then
 // tprefix[g] = sum_{h<g} ceil(max(N_h,1) / cpt); tprefix[nb] = total tiles.
-// Also resets the per-group shared screening threshold gtau[g].
+// Also resets the per-group shared screening threshold gtau[g] and the
+// dynamic hand-out counter.  One workgroup of 1024 threads, each over a
+// contiguous run of groups.
 __global__ void __launch_bounds__(1024) k_imp_tiles(const int64_t* __restrict__ n_samples,
-                                                    int64_t nb, int64_t cpt,
+                                                    int64_t nb, int64_t* __restrict__ cpt_out,
                                                     int64_t* __restrict__ tprefix,
                                                     uint32_t* __restrict__ gtau,
                                                     unsigned long long* __restrict__ next_tile) {
+  __shared__ int64_t wsum[16];
   if (threadIdx.x == 0) *next_tile = 0ull;
-  __shared__ int64_t part[1024];
   const int64_t chunk = (nb + 1023) / 1024;
   const int64_t g0 = threadIdx.x * chunk;
   const int64_t g1 = (g0 + chunk < nb) ? g0 + chunk : nb;
-  int64_t sum = 0;
+  int64_t cand = 0;
   for (int64_t g = g0; g < g1; ++g) {
     const int64_t n = n_samples[g] > 1 ? n_samples[g] : 1;
-    sum += (n + cpt - 1) / cpt;
+    cand += n;
     gtau[g] = ord_f32(-__builtin_inff());
   }
-  part[threadIdx.x] = sum;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    int64_t run = 0;
-    for (int i = 0; i < 1024; ++i) {
-      const int64_t v = part[i];
-      part[i] = run;
-      run += v;
-    }
-    tprefix[nb] = run;
+  int64_t T = 0;
+  (void)block_exclusive_scan_1024(cand, wsum, &T);
+  const int64_t cpt = imp_cand_per_tile(T);
+  int64_t tiles = 0;
+  for (int64_t g = g0; g < g1; ++g) {
+    const int64_t n = n_samples[g] > 1 ? n_samples[g] : 1;
+    tiles += (n + cpt - 1) / cpt;
   }
-  __syncthreads();
-  int64_t run = part[threadIdx.x];
+  int64_t all = 0;
+  int64_t run = block_exclusive_scan_1024(tiles, wsum, &all);
   for (int64_t g = g0; g < g1; ++g) {
     tprefix[g] = run;
     const int64_t n = n_samples[g] > 1 ? n_samples[g] : 1;
     run += (n + cpt - 1) / cpt;
+  }
+  if (threadIdx.x == 0) {
+    tprefix[nb] = all;
+    *cpt_out = cpt;
   }
 }
 
@@ -168,14 +217,25 @@ __device__ __forceinline__ bool imp_screen_dim(float tl, float ts, float pl, flo
 #ifndef CWQ_IMP_MIN_WAVES
 #define CWQ_IMP_MIN_WAVES 1  // waves/SIMD the register allocator must allow (tools/variants.sh)
 #endif
+// PER_BLOCK: group seeds from seeds.per_block (a batch of items); else
+// seed + base + g.  CPT_MAX: the launch's tile size is kImpCandPerTile (the
+// host knows its candidate count; k_imp_tiles picks the same size).  Both as
+// template flags: the pointer and the tile size held in SGPRs through the
+// loops cost I1 6% (more scalar spills in the screening loop).
+template <bool PER_BLOCK, bool CPT_MAX>
 __global__ void __launch_bounds__(256, CWQ_IMP_MIN_WAVES) k_imp_eval(
     const float* __restrict__ t_loc, const float* __restrict__ t_scale,
     const float* __restrict__ p_loc, const float* __restrict__ p_scale,
     const float* __restrict__ lnt, const float* __restrict__ lnp,
     const int64_t* __restrict__ block_off, const int64_t* __restrict__ n_samples, int64_t nb,
-    const int64_t* __restrict__ tprefix, int64_t cpt, int32_t seed, int64_t block_id_base,
+    const int64_t* __restrict__ tprefix, const int64_t* __restrict__ cpt_p, SeedSpec seeds,
     int allow_screen, uint32_t* __restrict__ gtau, unsigned long long* __restrict__ keys,
     unsigned long long* __restrict__ next_tile) {
+  const int64_t total = tprefix[nb];
+  // the grid is fixed (the tile count is only known on the device): workgroups
+  // without a tile of the static assignment leave at once
+  if (!next_tile && (int64_t)blockIdx.x >= total) return;
+  const int64_t cpt = CPT_MAX ? kImpCandPerTile : *cpt_p;
   __shared__ int64_t s_tile;
   __shared__ double logtab[32];
   __shared__ float4 coef[kImpScreenMaxD];   // A, B, C per dim (screening)
@@ -192,7 +252,6 @@ __global__ void __launch_bounds__(256, CWQ_IMP_MIN_WAVES) k_imp_eval(
   fill_logtab(logtab);
   const uint32_t wv = wave_id();
   const uint32_t lane = threadIdx.x & 63u;
-  const int64_t total = tprefix[nb];
 
   // Many groups: tiles differ in size by orders of magnitude (N_g from 1 to
   // ~4e5), so they are handed out one at a time through a global counter
@@ -233,7 +292,8 @@ __global__ void __launch_bounds__(256, CWQ_IMP_MIN_WAVES) k_imp_eval(
     const int64_t N = n_samples[g] > 1 ? n_samples[g] : 1;
     const int64_t n0 = (tq - tprefix[g]) * cpt;
     const int64_t n1 = (n0 + cpt < N) ? n0 + cpt : N;
-    const PhiloxStream st = generate_key(block_seed(seed, block_id_base + g), 42);
+    const PhiloxStream st = generate_key(
+        PER_BLOCK ? seeds.per_block[g] : block_seed(seeds.seed, seeds.base + g), 42);
     const int align = (int)(((uint64_t)(n0 + wv) * (uint64_t)d) & 3u);
     const float* tl = t_loc + off;
     const float* ts = t_scale + off;
@@ -373,10 +433,30 @@ __global__ void __launch_bounds__(256, CWQ_IMP_MIN_WAVES) k_imp_eval(
             }
           }
         } else {
-          for (int64_t n = n0 + 4 * (int64_t)lane + wv; n < n1; n += 256) {
-            const float sh = screen_row_imp<HI0>(st, lok, (uint64_t)n * (uint64_t)d, d, align, coef);
-            const float slack = E + __builtin_fabsf(sh) * 0x1p-22f;
-            if (sh + slack >= tau) keep(n, sh, slack);
+          // short rows, no pruning: every row screened, listed if it may be
+          // the best.  tau is shared in the wave after each of the first four
+          // rounds and every fourth after (a lane-private tau lists ~ln(rows)
+          // rows per lane, which overflowed the list into in-line exact rows),
+          // and with the workgroup and the group's other tiles every 16.
+          const int64_t iters = (n1 - n0 + 255) >> 8;  // wave-uniform trip count
+          for (int64_t it = 0; it < iters; ++it) {
+            const int64_t n = n0 + (it << 8) + 4 * (int64_t)lane + wv;
+            if (n < n1) {
+              const float sh =
+                  screen_row_imp<HI0>(st, lok, (uint64_t)n * (uint64_t)d, d, align, coef);
+              const float slack = E + __builtin_fabsf(sh) * 0x1p-22f;
+              if (sh + slack >= tau) keep(n, sh, slack);
+            }
+            if (it < 4 || (it & 3) == 3) tau = wave_max_f32(tau);
+            if ((it & 15) == 15) {
+              if (lane == 0) atomicMax(&tau_ord, ord_f32(tau));
+              uint32_t o = __atomic_load_n(&tau_ord, __ATOMIC_RELAXED);
+              const uint32_t o2 = __hip_atomic_load(&gtau[g], __ATOMIC_RELAXED,
+                                                    __HIP_MEMORY_SCOPE_AGENT);
+              if (lane == 0 && ord_f32(tau) > o2) atomicMax(&gtau[g], ord_f32(tau));
+              o = o > o2 ? o : o2;
+              tau = fmaxf(tau, unord_f32(o));
+            }
           }
         }
       };
@@ -445,7 +525,7 @@ __global__ void __launch_bounds__(256, CWQ_IMP_MIN_WAVES) k_imp_eval(
 __global__ void __launch_bounds__(256) k_imp_rows(
     const unsigned long long* __restrict__ keys, const int64_t* __restrict__ index_in,
     const float* __restrict__ p_loc, const float* __restrict__ p_scale,
-    const int64_t* __restrict__ block_off, int64_t nb, int32_t seed, int64_t block_id_base,
+    const int64_t* __restrict__ block_off, int64_t nb, SeedSpec seeds,
     int64_t* __restrict__ index_out, float* __restrict__ out_sample) {
   __shared__ double logtab[32];
   fill_logtab(logtab);
@@ -462,7 +542,7 @@ __global__ void __launch_bounds__(256) k_imp_rows(
     } else {
       idx = index_in[g];
     }
-    const PhiloxStream st = generate_key(block_seed(seed, block_id_base + g), 42);
+    const PhiloxStream st = generate_key(seeds.of(g), 42);
     for (int64_t j = lane; j < d; j += 64) {
       float v = __builtin_nanf("");
       if (idx >= 0) {
@@ -513,12 +593,17 @@ size_t importance_workspace_size(int64_t nb, int64_t total_dims) {
          up((size_t)nb * 4) + 256;
 }
 
+// block_seeds: device [nb] per-group seeds (a batch of items, each numbering
+// its groups from 0 with its own seed), or nullptr: seed + block_id_base + g.
+// total_cands: sum over groups of max(n_samples[g], 1) when the host knows it
+// (-1: unknown; it only selects a kernel instantiation, never the results)
 hipError_t launch_importance_encode(const float* t_loc, const float* t_scale, const float* p_loc,
                                     const float* p_scale, const int64_t* block_off,
                                     const int64_t* n_samples, int64_t nb, int64_t total_dims,
-                                    int32_t seed, int64_t block_id_base, int allow_screen,
+                                    int32_t seed, int64_t block_id_base,
+                                    const int32_t* block_seeds, int allow_screen,
                                     int64_t* out_index, float* out_sample, void* workspace,
-                                    hipStream_t stream) {
+                                    hipStream_t stream, int64_t total_cands) {
   if (nb <= 0) return hipSuccess;
   auto up = [](size_t v) { return (v + 255) / 256 * 256; };
   char* w = (char*)workspace;
@@ -528,20 +613,25 @@ hipError_t launch_importance_encode(const float* t_loc, const float* t_scale, co
   float* lnp = lnt + up((size_t)total_dims * 4) / 4;
   uint32_t* gtau = (uint32_t*)((char*)lnp + up((size_t)total_dims * 4));
   unsigned long long* next_tile = (unsigned long long*)((char*)gtau + up((size_t)nb * 4));
+  int64_t* cpt = (int64_t*)(next_tile + 1);
+  const SeedSpec ss{seed, block_id_base, block_seeds};
   hipError_t e = hipMemsetAsync(keys, 0, (size_t)nb * 8, stream);
   if (e != hipSuccess) return e;
   if (total_dims > 0)
     hipLaunchKernelGGL(k_imp_prep, dim3(grid_for(total_dims, 256, 65536)), dim3(256), 0, stream,
                        t_scale, p_scale, total_dims, lnt, lnp);
-  hipLaunchKernelGGL(k_imp_tiles, dim3(1), dim3(1024), 0, stream, n_samples, nb,
-                     kImpCandPerTile, tprefix, gtau, next_tile);
-  hipLaunchKernelGGL(k_imp_eval, dim3(256 * 16), dim3(256), 0, stream, t_loc, t_scale, p_loc,
-                     p_scale, lnt, lnp, block_off, n_samples, nb, tprefix, kImpCandPerTile, seed,
-                     block_id_base, allow_screen, gtau, keys,
+  hipLaunchKernelGGL(k_imp_tiles, dim3(1), dim3(1024), 0, stream, n_samples, nb, cpt, tprefix,
+                     gtau, next_tile);
+  const bool cmax = total_cands >= 0 && imp_cand_per_tile(total_cands) == kImpCandPerTile;
+  auto eval = block_seeds ? (cmax ? k_imp_eval<true, true> : k_imp_eval<true, false>)
+                          : (cmax ? k_imp_eval<false, true> : k_imp_eval<false, false>);
+  hipLaunchKernelGGL(eval, dim3((unsigned)kImpEvalGrid), dim3(256), 0, stream, t_loc, t_scale,
+                     p_loc, p_scale, lnt, lnp, block_off, n_samples, nb, (const int64_t*)tprefix,
+                     (const int64_t*)cpt, ss, allow_screen, gtau, keys,
                      nb >= CWQ_IMP_DYNAMIC_MIN_GROUPS ? next_tile : nullptr);
   hipLaunchKernelGGL(k_imp_rows, dim3(grid_for(nb, 4, 65536)), dim3(256), 0, stream,
                      (const unsigned long long*)keys, (const int64_t*)nullptr, p_loc, p_scale,
-                     block_off, nb, seed, block_id_base, out_index, out_sample);
+                     block_off, nb, ss, out_index, out_sample);
   return hipGetLastError();
 }
 
@@ -552,7 +642,7 @@ hipError_t launch_importance_decode(const int64_t* index, const float* p_loc,
   if (nb <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_imp_rows, dim3(grid_for(nb, 4, 65536)), dim3(256), 0, stream,
                      (const unsigned long long*)nullptr, index, p_loc, p_scale, block_off, nb,
-                     seed, block_id_base, (int64_t*)nullptr, out_sample);
+                     SeedSpec{seed, block_id_base, nullptr}, (int64_t*)nullptr, out_sample);
   return hipGetLastError();
 }
 

@@ -112,14 +112,18 @@ hipError_t launch_kl(const float* q_loc, const float* q_scale, const float* p_lo
                      const float* p_scale, int64_t n, float* out, hipStream_t stream);
 hipError_t launch_destandardise(const float* sample, const float* p_loc, const float* p_scale,
                                 int64_t n, float* out, hipStream_t stream);
+// the grouped importance coder's standardise + KL + outliers + standard prior
+// + KL against N(0, 1) + the outlier dims' target draw (seed - 1 per item:
+// item_off / seed1 device arrays of a batch, or item_off == nullptr and
+// seed1_one for one item), one launch (cwq_code_grouped_importance[_batch])
+hipError_t launch_imp_grouped_prep(const float* q_loc, const float* q_scale, const float* p_loc,
+                                   const float* p_scale, int64_t n, float limit,
+                                   const int64_t* item_off, const int32_t* seed1, int64_t n_items,
+                                   int32_t seed1_one, float* t_loc, float* t_scale, uint8_t* keep,
+                                   float* zeros, float* ones, float* kl2, float* tsamp,
+                                   hipStream_t stream);
 // standardise + KL + the standard prior's zeros/ones + nz zeroed u64 at zinfo
 // (nz <= 256), one launch (the grouped coder's first step)
-// the grouped importance coder's standardise + KL + outliers + standard prior
-// + KL against N(0, 1), one launch (cwq_code_grouped_importance)
-hipError_t launch_imp_grouped_prep(const float* q_loc, const float* q_scale, const float* p_loc,
-                                   const float* p_scale, int64_t n, float limit, float* t_loc,
-                                   float* t_scale, uint8_t* keep, float* zeros, float* ones,
-                                   float* kl2, hipStream_t stream);
 hipError_t launch_grouped_prep(const float* q_loc, const float* q_scale, const float* p_loc,
                                const float* p_scale, int64_t n, float* t_loc, float* t_scale,
                                float* kl, float* zeros, float* ones, unsigned long long* zinfo,
@@ -161,9 +165,10 @@ hipError_t launch_imp_outliers(const float* kl, int64_t n, float limit, float* t
 hipError_t launch_importance_encode(const float* t_loc, const float* t_scale, const float* p_loc,
                                     const float* p_scale, const int64_t* block_off,
                                     const int64_t* n_samples, int64_t nb, int64_t total_dims,
-                                    int32_t seed, int64_t block_id_base, int allow_screen,
+                                    int32_t seed, int64_t block_id_base,
+                                    const int32_t* block_seeds, int allow_screen,
                                     int64_t* out_index, float* out_sample, void* workspace,
-                                    hipStream_t stream);
+                                    hipStream_t stream, int64_t total_cands = -1);
 hipError_t launch_importance_decode(const int64_t* index, const float* p_loc,
                                     const float* p_scale, const int64_t* block_off, int64_t nb,
                                     int32_t seed, int64_t block_id_base, float* out_sample,

@@ -2979,17 +2979,26 @@ __global__ void __launch_bounds__(256) k_grouped_prep(
 }
 
 // The grouped importance coder's first launch (coded_importance_sampler.py:
-// 137-148, 160-163) in one pass: the standardised target (k_standardise's
+// 137-148, 150, 160-163) in one pass: the standardised target (k_standardise's
 // expressions), the per-dim KL (k_kl_normal_normal's) and the outlier test
 // (k_imp_outliers': bits = kl / np.float32(log 2) <= limit, NaN an outlier,
-// outliers standardised to N(0, 1)), the standard prior's zeros and ones, and
-// the KL of the (masked) standardised target against N(0, 1), which is what
-// the partition and the plan read.
+// outliers standardised to N(0, 1)), the standard prior's zeros and ones, the
+// KL of the (masked) standardised target against N(0, 1), which is what the
+// partition and the plan read, and, for the outlier dims only, the target draw
+// q_loc + q_scale z (:150; z element j of stateless_normal([1, D], [seed - 1,
+// 42]), k_stateless_normal_sample's expressions).  A batch of
+// items (item_off: device [n_items + 1], seed1: device [n_items] of
+// seed - 1) numbers each item's dims from 0 in its own stream; item_off ==
+// nullptr: one item with seed - 1 = seed1_one.
 __global__ void __launch_bounds__(256) k_imp_grouped_prep(
     const float* __restrict__ q_loc, const float* __restrict__ q_scale,
     const float* __restrict__ p_loc, const float* __restrict__ p_scale, int64_t n, float limit,
-    float* __restrict__ t_loc, float* __restrict__ t_scale, uint8_t* __restrict__ keep,
-    float* __restrict__ zeros, float* __restrict__ ones, float* __restrict__ kl2) {
+    const int64_t* __restrict__ item_off, const int32_t* __restrict__ seed1, int64_t n_items,
+    int32_t seed1_one, float* __restrict__ t_loc, float* __restrict__ t_scale,
+    uint8_t* __restrict__ keep, float* __restrict__ zeros, float* __restrict__ ones,
+    float* __restrict__ kl2, float* __restrict__ tsamp) {
+  __shared__ double logtab[32];
+  fill_logtab(logtab);
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x) {
     const float ql = q_loc[i], qs = q_scale[i], pl = p_loc[i], ps = p_scale[i];
@@ -3002,6 +3011,23 @@ __global__ void __launch_bounds__(256) k_imp_grouped_prep(
     if (!k) {
       tl = 0.0f;
       ts = 1.0f;
+      int64_t j = i;
+      int32_t sd = seed1_one;
+      if (item_off) {  // item of dim i: last it with item_off[it] <= i
+        int64_t lo = 0, hi = n_items;
+        while (hi - lo > 1) {
+          const int64_t mid = (lo + hi) >> 1;
+          if (item_off[mid] <= i) lo = mid; else hi = mid;
+        }
+        j = i - item_off[lo];
+        sd = seed1[lo];
+      }
+      const F4 z = normal4_dev(generate_key(sd, 42), (uint64_t)j >> 2, logtab);
+      const uint32_t w = (uint32_t)j & 3u;
+      const float zz = w == 0 ? z.a : (w == 1 ? z.b : (w == 2 ? z.c : z.d));
+      const float r = zz * 1.0f + 0.0f;  // rnd * stddev + mean
+      const float sm = qs * r;           // misc.py:14
+      tsamp[i] = ql + sm;                // misc.py:15
     }
     t_loc[i] = tl;
     t_scale[i] = ts;
@@ -3656,13 +3682,15 @@ hipError_t launch_grouped_prep(const float* q_loc, const float* q_scale, const f
 }
 
 hipError_t launch_imp_grouped_prep(const float* q_loc, const float* q_scale, const float* p_loc,
-                                   const float* p_scale, int64_t n, float limit, float* t_loc,
-                                   float* t_scale, uint8_t* keep, float* zeros, float* ones,
-                                   float* kl2, hipStream_t stream) {
+                                   const float* p_scale, int64_t n, float limit,
+                                   const int64_t* item_off, const int32_t* seed1, int64_t n_items,
+                                   int32_t seed1_one, float* t_loc, float* t_scale, uint8_t* keep,
+                                   float* zeros, float* ones, float* kl2, float* tsamp,
+                                   hipStream_t stream) {
   if (n <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_imp_grouped_prep, dim3(grid_for(n, 256, 65536)), dim3(256), 0, stream,
-                     q_loc, q_scale, p_loc, p_scale, n, limit, t_loc, t_scale, keep, zeros, ones,
-                     kl2);
+                     q_loc, q_scale, p_loc, p_scale, n, limit, item_off, seed1, n_items, seed1_one,
+                     t_loc, t_scale, keep, zeros, ones, kl2, tsamp);
   return hipGetLastError();
 }
 

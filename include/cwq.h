@@ -73,8 +73,9 @@ extern "C" {
  *   0.4  per-item ready flags of the batched grouped coder
  *        (cwq_options.item_ready);
  *   0.5  CWQ_ERR_ALLOC (host allocation failures are returned, never thrown);
- *        starts_host of the grouped _begin calls is read asynchronously. */
-#define CWQ_ABI_VERSION ((0 << 16) | 5)
+ *        starts_host of the grouped _begin calls is read asynchronously;
+ *   0.6  cwq_code_grouped_importance_batch. */
+#define CWQ_ABI_VERSION ((0 << 16) | 6)
 int cwq_version(void);
 
 /* Thread-local description of the last error ("" if none). */
@@ -344,6 +345,36 @@ int64_t cwq_code_grouped_importance(const float* q_loc, const float* q_scale,
                                     int64_t* n_outliers, double* kl_sum_out, void* workspace,
                                     size_t workspace_bytes, const cwq_options* opts,
                                     void* stream);
+
+/* A batch of independent code_grouped_importance_sample calls
+ * (coded_importance_sampler.py:112-274 once per item: the level-2 latents of
+ * a dataset's images, pln.py:350-359) in one call.  Item i is dims
+ * [item_off[i], item_off[i+1]) of the concatenated DEVICE q_* / p_* (item_off:
+ * HOST int64 [n_items + 1], item_off[0] == 0) and is coded exactly as
+ * cwq_code_grouped_importance on that slice with seed seeds[i] (HOST int32
+ * [n_items]): its own outliers and outlier draw ([seeds[i] - 1, 42] over its
+ * own dims), its own partition and plan, its groups numbered from 0 and coded
+ * with seeds[i] + g.  One preparation launch and one encode launch serve every
+ * item.  HOST outputs, item i's at the offsets shown:
+ *   sample_host [D_total] (item i's dims in place);
+ *   index_host + item_off[i] + i: its G_i argmax indices (capacity D_total +
+ *     n_items);
+ *   starts_host + item_off[i] + 2 i: its group starts incl. its trailing D_i,
+ *     n_starts[i] (= G_i + 1) of them (starts_cap >= D_total + 2 n_items);
+ *   outlier_idx_host / outlier_val_host + item_off[i]: its n_outliers[i]
+ *     outlier dims (local indices) and their unquantised draws;
+ *   kl_sum_out [n_items] (optional): each item's standardised KL in nats.
+ * opts->eval_ms_out receives the encode launches' milliseconds.  Returns the
+ * total number of groups, or a negative error code.  Blocks the host until
+ * the results are on it. */
+size_t cwq_code_grouped_importance_batch_workspace_size(int64_t D_total, int64_t n_items);
+int64_t cwq_code_grouped_importance_batch(
+    int64_t n_items, const int64_t* item_off, const float* q_loc, const float* q_scale,
+    const float* p_loc, const float* p_scale, const int32_t* seeds, float dim_kl_bit_limit,
+    int64_t size_threshold, double n_nats, float* sample_host, int64_t* index_host,
+    int64_t* starts_host, int64_t starts_cap, int64_t* n_starts, int64_t* outlier_idx_host,
+    float* outlier_val_host, int64_t* n_outliers, double* kl_sum_out, void* workspace,
+    size_t workspace_bytes, const cwq_options* opts, void* stream);
 
 /* ---- Arithmetic coder (code/coding.pyx:27-310), HOST functions ---------- */
 /* ArithmeticCoder(P, precision).encode(message): writes the code as '0'/'1'

@@ -1009,6 +1009,10 @@ CWQO_API void cwqo_quantize_quint16(const float* x, int64_t n, float mn, float m
                                     uint16_t* out) {
   float scale = (float)((65535.0 - 0.0) / ((double)mx - (double)mn));
   for (int64_t i = 0; i < n; ++i) {
+    if (x[i] != x[i]) { /* NaN: code 0, as x86's truncating conversion */
+      out[i] = 0;
+      continue;
+    }
     float v = x[i] < mx ? x[i] : mx;   /* cwiseMin(max_range) */
     v = v > mn ? v : mn;               /* cwiseMax(min_range) */
     float t = (v - mn) * scale;

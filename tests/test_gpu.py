@@ -9,6 +9,7 @@ is unpinned (the reference cannot run here).
 import hashlib
 import json
 import os
+import warnings
 
 import numpy as np
 import pytest
@@ -537,6 +538,60 @@ def test_importance_grouped_golden(cwq, golden):
     _assert_bits_equal(dec2, dec, "use_indices decode")
 
 
+def test_importance_batch_equals_single_calls(cwq, oracle):
+    """code_grouped_importance_sample_batch (one native call for every item)
+    returns exactly what one code_grouped_importance_sample per item returns,
+    item i with its own seed: I2's shape (24 level-2 latent sets of 2,304 dims,
+    20 bits/group, groups <= 3 dims) plus an empty item, a 1-dim item, an item
+    with outliers and a NaN dim, and a wrapped seed; item 0 also against the
+    oracle's whole pipeline."""
+    import compression_without_quantization_amd.coded_importance_sampler as I
+    from compression_without_quantization_amd.synthetic import make_latents
+    I.VERBOSE = False
+    lat, seeds = [], []
+    for i in range(24):
+        lat.append(make_latents(8 * 12 * 24, seed=5000 + i))
+        seeds.append(42 + 3 * i)
+    for D, kind in ((0, "empty"), (1, "one"), (500, "outliers")):
+        q_loc, q_scale, p_loc, p_scale = make_latents(max(D, 1), bits_per_dim=1.5, seed=77 + D)
+        q_loc, q_scale, p_loc, p_scale = q_loc[:D], q_scale[:D], p_loc[:D], p_scale[:D]
+        if kind == "outliers":
+            q_loc[::40] = p_loc[::40] + 40 * p_scale[::40]
+            q_loc[7] = np.nan
+        lat.append((q_loc, q_scale, p_loc, p_scale))
+        seeds.append(2 ** 31 - 2 if kind == "outliers" else -5)
+    dev = torch.device("cuda", 0)
+    ts = [cwq.Normal(torch.from_numpy(a).to(dev), torch.from_numpy(b).to(dev)) for a, b, _, _ in lat]
+    ps = [cwq.Normal(torch.from_numpy(c).to(dev), torch.from_numpy(d).to(dev)) for _, _, c, d in lat]
+    with warnings.catch_warnings():
+        warnings.simplefilter("error", RuntimeWarning)
+        batch = I.code_grouped_importance_sample_batch(None, ts, ps, seeds, 20,
+                                                       max_group_size_bits=2,
+                                                       dim_kl_bit_limit=16)
+    assert len(batch) == len(lat)
+    for i, (t, p, s) in enumerate(zip(ts, ps, seeds)):
+        one = I.code_grouped_importance_sample(None, t, p, s, 20, max_group_size_bits=2,
+                                               dim_kl_bit_limit=16)
+        b = batch[i]
+        _assert_bits_equal(b[0], one[0], f"batch sample, item {i}")
+        assert b[1] == one[1], i
+        assert np.array_equal(np.asarray(b[2]), np.asarray(one[2])), i
+        assert np.array_equal(b[3][0], one[3][0]) and np.array_equal(b[3][1], one[3][1]), i
+    assert batch[24][1] == "" and list(batch[24][2]) == [0]
+    assert batch[26][3][0].size >= 12
+    # index form, and item 0 against the oracle's pipeline
+    idx = I.code_grouped_importance_sample_batch(None, ts[:1], ps[:1], seeds[:1], 20,
+                                                 max_group_size_bits=2, dim_kl_bit_limit=16,
+                                                 return_indices=True)[0]
+    ql, qs, pl, pls = lat[0]
+    wsm, wi, wst, (oi, oq) = oracle.code_grouped_importance_sample(ql, qs, pl, pls, seeds[0], 20,
+                                                                   2, 16)
+    assert list(idx[1]) == list(wi)
+    assert np.array_equal(np.asarray(idx[2]), np.asarray(wst))
+    assert np.array_equal(idx[3][0], oi) and np.array_equal(idx[3][1], oq)
+    _assert_bits_equal(idx[0], wsm, "batch item 0 vs oracle")
+
+
 # ---------------------------------------------------------------------------
 # importance sampler screening pass (DESIGN.md §8): the screened encoder must
 # give the same indices and samples as the exact one, also where the bound is
@@ -867,9 +922,11 @@ def test_importance_grouped_fused_matches_stepwise(cwq, kind):
         res = {}
         for fused in (True, False):
             I.USE_FUSED = fused
-            res[fused] = I.code_grouped_importance_sample(None, t, p, 42, 16,
-                                                          max_group_size_bits=3,
-                                                          dim_kl_bit_limit=12)
+            with warnings.catch_warnings():
+                warnings.simplefilter("error", RuntimeWarning)  # no undefined NaN cast
+                res[fused] = I.code_grouped_importance_sample(None, t, p, 42, 16,
+                                                              max_group_size_bits=3,
+                                                              dim_kl_bit_limit=12)
     finally:
         I.USE_FUSED, I.VERBOSE = old
     a, b = res[True], res[False]
@@ -879,6 +936,9 @@ def test_importance_grouped_fused_matches_stepwise(cwq, kind):
     assert np.array_equal(a[3][0], b[3][0]) and np.array_equal(a[3][1], b[3][1])
     if kind == "outliers":
         assert a[3][0].size >= 15
+    if kind == "nan_dim":  # a NaN outlier draw is coded as 0 (quantize_quint16)
+        k = list(a[3][0]).index(17)
+        assert a[3][1][k] == 0 and np.isnan(a[0][17])
 
 
 def test_capi_from_plain_c(cwq):

@@ -65,6 +65,18 @@ def test_quint16_matches_oracle(oracle):
     assert np.max(np.abs(d[inside] - x[inside])) <= 60 / 65535 / 2 * 1.01
 
 
+def test_quint16_nan_is_zero(oracle):
+    """A NaN outlier draw has a defined code: 0 (the code of -30), in the
+    product and the oracle, without NumPy's undefined float -> uint16 cast."""
+    import warnings
+    x = np.array([np.nan, -np.nan, 1.0, np.inf, -np.inf], dtype=np.float32)
+    with warnings.catch_warnings():
+        warnings.simplefilter("error", RuntimeWarning)
+        q = quantize_quint16(x)
+    assert q.tolist() == [0, 0, 33860, 65535, 0]
+    assert np.array_equal(q, oracle.quantize_quint16(x))
+
+
 @pytest.mark.parametrize("case", range(5))
 def test_importance_grouping_matches_transcription(oracle, cwqlib, case):
     rng = np.random.default_rng(40 + case)
