@@ -31,6 +31,7 @@ same workload and checks the GPU's indices/samples on that sample bit-exactly
 import argparse
 import json
 import os
+import subprocess
 import sys
 import time
 
@@ -115,6 +116,11 @@ def parse():
                          "split over the ranks) or weak (that many blocks per rank)")
     ap.add_argument("--check-blocks", type=int, default=16,
                     help="N > 1: blocks per rank checked against the CPU oracle")
+    ap.add_argument("--rank-timeout", type=float,
+                    default=float(os.environ.get("CWQ_BENCH_RANK_TIMEOUT", "480")),
+                    help="N > 1: wall-clock seconds the ranks may take in all (the parent "
+                         "stops ranks still running then and exits 124); also the process "
+                         "group's timeout for its collectives")
     args = ap.parse_args()
     block = args.config in CONFIGS
     if args.steps is None:
@@ -786,39 +792,79 @@ def _importance_work(target, proposal, starts, kl_lim, dev):
     return int((np.maximum(n, 1) * sizes).sum())
 
 
+def _stop_processes(procs, grace=5.0):
+    """SIGTERM the exact processes given, SIGKILL those still alive after
+    `grace` seconds, and reap them all (nothing is left running)."""
+    import signal
+    for p in procs:
+        if p.poll() is None:
+            p.send_signal(signal.SIGTERM)
+    t_end = time.monotonic() + grace
+    for p in procs:
+        try:
+            p.wait(timeout=max(0.0, t_end - time.monotonic()))
+        except subprocess.TimeoutExpired:
+            p.kill()
+            p.wait()
+
+
+def run_rank_processes(cmds, deadline_s, poll=0.05):
+    """Start one process per (argv, env) of `cmds` (rank r = cmds[r]) and wait
+    for them, with a wall-clock deadline.  The first rank to fail stops the
+    others (exact PIDs) and its exit code is returned; past `deadline_s` the
+    ranks still running are named on stderr, stopped, and 124 is returned (the
+    code of `timeout`).  Returns 0 when every rank exits 0."""
+    procs = [subprocess.Popen(argv, env=env) for argv, env in cmds]
+    t_end = time.monotonic() + deadline_s
+    rc = 0
+    live = list(procs)
+    try:
+        while live:
+            for p in list(live):
+                c = p.poll()
+                if c is None:
+                    continue
+                live.remove(p)
+                if c != 0 and rc == 0:
+                    rc = c
+                    print(f"bench.py: rank {procs.index(p)} exited with {c}; stopping ranks "
+                          f"{[procs.index(q) for q in live]}", file=sys.stderr, flush=True)
+                    _stop_processes(live)
+                    live = []
+                    break
+            if live and time.monotonic() > t_end:
+                print(f"bench.py: ranks {[procs.index(q) for q in live]} still running after "
+                      f"the {deadline_s:g} s deadline (--rank-timeout); stopping them",
+                      file=sys.stderr, flush=True)
+                _stop_processes(live)
+                live = []
+                rc = rc or 124
+            time.sleep(poll)
+    finally:
+        _stop_processes([p for p in procs if p.poll() is None])
+    return rc
+
+
 def spawn_ranks(args):
     """`bench.py --gpus N` (N > 1) without a launcher: start N fresh rank
     processes (RANK/LOCAL_RANK/WORLD_SIZE/MASTER_* in their environment, one
     GPU each) and wait for them.  This parent never touches the GPU (it only
     imports torch), so no process that initialised HIP is replaced or forked.
-    If a rank fails the others are stopped (exact PIDs) and its code returned."""
-    import signal
+    If a rank fails the others are stopped (exact PIDs) and its code returned;
+    ranks still running at the --rank-timeout deadline are stopped and the
+    parent exits 124."""
     import socket
-    import subprocess
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
     port = s.getsockname()[1]
     s.close()
-    procs = []
+    cmds = []
     for r in range(args.gpus):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus),
                    LOCAL_WORLD_SIZE=str(args.gpus), MASTER_ADDR="127.0.0.1",
                    MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY="0")
-        procs.append(subprocess.Popen([sys.executable, "-u", os.path.abspath(__file__)]
-                                      + sys.argv[1:], env=env))
-    rc = 0
-    live = list(procs)
-    while live:
-        for p in list(live):
-            c = p.poll()
-            if c is None:
-                continue
-            live.remove(p)
-            if c != 0 and rc == 0:
-                rc = c
-                for q in live:
-                    q.send_signal(signal.SIGTERM)
-        time.sleep(0.05)
+        cmds.append(([sys.executable, "-u", os.path.abspath(__file__)] + sys.argv[1:], env))
+    rc = run_rank_processes(cmds, args.rank_timeout)
     sys.exit(rc if rc >= 0 else 128 - rc)
 
 
@@ -909,6 +955,14 @@ def rank_device_map(dist, rank, local_rank, dev):
     return allm
 
 
+def devices_distinct(rank_devices):
+    """True when no two ranks share a GPU (same host and PCI bus, or, without a
+    bus id, the same visible set and device index)."""
+    keys = [(m["host"], m["pci_bus"] if m["pci_bus"] is not None else (m["visible"], m["device"]))
+            for m in rank_devices]
+    return len(set(keys)) == len(keys)
+
+
 def oracle_check(O, host, d, bits, n_steps, seed, block_id_base, idx_h, samp_h, blocks, nthr):
     """Indices and sample words of `blocks` (local block numbers) against the
     CPU oracle: the checker, outside every timed region."""
@@ -953,14 +1007,18 @@ def main():
         # RCCL when every rank owns a GPU (the data path itself has no collective:
         # only the start/stop barriers and the max-reduce of the step time use
         # it); gloo when ranks share one device (a rehearsal on a 1-GPU box)
+        import datetime
+        pg_timeout = datetime.timedelta(seconds=max(30.0, min(args.rank_timeout, 300.0)))
         if ndev >= world:
-            dist.init_process_group("nccl", device_id=dev)
+            dist.init_process_group("nccl", device_id=dev, timeout=pg_timeout)
         else:
-            dist.init_process_group("gloo")
+            dist.init_process_group("gloo", timeout=pg_timeout)
         if dist.get_world_size() != args.gpus:
             raise SystemExit(f"bench.py: process group has {dist.get_world_size()} ranks, "
                              f"--gpus {args.gpus}")
     rank_devices = rank_device_map(dist, rank, local_rank, dev)
+    if dist is not None and dist.get_backend() == "nccl" and not devices_distinct(rank_devices):
+        raise SystemExit("bench.py: RCCL ranks must own distinct GPUs")  # (rank_device_map)
 
     nb_cfg, d, bits, n_steps, desc = CONFIGS[args.config]
     if args.blocks:
@@ -1259,7 +1317,8 @@ def main():
                        "world_size_checked": (dist.get_world_size() if dist else 1),
                        "shards": shards,
                        "backend": (dist.get_backend() if dist else None),
-                       "rank_devices": rank_devices},
+                       "rank_devices": rank_devices,
+                       "rank_devices_distinct": devices_distinct(rank_devices)},
             "roofline": roofline,
             "cpu_baseline": cpu,
             "parity": parity,

@@ -28,6 +28,8 @@ import array
 import concurrent.futures
 import ctypes
 import threading
+import warnings
+import weakref
 import time
 
 import numpy as np
@@ -492,7 +494,10 @@ def code_grouped_greedy_sample_batch(sess, targets, proposals, n_steps, n_bits_p
     # sample and starts this call returns share one block of torch's caching
     # host allocator (the arrays keep it alive)
     hneed = int(lib.cwq_code_grouped_greedy_batch_host_workspace_size(D, n_items, n_steps))
-    hws = _pinned_scratch(hneed)
+    # a deferred call runs while this thread may make other calls that use its
+    # cached staging (a single-item batch, code_grouped_greedy_sample): it takes
+    # its own page-locked block from a pool until the call has ended
+    hws = _pinned_take(hneed) if defer else _pinned_scratch(hneed)
     n_out = D + 2 * n_items
     out_t = torch.empty(max(D, 1) * 4 + n_out * 8, dtype=torch.uint8, pin_memory=True)
     out_np = out_t.numpy()
@@ -534,6 +539,11 @@ def code_grouped_greedy_sample_batch(sess, targets, proposals, n_steps, n_bits_p
         call()
         return [item(i) for i in range(n_items)]
     fut = _batch_thread().submit(call)
+    fin = None  # a deferred handle's finalizer (returns the buffers if result() never runs)
+
+    def release():  # the call has ended: a deferred call's buffers go back to their pools
+        _bits_give(bits_h)
+        _pinned_give(hws)
 
     def finish():
         out = []
@@ -553,11 +563,29 @@ def code_grouped_greedy_sample_batch(sess, targets, proposals, n_steps, n_bits_p
             out.extend(item(i) for i in range(len(out), n_items))
         finally:
             if defer:
-                fut.exception()  # (waits) the buffer is free once the call has ended
-                _bits_give(bits_h)
+                fut.exception()  # (waits) the buffers are free once the call has ended
+                if fin is not None and fin.detach() is not None:
+                    release()
         return out
 
-    return _Deferred(finish) if defer else finish()
+    if not defer:
+        return finish()
+    h = _Deferred(finish)
+    fin = weakref.finalize(h, _abandoned, fut, release)
+    return h
+
+
+def _abandoned(fut, release):
+    """A deferred batch handle collected without result(): once its call has
+    ended, its buffers return to the pools and an error it raised is reported
+    (nobody else will see it)."""
+    def done(f):
+        e = f.exception()
+        if e is not None:
+            warnings.warn(f"code_grouped_greedy_sample_batch(defer=True): the call failed and "
+                          f"its result() was never requested: {e!r}", RuntimeWarning)
+        release()
+    fut.add_done_callback(done)
 
 
 class _Done:
@@ -610,6 +638,25 @@ def _bits_give(b):
     with _bits_lock:
         if len(_bits_free) < 4:
             _bits_free.append(b)
+
+
+_pinned_free = []
+
+
+def _pinned_take(n):
+    """A page-locked host staging block of at least n bytes for a deferred
+    batch call (a torch pinned tensor; returned by _pinned_give)."""
+    with _bits_lock:
+        for k, b in enumerate(_pinned_free):
+            if b.numel() >= n:
+                return _pinned_free.pop(k)
+    return torch.empty(max(int(n), 1), dtype=torch.uint8, pin_memory=True)
+
+
+def _pinned_give(b):
+    with _bits_lock:
+        if len(_pinned_free) < 4:
+            _pinned_free.append(b)
 
 
 _batch_pool = None

@@ -184,6 +184,7 @@ __global__ void __launch_bounds__(256) k_part_exit(const int32_t* __restrict__ n
   __shared__ int32_t red[kPartThreads];
   if (info[4] > (unsigned long long)kPartMaxJump) return;  // host path
   const int64_t c = blockIdx.x;
+  if (c >= (D + kPartW - 1) / kPartW) return;  // a grid past the chunks (launch_partition checks)
   const int64_t b = c * kPartW;
   const int n = (int)(D - b < kPartW ? D - b : kPartW);
   const int32_t lim = (int32_t)(b + n);  // the chunk's end (the last chunk: D)
@@ -220,6 +221,7 @@ __global__ void __launch_bounds__(256) k_part_mark(const int32_t* __restrict__ n
   __shared__ int32_t s_entry;
   if (info[4] > (unsigned long long)kPartMaxJump) return;
   const int64_t c = blockIdx.x;
+  if (c >= (D + kPartW - 1) / kPartW) return;
   const int64_t b = c * kPartW;
   const int n = (int)(D - b < kPartW ? D - b : kPartW);
   const int32_t lim = (int32_t)(b + n);
@@ -305,6 +307,7 @@ __global__ void __launch_bounds__(256) k_part_sup(const int32_t* __restrict__ cn
   __shared__ int64_t red[kPartThreads];
   if (info[4] > (unsigned long long)kPartMaxJump || info[2]) return;
   const int64_t k0 = (int64_t)blockIdx.x * kPartSuper;
+  if (k0 >= nch) return;  // a grid past the superchunks
   int64_t v = 0;
   for (int64_t k = k0 + threadIdx.x; k < k0 + kPartSuper && k < nch; k += kPartThreads) v += cnt[k];
   red[threadIdx.x] = v;
@@ -335,6 +338,7 @@ __global__ void __launch_bounds__(256) k_part_emit(int64_t nchunks,
   __shared__ int32_t redm[kPartThreads];
   if (info[4] > (unsigned long long)kPartMaxJump || info[2]) return;
   const int64_t c = blockIdx.x;
+  if (c >= nchunks) return;  // a grid past the chunks
   const int64_t b = c * kPartW;
   // rank of the chunk's first node: the earlier chunks' counts (past
   // kPartDirect chunks: the earlier superchunks' sums, then the earlier chunks
@@ -530,6 +534,11 @@ hipError_t launch_partition(const float* kl, int64_t D, const int64_t* item_off,
                             int64_t size_threshold, float thr, int64_t* starts, int64_t* iinfo,
                             void* ws, unsigned long long* info, hipStream_t stream,
                             bool info_zeroed) {
+  // every per-chunk kernel indexes its chunk's counters, nodes and starts by
+  // blockIdx.x: its grid is exactly the chunk (superchunk) count (round 5: a
+  // work-in-progress launch of 256 workgroups over one chunk stored past the
+  // start list; the kernels now also return past the last chunk)
+  if (D < 1 || D >= (1LL << 30) || n_items < 1) return hipErrorInvalidValue;
   const int64_t nch = (D + kPartW - 1) / kPartW;
   int32_t* nxt = (int32_t*)ws;
   int32_t* exg = nxt + (D + 64);
@@ -539,6 +548,9 @@ hipError_t launch_partition(const float* kl, int64_t D, const int64_t* item_off,
   int32_t* cnt = conv + (nch + 64);
   int32_t* sup = cnt + (nch + 64);
   const int64_t nsup = (nch + kPartSuper - 1) / kPartSuper;
+  const dim3 gch((unsigned)nch), gsup((unsigned)nsup);
+  if ((int64_t)gch.x != nch || (int64_t)gsup.x != nsup || nch < 1 || nsup < 1)
+    return hipErrorInvalidValue;
   const bool single = item_off == nullptr && n_items == 1;
   if (!info_zeroed) {
     hipError_t e = hipMemsetAsync(info, 0, 8 * sizeof(unsigned long long), stream);
@@ -547,19 +559,17 @@ hipError_t launch_partition(const float* kl, int64_t D, const int64_t* item_off,
   }
   hipLaunchKernelGGL(k_part_next, dim3((unsigned)((D + 255) / 256)), dim3(256), 0, stream, kl, D,
                      item_off, n_items, size_threshold, thr, nxt, info);
-  hipLaunchKernelGGL(k_part_exit, dim3((unsigned)nch), dim3(kPartThreads), 0, stream, nxt, D, exg,
-                     conv, info);
-  hipLaunchKernelGGL(k_part_mark, dim3((unsigned)nch), dim3(kPartThreads), 0, stream, nxt, D, exg,
-                     conv, node, cnt, info);
+  hipLaunchKernelGGL(k_part_exit, gch, dim3(kPartThreads), 0, stream, nxt, D, exg, conv, info);
+  hipLaunchKernelGGL(k_part_mark, gch, dim3(kPartThreads), 0, stream, nxt, D, exg, conv, node, cnt,
+                     info);
   if (nch > kPartDirect)
-    hipLaunchKernelGGL(k_part_sup, dim3((unsigned)nsup), dim3(kPartThreads), 0, stream, cnt, nch,
-                       sup, info);
+    hipLaunchKernelGGL(k_part_sup, gsup, dim3(kPartThreads), 0, stream, cnt, nch, sup, info);
   if (single) {
-    hipLaunchKernelGGL(k_part_emit<true>, dim3((unsigned)nch), dim3(kPartThreads), 0, stream, nch,
+    hipLaunchKernelGGL(k_part_emit<true>, gch, dim3(kPartThreads), 0, stream, nch,
                        node, cnt, sup, gnode, info, kl, D, size_threshold, thr, nxt, starts, iinfo);
     return hipGetLastError();
   }
-  hipLaunchKernelGGL(k_part_emit<false>, dim3((unsigned)nch), dim3(kPartThreads), 0, stream, nch,
+  hipLaunchKernelGGL(k_part_emit<false>, gch, dim3(kPartThreads), 0, stream, nch,
                      node, cnt, sup, gnode, info, kl, D, size_threshold, thr, nxt, starts, iinfo);
   hipLaunchKernelGGL(k_part_ihdr, dim3((unsigned)((n_items + 255) / 256)), dim3(256), 0, stream,
                      kl, D, item_off, n_items, size_threshold, thr, gnode, starts, iinfo, info);

@@ -134,3 +134,68 @@ def test_rank_device_map_refuses_shared_gpu_under_rccl(monkeypatch):
     assert len(bench.rank_device_map(FakeDist("gloo", [0, 0]), 0, 0, dev)) == 2
     with pytest.raises(SystemExit, match="share GPU"):
         bench.rank_device_map(FakeDist("nccl", [0, 1, 1]), 0, 0, dev)
+
+
+def test_rank_deadline_stops_stuck_and_failed_ranks():
+    """bench.py --gpus N's own launcher cannot hang the SCALE run: a rank that
+    exits non-zero stops the others at once (its code is returned), and ranks
+    still running at the deadline are stopped and 124 returned, within the
+    deadline plus the stop grace, with no child left running."""
+    import subprocess
+    import sys
+    import time
+    from conftest import REPO
+    sys.path.insert(0, REPO)
+    import bench
+    env = dict(os.environ)
+    sleeper = [sys.executable, "-c", "import time; time.sleep(600)"]
+    failer = [sys.executable, "-c", "import time, sys; time.sleep(0.5); sys.exit(3)"]
+    ok = [sys.executable, "-c", "pass"]
+    # one rank fails, one would sleep for ten minutes
+    t0 = time.monotonic()
+    procs = []
+    real_popen = subprocess.Popen
+
+    def track(*a, **k):
+        p = real_popen(*a, **k)
+        procs.append(p)
+        return p
+    try:
+        subprocess.Popen = track
+        rc = bench.run_rank_processes([(failer, env), (sleeper, env)], deadline_s=60)
+        assert rc == 3
+        assert time.monotonic() - t0 < 30
+        assert all(p.poll() is not None for p in procs)
+        # both sleep past the deadline: stopped, 124
+        procs.clear()
+        t0 = time.monotonic()
+        rc = bench.run_rank_processes([(sleeper, env), (ok, env), (sleeper, env)], deadline_s=2)
+        assert rc == 124
+        assert time.monotonic() - t0 < 2 + 5 + 5
+        assert all(p.poll() is not None for p in procs)
+        # a rank that ignores SIGTERM is killed after the grace period
+        stubborn = [sys.executable, "-c", "import signal, time; "
+                    "signal.signal(signal.SIGTERM, signal.SIG_IGN); time.sleep(600)"]
+        procs.clear()
+        t0 = time.monotonic()
+        rc = bench.run_rank_processes([(stubborn, env)], deadline_s=1)
+        assert rc == 124 and time.monotonic() - t0 < 1 + 5 + 5
+        assert all(p.poll() is not None for p in procs)
+        assert bench.run_rank_processes([(ok, env), (ok, env)], deadline_s=60) == 0
+    finally:
+        subprocess.Popen = real_popen
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+
+
+def test_devices_distinct():
+    import sys
+    from conftest import REPO
+    sys.path.insert(0, REPO)
+    import bench
+    m = [{"host": "h", "pci_bus": b, "visible": None, "device": i} for i, b in enumerate([3, 4])]
+    assert bench.devices_distinct(m)
+    assert not bench.devices_distinct(m + [dict(m[0], device=5)])
+    m2 = [{"host": "h", "pci_bus": None, "visible": "0,1", "device": i} for i in (0, 1, 1)]
+    assert not bench.devices_distinct(m2) and bench.devices_distinct(m2[:2])

@@ -274,6 +274,40 @@ def test_grouped_batch_deferred_overlapping_calls(cwq):
         with pytest.raises(Exception):
             bad.result()
 
+    # synchronous calls on this thread while deferred batches are in flight: a
+    # single-item batch and code_grouped_greedy_sample run here, on this
+    # thread's page-locked staging, while the queued calls use their own
+    (tg0, pr0), sd0 = jobs[0]
+    (tg1, pr1), sd1 = jobs[1]
+    want0 = cwq.code_grouped_greedy_sample_batch(None, tg0, pr0, 1, 8, sd0)
+    want1 = cwq.code_grouped_greedy_sample_batch(None, tg1, pr1, 1, 8, sd1)
+    one_want = cwq.code_grouped_greedy_sample_batch(None, tg1[:1], pr1[:1], 1, 8, 3)
+    single_want = cwq.code_grouped_greedy_sample(None, tg0[0], pr0[0], 1, 8, 4)
+    for _ in range(3):
+        h0 = cwq.code_grouped_greedy_sample_batch(None, tg0, pr0, 1, 8, sd0, defer=True)
+        h1 = cwq.code_grouped_greedy_sample_batch(None, tg1, pr1, 1, 8, sd1, defer=True)
+        one = cwq.code_grouped_greedy_sample_batch(None, tg1[:1], pr1[:1], 1, 8, 3)
+        single = cwq.code_grouped_greedy_sample(None, tg0[0], pr0[0], 1, 8, 4)
+        for got, want in ((h0.result(), want0), (h1.result(), want1), (one, one_want)):
+            for (gs, gb, gst), (ws, wb, wst) in zip(got, want):
+                assert gb == wb and gst.tolist() == wst.tolist()
+                assert np.array_equal(_u32(gs), _u32(ws))
+        assert single[1] == single_want[1] and list(single[2]) == list(single_want[2])
+        assert np.array_equal(_u32(single[0]), _u32(single_want[0]))
+    # a handle dropped without result(): its buffers return to the pools once
+    # its call ends, and its error (if any) is reported as a warning
+    import gc
+    import warnings
+    from compression_without_quantization_amd import coded_greedy_sampler as S
+    with warnings.catch_warnings(record=True) as w:
+        warnings.simplefilter("always")
+        dropped = cwq.code_grouped_greedy_sample_batch(None, tg, pr, 1, 40, 0, defer=True)
+        del dropped
+        gc.collect()
+        cwq.code_grouped_greedy_sample_batch(None, tg1, pr1, 1, 8, sd1, defer=True).result()
+    assert any("result() was never requested" in str(x.message) for x in w)
+    assert len(S._pinned_free) >= 1 and len(S._bits_free) >= 1
+
 
 def test_grouped_batch_many_items(cwq):
     """More items than the device partition keeps in LDS (1,024): 1,300 items
