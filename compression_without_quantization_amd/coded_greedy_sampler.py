@@ -27,6 +27,7 @@ All arithmetic runs in libcwq.so; nothing here computes samples on the CPU.
 import array
 import concurrent.futures
 import ctypes
+import functools
 import threading
 import warnings
 import weakref
@@ -287,6 +288,7 @@ def decode_greedy_sample(sample_index, p_loc, p_scale, n_bits_per_step, n_steps,
     return _like_input(sample, p_loc)
 
 
+@functools.lru_cache(maxsize=64)
 def group_size_threshold(max_group_size_bits):
     """Smallest s with np.log(s + 1) / np.log(2) >= max_group_size_bits (:230-232)."""
     bits = max_group_size_bits

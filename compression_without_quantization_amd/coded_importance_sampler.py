@@ -22,6 +22,7 @@ Deliberate differences from the TF1 reference:
   * results are concrete values; `sess` is accepted and ignored.
 """
 import ctypes
+import functools
 
 import numpy as np
 import torch
@@ -40,6 +41,7 @@ def _stream(dev):
     return torch.cuda.current_stream(dev).cuda_stream
 
 
+@functools.lru_cache(maxsize=64)
 def importance_group_size_threshold(max_group_size_bits):
     """Smallest s with np.log(s + 1) / np.log(2) > max_group_size_bits (:185-187)."""
     bits = max_group_size_bits

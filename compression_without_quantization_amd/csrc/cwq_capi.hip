@@ -676,10 +676,49 @@ bool device_partition_enabled() {
   }();
   return on;
 }
+// The single grouped call's device partition pays off from this many dims: below
+// it the host loop over the copied KL (one round trip instead of seven chained
+// launches and two) is faster (tools/single_call_laps.py: 2,304 dims 120 ->
+// 90 us a call).  CWQ_DEV_PART_MIN_D overrides it (A/B timing; results never
+// depend on the path).
+int64_t dev_partition_min_dims() {
+  static const int64_t v = [] {
+    const char* e = getenv("CWQ_DEV_PART_MIN_D");
+    return e && *e ? (int64_t)atoll(e) : (int64_t)16384;
+  }();
+  return v;
+}
 // :81-87, :288 (and binary_io.py:41-53) each of n indices as n_bits LSB-first
 // '0'/'1' chars; returns n * n_bits, or CWQ_ERR_INVALID for an index that does
 // not fit (to_bit_string raises there).
+// BMI2 form (runtime-dispatched): a byte of the index becomes its 8 chars with
+// one pdep (bit k -> the low bit of byte k, LSB first) and an OR with '0'x8;
+// C2's 41.5k 8-bit indices: ~16 us against ~31 us through the table.
+__attribute__((target("bmi2"))) int64_t write_bitcode_pdep(const int32_t* idx, int64_t n,
+                                                           int n_bits, char* o) {
+  constexpr uint64_t kLow = 0x0101010101010101ull, kZero = 0x3030303030303030ull;
+  const int full = n_bits >> 3, rem = n_bits & 7;
+  const uint64_t rmask = kLow & ((1ull << (8 * rem)) - 1);  // rem < 8: the first rem bytes
+  for (int64_t i = 0; i < n; ++i) {
+    const uint32_t v = (uint32_t)idx[i];
+    if (n_bits < 31 && (v >> n_bits) != 0)
+      return fail(CWQ_ERR_INVALID, "index %u does not fit %d bits", v, n_bits);
+    for (int k = 0; k < full; ++k) {
+      const uint64_t w = _pdep_u64((v >> (8 * k)) & 0xffu, kLow) | kZero;
+      memcpy(o, &w, 8);
+      o += 8;
+    }
+    if (rem) {
+      const uint64_t w = _pdep_u64(v >> (8 * full), rmask) | (kZero & ((1ull << (8 * rem)) - 1));
+      memcpy(o, &w, (size_t)rem);
+      o += rem;
+    }
+  }
+  return n * n_bits;
+}
 int64_t write_bitcode(const int32_t* idx, int64_t n, int n_bits, char* o) {
+  static const bool bmi2 = __builtin_cpu_supports("bmi2");
+  if (bmi2) return write_bitcode_pdep(idx, n, n_bits, o);
   static const struct ByteChars {  // byte value -> its 8 LSB-first '0'/'1' chars
     uint64_t c[256];
     ByteChars() {
@@ -770,8 +809,8 @@ int64_t grouped_begin(const float* q_loc, const float* q_scale, const float* p_l
     // :193-199 standardise; :201, :210 per-dim KL(target || proposal); the
     // standard prior (zeros, ones) and the partition's counters, one launch
     unsigned long long* g_part_info = part_info_host();
-    const bool try_dev = device_partition_enabled() && cwq::partition_applies(D, size_threshold) &&
-                         g_part_info != nullptr;
+    const bool try_dev = device_partition_enabled() && D >= dev_partition_min_dims() &&
+                         cwq::partition_applies(D, size_threshold) && g_part_info != nullptr;
     unsigned long long* info_d = (unsigned long long*)(w + l.pinfo);
     if ((e = cwq::launch_grouped_prep(q_loc, q_scale, p_loc, p_scale, D, t_loc, t_scale, kl, zeros,
                                       ones, info_d, try_dev ? 16 : 0, s)) != hipSuccess)
@@ -806,7 +845,10 @@ int64_t grouped_begin(const float* q_loc, const float* q_scale, const float* p_l
       if ((e = hipMemcpyAsync(g_kl_host.data(), kl, (size_t)D * 4, hipMemcpyDeviceToHost, s)) !=
           hipSuccess)
         return hip_fail(e, "KL to host");
-      if ((e = hipStreamSynchronize(s)) != hipSuccess) return hip_fail(e, "sync");
+      if (pev.ev.empty() && !pev.made(1, s, hipEventDisableTiming))
+        return fail(CWQ_ERR_HIP, "%s: events failed", who);
+      if ((e = hipEventRecord(pev.ev[0], s)) != hipSuccess || (e = wait_event(pev.ev[0])) != hipSuccess)
+        return hip_fail(e, "sync");
       kl_on_host = true;
     }
   }
@@ -858,19 +900,22 @@ int64_t grouped_begin(const float* q_loc, const float* q_scale, const float* p_l
       return fail(CWQ_ERR_HIP, "%s: events failed", who);
     }
   }
-  // :273-284 one greedy coder per group, seed + g
-  if (o.eval_ms_out && (!tev->made(2, s, hipEventDefault) ||
-                        hipEventRecord(tev->ev[0], s) != hipSuccess))
-    return fail(CWQ_ERR_HIP, "%s: timing events failed", who);
+  // :273-284 one greedy coder per group, seed + g.  eval_ms_out: this call's
+  // two events go to the encoder as its eval events, so they bracket the
+  // candidate-scoring launches and not the destandardisation after them
+  cwq_options oe = o;
+  if (o.eval_ms_out && !o.eval_start_event) {
+    if (!tev->made(2, s, hipEventDefault))
+      return fail(CWQ_ERR_HIP, "%s: timing events failed", who);
+    oe.eval_start_event = tev->ev[0];
+    oe.eval_stop_event = tev->ev[1];
+  }
+  oe.eval_ms_out = nullptr;
   // (and :292 destandardise into out, folded into the encoder's last launch)
   if ((rc = encode_impl(t_loc, t_scale, zeros, ones, offs, 0, G, D, maxd, n_bits_per_step,
                         n_steps, seed, rho, 0, idx, sample, w + l.enc, workspace_bytes - l.enc,
-                        opts, stream, nullptr, out, p_loc, p_scale)) < 0)
+                        &oe, stream, nullptr, out, p_loc, p_scale)) < 0)
     return rc;
-  if (o.eval_ms_out && (e = hipEventRecord(tev->ev[1], s)) != hipSuccess) {
-    (void)hipStreamSynchronize(s);
-    return hip_fail(e, "event");
-  }
   if ((e = hipMemcpyAsync(idx_host, idx, (size_t)(G * n_steps) * 4, hipMemcpyDeviceToHost, s)) !=
       hipSuccess)
     return hip_fail(e, "indices to host");
@@ -983,7 +1028,17 @@ int64_t cwq_code_grouped_greedy_end(const int32_t* idx_host, int64_t G, int n_st
   if (G < 0 || n_steps < 1 || n_bits_per_step < 0 || n_bits_per_step > CWQ_MAX_BITS_PER_STEP)
     return fail(CWQ_ERR_INVALID, "%s: bad sizes", who);
   hipError_t e;
-  if ((e = hipStreamSynchronize((hipStream_t)stream)) != hipSuccess) return hip_fail(e, "sync");
+  // a polled event rather than a blocking stream wait (its wake-up cost ~20 us
+  // a call)
+  {
+    CallEvents ev;
+    if (!ev.made(1, (hipStream_t)stream, hipEventDisableTiming) ||
+        hipEventRecord(ev.ev[0], (hipStream_t)stream) != hipSuccess) {
+      if ((e = hipStreamSynchronize((hipStream_t)stream)) != hipSuccess) return hip_fail(e, "sync");
+    } else if ((e = wait_event(ev.ev[0])) != hipSuccess) {
+      return hip_fail(e, "sync");
+    }
+  }
   if (G > 0 && !idx_host) return fail(CWQ_ERR_INVALID, "%s: null pointer", who);
   const int64_t nw = grouped_bits(idx_host, G, n_steps, n_bits_per_step, bits_host, bits_cap, who);
   if (nw < 0) return nw;
@@ -1305,19 +1360,17 @@ int64_t batch_device_path(int64_t n_items, const int64_t* item_off, int64_t D, i
         (e = hipEventRecord((hipEvent_t)o.eval_start_event, s)) != hipSuccess)
       rc = hip_fail(e, "event");
     if (rc == CWQ_OK && Gc > 0) {
-      if (o.eval_ms_out && (e = hipEventRecord(tev.ev[(size_t)(2 * c)], s)) != hipSuccess)
-        rc = hip_fail(e, "event");
+      // eval_ms_out: the chunk's events bracket its scoring launches (inside
+      // the encoder, before the destandardisation)
       cwq_options oc = o;
-      oc.eval_start_event = oc.eval_stop_event = nullptr;
+      oc.eval_start_event = o.eval_ms_out ? tev.ev[(size_t)(2 * c)] : nullptr;
+      oc.eval_stop_event = o.eval_ms_out ? tev.ev[(size_t)(2 * c + 1)] : nullptr;
       oc.eval_ms_out = nullptr;
       if (rc == CWQ_OK)  // :273-284 the chunk's groups in one launch sequence
         rc = encode_impl(t_loc + a, t_scale + a, zeros + a, ones + a, offs + gb + c, 0, Gc, Dc,
                          cmaxd[(size_t)c], n_bits_per_step, n_steps, 0, rho, 0,
                          idx + gb * n_steps, sample + a, w + l.enc, workspace_bytes - l.enc, &oc,
                          s, bseed + gb, out + a, p_loc + a, p_scale + a);  // + :292
-      if (rc == CWQ_OK && o.eval_ms_out &&
-          (e = hipEventRecord(tev.ev[(size_t)(2 * c + 1)], s)) != hipSuccess)
-        rc = hip_fail(e, "event");
     } else if (rc == CWQ_OK && Dc > 0 &&
                (e = hipMemsetAsync(out + a, 0, (size_t)Dc * 4, s)) != hipSuccess) {
       rc = hip_fail(e, "memset");
@@ -1747,21 +1800,18 @@ int64_t cwq_code_grouped_greedy_batch(
           (e = hipEventRecord(h2d_ev[c], h2d)) != hipSuccess ||
           (e = hipStreamWaitEvent(s, h2d_ev[c], 0)) != hipSuccess)
         rc = hip_fail(e, "layout to device");
-      if (rc == CWQ_OK && o.eval_ms_out)
-        if ((e = hipEventRecord(tev.ev[(size_t)(2 * c)], s)) != hipSuccess)
-          rc = hip_fail(e, "event");
-      // :273-284 the chunk's groups in one launch sequence (events: none here)
+      // :273-284 the chunk's groups in one launch sequence; eval_ms_out: the
+      // chunk's events bracket its scoring launches (inside the encoder, before
+      // the destandardisation)
       cwq_options oc = o;
-      oc.eval_start_event = oc.eval_stop_event = nullptr;
+      oc.eval_start_event = o.eval_ms_out ? tev.ev[(size_t)(2 * c)] : nullptr;
+      oc.eval_stop_event = o.eval_ms_out ? tev.ev[(size_t)(2 * c + 1)] : nullptr;
       oc.eval_ms_out = nullptr;
       if (rc == CWQ_OK)
         rc = encode_impl(t_loc + a, t_scale + a, zeros + a, ones + a, offs + gb + c, 0, ch.G, Dc,
                          ch.maxd, n_bits_per_step, n_steps, 0, rho, 0, idx + gb * n_steps,
                          sample + a, w + l.enc, workspace_bytes - l.enc, &oc, stream, bseed + gb,
                          out + a, p_loc + a, p_scale + a);  // + :292 destandardise
-      if (rc == CWQ_OK && o.eval_ms_out)
-        if ((e = hipEventRecord(tev.ev[(size_t)(2 * c + 1)], s)) != hipSuccess)
-          rc = hip_fail(e, "event");
     } else if (rc == CWQ_OK && Dc > 0) {  // no groups (empty items only): the sample is zeros
       if ((e = hipMemsetAsync(out + a, 0, (size_t)Dc * 4, s)) != hipSuccess)
         rc = hip_fail(e, "memset");
