@@ -2,7 +2,8 @@
 profiles/traffic_<config>.json that lists its counter CSVs is recomputed from
 those CSVs with tools/pmc_frac.py (the dominant kernel's VALU issue fraction
 and HBM bytes, and the step totals over the scoring kernels), and every
-round-5 bench line that quotes a traffic or VALU figure quotes that file's."""
+bench line of the latest round that quotes a traffic or VALU figure quotes
+that file's."""
 import glob
 import json
 import math
@@ -65,16 +66,23 @@ def test_traffic_json_recomputes_from_its_csvs(path):
                        tot.get("WRITE_SIZE", [0.0])[0]) * 1024.0, agg["hbm_bytes_per_step"])
 
 
+def _latest_round_lines():
+    rounds = sorted({os.path.basename(f)[:3] for f in
+                     glob.glob(os.path.join(REPO, "profiles", "r??_bench_*.json"))})
+    assert rounds, "no bench lines under profiles/"
+    r = rounds[-1]
+    return r, sorted(glob.glob(os.path.join(REPO, "profiles", f"{r}_bench_*.json")))
+
+
 def test_bench_lines_quote_the_traffic_files():
-    lines = sorted(glob.glob(os.path.join(REPO, "profiles", "r05_bench_*.json")))
-    assert lines, "no round-5 bench lines"
+    rnd, lines = _latest_round_lines()
     checked = 0
     for f in lines:
         with open(f) as fh:
             d = json.load(fh)
         for k in ("metric", "value", "unit", "roofline", "cpu_baseline", "parity"):
             assert k in d, (f, k)
-        cfg = os.path.basename(f)[len("r05_bench_"):-len(".json")]
+        cfg = os.path.basename(f)[len(f"{rnd}_bench_"):-len(".json")]
         tf = os.path.join(REPO, "profiles", f"traffic_{cfg}.json")
         r = d["roofline"]
         if not os.path.exists(tf) or r.get("valu", {}).get("valu_issue_frac") is None:
