@@ -354,18 +354,29 @@ def code_grouped_importance_sample_batch(sess, targets, proposals, seeds, n_bits
     if len(seeds) != n_items:
         raise ValueError("one seed per item")
     seeds32 = np.array([int(np.int32(np.uint32(s & 0xFFFFFFFF))) for s in seeds], dtype=np.int32)
-    for t, p in zip(targets, proposals):
-        if not _is_float32(t.loc) or not _is_float32(t.scale):
-            raise Exception("Target datatype must be float32!")   # :126-129
-        if not _is_float32(p.loc) or not _is_float32(p.scale):
-            raise Exception("Proposal datatype must be float32!")
-    dev = _device_of(*[a for t, p in zip(targets, proposals)
-                       for a in (t.loc, t.scale, p.loc, p.scale)])
+    raw = ([t.loc for t in targets], [t.scale for t in targets], [p.loc for p in proposals],
+           [p.scale for p in proposals])
+    f32 = torch.float32
+    # the common case (float32 CUDA tensors on one device): the checks and the
+    # concatenation without per-array wrapper calls (24 items: ~0.3 ms less)
+    fast = all(type(a) is torch.Tensor and a.dtype is f32 and a.is_cuda for c in raw for a in c)
+    if fast:
+        dev = raw[0][0].device
+        fast = all(a.device == dev for c in raw for a in c)
+    if not fast:
+        for t, p in zip(targets, proposals):
+            if not _is_float32(t.loc) or not _is_float32(t.scale):
+                raise Exception("Target datatype must be float32!")   # :126-129
+            if not _is_float32(p.loc) or not _is_float32(p.scale):
+                raise Exception("Proposal datatype must be float32!")
+        dev = _device_of(*[a for c in raw for a in c])
     with torch.cuda.device(dev):
-        cols = [[_f32(getattr(d, k), dev, n).reshape(-1) for d in ds]
-                for ds, k, n in ((targets, "loc", "target.loc"), (targets, "scale", "target.scale"),
-                                 (proposals, "loc", "proposal.loc"),
-                                 (proposals, "scale", "proposal.scale"))]
+        if fast:
+            cols = [[a.reshape(-1) for a in c] for c in raw]
+        else:
+            cols = [[_f32(a, dev, n).reshape(-1) for a in c]
+                    for c, n in zip(raw, ("target.loc", "target.scale", "proposal.loc",
+                                          "proposal.scale"))]
         sizes = np.array([a.numel() for a in cols[0]], dtype=np.int64)
         if any([a.numel() for a in c] != sizes.tolist() for c in cols[1:]):
             raise ValueError("target and proposal of an item must have the same size")
@@ -379,7 +390,7 @@ def code_grouped_importance_sample_batch(sess, targets, proposals, seeds, n_bits
         starts_h = np.empty(D + 2 * n_items, dtype=np.int64)
         n_starts = np.zeros(n_items, dtype=np.int64)
         out_i = np.empty(max(D, 1), dtype=np.int64)
-        out_v = np.empty(max(D, 1), dtype=np.float32)
+        out_v = np.zeros(max(D, 1), dtype=np.float32)  # quantised whole below
         n_out = np.zeros(n_items, dtype=np.int64)
         kl_sum = np.zeros(n_items, dtype=np.float64)
         _lib.check(lib.cwq_code_grouped_importance_batch(
@@ -391,6 +402,26 @@ def code_grouped_importance_sample_batch(sess, targets, proposals, seeds, n_bits
             out_v.ctypes.data, n_out.ctypes.data, kl_sum.ctypes.data, ws.data_ptr(), ws.numel(),
             _lib.options(prune_mode, eval_ms_out=eval_ms_out), _stream(dev)),
             "cwq_code_grouped_importance_batch")
+    # every item's index + 1 values, outlier codes and bit strings in one pass
+    # each (one native Elias-delta call, one quint16 pass; per-item calls cost
+    # ~20 us apiece), then split per item
+    ns_all = n_starts.astype(np.int64)
+    G = np.maximum(ns_all - 1, 0)
+    src = np.concatenate([np.arange(item_off[i] + i, item_off[i] + i + G[i], dtype=np.int64)
+                          for i in range(n_items)]) if int(G.sum()) else np.zeros(0, np.int64)
+    vals = index_h[src] + 1
+    goff = np.concatenate([[0], np.cumsum(G)])
+    q_all = quantize_quint16(out_v[:D]) if D else np.zeros(0, np.uint16)
+    codes = None
+    if not return_indices:
+        codes = elias_delta_code_many(vals)
+        if vals.size:  # code lengths: 2 floor(log2(n + 1)) + n + 1, n = floor(log2 x)
+            nb_ = np.frexp(vals.astype(np.float64))[1].astype(np.int64) - 1
+            ln = 2 * (np.frexp((nb_ + 1).astype(np.float64))[1].astype(np.int64) - 1) + nb_ + 1
+            coff = np.concatenate([[0], np.cumsum(ln)])[goff]
+        else:
+            coff = np.zeros(n_items + 1, np.int64)
+    vals_l = vals.tolist()
     res = []
     for i in range(n_items):
         a, b = int(item_off[i]), int(item_off[i + 1])
@@ -401,12 +432,12 @@ def code_grouped_importance_sample_batch(sess, targets, proposals, seeds, n_bits
                   "estimated number of groups: {},"
                   "coding {} dimensions".format(total_kl_bits, n_bits_per_group,
                                                 total_kl_bits // n_bits_per_group + 1, b - a))
-        ns, no = int(n_starts[i]), int(n_out[i])
+        ns, no = int(ns_all[i]), int(n_out[i])
         gs = starts_h[a + 2 * i:a + 2 * i + ns].copy()
-        indices = tuple((index_h[a + i:a + i + ns - 1] + 1).tolist())
-        extras = (out_i[a:a + no].copy(), quantize_quint16(out_v[a:a + no]))
+        indices = tuple(vals_l[goff[i]:goff[i + 1]])
+        extras = (out_i[a:a + no].copy(), q_all[a:a + no].copy())
         smp = sample_h[a:b].copy()
-        code = indices if return_indices else elias_delta_code_many(indices)
+        code = indices if return_indices else codes[coff[i]:coff[i + 1]]
         res.append((smp, code, gs, extras))
     return res
 

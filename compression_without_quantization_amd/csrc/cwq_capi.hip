@@ -1962,6 +1962,18 @@ int64_t grouped_importance_impl(int64_t I, const int64_t* item_off, const float*
   if (oi.eval_ms_out) *oi.eval_ms_out = 0.0f;
   if (D == 0) return ok();
   hipStream_t s = (hipStream_t)stream;
+#ifdef CWQ_PHASE_TIMES  // tuning builds: per-phase host wall times to stderr
+  struct timespec ts0, ts1;
+  clock_gettime(CLOCK_MONOTONIC, &ts0);
+  auto lap = [&](const char* what) {
+    clock_gettime(CLOCK_MONOTONIC, &ts1);
+    fprintf(stderr, "[cwq imp] %-10s %8.1f us\n", what,
+            (ts1.tv_sec - ts0.tv_sec) * 1e6 + (ts1.tv_nsec - ts0.tv_nsec) * 1e-3);
+    ts0 = ts1;
+  };
+#else
+  auto lap = [](const char*) {};
+#endif
   char* w = (char*)workspace;
   float* t_loc = (float*)(w + l.t_loc);
   float* t_scale = (float*)(w + l.t_scale);
@@ -2048,7 +2060,9 @@ int64_t grouped_importance_impl(int64_t I, const int64_t* item_off, const float*
       (e = hipMemcpyAsync(ts_h, tsamp, Dz * 4, hipMemcpyDeviceToHost, s)) != hipSuccess ||
       (e = hipEventRecord(hev.ev[0], s)) != hipSuccess)
     return drain_fail(e, "to host");
+  lap("prep queued");
   if ((e = wait_event(hev.ev[0])) != hipSuccess) return drain_fail(e, "sync");
+  lap("kl in");
   // per item: outliers, :164-203 the sequential partition (strict >), :48-51
   // ceil(exp(sum KL)) per group, and its groups' global offsets and seeds
   int64_t Gtot = 0;
@@ -2081,6 +2095,7 @@ int64_t grouped_importance_impl(int64_t I, const int64_t* item_off, const float*
     Gtot += G;
   }
   offs_h[Gtot] = D;
+  lap("planned");
   int64_t tcand = 0;  // the launch's candidates (selects the encoder's instantiation)
   for (int64_t g = 0; g < Gtot; ++g) tcand += ns_h[g] > 1 ? ns_h[g] : 1;
   if (Gtot > 0) {
@@ -2119,7 +2134,9 @@ int64_t grouped_importance_impl(int64_t I, const int64_t* item_off, const float*
       (e = hipMemcpyAsync(out_h, out, Dz * 4, hipMemcpyDeviceToHost, s)) != hipSuccess ||
       (e = hipEventRecord(hev.ev[1], s)) != hipSuccess)
     return drain_fail(e, "to host");
+  lap("enqueued");
   if ((e = wait_event(hev.ev[1])) != hipSuccess) return drain_fail(e, "sync");
+  lap("done");
   int64_t gb = 0;
   for (int64_t i = 0; i < I; ++i) {
     const int64_t G = n_starts[i] - 1;
@@ -2127,6 +2144,7 @@ int64_t grouped_importance_impl(int64_t I, const int64_t* item_off, const float*
     gb += G;
   }
   for (int64_t j = 0; j < D; ++j) sample_host[j] = keep_h[j] ? out_h[j] : ts_h[j];
+  lap("out");
   cwq::set_error(CWQ_OK, "");
   return Gtot;
 }
