@@ -272,7 +272,7 @@ def _code_grouped_importance_on(dev, target, proposal, seed, n_bits_per_group,
     n_samples = num_samples_plan(kl_divs, starts)
     idx, sample = importance_encode_blocks(t_loc, t_scale, zeros, ones, starts, n_samples, seed,
                                            prune_mode=prune_mode)
-    indices = tuple(int(v) + 1 for v in idx.cpu().numpy())
+    indices = tuple((idx.cpu().numpy() + 1).tolist())
     if return_indices_only:
         return indices
     out = torch.empty(D, dtype=torch.float32, device=dev)         # :265 rescale
@@ -319,7 +319,7 @@ def _code_grouped_fused(lib, dev, q_loc, q_scale, p_loc, p_scale, D, seed, n_bit
     no = int(n_out[0])
     outlier_extras = (out_i[:no].copy(), quantize_quint16(out_v[:no]))
     group_start_indices = starts_h[:G + 1].copy()
-    indices = tuple(int(v) + 1 for v in index_h[:G])
+    indices = tuple((index_h[:G] + 1).tolist())
     sample_h = sample_h[:D].copy()
     if return_indices:
         return sample_h, indices, group_start_indices, outlier_extras
@@ -407,10 +407,11 @@ def code_grouped_importance_sample_batch(sess, targets, proposals, seeds, n_bits
     # ~20 us apiece), then split per item
     ns_all = n_starts.astype(np.int64)
     G = np.maximum(ns_all - 1, 0)
-    src = np.concatenate([np.arange(item_off[i] + i, item_off[i] + i + G[i], dtype=np.int64)
-                          for i in range(n_items)]) if int(G.sum()) else np.zeros(0, np.int64)
-    vals = index_h[src] + 1
     goff = np.concatenate([[0], np.cumsum(G)])
+    # item i's indices sit at index_h[item_off[i] + i + g], g < G_i
+    src = np.arange(goff[-1], dtype=np.int64) + np.repeat(
+        item_off[:-1] + np.arange(n_items, dtype=np.int64) - goff[:-1], G)
+    vals = index_h[src] + 1
     q_all = quantize_quint16(out_v[:D]) if D else np.zeros(0, np.uint16)
     codes = None
     if not return_indices:

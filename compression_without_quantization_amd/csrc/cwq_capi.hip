@@ -2004,7 +2004,7 @@ int64_t grouped_importance_impl(int64_t I, const int64_t* item_off, const float*
   const size_t o_kl = htake(Dz * 4), o_ts = htake(Dz * 4), o_out = htake(Dz * 4),
                o_keep = htake(Dz), o_idx = htake(Gz * 8), o_offs = htake((Gz + 1) * 8),
                o_ns = htake(Gz * 8), o_gs = htake(Gz * 4), o_items = htake((Iz + 1) * 8),
-               o_s1 = htake(Iz * 4);
+               o_s1 = htake(Iz * 4), o_nst = htake(I > 1 ? Gz * 8 : 0);
   char* hp = (char*)tl_imp_pin.get(ho, ho + ho / 4);
   if (!hp) {  // no page-locked memory: pageable staging (slower copies)
     tl_imp_pageable.resize(ho);
@@ -2020,8 +2020,8 @@ int64_t grouped_importance_impl(int64_t I, const int64_t* item_off, const float*
   int32_t* gs_h = (int32_t*)(hp + o_gs);
   int64_t* items_h = (int64_t*)(hp + o_items);
   int32_t* s1_h = (int32_t*)(hp + o_s1);
+  int64_t* nst_h = I > 1 ? (int64_t*)(hp + o_nst) : ns_h;  // item i's plan at item_off[i] + i
   hipError_t e = hipSuccess;
-  int rc;
   // every failure after the first copy or launch drains the stream first: the
   // staging buffer may be reused (or reallocated) by this thread's next call
   auto drain_fail = [&](hipError_t err, const char* where) -> int64_t {
@@ -2064,30 +2064,50 @@ int64_t grouped_importance_impl(int64_t I, const int64_t* item_off, const float*
   if ((e = wait_event(hev.ev[0])) != hipSuccess) return drain_fail(e, "sync");
   lap("kl in");
   // per item: outliers, :164-203 the sequential partition (strict >), :48-51
-  // ceil(exp(sum KL)) per group, and its groups' global offsets and seeds
+  // ceil(exp(sum KL)) per group (a batch: items on the host pool's threads;
+  // I2's 24 items took 240 us in one thread), then every group's global
+  // offset, seed and count in order
+  std::atomic<int64_t> next_item{0}, item_rc{0};
+  auto plan_items = [&]() {
+    for (int64_t i; (i = next_item.fetch_add(1)) < I && item_rc.load() == 0;) {
+      const int64_t a = item_off[i], Di = item_off[i + 1] - a;
+      int64_t no = 0;
+      for (int64_t j = 0; j < Di; ++j)
+        if (!keep_h[a + j]) {
+          outlier_idx_host[a + no] = j;
+          outlier_val_host[a + no] = ts_h[a + j];
+          ++no;
+        }
+      n_outliers[i] = no;
+      if (kl_sum_out) {  // log line only
+        double t = 0.0;
+        for (int64_t j = 0; j < Di; ++j) t += (double)kl_h[a + j];
+        kl_sum_out[i] = t;
+      }
+      if (Di == 0) continue;
+      int64_t* st = starts_host + a + 2 * i;
+      const int64_t n = group_starts_impl(kl_h + a, Di, size_threshold, n_nats, st, Di + 2, true);
+      int64_t r = n < 0 ? n : cwq_importance_plan(kl_h + a, st, n - 1, nst_h + a + (I > 1 ? i : 0));
+      if (r < 0) {
+        int64_t z = 0;
+        item_rc.compare_exchange_strong(z, r);
+        continue;
+      }
+      n_starts[i] = n;
+    }
+  };
+  const int64_t nw = I > 1 ? std::min<int64_t>(host_threads() - 1, I - 1) : 0;
+  if (nw > 0 && D >= 4096)
+    HostPool::get().run(nw, plan_items);
+  else
+    plan_items();
+  if (item_rc.load() < 0)
+    return drain_rc(fail((int)item_rc.load(), "%s: item partition / plan failed", who));
   int64_t Gtot = 0;
   for (int64_t i = 0; i < I; ++i) {
-    const int64_t a = item_off[i], Di = item_off[i + 1] - a;
-    int64_t no = 0;
-    for (int64_t j = 0; j < Di; ++j)
-      if (!keep_h[a + j]) {
-        outlier_idx_host[a + no] = j;
-        outlier_val_host[a + no] = ts_h[a + j];
-        ++no;
-      }
-    n_outliers[i] = no;
-    if (kl_sum_out) {  // log line only
-      double t = 0.0;
-      for (int64_t j = 0; j < Di; ++j) t += (double)kl_h[a + j];
-      kl_sum_out[i] = t;
-    }
-    if (Di == 0) continue;
-    int64_t* st = starts_host + a + 2 * i;
-    const int64_t n = group_starts_impl(kl_h + a, Di, size_threshold, n_nats, st, Di + 2, true);
-    if (n < 0) return drain_rc(n);
-    const int64_t G = n - 1;
-    n_starts[i] = n;
-    if ((rc = cwq_importance_plan(kl_h + a, st, G, ns_h + Gtot)) < 0) return drain_rc(rc);
+    const int64_t a = item_off[i], G = n_starts[i] - 1;
+    const int64_t* st = starts_host + a + 2 * i;
+    if (I > 1 && G > 0) memcpy(ns_h + Gtot, nst_h + a + i, (size_t)G * 8);
     for (int64_t g = 0; g < G; ++g) {
       offs_h[Gtot + g] = a + st[g];
       gs_h[Gtot + g] = (int32_t)((uint32_t)seeds[i] + (uint32_t)g);  // :243 seed + g
