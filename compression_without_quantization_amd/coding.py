@@ -30,14 +30,21 @@ class ArithmeticCoder(object):
         lib = _lib.load()
         msg = np.ascontiguousarray(np.asarray(message, dtype=np.int64).reshape(-1))
         P = self._P
-        n = lib.cwq_ac_encode(P.ctypes.data, P.size, self._precision,
-                              msg.ctypes.data if msg.size else None, msg.size, None, 0)
+        mp = msg.ctypes.data if msg.size else None
+        # one pass into a buffer of a generous size (group sizes code at a few
+        # bits a symbol); a message that needs more is sized by a counting pass
+        cap = 32 * msg.size + 1024
+        buf = np.empty(cap, dtype=np.uint8)
+        n = lib.cwq_ac_encode(P.ctypes.data, P.size, self._precision, mp, msg.size,
+                              buf.ctypes.data, cap)
+        if n == -4:  # CWQ_ERR_CAPACITY
+            n = _lib.check(lib.cwq_ac_encode(P.ctypes.data, P.size, self._precision, mp,
+                                             msg.size, None, 0), "cwq_ac_encode")
+            buf = np.empty(max(n, 1), dtype=np.uint8)
+            n = lib.cwq_ac_encode(P.ctypes.data, P.size, self._precision, mp, msg.size,
+                                  buf.ctypes.data, n)
         _lib.check(n, "cwq_ac_encode")
-        buf = np.empty(max(n, 1), dtype=np.uint8)
-        n2 = lib.cwq_ac_encode(P.ctypes.data, P.size, self._precision,
-                               msg.ctypes.data if msg.size else None, msg.size, buf.ctypes.data, n)
-        _lib.check(n2, "cwq_ac_encode")
-        return list(buf[:n2].tobytes().decode("ascii"))
+        return list(buf[:n].tobytes().decode("ascii"))
 
     def decode_fast(self, code, verbose=False):
         """coding.pyx:220-310 -> list of symbols up to and including EOF (0)."""
