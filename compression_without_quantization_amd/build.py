@@ -15,6 +15,8 @@ HEADERS = ["cwq_math.h", "cwq_kernels.h", "cwq_device.h", "cwq_debug.h"]
 # -fhip-fp32-correctly-rounded-divide-sqrt); no fast-math.
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off", "-fno-fast-math",
          "-fPIC", "-shared", "-Wall", "-Wno-unused-function"]
+# the batch call's result copies go to the SDMA engines through the HSA runtime
+LIBS = ["-L/opt/rocm/lib", "-lhsa-runtime64"]
 
 
 def _stale():
@@ -30,7 +32,7 @@ def _stale():
 def build(force=False, verbose=True):
     if not force and not _stale():
         return OUT
-    cmd = ["hipcc"] + FLAGS + ["-o", OUT] + [os.path.join(CSRC, s) for s in SOURCES]
+    cmd = ["hipcc"] + FLAGS + ["-o", OUT] + [os.path.join(CSRC, s) for s in SOURCES] + LIBS
     if verbose:
         print(" ".join(cmd), flush=True)
     subprocess.check_call(cmd)
