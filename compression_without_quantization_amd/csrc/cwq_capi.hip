@@ -1497,20 +1497,27 @@ int64_t batch_device_path(int64_t n_items, const int64_t* item_off, int64_t D, i
   // SDMA: the first thread in issues every copy, in order (the start lists
   // once the layout is done, then each chunk's results once it is coded);
   // every slot is released, also on an error, so no waiter hangs
+  // a copy the SDMA path refuses is made with a synchronous HIP copy instead
+  // (the event has completed: the data is final)
+  auto copy = [&](int k, void* dst, const void* src, size_t bytes) {
+    return sd.copy(k, dst, src, bytes) ||
+           (hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, d2h) == hipSuccess &&
+            hipStreamSynchronize(d2h) == hipSuccess);
+  };
   auto issue = [&]() {
     bool ok = npk == 0 || (wait_event(layout_ev) == hipSuccess &&
-                           sd.copy((int)K, pstage, pst_d, (size_t)npk * 8));
+                           copy((int)K, pstage, pst_d, (size_t)npk * 8));
     sd.release((int)K, !ok);
     for (int64_t c = 0; c < K; ++c) {
       if (ok && c < c_done) {
         const int64_t a = item_off[ci[(size_t)c]], Dc = item_off[ci[(size_t)c + 1]] - a;
         const int64_t gb = a + ci[(size_t)c], Gc = cG[(size_t)c];
         ok = wait_event(res_ev[c]) == hipSuccess &&
-             sd.copy((int)c, idx_h + gb * n_steps, idx + gb * n_steps,
-                     (size_t)(Gc * n_steps) * 4) &&
-             sd.copy((int)c, sample_host + a, out + a, (size_t)Dc * 4);
+             copy((int)c, idx_h + gb * n_steps, idx + gb * n_steps,
+                  (size_t)(Gc * n_steps) * 4) &&
+             copy((int)c, sample_host + a, out + a, (size_t)Dc * 4);
       }
-      sd.release((int)c, !ok);
+      sd.release((int)c, !ok);  // waiters see the failure: no slot is left held
     }
   };
   auto bits_worker = [&]() {

@@ -592,6 +592,46 @@ def test_importance_batch_equals_single_calls(cwq, oracle):
     _assert_bits_equal(idx[0], wsm, "batch item 0 vs oracle")
 
 
+def test_importance_instantiations_agree_on_large_groups(cwq):
+    """Launches large enough for the largest tile size (>= 2^25 candidates):
+    the batched call (per-group seeds, tile size known on the host), the fused
+    single call (seed + g, tile size known on the host) and the step-by-step
+    path (cwq_importance_encode: tile size chosen on the device) run the three
+    k_imp_eval instantiations over the same groups; all must agree bit for bit."""
+    import compression_without_quantization_amd.coded_importance_sampler as I
+    from compression_without_quantization_amd.synthetic import make_latents
+    I.VERBOSE = False
+    lat = [make_latents(6000, bits_per_dim=1.6, seed=900 + i) for i in range(2)]
+    dev = torch.device("cuda", 0)
+    ts = [cwq.Normal(torch.from_numpy(a).to(dev), torch.from_numpy(b).to(dev)) for a, b, _, _ in lat]
+    ps = [cwq.Normal(torch.from_numpy(c).to(dev), torch.from_numpy(d).to(dev)) for _, _, c, d in lat]
+    batch = I.code_grouped_importance_sample_batch(None, ts, ps, [11, 12], 20)
+    old = I.USE_FUSED
+    try:
+        for i, (t, p) in enumerate(zip(ts, ps)):
+            want = {}
+            for fused in (True, False):
+                I.USE_FUSED = fused
+                want[fused] = I.code_grouped_importance_sample(None, t, p, 11 + i, 20)
+            n = I.num_samples_plan(
+                I._kl(dev, *(x.reshape(-1) for x in (*_std_target(t, p), torch.zeros(6000, device=dev),
+                                                      torch.ones(6000, device=dev)))).cpu().numpy(),
+                np.asarray(want[True][2]))
+            assert int(np.maximum(n, 1).sum()) >= 1 << 25, "not a largest-tile launch"
+            for w in want.values():
+                _assert_bits_equal(batch[i][0], w[0], f"large groups, item {i}")
+                assert batch[i][1] == w[1]
+                assert np.array_equal(np.asarray(batch[i][2]), np.asarray(w[2]))
+    finally:
+        I.USE_FUSED = old
+
+
+def _std_target(t, p):
+    """The standardised target (coded_importance_sampler.py:137-138) of a latent
+    with no outliers (the test's latents have none above 16 bits)."""
+    return (t.loc - p.loc) / p.scale, t.scale / p.scale
+
+
 # ---------------------------------------------------------------------------
 # importance sampler screening pass (DESIGN.md §8): the screened encoder must
 # give the same indices and samples as the exact one, also where the bound is
