@@ -14,7 +14,8 @@ part=$1; shift
 bargs() {  # per-config bench arguments of the evidence lines
   case $1 in
     c4) echo "--config c4" ;;
-    c5|c2cli|c2low|i1|pln) echo "--config $1 --steps 3 --warmup 1" ;;
+    c5|c2cli|c2low|i1) echo "--config $1 --steps 3 --warmup 1" ;;
+    pln) echo "--config pln --steps 3 --warmup 2" ;;  # the capture (last warmup) warm
     c2) echo "--config c2 --steps 100 --warmup 5" ;;
     *) echo "--config $1 --steps 20 --warmup 3" ;;
   esac
