@@ -9,7 +9,8 @@
 //     the host, binary_io.py:7-39).
 // Groups have very different N_g, so work is cut into fixed-size tiles of one
 // group's candidates; a device prefix over tiles-per-group lets a persistent
-// grid find each tile's group by binary search (no host round trip).
+// grid find each tile's group by binary search (no host round trip); groups
+// of at most kImpSmallN candidates take one wave each instead (k_imp_small).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -56,6 +57,20 @@ __host__ __device__ inline int64_t imp_cand_per_tile(int64_t T) {
   return cpt;
 }
 
+// Groups of at most this many candidates are coded by k_imp_small (one wave
+// per group, every row exact) and get no k_imp_eval tile: most groups of a
+// batch of small latents draw a few dozen candidates (I2: 81% of 13,852
+// groups have N <= 128, 1.6% of the candidates), and a tile's fixed cost (its
+// group search, the screening constants, four barriers, the hand-out
+// counter) exceeded their rows' work.  A/B (tools/variants.sh is0..is1024,
+// one box, two rounds): I2's scoring 0.299 -> 0.207 ms, pln_is 0.36 -> 0.18 ms,
+// I1 unchanged (8.39 / 8.41 ms); 128 and 256 tie, 1024 is slower on I1.
+// 0 disables.
+#ifndef CWQ_IMP_SMALL_N
+#define CWQ_IMP_SMALL_N 128
+#endif
+constexpr int64_t kImpSmallN = CWQ_IMP_SMALL_N;
+
 // Exclusive prefix over the 1024 threads of the workgroup (inclusive wave scans
 // by shuffles, then the 16 wave totals).  Returns the prefix and
 // sets *total.
@@ -82,7 +97,8 @@ __device__ __forceinline__ int64_t block_exclusive_scan_1024(int64_t v, int64_t*
 }
 
 // Chooses the launch's candidates per tile (*cpt_out), then
-// tprefix[g] = sum_{h<g} ceil(max(N_h,1) / cpt); tprefix[nb] = total tiles.
+// tprefix[g] = sum_{h<g} tiles(N_h), tiles(N) = 0 for max(N, 1) <= kImpSmallN
+// (k_imp_small's groups), else ceil(N / cpt); tprefix[nb] = total tiles.
 // Also resets the per-group shared screening threshold gtau[g] and the
 // dynamic hand-out counter.  One workgroup of 1024 threads, each over a
 // contiguous run of groups.
@@ -133,13 +149,15 @@ __global__ void __launch_bounds__(1024) k_imp_tiles(const int64_t* __restrict__ 
     }
     return n_samples[g] > 1 ? n_samples[g] : 1;
   };
+  // a group k_imp_small codes takes no tile
+  auto ntiles = [&](int64_t n) -> int64_t { return n <= kImpSmallN ? 0 : (n + cpt - 1) / cpt; };
   int64_t tiles = 0;
-  for (int64_t g = g0; g < g1; ++g) tiles += (count(g) + cpt - 1) / cpt;
+  for (int64_t g = g0; g < g1; ++g) tiles += ntiles(count(g));
   int64_t all = 0;
   int64_t run = block_exclusive_scan_1024(tiles, wsum, &all);
   for (int64_t g = g0; g < g1; ++g) {
     tprefix[g] = run;
-    run += (count(g) + cpt - 1) / cpt;
+    run += ntiles(count(g));
   }
   if (threadIdx.x == 0) {
     tprefix[nb] = all;
@@ -543,6 +561,51 @@ __global__ void __launch_bounds__(256, CWQ_IMP_MIN_WAVES) k_imp_eval(
   }
 }
 
+// The groups of at most kImpSmallN candidates (no k_imp_eval tile): one wave
+// per group, every row exact (the same rows, sums and argmax keys as
+// k_imp_eval's exact evaluation, so the emitted index is the same), the
+// wave's best key stored to keys[g] (zeroed by the launcher; no other kernel
+// writes a small group's key).
+__global__ void __launch_bounds__(256) k_imp_small(
+    const float* __restrict__ t_loc, const float* __restrict__ t_scale,
+    const float* __restrict__ p_loc, const float* __restrict__ p_scale,
+    const float* __restrict__ lnt, const float* __restrict__ lnp,
+    const int64_t* __restrict__ block_off, const int64_t* __restrict__ n_samples, int64_t nb,
+    SeedSpec seeds, unsigned long long* __restrict__ keys) {
+  __shared__ double logtab[32];
+  fill_logtab(logtab);
+  const uint32_t wv = wave_id();
+  const uint32_t lane = threadIdx.x & 63u;
+  for (int64_t g = (int64_t)blockIdx.x * 4 + wv; g < nb; g += (int64_t)gridDim.x * 4) {
+    const int64_t N = n_samples[g] > 1 ? n_samples[g] : 1;
+    if (N > kImpSmallN) continue;  // wave-uniform
+    const int64_t off = block_off[g];
+    const int64_t d = block_off[g + 1] - off;
+    const PhiloxStream st = generate_key(seeds.of(g), 42);
+    const float* tl = t_loc + off;
+    const float* ts = t_scale + off;
+    const float* pl = p_loc + off;
+    const float* ps = p_scale + off;
+    const float* ct = lnt + off;
+    const float* cp = lnp + off;
+    uint64_t bestk = 0;
+    for (int64_t n = lane; n < N; n += 64) {
+      const float v = eval_row_f<0>(st, (uint64_t)n * (uint64_t)d, d, (int)(((uint64_t)n * d) & 3u),
+                                    logtab, [&](int64_t e, float zz) -> float {
+                                      float x = ps[e] * zz;  // misc.py:14
+                                      x = pl[e] + x;         // misc.py:15
+                                      const float lt = log_prob(x, tl[e], ts[e], ct[e]);
+                                      const float lq = log_prob(x, pl[e], ps[e], cp[e]);
+                                      return lt - lq;        // :60
+                                    });
+      const uint64_t k = argmax_key(v, (uint32_t)n);
+      bestk = k > bestk ? k : bestk;
+    }
+    bestk = wave_max_u64(bestk);
+    if (lane == 0 && bestk) keys[g] = (unsigned long long)bestk;
+  }
+}
+
 // Row `index` of group g's candidate stream: p_loc + p_scale * z (misc.py:14-15).
 // With keys != nullptr the index comes from the argmax key (encoder), else
 // from index_in (decoder, coded_importance_sampler.py:82-109).
@@ -653,6 +716,9 @@ hipError_t launch_importance_encode(const float* t_loc, const float* t_scale, co
                      p_loc, p_scale, lnt, lnp, block_off, n_samples, nb, (const int64_t*)tprefix,
                      (const int64_t*)cpt, ss, allow_screen, gtau, keys,
                      nb >= CWQ_IMP_DYNAMIC_MIN_GROUPS ? next_tile : nullptr);
+  if (kImpSmallN > 0)
+    hipLaunchKernelGGL(k_imp_small, dim3(grid_for(nb, 4, 65536)), dim3(256), 0, stream, t_loc,
+                       t_scale, p_loc, p_scale, lnt, lnp, block_off, n_samples, nb, ss, keys);
   hipLaunchKernelGGL(k_imp_rows, dim3(grid_for(nb, 4, 65536)), dim3(256), 0, stream,
                      (const unsigned long long*)keys, (const int64_t*)nullptr, p_loc, p_scale,
                      block_off, nb, ss, out_index, out_sample);

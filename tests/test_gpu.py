@@ -482,6 +482,30 @@ def test_importance_encode_vs_oracle(cwq, oracle):
     _assert_bits_equal(dec.cpu().numpy(), ws, "importance decode")
 
 
+@pytest.mark.parametrize("kind", ["random", "ties"])
+def test_importance_small_group_threshold(cwq, oracle, kind):
+    """Groups of at most 128 candidates are coded by k_imp_small (one wave,
+    exact rows), larger ones by k_imp_eval's tiles: counts either side of the
+    threshold (and 1, 64, 65) give the oracle's indices and samples."""
+    rng = np.random.default_rng(31 if kind == "random" else 32)
+    counts = [1, 2, 63, 64, 65, 127, 128, 129, 130, 255, 256, 257, 1000, 5000]
+    ns = np.array(counts * 3, dtype=np.int64)
+    rng.shuffle(ns)
+    sizes = rng.integers(1, 17, ns.size)
+    off = np.concatenate([[0], np.cumsum(sizes)]).astype(np.int64)
+    D = int(off[-1])
+    tl = (rng.standard_normal(D) * 0.8).astype(np.float32)
+    ts = rng.uniform(0.25, 0.95, D).astype(np.float32)
+    if kind == "ties":  # every score 0: the lowest index wins in both kernels
+        tl[:], ts[:] = 0.0, 1.0
+    pl = np.zeros(D, np.float32)
+    ps = np.ones(D, np.float32)
+    wi, ws = oracle.importance_encode(tl, ts, pl, ps, off, ns, 4321, 5)
+    gi, gs = cwq.importance_encode_blocks(tl, ts, pl, ps, off, ns, 4321, block_id_base=5)
+    assert np.array_equal(gi.cpu().numpy(), wi)
+    _assert_bits_equal(gs.cpu().numpy(), ws, f"importance small/large groups ({kind})")
+
+
 def test_importance_single_block_api(cwq, oracle):
     rng = np.random.default_rng(22)
     d = 6
