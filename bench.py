@@ -64,10 +64,10 @@ IMPORTANCE = {
     # name: (images, latent dims, n_bits_per_group, max_group_size_bits, dim_kl_bit_limit, desc)
     "i1": (1, 32 * 48 * 128, 20, 4, 16,
            "I1: one image's PLN level-1 latents (196,608 dims), grouped importance coder, "
-           "20 bits/group, groups <= 15 dims (miracle_arguments.py:177-183)"),
+           "20 bits/group, groups <= 16 dims (miracle_arguments.py:177-183)"),
     "i2": (24, 8 * 12 * 24, 20, 2, 16,
            "I2: 24 images' PLN level-2 latents (2,304 dims each), grouped importance coder, "
-           "20 bits/group, groups <= 3 dims (miracle_arguments.py:168-174)"),
+           "20 bits/group, groups <= 4 dims (miracle_arguments.py:168-174)"),
 }
 PLN = {
     # name: (images, H, W, level-1 coder, description)
@@ -77,7 +77,7 @@ PLN = {
             "(miracle.py compress/decompress defaults, miracle_arguments.py:146-189)"),
     "pln_is": (1, 512, 768, "importance",
                "PLN image codec, level 1 through the importance coder (--use_importance_sampling: "
-               "20 bits/group, groups <= 15 dims), level 2 as pln; the path the reference's "
+               "20 bits/group, groups <= 16 dims), level 2 as pln; the path the reference's "
                "kodim05 timings most likely used (SURVEY.md 6)"),
 }
 CONFIGS = {

@@ -122,11 +122,11 @@ def elias_delta_code_many(values):
     if x.min() < 1 or x.max() >= (1 << 30):
         return ''.join(elias_delta_code(int(v)) for v in x)
     lib = _lib.load()
-    n = _lib.check(lib.cwq_elias_delta_encode(x.ctypes.data, x.size, None, 0), "elias encode")
-    buf = np.empty(n, dtype=np.uint8)
-    _lib.check(lib.cwq_elias_delta_encode(x.ctypes.data, x.size, buf.ctypes.data, n),
-               "elias encode")
-    return buf.tobytes().decode('ascii')
+    # one pass into a buffer of the longest codes (x < 2^30: at most 38 chars)
+    buf = np.empty(38 * x.size, dtype=np.uint8)
+    n = _lib.check(lib.cwq_elias_delta_encode(x.ctypes.data, x.size, buf.ctypes.data, buf.size),
+                   "elias encode")
+    return str(memoryview(buf)[:n], 'ascii')
 
 
 def elias_delta_decode_many(bitcode, count):

@@ -380,9 +380,11 @@ def code_grouped_importance_sample_batch(sess, targets, proposals, seeds, n_bits
         sizes = np.array([a.numel() for a in cols[0]], dtype=np.int64)
         if any([a.numel() for a in c] != sizes.tolist() for c in cols[1:]):
             raise ValueError("target and proposal of an item must have the same size")
-        cat = [torch.cat(c) for c in cols]
+        # the four concatenated inputs as four quarters of one buffer (one cat)
         item_off = np.concatenate([[0], np.cumsum(sizes)]).astype(np.int64)
         D = int(item_off[-1])
+        big = torch.cat([a for c in cols for a in c])
+        cat = [big[k * D:(k + 1) * D] for k in range(4)]
         need = int(lib.cwq_code_grouped_importance_batch_workspace_size(D, n_items))
         ws = torch.empty(max(need, 1), dtype=torch.uint8, device=dev)
         sample_h = np.empty(max(D, 1), dtype=np.float32)
@@ -403,8 +405,9 @@ def code_grouped_importance_sample_batch(sess, targets, proposals, seeds, n_bits
             _lib.options(prune_mode, eval_ms_out=eval_ms_out), _stream(dev)),
             "cwq_code_grouped_importance_batch")
     # every item's index + 1 values, outlier codes and bit strings in one pass
-    # each (one native Elias-delta call, one quint16 pass; per-item calls cost
-    # ~20 us apiece), then split per item
+    # each (one native Elias-delta call, one quint16 pass over the outliers
+    # only; per-item calls cost ~20 us apiece), then split per item.  The
+    # per-item arrays are views of this call's buffers (disjoint slices).
     ns_all = n_starts.astype(np.int64)
     G = np.maximum(ns_all - 1, 0)
     goff = np.concatenate([[0], np.cumsum(G)])
@@ -412,17 +415,20 @@ def code_grouped_importance_sample_batch(sess, targets, proposals, seeds, n_bits
     src = np.arange(goff[-1], dtype=np.int64) + np.repeat(
         item_off[:-1] + np.arange(n_items, dtype=np.int64) - goff[:-1], G)
     vals = index_h[src] + 1
-    q_all = quantize_quint16(out_v[:D]) if D else np.zeros(0, np.uint16)
-    codes = None
-    if not return_indices:
+    # item i's outliers sit at out_i / out_v[item_off[i] : item_off[i] + n_out[i]]
+    ooff = np.concatenate([[0], np.cumsum(n_out)])
+    osrc = np.arange(ooff[-1], dtype=np.int64) + np.repeat(item_off[:-1] - ooff[:-1], n_out)
+    o_idx = out_i[osrc]
+    o_q = quantize_quint16(out_v[osrc])
+    if return_indices:
+        vals_l = vals.tolist()
+    else:
         codes = elias_delta_code_many(vals)
         if vals.size:  # code lengths: 2 floor(log2(n + 1)) + n + 1, n = floor(log2 x)
-            nb_ = np.frexp(vals.astype(np.float64))[1].astype(np.int64) - 1
-            ln = 2 * (np.frexp((nb_ + 1).astype(np.float64))[1].astype(np.int64) - 1) + nb_ + 1
-            coff = np.concatenate([[0], np.cumsum(ln)])[goff]
+            nb_ = np.frexp(vals)[1] - 1
+            coff = np.concatenate([[0], np.cumsum(_ELIAS_LEN[nb_])])[goff]
         else:
             coff = np.zeros(n_items + 1, np.int64)
-    vals_l = vals.tolist()
     res = []
     for i in range(n_items):
         a, b = int(item_off[i]), int(item_off[i + 1])
@@ -433,14 +439,16 @@ def code_grouped_importance_sample_batch(sess, targets, proposals, seeds, n_bits
                   "estimated number of groups: {},"
                   "coding {} dimensions".format(total_kl_bits, n_bits_per_group,
                                                 total_kl_bits // n_bits_per_group + 1, b - a))
-        ns, no = int(ns_all[i]), int(n_out[i])
-        gs = starts_h[a + 2 * i:a + 2 * i + ns].copy()
-        indices = tuple(vals_l[goff[i]:goff[i + 1]])
-        extras = (out_i[a:a + no].copy(), q_all[a:a + no].copy())
-        smp = sample_h[a:b].copy()
-        code = indices if return_indices else codes[coff[i]:coff[i + 1]]
-        res.append((smp, code, gs, extras))
+        o0, o1 = int(ooff[i]), int(ooff[i + 1])
+        gs = starts_h[a + 2 * i:a + 2 * i + int(ns_all[i])]
+        code = (tuple(vals_l[goff[i]:goff[i + 1]]) if return_indices
+                else codes[coff[i]:coff[i + 1]])
+        res.append((sample_h[a:b], code, gs, (o_idx[o0:o1], o_q[o0:o1])))
     return res
+
+
+# Elias-delta code length by n = floor(log2 x): n + 2 floor(log2(n + 1)) + 1
+_ELIAS_LEN = np.array([n + 2 * (int(n + 1).bit_length() - 1) + 1 for n in range(64)], np.int64)
 
 
 def _group_kls(kl_divs, starts):
