@@ -316,14 +316,15 @@ def _code_grouped_fused(lib, dev, q_loc, q_scale, p_loc, p_scale, D, seed, n_bit
               "estimated number of groups: {},"
               "coding {} dimensions".format(total_kl_bits, n_bits_per_group,
                                             total_kl_bits // n_bits_per_group + 1, D))
+    # views of this call's buffers; the indices + 1 coded straight from the array
     no = int(n_out[0])
-    outlier_extras = (out_i[:no].copy(), quantize_quint16(out_v[:no]))
-    group_start_indices = starts_h[:G + 1].copy()
-    indices = tuple((index_h[:G] + 1).tolist())
-    sample_h = sample_h[:D].copy()
+    outlier_extras = (out_i[:no], quantize_quint16(out_v[:no]))
+    group_start_indices = starts_h[:G + 1]
+    vals = index_h[:G] + 1
+    sample_h = sample_h[:D]
     if return_indices:
-        return sample_h, indices, group_start_indices, outlier_extras
-    return sample_h, elias_delta_code_many(indices), group_start_indices, outlier_extras
+        return sample_h, tuple(vals.tolist()), group_start_indices, outlier_extras
+    return sample_h, elias_delta_code_many(vals), group_start_indices, outlier_extras
 
 
 def code_grouped_importance_sample_batch(sess, targets, proposals, seeds, n_bits_per_group,

@@ -21,6 +21,7 @@
 #include <stdint.h>
 #include <stddef.h>
 #include <string.h>
+#include <immintrin.h>
 
 #include <vector>
 
@@ -187,22 +188,49 @@ int64_t cwq_ac_decode(const int64_t* counts, int64_t K, int precision, const cha
 // vectorised: the reference's float64 formulas n = floor(log2 x),
 // l = floor(log2(n + 1)) equal the bit lengths for 1 <= x < 2^30
 // (tests/test_importance.py); larger x is rejected so the caller can fall back.
+// The code of v is l '0's, n + 1 in l + 1 bits and v's low n bits, all MSB
+// first: the len = 2l + 1 + n bit binary of W = ((n + 1) << n) | (v mod 2^n)
+// (its top bit is n + 1's, so the l leading zeros are the padding).
+namespace {
+int elias_len(int64_t v, uint64_t* w) {
+  const int nb = 63 - __builtin_clzll((unsigned long long)v);        // n = floor(log2 v)
+  const int l = 63 - __builtin_clzll((unsigned long long)(nb + 1));  // floor(log2(n + 1))
+  *w = ((uint64_t)(nb + 1) << nb) | ((uint64_t)v & ((1ull << nb) - 1));
+  return 2 * l + 1 + nb;
+}
+void elias_chars(uint64_t w, int len, char* o) {
+  for (int k = len - 1; k >= 0; --k) *o++ = (char)('0' + ((w >> k) & 1));
+}
+// BMI2: the code left-aligned in 64 bits, then 8 chars per pdep (bit k -> the
+// low bit of byte k), a byte swap (the first char is the byte's top bit) and
+// an OR with '0' x 8; writes whole 8-byte words, so it needs 8 * ceil(len / 8)
+// bytes of room (<= 40).  14k I2 indices: ~3x faster than a char at a time.
+__attribute__((target("bmi2"))) void elias_chars_pdep(uint64_t w, int len, char* o) {
+  constexpr uint64_t kLow = 0x0101010101010101ull, kZero = 0x3030303030303030ull;
+  const uint64_t a = w << (64 - len);
+  for (int k = 0; k < len; k += 8) {
+    const uint64_t c = __builtin_bswap64(_pdep_u64((a >> (56 - k)) & 0xffu, kLow)) | kZero;
+    memcpy(o + k, &c, 8);
+  }
+}
+}  // namespace
+
 int64_t cwq_elias_delta_encode(const int64_t* x, int64_t n, char* out, int64_t cap) {
   if (n < 0 || (n > 0 && !x)) return cwq::set_error(CWQ_ERR_INVALID, "cwq_elias_delta_encode: bad arguments");
+  static const bool bmi2 = __builtin_cpu_supports("bmi2");
   int64_t pos = 0;
   for (int64_t i = 0; i < n; ++i) {
     const int64_t v = x[i];
     if (v < 1 || v >= ((int64_t)1 << 30))
       return cwq::set_error(CWQ_ERR_INVALID, "cwq_elias_delta_encode: value outside [1, 2^30)");
-    const int nb = 63 - __builtin_clzll((unsigned long long)v);          // n = floor(log2 v)
-    const int l = 63 - __builtin_clzll((unsigned long long)(nb + 1));    // floor(log2(n + 1))
-    const int64_t len = (int64_t)l + (l + 1) + nb;
+    uint64_t w;
+    const int len = elias_len(v, &w);
     if (out) {
       if (pos + len > cap) return cwq::set_error(CWQ_ERR_CAPACITY, "cwq_elias_delta_encode: cap");
-      char* o = out + pos;
-      for (int k = 0; k < l; ++k) *o++ = '0';
-      for (int k = l; k >= 0; --k) *o++ = (char)('0' + (((nb + 1) >> k) & 1));  // n+1, MSB first
-      for (int k = nb - 1; k >= 0; --k) *o++ = (char)('0' + ((v >> k) & 1));     // v without its top bit
+      if (bmi2 && pos + 40 <= cap)
+        elias_chars_pdep(w, len, out + pos);
+      else
+        elias_chars(w, len, out + pos);
     }
     pos += len;
   }

@@ -1157,14 +1157,19 @@ class HostPool {
       started = std::min<int64_t>(n, (int64_t)threads_);
       job_ = &f;
       active_ = started;
-      left_ = started;
+      running_ = 0;
       ++gen_;
     }
     cv_.notify_all();
     f();
+    // the caller's f() returns once the job's work is claimed (every user's f
+    // claims work items until none is left): helpers that have not woken yet
+    // skip the job instead of being waited for (a futex wake-up can take tens
+    // of microseconds: I2's 24-item planning waited ~70 us for them); helpers
+    // inside f() finish the items they hold
     std::unique_lock<std::mutex> lk(m_);
-    done_.wait(lk, [&] { return left_ == 0; });
     job_ = nullptr;
+    done_.wait(lk, [&] { return running_ == 0; });
   }
 
  private:
@@ -1176,12 +1181,13 @@ class HostPool {
         std::unique_lock<std::mutex> lk(m_);
         cv_.wait(lk, [&] { return gen_ != seen; });
         seen = gen_;
-        if (id >= active_) continue;
+        if (id >= active_ || !job_) continue;  // not needed, or the job has closed
         f = job_;
+        ++running_;
       }
       (*f)();
       std::lock_guard<std::mutex> lk(m_);
-      if (--left_ == 0) done_.notify_all();
+      if (--running_ == 0) done_.notify_all();
     }
   }
   std::mutex run_m_, m_;
@@ -1189,7 +1195,7 @@ class HostPool {
   const std::function<void()>* job_ = nullptr;
   pid_t pid_ = getpid();
   uint64_t gen_ = 0;
-  int64_t threads_ = 0, active_ = 0, left_ = 0;
+  int64_t threads_ = 0, active_ = 0, running_ = 0;
 };
 // Chunks a batch is pipelined in (CWQ_BATCH_CHUNKS, default below): the host
 // phases of one chunk run while the device codes another.
@@ -2013,11 +2019,16 @@ int64_t cwq_code_grouped_greedy_batch(
 // ---------------------------------------------------------------------------
 namespace {
 struct GroupedImpWs {
-  size_t t_loc, t_scale, kl2, zeros, ones, tsamp, sample, out, keep, offs, nsamp, idx, gseed,
-      items, seed1, enc, total;
+  size_t t_loc, t_scale, zeros, ones, sample, res, d2h, plan, items, enc, total;
+  size_t a4;  // align_up(4 D, 256): the stride inside the packed regions
 };
 // D dims in I items: at most D + I groups (an item's partition has at most
-// D_i + 1 groups)
+// D_i + 1 groups).  What crosses PCIe sits in packed regions, one copy each,
+// laid out identically in the host staging: d2h = [KL | outlier draws | kept
+// flags] (to the host after the preparation launch), res = [sample | indices]
+// (to the host at the end), plan = [counts | offsets | seeds] (to the device;
+// the offsets and seeds start at offsets set by the call's group count, see
+// imp_plan_offsets), items = [item offsets | seeds - 1] (to the device, batches).
 GroupedImpWs grouped_imp_ws(int64_t D, int64_t I) {
   GroupedImpWs l;
   size_t o = 0;
@@ -2027,24 +2038,26 @@ GroupedImpWs grouped_imp_ws(int64_t D, int64_t I) {
     return at;
   };
   const size_t n = (size_t)(D > 0 ? D : 0), ni = (size_t)(I > 0 ? I : 0), g = n + ni;
+  l.a4 = align_up(n * 4, 256);
   l.t_loc = take(n * 4);
   l.t_scale = take(n * 4);
-  l.kl2 = take(n * 4);
   l.zeros = take(n * 4);
   l.ones = take(n * 4);
-  l.tsamp = take(n * 4);
   l.sample = take(n * 4);
-  l.out = take(n * 4);
-  l.keep = take(n);
-  l.offs = take((g + 1) * 8);
-  l.nsamp = take(g * 8);
-  l.idx = take(g * 8);
-  l.gseed = take(g * 4);
-  l.items = take((ni + 1) * 8);
-  l.seed1 = take(ni * 4);
+  l.res = take(l.a4 + g * 8);
+  l.d2h = take(2 * l.a4 + n);
+  l.plan = take(align_up(g * 8, 256) + align_up((g + 1) * 8, 256) + g * 4);
+  l.items = take(align_up((ni + 1) * 8, 256) + ni * 4);
   l.enc = take(cwq::importance_workspace_size((int64_t)g, (int64_t)n));
   l.total = o;
   return l;
+}
+// The plan region for G groups: counts at 0, offsets at *po, seeds at *pg;
+// returns the bytes one copy moves (the seeds only with per-item seeds).
+size_t imp_plan_offsets(int64_t G, bool seeds, size_t* po, size_t* pg) {
+  *po = align_up((size_t)G * 8, 256);
+  *pg = *po + align_up((size_t)(G + 1) * 8, 256);
+  return seeds ? *pg + (size_t)G * 4 : *po + (size_t)(G + 1) * 8;
 }
 thread_local PinnedTl tl_imp_pin;             // the grouped importance calls' host staging
 thread_local std::vector<char> tl_imp_pageable;  // ... when page-locked memory is unavailable
@@ -2101,19 +2114,17 @@ int64_t grouped_importance_impl(int64_t I, const int64_t* item_off, const float*
   char* w = (char*)workspace;
   float* t_loc = (float*)(w + l.t_loc);
   float* t_scale = (float*)(w + l.t_scale);
-  float* kl2 = (float*)(w + l.kl2);
+  float* kl2 = (float*)(w + l.d2h);
+  float* tsamp = (float*)(w + l.d2h + l.a4);
+  uint8_t* keep = (uint8_t*)(w + l.d2h + 2 * l.a4);
   float* zeros = (float*)(w + l.zeros);
   float* ones = (float*)(w + l.ones);
-  float* tsamp = (float*)(w + l.tsamp);
   float* sample = (float*)(w + l.sample);
-  float* out = (float*)(w + l.out);
-  uint8_t* keep = (uint8_t*)(w + l.keep);
-  int64_t* offs = (int64_t*)(w + l.offs);
-  int64_t* nsamp = (int64_t*)(w + l.nsamp);
-  int64_t* idx = (int64_t*)(w + l.idx);
-  int32_t* gseed = (int32_t*)(w + l.gseed);
+  float* out = (float*)(w + l.res);
+  int64_t* idx = (int64_t*)(w + l.res + l.a4);
+  int64_t* nsamp = (int64_t*)(w + l.plan);
   int64_t* items_d = (int64_t*)(w + l.items);
-  int32_t* seed1_d = (int32_t*)(w + l.seed1);
+  int32_t* seed1_d = (int32_t*)(w + l.items + align_up((size_t)(I + 1) * 8, 256));
   // the host side's arrays in this thread's page-locked staging (pageable
   // memory is staged by the runtime: I1's 2.9 MB of copies took ~0.5 ms more),
   // waits polled on events (a blocking wait's wake-up cost I2's small calls
@@ -2125,25 +2136,24 @@ int64_t grouped_importance_impl(int64_t I, const int64_t* item_off, const float*
     ho = align_up(ho + b, 256);
     return at;
   };
-  const size_t o_kl = htake(Dz * 4), o_ts = htake(Dz * 4), o_out = htake(Dz * 4),
-               o_keep = htake(Dz), o_idx = htake(Gz * 8), o_offs = htake((Gz + 1) * 8),
-               o_ns = htake(Gz * 8), o_gs = htake(Gz * 4), o_items = htake((Iz + 1) * 8),
-               o_s1 = htake(Iz * 4), o_nst = htake(I > 1 ? Gz * 8 : 0);
+  // the packed regions (same layout as the device's) and the batch's per-item plans
+  const size_t o_d2h = htake(2 * l.a4 + Dz), o_res = htake(l.a4 + Gz * 8),
+               o_plan = htake(align_up(Gz * 8, 256) + align_up((Gz + 1) * 8, 256) + Gz * 4),
+               o_items = htake(align_up((Iz + 1) * 8, 256) + Iz * 4),
+               o_nst = htake(I > 1 ? Gz * 8 : 0);
   char* hp = (char*)tl_imp_pin.get(ho, ho + ho / 4);
   if (!hp) {  // no page-locked memory: pageable staging (slower copies)
     tl_imp_pageable.resize(ho);
     hp = tl_imp_pageable.data();
   }
-  float* kl_h = (float*)(hp + o_kl);
-  float* ts_h = (float*)(hp + o_ts);
-  float* out_h = (float*)(hp + o_out);
-  uint8_t* keep_h = (uint8_t*)(hp + o_keep);
-  int64_t* idx_h = (int64_t*)(hp + o_idx);
-  int64_t* offs_h = (int64_t*)(hp + o_offs);
-  int64_t* ns_h = (int64_t*)(hp + o_ns);
-  int32_t* gs_h = (int32_t*)(hp + o_gs);
+  float* kl_h = (float*)(hp + o_d2h);
+  float* ts_h = (float*)(hp + o_d2h + l.a4);
+  uint8_t* keep_h = (uint8_t*)(hp + o_d2h + 2 * l.a4);
+  float* out_h = (float*)(hp + o_res);
+  int64_t* idx_h = (int64_t*)(hp + o_res + l.a4);
+  int64_t* ns_h = (int64_t*)(hp + o_plan);
   int64_t* items_h = (int64_t*)(hp + o_items);
-  int32_t* s1_h = (int32_t*)(hp + o_s1);
+  int32_t* s1_h = (int32_t*)(hp + o_items + align_up((Iz + 1) * 8, 256));
   int64_t* nst_h = I > 1 ? (int64_t*)(hp + o_nst) : ns_h;  // item i's plan at item_off[i] + i
   hipError_t e = hipSuccess;
   // every failure after the first copy or launch drains the stream first: the
@@ -2167,9 +2177,8 @@ int64_t grouped_importance_impl(int64_t I, const int64_t* item_off, const float*
   if (I > 1) {
     memcpy(items_h, item_off, (Iz + 1) * 8);
     for (int64_t i = 0; i < I; ++i) s1_h[i] = (int32_t)((uint32_t)seeds[i] - 1u);
-    if ((e = hipMemcpyAsync(items_d, items_h, (Iz + 1) * 8, hipMemcpyHostToDevice, s)) !=
-            hipSuccess ||
-        (e = hipMemcpyAsync(seed1_d, s1_h, Iz * 4, hipMemcpyHostToDevice, s)) != hipSuccess)
+    if ((e = hipMemcpyAsync(items_d, items_h, align_up((Iz + 1) * 8, 256) + Iz * 4,
+                            hipMemcpyHostToDevice, s)) != hipSuccess)
       return drain_fail(e, "items to device");
     items_arg = items_d;
     seed1_arg = seed1_d;
@@ -2179,9 +2188,7 @@ int64_t grouped_importance_impl(int64_t I, const int64_t* item_off, const float*
                                         (int32_t)((uint32_t)seeds[0] - 1u), t_loc, t_scale, keep,
                                         zeros, ones, kl2, tsamp, s)) != hipSuccess)
     return drain_fail(e, "standardise / KL / outliers");
-  if ((e = hipMemcpyAsync(kl_h, kl2, Dz * 4, hipMemcpyDeviceToHost, s)) != hipSuccess ||
-      (e = hipMemcpyAsync(keep_h, keep, Dz, hipMemcpyDeviceToHost, s)) != hipSuccess ||
-      (e = hipMemcpyAsync(ts_h, tsamp, Dz * 4, hipMemcpyDeviceToHost, s)) != hipSuccess ||
+  if ((e = hipMemcpyAsync(kl_h, kl2, 2 * l.a4 + Dz, hipMemcpyDeviceToHost, s)) != hipSuccess ||
       (e = hipEventRecord(hev.ev[0], s)) != hipSuccess)
     return drain_fail(e, "to host");
   lap("prep queued");
@@ -2228,6 +2235,14 @@ int64_t grouped_importance_impl(int64_t I, const int64_t* item_off, const float*
   if (item_rc.load() < 0)
     return drain_rc(fail((int)item_rc.load(), "%s: item partition / plan failed", who));
   int64_t Gtot = 0;
+  for (int64_t i = 0; i < I; ++i) Gtot += n_starts[i] - 1 > 0 ? n_starts[i] - 1 : 0;
+  size_t po = 0, pg = 0;
+  const size_t plan_bytes = imp_plan_offsets(Gtot, I > 1, &po, &pg);
+  int64_t* offs_h = (int64_t*)(hp + o_plan + po);
+  int32_t* gs_h = (int32_t*)(hp + o_plan + pg);
+  int64_t* offs = (int64_t*)(w + l.plan + po);
+  int32_t* gseed = (int32_t*)(w + l.plan + pg);
+  Gtot = 0;
   for (int64_t i = 0; i < I; ++i) {
     const int64_t a = item_off[i], G = n_starts[i] - 1;
     const int64_t* st = starts_host + a + 2 * i;
@@ -2243,12 +2258,7 @@ int64_t grouped_importance_impl(int64_t I, const int64_t* item_off, const float*
   int64_t tcand = 0;  // the launch's candidates (selects the encoder's instantiation)
   for (int64_t g = 0; g < Gtot; ++g) tcand += ns_h[g] > 1 ? ns_h[g] : 1;
   if (Gtot > 0) {
-    if ((e = hipMemcpyAsync(offs, offs_h, (size_t)(Gtot + 1) * 8, hipMemcpyHostToDevice, s)) !=
-            hipSuccess ||
-        (e = hipMemcpyAsync(nsamp, ns_h, (size_t)Gtot * 8, hipMemcpyHostToDevice, s)) !=
-            hipSuccess ||
-        (I > 1 && (e = hipMemcpyAsync(gseed, gs_h, (size_t)Gtot * 4, hipMemcpyHostToDevice, s)) !=
-                      hipSuccess))
+    if ((e = hipMemcpyAsync(nsamp, ns_h, plan_bytes, hipMemcpyHostToDevice, s)) != hipSuccess)
       return drain_fail(e, "plan to device");
     // :212-245 every group's importance coder; eval_ms_out: its launches timed
     // with events of this call (the call synchronises anyway)
@@ -2273,9 +2283,8 @@ int64_t grouped_importance_impl(int64_t I, const int64_t* item_off, const float*
   // :265 rescale, :267 outliers keep their target draw
   if ((e = cwq::launch_destandardise(sample, p_loc, p_scale, D, out, s)) != hipSuccess)
     return drain_fail(e, "destandardise");
-  if ((Gtot > 0 && (e = hipMemcpyAsync(idx_h, idx, (size_t)Gtot * 8, hipMemcpyDeviceToHost, s)) !=
-                       hipSuccess) ||
-      (e = hipMemcpyAsync(out_h, out, Dz * 4, hipMemcpyDeviceToHost, s)) != hipSuccess ||
+  if ((e = hipMemcpyAsync(out_h, out, Gtot > 0 ? l.a4 + (size_t)Gtot * 8 : Dz * 4,
+                          hipMemcpyDeviceToHost, s)) != hipSuccess ||
       (e = hipEventRecord(hev.ev[1], s)) != hipSuccess)
     return drain_fail(e, "to host");
   lap("enqueued");
