@@ -457,13 +457,14 @@ def code_grouped_greedy_sample_batch(sess, targets, proposals, n_steps, n_bits_p
         if any([a.numel() for a in c] != sz for c in cols[1:]):
             raise ValueError("target and proposal of an item must have the same size")
         sizes = np.array(sz, dtype=np.int64)
+        D0 = int(sizes.sum())
         try:
             # concatenation along dim 0 of equal trailing shapes is the concatenation
-            # of the flattened arrays (1-D latents: always)
-            cat = [torch.cat(c).reshape(-1) for c in cols]
+            # of the flattened arrays (1-D latents: always); the four columns as
+            # the four quarters of one buffer (one cat of 4 n_items tensors)
+            big = torch.cat([a for c in cols for a in c]).reshape(-1)
+            cat = [big[k * D0:(k + 1) * D0] for k in range(4)] if big.numel() == 4 * D0 else None
         except RuntimeError:
-            cat = None
-        if cat is not None and any(int(x.numel()) != int(sizes.sum()) for x in cat):
             cat = None
         if cat is not None:
             dev = cat[0].device
