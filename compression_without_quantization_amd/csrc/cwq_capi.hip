@@ -1131,6 +1131,9 @@ int64_t host_threads() {
 // never destroyed (its threads sleep on a condition variable through process
 // exit).  run() executes f on up to n pool threads and the calling thread and
 // returns once every one of them has returned; concurrent run()s queue.
+#ifndef CWQ_POOL_WAIT_ALL
+#define CWQ_POOL_WAIT_ALL 0  // 1: run() also waits for every started helper (A/B)
+#endif
 class HostPool {
  public:
   static HostPool& get() {
@@ -1158,6 +1161,7 @@ class HostPool {
       job_ = &f;
       active_ = started;
       running_ = 0;
+      left_ = started;
       ++gen_;
     }
     cv_.notify_all();
@@ -1168,6 +1172,7 @@ class HostPool {
     // of microseconds: I2's 24-item planning waited ~70 us for them); helpers
     // inside f() finish the items they hold
     std::unique_lock<std::mutex> lk(m_);
+    if (CWQ_POOL_WAIT_ALL) done_.wait(lk, [&] { return left_ == 0; });  // A/B: the old rule
     job_ = nullptr;
     done_.wait(lk, [&] { return running_ == 0; });
   }
@@ -1187,7 +1192,8 @@ class HostPool {
       }
       (*f)();
       std::lock_guard<std::mutex> lk(m_);
-      if (--running_ == 0) done_.notify_all();
+      --left_;
+      if (--running_ == 0 || left_ == 0) done_.notify_all();
     }
   }
   std::mutex run_m_, m_;
@@ -1195,7 +1201,7 @@ class HostPool {
   const std::function<void()>* job_ = nullptr;
   pid_t pid_ = getpid();
   uint64_t gen_ = 0;
-  int64_t threads_ = 0, active_ = 0, running_ = 0;
+  int64_t threads_ = 0, active_ = 0, running_ = 0, left_ = 0;
 };
 // Chunks a batch is pipelined in (CWQ_BATCH_CHUNKS, default below): the host
 // phases of one chunk run while the device codes another.
