@@ -2275,7 +2275,8 @@ int64_t grouped_importance_impl(int64_t I, const int64_t* item_off, const float*
         (e = cwq::launch_importance_encode(t_loc, t_scale, zeros, ones, offs, nsamp, Gtot, D,
                                            seeds[0], 0, I > 1 ? gseed : nullptr,
                                            oi.prune_mode >= 2 ? 1 : 0, idx, sample, w + l.enc,
-                                           s, tcand)) != hipSuccess ||
+                                           s, tcand, cwq::importance_tile_count(ns_h, Gtot, tcand))) !=
+            hipSuccess ||
         (oi.eval_ms_out && (e = hipEventRecord(tev.ev[1], s)) != hipSuccess))
       return drain_fail(e, "importance encode");
     if (oi.eval_ms_out) {

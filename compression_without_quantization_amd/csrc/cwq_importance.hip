@@ -256,6 +256,14 @@ __device__ __forceinline__ bool imp_screen_dim(float tl, float ts, float pl, flo
 #ifndef CWQ_IMP_DYNAMIC_MIN_GROUPS
 #define CWQ_IMP_DYNAMIC_MIN_GROUPS 4096  // dynamic tile hand-out from this many groups
 #endif
+// ... or, when the host knows the launch's tile count, from this many tiles:
+// below it the one-address hand-out counter (an atomic per tile from every
+// workgroup) cost more than the balance it buys (I2's batch, ~4.4k tiles:
+// 0.206 -> 0.185 ms static; pln_is 0.18 -> 0.13 ms; I1's 99.9k tiles need it:
+// 8.40 -> 9.83 ms static)
+#ifndef CWQ_IMP_DYNAMIC_MIN_TILES
+#define CWQ_IMP_DYNAMIC_MIN_TILES 8192
+#endif
 #ifndef CWQ_IMP_MIN_WAVES
 #define CWQ_IMP_MIN_WAVES 1  // waves/SIMD the register allocator must allow (tools/variants.sh)
 #endif
@@ -690,7 +698,8 @@ hipError_t launch_importance_encode(const float* t_loc, const float* t_scale, co
                                     int32_t seed, int64_t block_id_base,
                                     const int32_t* block_seeds, int allow_screen,
                                     int64_t* out_index, float* out_sample, void* workspace,
-                                    hipStream_t stream, int64_t total_cands) {
+                                    hipStream_t stream, int64_t total_cands,
+                                    int64_t total_tiles) {
   if (nb <= 0) return hipSuccess;
   auto up = [](size_t v) { return (v + 255) / 256 * 256; };
   char* w = (char*)workspace;
@@ -715,7 +724,10 @@ hipError_t launch_importance_encode(const float* t_loc, const float* t_scale, co
   hipLaunchKernelGGL(eval, dim3((unsigned)kImpEvalGrid), dim3(256), 0, stream, t_loc, t_scale,
                      p_loc, p_scale, lnt, lnp, block_off, n_samples, nb, (const int64_t*)tprefix,
                      (const int64_t*)cpt, ss, allow_screen, gtau, keys,
-                     nb >= CWQ_IMP_DYNAMIC_MIN_GROUPS ? next_tile : nullptr);
+                     (total_tiles >= 0 ? total_tiles >= CWQ_IMP_DYNAMIC_MIN_TILES
+                                       : nb >= CWQ_IMP_DYNAMIC_MIN_GROUPS)
+                         ? next_tile
+                         : nullptr);
   if (kImpSmallN > 0)
     hipLaunchKernelGGL(k_imp_small, dim3(grid_for(nb, 4, 65536)), dim3(256), 0, stream, t_loc,
                        t_scale, p_loc, p_scale, lnt, lnp, block_off, n_samples, nb, ss, keys);
@@ -723,6 +735,16 @@ hipError_t launch_importance_encode(const float* t_loc, const float* t_scale, co
                      (const unsigned long long*)keys, (const int64_t*)nullptr, p_loc, p_scale,
                      block_off, nb, ss, out_index, out_sample);
   return hipGetLastError();
+}
+
+int64_t importance_tile_count(const int64_t* n_samples_host, int64_t nb, int64_t total_cands) {
+  const int64_t cpt = imp_cand_per_tile(total_cands);  // k_imp_tiles' rule
+  int64_t tiles = 0;
+  for (int64_t g = 0; g < nb; ++g) {
+    const int64_t n = n_samples_host[g] > 1 ? n_samples_host[g] : 1;
+    tiles += n <= kImpSmallN ? 0 : (n + cpt - 1) / cpt;
+  }
+  return tiles;
 }
 
 hipError_t launch_importance_decode(const int64_t* index, const float* p_loc,
