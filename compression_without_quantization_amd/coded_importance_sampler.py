@@ -372,19 +372,26 @@ def code_grouped_importance_sample_batch(sess, targets, proposals, seeds, n_bits
                 raise Exception("Proposal datatype must be float32!")
         dev = _device_of(*[a for c in raw for a in c])
     with torch.cuda.device(dev):
-        if fast:
-            cols = [[a.reshape(-1) for a in c] for c in raw]
-        else:
-            cols = [[_f32(a, dev, n).reshape(-1) for a in c]
-                    for c, n in zip(raw, ("target.loc", "target.scale", "proposal.loc",
-                                          "proposal.scale"))]
-        sizes = np.array([a.numel() for a in cols[0]], dtype=np.int64)
-        if any([a.numel() for a in c] != sizes.tolist() for c in cols[1:]):
+        cols = raw if fast else [[_f32(a, dev, n) for a in c]
+                                 for c, n in zip(raw, ("target.loc", "target.scale",
+                                                       "proposal.loc", "proposal.scale"))]
+        sz = [a.numel() for a in cols[0]]
+        if any([a.numel() for a in c] != sz for c in cols[1:]):
             raise ValueError("target and proposal of an item must have the same size")
-        # the four concatenated inputs as four quarters of one buffer (one cat)
+        sizes = np.array(sz, dtype=np.int64)
+        # the four concatenated inputs as four quarters of one buffer (one cat;
+        # along dim 0 of equal trailing shapes it is the concatenation of the
+        # flattened arrays, 1-D latents always; else each array flattened first,
+        # which cost 65 us for I2's 96 arrays)
         item_off = np.concatenate([[0], np.cumsum(sizes)]).astype(np.int64)
         D = int(item_off[-1])
-        big = torch.cat([a for c in cols for a in c])
+        flat = [a for c in cols for a in c]
+        try:
+            big = torch.cat(flat).reshape(-1)
+        except RuntimeError:
+            big = None
+        if big is None or big.numel() != 4 * D:
+            big = torch.cat([a.reshape(-1) for a in flat])
         cat = [big[k * D:(k + 1) * D] for k in range(4)]
         need = int(lib.cwq_code_grouped_importance_batch_workspace_size(D, n_items))
         ws = torch.empty(max(need, 1), dtype=torch.uint8, device=dev)

@@ -100,8 +100,7 @@ __device__ __forceinline__ int64_t block_exclusive_scan_1024(int64_t v, int64_t*
 // tprefix[g] = sum_{h<g} tiles(N_h), tiles(N) = 0 for max(N, 1) <= kImpSmallN
 // (k_imp_small's groups), else ceil(N / cpt); tprefix[nb] = total tiles.
 // Also resets the per-group shared screening threshold gtau[g] and the
-// dynamic hand-out counter.  One workgroup of 1024 threads, each over a
-// contiguous run of groups.
+// dynamic hand-out counter.  One workgroup of 1024 threads.
 __global__ void __launch_bounds__(1024) k_imp_tiles(const int64_t* __restrict__ n_samples,
                                                     int64_t nb, int64_t* __restrict__ cpt_out,
                                                     int64_t* __restrict__ tprefix,
@@ -109,58 +108,55 @@ __global__ void __launch_bounds__(1024) k_imp_tiles(const int64_t* __restrict__ 
                                                     unsigned long long* __restrict__ next_tile) {
   __shared__ int64_t wsum[16];
   if (threadIdx.x == 0) *next_tile = 0ull;
-  const int64_t chunk = (nb + 1023) / 1024;
-  const int64_t g0 = threadIdx.x * chunk;
-  const int64_t g1 = (g0 + chunk < nb) ? g0 + chunk : nb;
-  // up to kRegs groups per thread (nb <= 16,384): every count loaded at once
-  // into registers (one memory latency, not one per group: I2's 13,852 groups
-  // took 36 us with the loads in the loop)
-  constexpr int kRegs = 16;
-  const bool in_regs = chunk <= kRegs;
+  // thread t takes groups t, t + 1024, ... (coalesced loads and stores); the
+  // prefix is one block scan per 1,024 groups with a running carry.  (I2's
+  // 13,852 groups: ~27 us either way -- neither the strided accesses nor the
+  // 64-bit divisions of the previous per-thread-run form were the cost)
+  const int64_t rounds = (nb + 1023) / 1024;
+  constexpr int kRegs = 16;  // nb <= 16,384: every count held in registers
+  const bool in_regs = rounds <= kRegs;
+  auto count_at = [&](int64_t g) -> int64_t {
+    const int64_t n = n_samples[g];
+    return n > 1 ? n : 1;
+  };
   int64_t nv[kRegs];
   int64_t cand = 0;
   if (in_regs) {
 #pragma unroll
-    for (int i = 0; i < kRegs; ++i) nv[i] = g0 + i < g1 ? n_samples[g0 + i] : 1;
+    for (int r = 0; r < kRegs; ++r) {
+      const int64_t g = (int64_t)r * 1024 + threadIdx.x;
+      nv[r] = g < nb ? count_at(g) : 0;
+    }
 #pragma unroll
-    for (int i = 0; i < kRegs; ++i) {
-      nv[i] = nv[i] > 1 ? nv[i] : 1;
-      if (g0 + i < g1) {
-        cand += nv[i];
-        gtau[g0 + i] = ord_f32(-__builtin_inff());
-      }
-    }
+    for (int r = 0; r < kRegs; ++r) cand += nv[r];
   } else {
-    for (int64_t g = g0; g < g1; ++g) {
-      const int64_t n = n_samples[g] > 1 ? n_samples[g] : 1;
-      cand += n;
-      gtau[g] = ord_f32(-__builtin_inff());
-    }
+    for (int64_t g = threadIdx.x; g < nb; g += 1024) cand += count_at(g);
   }
+  for (int64_t g = threadIdx.x; g < nb; g += 1024) gtau[g] = ord_f32(-__builtin_inff());
   int64_t T = 0;
   (void)block_exclusive_scan_1024(cand, wsum, &T);
   const int64_t cpt = imp_cand_per_tile(T);
-  auto count = [&](int64_t g) -> int64_t {
+  // a group k_imp_small codes takes no tile; cpt is a power of two
+  const int lg = __builtin_ctzll((unsigned long long)cpt);
+  auto ntiles = [&](int64_t n) -> int64_t { return n <= kImpSmallN ? 0 : (n + cpt - 1) >> lg; };
+  int64_t carry = 0;
+  for (int64_t r = 0; r < rounds; ++r) {
+    const int64_t g = r * 1024 + threadIdx.x;
+    int64_t n = 0;
     if (in_regs) {
-      int64_t n = 1;
 #pragma unroll
-      for (int i = 0; i < kRegs; ++i) n = g - g0 == i ? nv[i] : n;
-      return n;
+      for (int i = 0; i < kRegs; ++i) n = r == i ? nv[i] : n;
+    } else if (g < nb) {
+      n = count_at(g);
     }
-    return n_samples[g] > 1 ? n_samples[g] : 1;
-  };
-  // a group k_imp_small codes takes no tile
-  auto ntiles = [&](int64_t n) -> int64_t { return n <= kImpSmallN ? 0 : (n + cpt - 1) / cpt; };
-  int64_t tiles = 0;
-  for (int64_t g = g0; g < g1; ++g) tiles += ntiles(count(g));
-  int64_t all = 0;
-  int64_t run = block_exclusive_scan_1024(tiles, wsum, &all);
-  for (int64_t g = g0; g < g1; ++g) {
-    tprefix[g] = run;
-    run += ntiles(count(g));
+    const int64_t v = g < nb ? ntiles(n) : 0;
+    int64_t tot = 0;
+    const int64_t ex = block_exclusive_scan_1024(v, wsum, &tot);
+    if (g < nb) tprefix[g] = carry + ex;
+    carry += tot;
   }
   if (threadIdx.x == 0) {
-    tprefix[nb] = all;
+    tprefix[nb] = carry;
     *cpt_out = cpt;
   }
 }
