@@ -2274,9 +2274,9 @@ int64_t grouped_importance_impl(int64_t I, const int64_t* item_off, const float*
     if ((oi.eval_ms_out && (e = hipEventRecord(tev.ev[0], s)) != hipSuccess) ||
         (e = cwq::launch_importance_encode(t_loc, t_scale, zeros, ones, offs, nsamp, Gtot, D,
                                            seeds[0], 0, I > 1 ? gseed : nullptr,
-                                           oi.prune_mode >= 2 ? 1 : 0, idx, sample, w + l.enc,
-                                           s, tcand, cwq::importance_tile_count(ns_h, Gtot, tcand))) !=
-            hipSuccess ||
+                                           oi.prune_mode >= 2 ? 1 : 0, idx, nullptr, w + l.enc,
+                                           s, tcand, cwq::importance_tile_count(ns_h, Gtot, tcand),
+                                           p_loc, p_scale, out)) != hipSuccess ||
         (oi.eval_ms_out && (e = hipEventRecord(tev.ev[1], s)) != hipSuccess))
       return drain_fail(e, "importance encode");
     if (oi.eval_ms_out) {
@@ -2284,12 +2284,13 @@ int64_t grouped_importance_impl(int64_t I, const int64_t* item_off, const float*
           (e = hipEventElapsedTime(oi.eval_ms_out, tev.ev[0], tev.ev[1])) != hipSuccess)
         return drain_fail(e, "event time");
     }
-  } else {
-    if ((e = hipMemsetAsync(sample, 0, Dz * 4, s)) != hipSuccess) return drain_fail(e, "memset");
+  } else {  // (no groups: D == 0 returned above; kept for completeness)
+    if ((e = hipMemsetAsync(sample, 0, Dz * 4, s)) != hipSuccess ||
+        (e = cwq::launch_destandardise(sample, p_loc, p_scale, D, out, s)) != hipSuccess)
+      return drain_fail(e, "destandardise");
   }
-  // :265 rescale, :267 outliers keep their target draw
-  if ((e = cwq::launch_destandardise(sample, p_loc, p_scale, D, out, s)) != hipSuccess)
-    return drain_fail(e, "destandardise");
+  // :265 rescale: in the encoder's row launch (every dim is in a group);
+  // :267 outliers keep their target draw
   if ((e = hipMemcpyAsync(out_h, out, Gtot > 0 ? l.a4 + (size_t)Gtot * 8 : Dz * 4,
                           hipMemcpyDeviceToHost, s)) != hipSuccess ||
       (e = hipEventRecord(hev.ev[1], s)) != hipSuccess)

@@ -99,13 +99,14 @@ __device__ __forceinline__ int64_t block_exclusive_scan_1024(int64_t v, int64_t*
 // Chooses the launch's candidates per tile (*cpt_out), then
 // tprefix[g] = sum_{h<g} tiles(N_h), tiles(N) = 0 for max(N, 1) <= kImpSmallN
 // (k_imp_small's groups), else ceil(N / cpt); tprefix[nb] = total tiles.
-// Also resets the per-group shared screening threshold gtau[g] and the
-// dynamic hand-out counter.  One workgroup of 1024 threads.
+// Also resets the per-group shared screening threshold gtau[g], the argmax
+// keys and the dynamic hand-out counter.  One workgroup of 1024 threads.
 __global__ void __launch_bounds__(1024) k_imp_tiles(const int64_t* __restrict__ n_samples,
                                                     int64_t nb, int64_t* __restrict__ cpt_out,
                                                     int64_t* __restrict__ tprefix,
                                                     uint32_t* __restrict__ gtau,
-                                                    unsigned long long* __restrict__ next_tile) {
+                                                    unsigned long long* __restrict__ next_tile,
+                                                    unsigned long long* __restrict__ keys) {
   __shared__ int64_t wsum[16];
   if (threadIdx.x == 0) *next_tile = 0ull;
   // thread t takes groups t, t + 1024, ... (coalesced loads and stores); the
@@ -132,7 +133,10 @@ __global__ void __launch_bounds__(1024) k_imp_tiles(const int64_t* __restrict__ 
   } else {
     for (int64_t g = threadIdx.x; g < nb; g += 1024) cand += count_at(g);
   }
-  for (int64_t g = threadIdx.x; g < nb; g += 1024) gtau[g] = ord_f32(-__builtin_inff());
+  for (int64_t g = threadIdx.x; g < nb; g += 1024) {
+    gtau[g] = ord_f32(-__builtin_inff());
+    keys[g] = 0ull;  // every group's argmax key (no separate memset launch)
+  }
   int64_t T = 0;
   (void)block_exclusive_scan_1024(cand, wsum, &T);
   const int64_t cpt = imp_cand_per_tile(T);
@@ -612,12 +616,17 @@ __global__ void __launch_bounds__(256) k_imp_small(
 
 // Row `index` of group g's candidate stream: p_loc + p_scale * z (misc.py:14-15).
 // With keys != nullptr the index comes from the argmax key (encoder), else
-// from index_in (decoder, coded_importance_sampler.py:82-109).
+// from index_in (decoder, coded_importance_sampler.py:82-109).  out_sample
+// (if given) gets the row; dst_out (if given) the row destandardised,
+// dst_scale * row + dst_loc, exactly as k_destandardise computes it (the
+// grouped calls' :265 rescale without a launch of its own).
 __global__ void __launch_bounds__(256) k_imp_rows(
     const unsigned long long* __restrict__ keys, const int64_t* __restrict__ index_in,
     const float* __restrict__ p_loc, const float* __restrict__ p_scale,
     const int64_t* __restrict__ block_off, int64_t nb, SeedSpec seeds,
-    int64_t* __restrict__ index_out, float* __restrict__ out_sample) {
+    int64_t* __restrict__ index_out, float* __restrict__ out_sample,
+    const float* __restrict__ dst_loc, const float* __restrict__ dst_scale,
+    float* __restrict__ dst_out) {
   __shared__ double logtab[32];
   fill_logtab(logtab);
   const uint32_t wv = wave_id();
@@ -644,7 +653,11 @@ __global__ void __launch_bounds__(256) k_imp_rows(
         v = p_scale[off + j] * zz;
         v = p_loc[off + j] + v;
       }
-      out_sample[off + j] = v;
+      if (out_sample) out_sample[off + j] = v;
+      if (dst_out) {
+        const float m = dst_scale[off + j] * v;
+        dst_out[off + j] = m + dst_loc[off + j];
+      }
     }
   }
 }
@@ -695,7 +708,8 @@ hipError_t launch_importance_encode(const float* t_loc, const float* t_scale, co
                                     const int32_t* block_seeds, int allow_screen,
                                     int64_t* out_index, float* out_sample, void* workspace,
                                     hipStream_t stream, int64_t total_cands,
-                                    int64_t total_tiles) {
+                                    int64_t total_tiles, const float* dst_loc,
+                                    const float* dst_scale, float* dst_out) {
   if (nb <= 0) return hipSuccess;
   auto up = [](size_t v) { return (v + 255) / 256 * 256; };
   char* w = (char*)workspace;
@@ -707,13 +721,11 @@ hipError_t launch_importance_encode(const float* t_loc, const float* t_scale, co
   unsigned long long* next_tile = (unsigned long long*)((char*)gtau + up((size_t)nb * 4));
   int64_t* cpt = (int64_t*)(next_tile + 1);
   const SeedSpec ss{seed, block_id_base, block_seeds};
-  hipError_t e = hipMemsetAsync(keys, 0, (size_t)nb * 8, stream);
-  if (e != hipSuccess) return e;
   if (total_dims > 0)
     hipLaunchKernelGGL(k_imp_prep, dim3(grid_for(total_dims, 256, 65536)), dim3(256), 0, stream,
                        t_scale, p_scale, total_dims, lnt, lnp);
   hipLaunchKernelGGL(k_imp_tiles, dim3(1), dim3(1024), 0, stream, n_samples, nb, cpt, tprefix,
-                     gtau, next_tile);
+                     gtau, next_tile, keys);
   const bool cmax = total_cands >= 0 && imp_cand_per_tile(total_cands) == kImpCandPerTile;
   auto eval = block_seeds ? (cmax ? k_imp_eval<true, true> : k_imp_eval<true, false>)
                           : (cmax ? k_imp_eval<false, true> : k_imp_eval<false, false>);
@@ -729,7 +741,7 @@ hipError_t launch_importance_encode(const float* t_loc, const float* t_scale, co
                        t_scale, p_loc, p_scale, lnt, lnp, block_off, n_samples, nb, ss, keys);
   hipLaunchKernelGGL(k_imp_rows, dim3(grid_for(nb, 4, 65536)), dim3(256), 0, stream,
                      (const unsigned long long*)keys, (const int64_t*)nullptr, p_loc, p_scale,
-                     block_off, nb, ss, out_index, out_sample);
+                     block_off, nb, ss, out_index, out_sample, dst_loc, dst_scale, dst_out);
   return hipGetLastError();
 }
 
@@ -750,7 +762,8 @@ hipError_t launch_importance_decode(const int64_t* index, const float* p_loc,
   if (nb <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_imp_rows, dim3(grid_for(nb, 4, 65536)), dim3(256), 0, stream,
                      (const unsigned long long*)nullptr, index, p_loc, p_scale, block_off, nb,
-                     SeedSpec{seed, block_id_base, nullptr}, (int64_t*)nullptr, out_sample);
+                     SeedSpec{seed, block_id_base, nullptr}, (int64_t*)nullptr, out_sample,
+                     (const float*)nullptr, (const float*)nullptr, (float*)nullptr);
   return hipGetLastError();
 }
 

@@ -169,7 +169,8 @@ hipError_t launch_importance_encode(const float* t_loc, const float* t_scale, co
                                     const int32_t* block_seeds, int allow_screen,
                                     int64_t* out_index, float* out_sample, void* workspace,
                                     hipStream_t stream, int64_t total_cands = -1,
-                                    int64_t total_tiles = -1);
+                                    int64_t total_tiles = -1, const float* dst_loc = nullptr,
+                                    const float* dst_scale = nullptr, float* dst_out = nullptr);
 // The encode launch's k_imp_eval tile count from host copies of the plan
 // (total_cands: sum of max(N_g, 1)); it only selects the tile hand-out.
 int64_t importance_tile_count(const int64_t* n_samples_host, int64_t nb, int64_t total_cands);
