@@ -1,8 +1,8 @@
 """The body of code_grouped_importance_sample_batch (fast path) on I2's
 batch, re-run with a lap after each piece (GPU box): argument checks and
 concatenation, host buffers, the native call, then the wrapper's result
-work (index gather, quint16, Elias-delta, code lengths, the per-item
-tuples and copies).  Host wall time, averaged.
+work (index gather, quint16 of the outliers, Elias-delta, code lengths, the
+per-item views).  Host wall time, averaged.
 
   python tools/imp_batch_body_laps.py [calls]"""
 import os
