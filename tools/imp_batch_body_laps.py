@@ -38,11 +38,12 @@ for it in range(N + 20):
     n_items = len(T)
     seeds32 = np.full(n_items, 42, dtype=np.int32)
     raw = ([t.loc for t in T], [t.scale for t in T], [p.loc for p in P], [p.scale for p in P])
-    cols = [[a.reshape(-1) for a in c] for c in raw]
-    sizes = np.array([a.numel() for a in cols[0]], dtype=np.int64)
+    sz = [a.numel() for a in raw[0]]
+    bad = any([a.numel() for a in c] != sz for c in raw[1:])
+    sizes = np.array(sz, dtype=np.int64)
     item_off = np.concatenate([[0], np.cumsum(sizes)]).astype(np.int64)
     D = int(item_off[-1])
-    big = torch.cat([a for c in cols for a in c])
+    big = torch.cat([a for c in raw for a in c]).reshape(-1)
     cat = [big[k * D:(k + 1) * D] for k in range(4)]
     ts.append(time.perf_counter())
     need = int(lib.cwq_code_grouped_importance_batch_workspace_size(D, n_items))
